@@ -1,0 +1,41 @@
+# Build recipes (no cmake): the HIP product library, the synthetic-input
+# library, and the CPU oracle (test infrastructure).  `python -c "import
+# __graft_entry__ as g; g.build()"` runs `make all`.
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+PKG      := gf-pl-slam_amd
+LIBDIR   := $(PKG)/lib
+
+# -ffp-contract=off everywhere: bit-identical fp64 between kernels and oracle (pin N1)
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fPIC -shared \
+            -Wall -Wno-unused-result -Iinclude
+CXXFLAGS := -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wall -Iinclude
+# the oracle doubles as the timed CPU baseline: reference flags are -O3 -march=native
+# (CMakeLists.txt:68); x86-64-v3 keeps the .so runnable on the GPU host.
+ORACLEFLAGS := $(CXXFLAGS) -march=x86-64-v3
+
+HIP_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cpp)
+HIP_HDR  := $(wildcard $(PKG)/csrc/*.hpp) include/gfpl.h
+
+all: $(LIBDIR)/libgfpl_hip.so $(LIBDIR)/libgfpl_synth.so oracle/liboracle.so
+
+$(LIBDIR)/libgfpl_hip.so: $(HIP_SRC) $(HIP_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) $(HIP_SRC) -o $@
+
+$(LIBDIR)/libgfpl_synth.so: $(PKG)/synth/gfpl_synth.cpp $(PKG)/synth/gfpl_synth.h include/gfpl.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(CXXFLAGS) -march=x86-64-v3 $< -o $@ -lpthread
+
+oracle/liboracle.so: oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h include/gfpl.h
+	$(CXX) $(ORACLEFLAGS) $< -o $@
+
+oracle: oracle/liboracle.so
+synth: $(LIBDIR)/libgfpl_synth.so
+hip: $(LIBDIR)/libgfpl_hip.so
+
+clean:
+	rm -f $(LIBDIR)/*.so oracle/liboracle.so
+
+.PHONY: all clean oracle synth hip

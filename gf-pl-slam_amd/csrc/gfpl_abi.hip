@@ -1,0 +1,553 @@
+// gfpl_abi.hip — the extern "C" boundary (include/gfpl.h): contexts, resident
+// sequence batches, stage/step entry points and state transfer.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gfpl.h"
+#include "gfpl_kernels.hpp"
+
+using namespace gfpl;
+
+struct gfpl_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    gfpl_camera cam{};
+    gfpl_config cfg{};
+    bool has_cam = false, has_cfg = false;
+    bool timing = false;
+    hipEvent_t ev[8]{};
+    float stage_ms[7]{};
+};
+
+struct gfpl_seqbatch {
+    gfpl_ctx* ctx = nullptr;
+    int B = 0, kp_cap = 0, kl_cap = 0, mpt_cap = 0, mls_cap = 0;
+    void* base = nullptr;
+    int64_t bytes = 0;
+    DevFrame slot[2];
+    int prev_slot = 0;
+    bool initialized = false;
+    bool has_curr = false;
+    DevTrack tr{};
+    DevScratch scr{};
+};
+
+namespace {
+
+#define HIPCHK(x)                                                   \
+    do {                                                            \
+        hipError_t e_ = (x);                                        \
+        if (e_ != hipSuccess) {                                     \
+            std::fprintf(stderr, "gfpl: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return GFPL_E_HIP;                                      \
+        }                                                           \
+    } while (0)
+
+// bump allocator over one device allocation (256-B aligned fields)
+struct Carver {
+    size_t off = 0;
+    char* base = nullptr;
+    template <typename T>
+    T* take(size_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+void carve(Carver& c, gfpl_seqbatch* sb) {
+    const size_t B = sb->B, P = (size_t)B * sb->kp_cap, L = (size_t)B * sb->kl_cap;
+    for (int s = 0; s < 2; ++s) {
+        DevFrame& f = sb->slot[s];
+        f.pt.pl = c.take<double>(P * 2); f.pt.pl_obs = c.take<double>(P * 2);
+        f.pt.disp = c.take<double>(P); f.pt.P = c.take<double>(P * 3); f.pt.sigma2 = c.take<double>(P);
+        f.pt.idx = c.take<int32_t>(P); f.pt.level = c.take<int32_t>(P); f.pt.inlier = c.take<uint8_t>(P);
+        f.pt.desc = c.take<uint8_t>(P * 32); f.pt.n = c.take<int32_t>(B);
+        f.ls.spl = c.take<double>(L * 2); f.ls.epl = c.take<double>(L * 2);
+        f.ls.spl_obs = c.take<double>(L * 2); f.ls.epl_obs = c.take<double>(L * 2);
+        f.ls.sdisp = c.take<double>(L); f.ls.edisp = c.take<double>(L);
+        f.ls.sdisp_obs = c.take<double>(L); f.ls.edisp_obs = c.take<double>(L);
+        f.ls.angle = c.take<double>(L); f.ls.sigma2 = c.take<double>(L);
+        f.ls.sP = c.take<double>(L * 3); f.ls.eP = c.take<double>(L * 3);
+        f.ls.le = c.take<double>(L * 3); f.ls.le_obs = c.take<double>(L * 3);
+        f.ls.covS = c.take<double>(L * 9); f.ls.covE = c.take<double>(L * 9);
+        f.ls.cut = c.take<double>(L * 2); f.ls.invcov = c.take<double>(L * 36);
+        f.ls.idx = c.take<int32_t>(L); f.ls.level = c.take<int32_t>(L); f.ls.inlier = c.take<uint8_t>(L);
+        f.ls.desc = c.take<uint8_t>(L * 32); f.ls.n = c.take<int32_t>(B);
+        f.pose.Tfw = c.take<double>(B * 16); f.pose.DT = c.take<double>(B * 16);
+        f.pose.DT_cov = c.take<double>(B * 36); f.pose.Tfw_cov = c.take<double>(B * 36);
+        f.pose.DT_cov_eig = c.take<double>(B * 6);
+        f.pose.err_norm = c.take<double>(B); f.pose.time_stamp = c.take<double>(B);
+    }
+    sb->tr.matched_pt = c.take<int32_t>(B * sb->mpt_cap);
+    sb->tr.n_matched_pt = c.take<int32_t>(B);
+    sb->tr.matched_ls = c.take<int32_t>(B * sb->mls_cap);
+    sb->tr.n_matched_ls = c.take<int32_t>(B);
+    sb->tr.n_inliers = c.take<int32_t>(B);
+    sb->tr.n_inliers_pt = c.take<int32_t>(B);
+    sb->tr.n_inliers_ls = c.take<int32_t>(B);
+    sb->tr.num_frame_loss = c.take<int32_t>(B);
+    sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
+    sb->scr.cut_pt = c.take<double>(B * sb->mpt_cap * 21);
+    sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
+    sb->scr.bytes = c.take<int64_t>(B);
+    sb->scr.n_subpix = c.take<int32_t>(B);
+}
+
+DevCam devcam(const gfpl_camera& c) {
+    DevCam d;
+    d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy; d.b = c.b;
+    d.width = c.width; d.height = c.height; d.n_levels = c.n_levels;
+    for (int i = 0; i < GFPL_MAX_LEVELS; ++i) {
+        d.scale[i] = c.scale[i]; d.inv_scale[i] = c.inv_scale[i];
+        d.lvl_cols[i] = c.lvl_cols[i]; d.lvl_rows[i] = c.lvl_rows[i];
+        d.lvl_offset[i] = c.lvl_offset[i];
+        d.sigma2_pt[i] = c.sigma2_pt[i]; d.sigma2_ln[i] = c.sigma2_ln[i];
+    }
+    d.pyr_bytes = c.pyr_bytes;
+    return d;
+}
+
+KParams params(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.cam = devcam(sb->ctx->cam);
+    p.cfg = sb->ctx->cfg;
+    p.prev = sb->slot[sb->prev_slot];
+    p.curr = sb->slot[1 - sb->prev_slot];
+    p.tr = sb->tr;
+    p.scr = sb->scr;
+    if (in) p.in = *in;
+    p.B = sb->B; p.kp_cap = sb->kp_cap; p.kl_cap = sb->kl_cap;
+    p.mpt_cap = sb->mpt_cap; p.mls_cap = sb->mls_cap;
+    return p;
+}
+
+int check_in(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (!in) return GFPL_E_INVALID;
+    if (in->batch != sb->B || in->kp_cap != sb->kp_cap || in->kl_cap != sb->kl_cap) return GFPL_E_INVALID;
+    if (!in->n_kp_l || !in->n_kp_r || !in->kp_l || !in->kp_r || !in->pdesc_l || !in->pdesc_r || !in->n_kl_l ||
+        !in->n_kl_r || !in->kl_l || !in->kl_r || !in->ldesc_l || !in->ldesc_r || !in->pyr_r || !in->time_stamp)
+        return GFPL_E_INVALID;
+    return GFPL_OK;
+}
+
+int cfg_supported(const gfpl_config& c) {
+    if (!c.best_lr_matches || !c.lr_in_parallel || !c.cut_with_max_vol) return GFPL_E_UNSUPPORTED;
+    if (c.max_point_match_num < 1 || c.max_point_match_num > GFPL_MAX_MATCHED_PT) return GFPL_E_INVALID;
+    if (c.max_line_match_num < 1 || c.max_line_match_num > GFPL_MAX_MATCHED_LS) return GFPL_E_INVALID;
+    return GFPL_OK;
+}
+
+void tmark(gfpl_ctx* c, int i) {
+    if (c->timing) (void)hipEventRecord(c->ev[i], c->stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gfpl_create(int device, void* stream, gfpl_ctx** out) {
+    if (!out) return GFPL_E_INVALID;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return GFPL_E_NO_DEVICE;
+    if (device < 0 || device >= n) return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(device));
+    gfpl_ctx* c = new gfpl_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)stream;
+    gfpl_config_default(&c->cfg);
+    c->has_cfg = true;
+    for (int i = 0; i < 8; ++i)
+        if (hipEventCreate(&c->ev[i]) != hipSuccess) { delete c; return GFPL_E_HIP; }
+    *out = c;
+    return GFPL_OK;
+}
+
+int gfpl_destroy(gfpl_ctx* c) {
+    if (!c) return GFPL_E_INVALID;
+    for (int i = 0; i < 8; ++i)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    delete c;
+    return GFPL_OK;
+}
+
+int gfpl_set_camera(gfpl_ctx* c, const gfpl_camera* cam) {
+    if (!c || !cam || cam->n_levels < 1 || cam->n_levels > GFPL_MAX_LEVELS) return GFPL_E_INVALID;
+    c->cam = *cam;
+    c->has_cam = true;
+    return GFPL_OK;
+}
+
+int gfpl_set_config(gfpl_ctx* c, const gfpl_config* cfg) {
+    if (!c || !cfg) return GFPL_E_INVALID;
+    int e = cfg_supported(*cfg);
+    if (e) return e;
+    c->cfg = *cfg;
+    c->has_cfg = true;
+    return GFPL_OK;
+}
+
+int gfpl_get_camera(const gfpl_ctx* c, gfpl_camera* cam) {
+    if (!c || !cam || !c->has_cam) return GFPL_E_INVALID;
+    *cam = c->cam;
+    return GFPL_OK;
+}
+
+int gfpl_get_config(const gfpl_ctx* c, gfpl_config* cfg) {
+    if (!c || !cfg) return GFPL_E_INVALID;
+    *cfg = c->cfg;
+    return GFPL_OK;
+}
+
+int gfpl_synchronize(gfpl_ctx* c) {
+    if (!c) return GFPL_E_INVALID;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GFPL_OK;
+}
+
+int gfpl_seqbatch_create(gfpl_ctx* c, int batch, int kp_cap, int kl_cap, gfpl_seqbatch** out) {
+    if (!c || !out || batch < 1 || kp_cap < 2 || kl_cap < 2 || kp_cap > 16384 || kl_cap > 1536 || !c->has_cam)
+        return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    gfpl_seqbatch* sb = new gfpl_seqbatch();
+    sb->ctx = c;
+    sb->B = batch;
+    sb->kp_cap = (kp_cap + 1) & ~1;
+    sb->kl_cap = (kl_cap + 1) & ~1;
+    sb->mpt_cap = c->cfg.max_point_match_num;
+    sb->mls_cap = c->cfg.max_line_match_num;
+    Carver dry;
+    carve(dry, sb);
+    sb->bytes = (int64_t)dry.off;
+    if (hipMalloc(&sb->base, dry.off) != hipSuccess) { delete sb; return GFPL_E_HIP; }
+    if (hipMemsetAsync(sb->base, 0, dry.off, c->stream) != hipSuccess) { (void)hipFree(sb->base); delete sb; return GFPL_E_HIP; }
+    Carver real;
+    real.base = (char*)sb->base;
+    carve(real, sb);
+    if (sb->kp_cap != kp_cap || sb->kl_cap != kl_cap) {   // caps must match the input layout
+        (void)hipFree(sb->base); delete sb; return GFPL_E_INVALID;
+    }
+    *out = sb;
+    return GFPL_OK;
+}
+
+int gfpl_seqbatch_destroy(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    (void)hipStreamSynchronize(sb->ctx->stream);
+    if (sb->base) (void)hipFree(sb->base);
+    delete sb;
+    return GFPL_OK;
+}
+
+int64_t gfpl_seqbatch_bytes(const gfpl_seqbatch* sb) { return sb ? sb->bytes : 0; }
+
+int gfpl_initialize(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (!sb) return GFPL_E_INVALID;
+    int e = check_in(sb, in);
+    if (e) return e;
+    KParams p = params(sb, in);
+    p.curr = sb->slot[sb->prev_slot];   // the initial frame becomes prev_frame
+    HIPCHK(launch_init(p, sb->ctx->stream));
+    sb->initialized = true;
+    sb->has_curr = false;
+    return GFPL_OK;
+}
+
+int gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized) return GFPL_E_STATE;
+    int e = check_in(sb, in);
+    if (e) return e;
+    HIPCHK(launch_stereo_points(params(sb, in), sb->ctx->stream));
+    sb->has_curr = true;
+    return GFPL_OK;
+}
+
+int gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized) return GFPL_E_STATE;
+    int e = check_in(sb, in);
+    if (e) return e;
+    HIPCHK(launch_stereo_lines(params(sb, in), sb->ctx->stream));
+    sb->has_curr = true;
+    return GFPL_OK;
+}
+
+int gfpl_line_uncertainty(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized) return GFPL_E_STATE;
+    HIPCHK(launch_line_uncertainty(params(sb, nullptr), sb->ctx->stream));
+    return GFPL_OK;
+}
+
+int gfpl_cross_points(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(launch_cross_points(params(sb, nullptr), sb->ctx->stream));
+    return GFPL_OK;
+}
+
+int gfpl_cross_lines(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(launch_cross_lines(params(sb, nullptr), sb->ctx->stream));
+    return GFPL_OK;
+}
+
+int gfpl_line_cut(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(launch_line_cut(params(sb, nullptr), sb->ctx->stream));
+    return GFPL_OK;
+}
+
+int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized) return GFPL_E_STATE;
+    int e = check_in(sb, in);
+    if (e) return e;
+    gfpl_ctx* c = sb->ctx;
+    KParams p = params(sb, in);
+    tmark(c, 0);
+    HIPCHK(launch_stereo_points(p, c->stream));
+    tmark(c, 1);
+    HIPCHK(launch_stereo_lines(p, c->stream));
+    tmark(c, 2);
+    // predictFramePose is fused into cross_points (src/stereoFrameHandler.cpp:100)
+    if (c->cfg.use_line_conf_cut) HIPCHK(launch_line_uncertainty(p, c->stream));   // :103-106
+    HIPCHK(launch_cross_points(p, c->stream));
+    tmark(c, 3);
+    HIPCHK(launch_cross_lines(p, c->stream));
+    tmark(c, 4);
+    if (c->cfg.use_line_conf_cut) HIPCHK(launch_line_cut(p, c->stream));
+    tmark(c, 5);
+    HIPCHK(launch_step_bytes(p, c->stream));
+    sb->has_curr = true;
+    return GFPL_OK;
+}
+
+int gfpl_optimize_pose(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(launch_pose(params(sb, nullptr), sb->ctx->stream));
+    tmark(sb->ctx, 6);
+    return GFPL_OK;
+}
+
+int gfpl_update_frame(gfpl_seqbatch* sb) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    sb->prev_slot = 1 - sb->prev_slot;
+    sb->has_curr = false;
+    return GFPL_OK;
+}
+
+int gfpl_frame_step(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    int e = gfpl_insert_stereo_pair(sb, in);
+    if (e) return e;
+    e = gfpl_optimize_pose(sb);
+    if (e) return e;
+    return gfpl_update_frame(sb);
+}
+
+int gfpl_knn2_hamming(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* idx,
+                      float* dist) {
+    if (!c || !q || !t || !idx || !dist || nq < 0 || (cell != 1 && cell != 2)) return GFPL_E_INVALID;
+    if (nt < 2) return GFPL_E_TOO_FEW_TRAIN;
+    if (nq == 0) return GFPL_OK;
+    HIPCHK(launch_knn2(q, nq, t, nt, cell, idx, dist, c->stream));
+    return GFPL_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ transfer --
+namespace {
+template <typename T>
+hipError_t d2h(T* dst, const T* src, size_t n, hipStream_t s) {
+    if (!dst || n == 0) return hipSuccess;
+    return hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, s);
+}
+template <typename T>
+hipError_t h2d(T* dst, const T* src, size_t n, hipStream_t s) {
+    if (!src || n == 0) return hipSuccess;
+    return hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, s);
+}
+}  // namespace
+
+extern "C" {
+
+#define XFER(fn, a, b, n) HIPCHK(fn(a, b, n, s))
+
+int gfpl_read_frame(gfpl_seqbatch* sb, int which, int seq, gfpl_frame_host* o) {
+    if (!sb || !o || seq < 0 || seq >= sb->B || (which != GFPL_PREV && which != GFPL_CURR)) return GFPL_E_INVALID;
+    hipStream_t s = sb->ctx->stream;
+    const DevFrame& f = sb->slot[which == GFPL_PREV ? sb->prev_slot : 1 - sb->prev_slot];
+    HIPCHK(hipStreamSynchronize(s));
+    int np = 0, nl = 0;
+    HIPCHK(hipMemcpy(&np, f.pt.n + seq, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&nl, f.ls.n + seq, 4, hipMemcpyDeviceToHost));
+    o->n_pt = np; o->n_ls = nl;
+    const size_t P = (size_t)seq * sb->kp_cap, L = (size_t)seq * sb->kl_cap;
+    XFER(d2h, o->pt_pl, f.pt.pl + 2 * P, 2 * (size_t)np);
+    XFER(d2h, o->pt_pl_obs, f.pt.pl_obs + 2 * P, 2 * (size_t)np);
+    XFER(d2h, o->pt_disp, f.pt.disp + P, (size_t)np);
+    XFER(d2h, o->pt_P, f.pt.P + 3 * P, 3 * (size_t)np);
+    XFER(d2h, o->pt_sigma2, f.pt.sigma2 + P, (size_t)np);
+    XFER(d2h, o->pt_idx, f.pt.idx + P, (size_t)np);
+    XFER(d2h, o->pt_level, f.pt.level + P, (size_t)np);
+    XFER(d2h, o->pt_inlier, f.pt.inlier + P, (size_t)np);
+    XFER(d2h, o->pdesc, f.pt.desc + 32 * P, 32 * (size_t)np);
+    XFER(d2h, o->ls_spl, f.ls.spl + 2 * L, 2 * (size_t)nl);
+    XFER(d2h, o->ls_epl, f.ls.epl + 2 * L, 2 * (size_t)nl);
+    XFER(d2h, o->ls_spl_obs, f.ls.spl_obs + 2 * L, 2 * (size_t)nl);
+    XFER(d2h, o->ls_epl_obs, f.ls.epl_obs + 2 * L, 2 * (size_t)nl);
+    XFER(d2h, o->ls_sdisp, f.ls.sdisp + L, (size_t)nl);
+    XFER(d2h, o->ls_edisp, f.ls.edisp + L, (size_t)nl);
+    XFER(d2h, o->ls_sdisp_obs, f.ls.sdisp_obs + L, (size_t)nl);
+    XFER(d2h, o->ls_edisp_obs, f.ls.edisp_obs + L, (size_t)nl);
+    XFER(d2h, o->ls_angle, f.ls.angle + L, (size_t)nl);
+    XFER(d2h, o->ls_sigma2, f.ls.sigma2 + L, (size_t)nl);
+    XFER(d2h, o->ls_sP, f.ls.sP + 3 * L, 3 * (size_t)nl);
+    XFER(d2h, o->ls_eP, f.ls.eP + 3 * L, 3 * (size_t)nl);
+    XFER(d2h, o->ls_le, f.ls.le + 3 * L, 3 * (size_t)nl);
+    XFER(d2h, o->ls_le_obs, f.ls.le_obs + 3 * L, 3 * (size_t)nl);
+    XFER(d2h, o->ls_covS, f.ls.covS + 9 * L, 9 * (size_t)nl);
+    XFER(d2h, o->ls_covE, f.ls.covE + 9 * L, 9 * (size_t)nl);
+    XFER(d2h, o->ls_cut, f.ls.cut + 2 * L, 2 * (size_t)nl);
+    XFER(d2h, o->ls_invcov, f.ls.invcov + 36 * L, 36 * (size_t)nl);
+    XFER(d2h, o->ls_idx, f.ls.idx + L, (size_t)nl);
+    XFER(d2h, o->ls_level, f.ls.level + L, (size_t)nl);
+    XFER(d2h, o->ls_inlier, f.ls.inlier + L, (size_t)nl);
+    XFER(d2h, o->ldesc, f.ls.desc + 32 * L, 32 * (size_t)nl);
+    XFER(d2h, o->Tfw, f.pose.Tfw + 16 * seq, 16);
+    XFER(d2h, o->DT, f.pose.DT + 16 * seq, 16);
+    XFER(d2h, o->DT_cov, f.pose.DT_cov + 36 * seq, 36);
+    XFER(d2h, o->Tfw_cov, f.pose.Tfw_cov + 36 * seq, 36);
+    XFER(d2h, o->DT_cov_eig, f.pose.DT_cov_eig + 6 * seq, 6);
+    XFER(d2h, &o->err_norm, f.pose.err_norm + seq, 1);
+    XFER(d2h, &o->time_stamp, f.pose.time_stamp + seq, 1);
+    HIPCHK(hipStreamSynchronize(s));
+    return GFPL_OK;
+}
+
+int gfpl_write_frame(gfpl_seqbatch* sb, int which, int seq, const gfpl_frame_host* o) {
+    if (!sb || !o || seq < 0 || seq >= sb->B || (which != GFPL_PREV && which != GFPL_CURR)) return GFPL_E_INVALID;
+    if (o->n_pt < 0 || o->n_pt > sb->kp_cap || o->n_ls < 0 || o->n_ls > sb->kl_cap) return GFPL_E_CAPACITY;
+    hipStream_t s = sb->ctx->stream;
+    DevFrame& f = sb->slot[which == GFPL_PREV ? sb->prev_slot : 1 - sb->prev_slot];
+    const int np = o->n_pt, nl = o->n_ls;
+    const size_t P = (size_t)seq * sb->kp_cap, L = (size_t)seq * sb->kl_cap;
+    XFER(h2d, f.pt.n + seq, &o->n_pt, 1);
+    XFER(h2d, f.ls.n + seq, &o->n_ls, 1);
+    XFER(h2d, f.pt.pl + 2 * P, o->pt_pl, 2 * (size_t)np);
+    XFER(h2d, f.pt.pl_obs + 2 * P, o->pt_pl_obs, 2 * (size_t)np);
+    XFER(h2d, f.pt.disp + P, o->pt_disp, (size_t)np);
+    XFER(h2d, f.pt.P + 3 * P, o->pt_P, 3 * (size_t)np);
+    XFER(h2d, f.pt.sigma2 + P, o->pt_sigma2, (size_t)np);
+    XFER(h2d, f.pt.idx + P, o->pt_idx, (size_t)np);
+    XFER(h2d, f.pt.level + P, o->pt_level, (size_t)np);
+    XFER(h2d, f.pt.inlier + P, o->pt_inlier, (size_t)np);
+    XFER(h2d, f.pt.desc + 32 * P, o->pdesc, 32 * (size_t)np);
+    XFER(h2d, f.ls.spl + 2 * L, o->ls_spl, 2 * (size_t)nl);
+    XFER(h2d, f.ls.epl + 2 * L, o->ls_epl, 2 * (size_t)nl);
+    XFER(h2d, f.ls.spl_obs + 2 * L, o->ls_spl_obs, 2 * (size_t)nl);
+    XFER(h2d, f.ls.epl_obs + 2 * L, o->ls_epl_obs, 2 * (size_t)nl);
+    XFER(h2d, f.ls.sdisp + L, o->ls_sdisp, (size_t)nl);
+    XFER(h2d, f.ls.edisp + L, o->ls_edisp, (size_t)nl);
+    XFER(h2d, f.ls.sdisp_obs + L, o->ls_sdisp_obs, (size_t)nl);
+    XFER(h2d, f.ls.edisp_obs + L, o->ls_edisp_obs, (size_t)nl);
+    XFER(h2d, f.ls.angle + L, o->ls_angle, (size_t)nl);
+    XFER(h2d, f.ls.sigma2 + L, o->ls_sigma2, (size_t)nl);
+    XFER(h2d, f.ls.sP + 3 * L, o->ls_sP, 3 * (size_t)nl);
+    XFER(h2d, f.ls.eP + 3 * L, o->ls_eP, 3 * (size_t)nl);
+    XFER(h2d, f.ls.le + 3 * L, o->ls_le, 3 * (size_t)nl);
+    XFER(h2d, f.ls.le_obs + 3 * L, o->ls_le_obs, 3 * (size_t)nl);
+    XFER(h2d, f.ls.covS + 9 * L, o->ls_covS, 9 * (size_t)nl);
+    XFER(h2d, f.ls.covE + 9 * L, o->ls_covE, 9 * (size_t)nl);
+    XFER(h2d, f.ls.cut + 2 * L, o->ls_cut, 2 * (size_t)nl);
+    XFER(h2d, f.ls.invcov + 36 * L, o->ls_invcov, 36 * (size_t)nl);
+    XFER(h2d, f.ls.idx + L, o->ls_idx, (size_t)nl);
+    XFER(h2d, f.ls.level + L, o->ls_level, (size_t)nl);
+    XFER(h2d, f.ls.inlier + L, o->ls_inlier, (size_t)nl);
+    XFER(h2d, f.ls.desc + 32 * L, o->ldesc, 32 * (size_t)nl);
+    XFER(h2d, f.pose.Tfw + 16 * seq, o->Tfw, 16);
+    XFER(h2d, f.pose.DT + 16 * seq, o->DT, 16);
+    XFER(h2d, f.pose.DT_cov + 36 * seq, o->DT_cov, 36);
+    XFER(h2d, f.pose.Tfw_cov + 36 * seq, o->Tfw_cov, 36);
+    XFER(h2d, f.pose.DT_cov_eig + 6 * seq, o->DT_cov_eig, 6);
+    XFER(h2d, f.pose.err_norm + seq, &o->err_norm, 1);
+    XFER(h2d, f.pose.time_stamp + seq, &o->time_stamp, 1);
+    HIPCHK(hipStreamSynchronize(s));
+    sb->initialized = true;
+    if (which == GFPL_CURR) sb->has_curr = true;
+    return GFPL_OK;
+}
+
+int gfpl_read_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* o) {
+    if (!sb || !o || seq < 0 || seq >= sb->B) return GFPL_E_INVALID;
+    hipStream_t s = sb->ctx->stream;
+    HIPCHK(hipStreamSynchronize(s));
+    std::memset(o, 0, sizeof(*o));
+    XFER(d2h, &o->n_matched_pt, sb->tr.n_matched_pt + seq, 1);
+    XFER(d2h, &o->n_matched_ls, sb->tr.n_matched_ls + seq, 1);
+    XFER(d2h, &o->n_inliers, sb->tr.n_inliers + seq, 1);
+    XFER(d2h, &o->n_inliers_pt, sb->tr.n_inliers_pt + seq, 1);
+    XFER(d2h, &o->n_inliers_ls, sb->tr.n_inliers_ls + seq, 1);
+    XFER(d2h, &o->num_frame_loss, sb->tr.num_frame_loss + seq, 1);
+    HIPCHK(hipStreamSynchronize(s));
+    XFER(d2h, o->matched_pt, sb->tr.matched_pt + (size_t)seq * sb->mpt_cap, (size_t)o->n_matched_pt);
+    XFER(d2h, o->matched_ls, sb->tr.matched_ls + (size_t)seq * sb->mls_cap, (size_t)o->n_matched_ls);
+    HIPCHK(hipStreamSynchronize(s));
+    return GFPL_OK;
+}
+
+int gfpl_write_track(gfpl_seqbatch* sb, int seq, const gfpl_track_host* o) {
+    if (!sb || !o || seq < 0 || seq >= sb->B) return GFPL_E_INVALID;
+    if (o->n_matched_pt < 0 || o->n_matched_pt > sb->mpt_cap || o->n_matched_ls < 0 || o->n_matched_ls > sb->mls_cap)
+        return GFPL_E_CAPACITY;
+    hipStream_t s = sb->ctx->stream;
+    XFER(h2d, sb->tr.n_matched_pt + seq, &o->n_matched_pt, 1);
+    XFER(h2d, sb->tr.n_matched_ls + seq, &o->n_matched_ls, 1);
+    XFER(h2d, sb->tr.n_inliers + seq, &o->n_inliers, 1);
+    XFER(h2d, sb->tr.n_inliers_pt + seq, &o->n_inliers_pt, 1);
+    XFER(h2d, sb->tr.n_inliers_ls + seq, &o->n_inliers_ls, 1);
+    XFER(h2d, sb->tr.num_frame_loss + seq, &o->num_frame_loss, 1);
+    XFER(h2d, sb->tr.matched_pt + (size_t)seq * sb->mpt_cap, o->matched_pt, (size_t)o->n_matched_pt);
+    XFER(h2d, sb->tr.matched_ls + (size_t)seq * sb->mls_cap, o->matched_ls, (size_t)o->n_matched_ls);
+    HIPCHK(hipStreamSynchronize(s));
+    return GFPL_OK;
+}
+
+int gfpl_set_timing(gfpl_ctx* c, int enable) {
+    if (!c) return GFPL_E_INVALID;
+    c->timing = enable != 0;
+    return GFPL_OK;
+}
+
+int gfpl_get_stage_times(gfpl_ctx* c, float* ms7) {
+    if (!c || !ms7) return GFPL_E_INVALID;
+    if (!c->timing) return GFPL_E_STATE;
+    HIPCHK(hipEventSynchronize(c->ev[6]));
+    for (int i = 0; i < 6; ++i) HIPCHK(hipEventElapsedTime(&ms7[i], c->ev[i], c->ev[i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms7[6], c->ev[0], c->ev[6]));
+    return GFPL_OK;
+}
+
+int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {
+    if (!sb || !bytes) return GFPL_E_INVALID;
+    std::vector<int64_t> v(sb->B);
+    HIPCHK(hipStreamSynchronize(sb->ctx->stream));
+    HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * sb->B, hipMemcpyDeviceToHost));
+    int64_t s = 0;
+    for (int64_t x : v) s += x;
+    *bytes = s;
+    return GFPL_OK;
+}
+
+}  // extern "C"

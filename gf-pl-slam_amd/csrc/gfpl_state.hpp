@@ -1,0 +1,86 @@
+// gfpl_state.hpp — HBM layout of B resident sequences (one StereoFrameHandler
+// each) and the parameter block every kernel receives by value.
+//
+// Layout: structure-of-arrays per frame slot, [B][cap][k] per field, so lane i
+// of a wave touches feature i of one sequence (coalesced 8/16/24-B rows).
+// Two frame slots ping-pong between prev and curr (updateFrame_ECCV18 is a
+// pointer swap, src/stereoFrameHandler.cpp:910-912).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/gfpl.h"
+#include "gfpl_device.hpp"
+
+namespace gfpl {
+
+struct DevPoints {            // StVO::PointFeature (include/stereoFeatures.h:36-60)
+    double* pl;      // [B*cap*2]
+    double* pl_obs;  // [B*cap*2]
+    double* disp;    // [B*cap]
+    double* P;       // [B*cap*3]
+    double* sigma2;  // [B*cap]
+    int32_t* idx;    // [B*cap]
+    int32_t* level;  // [B*cap]
+    uint8_t* inlier; // [B*cap]
+    uint8_t* desc;   // [B*cap*32]  pdesc_l
+    int32_t* n;      // [B]
+};
+
+struct DevLines {             // StVO::LineFeature (include/stereoFeatures.h:62-124)
+    double *spl, *epl, *spl_obs, *epl_obs;        // [B*cap*2]
+    double *sdisp, *edisp, *sdisp_obs, *edisp_obs; // [B*cap]
+    double *angle, *sigma2;                        // [B*cap]
+    double *sP, *eP, *le, *le_obs;                 // [B*cap*3]
+    double *covS, *covE;                           // [B*cap*9]
+    double *cut;                                   // [B*cap*2]
+    double *invcov;                                // [B*cap*36]
+    int32_t *idx, *level;                          // [B*cap]
+    uint8_t *inlier;                               // [B*cap]
+    uint8_t *desc;                                 // [B*cap*32]  ldesc_l
+    int32_t* n;                                    // [B]
+};
+
+struct DevPose {
+    double *Tfw, *DT;            // [B*16]
+    double *DT_cov, *Tfw_cov;    // [B*36]
+    double *DT_cov_eig;          // [B*6]
+    double *err_norm, *time_stamp; // [B]
+};
+
+struct DevFrame {
+    DevPoints pt;
+    DevLines ls;
+    DevPose pose;
+};
+
+struct DevTrack {
+    int32_t* matched_pt;   // [B*mpt_cap]
+    int32_t* n_matched_pt; // [B]
+    int32_t* matched_ls;   // [B*mls_cap]
+    int32_t* n_matched_ls; // [B]
+    int32_t* n_inliers;    // [B]
+    int32_t* n_inliers_pt; // [B]
+    int32_t* n_inliers_ls; // [B]
+    int32_t* num_frame_loss; // [B]
+};
+
+struct DevScratch {
+    double* cut_ls;   // [B*mls_cap*21] lower-triangle info of matched lines
+    double* cut_pt;   // [B*mpt_cap*21] lower-triangle info of matched points
+    int32_t* knn;     // [B*4*kcap] initial-frame knn results (idx0, d0, d1, ...)
+    int64_t* bytes;   // [B] algorithmic bytes of the last step
+    int32_t* n_subpix; // [B] left keypoints that reached the sub-pixel SAD (M_o)
+};
+
+// Everything a kernel needs, passed by value (kernarg segment).
+struct KParams {
+    DevCam cam;
+    gfpl_config cfg;
+    DevFrame prev, curr;
+    DevTrack tr;
+    DevScratch scr;
+    gfpl_frames in;       // device pointers of the current input batch
+    int B, kp_cap, kl_cap, mpt_cap, mls_cap;
+};
+
+}  // namespace gfpl

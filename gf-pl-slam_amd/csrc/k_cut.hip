@@ -1,0 +1,284 @@
+// k_cut.hip — good-line-cut: estimateProjUncertainty_submodular(0.05, {0,1})
+// (src/stereoFrameHandler.cpp:1618-1764) with getPoseInfoOnLine (:1342-1411),
+// getPoseInfoPoint (:1414-1447), updateEndPointByRatio (:1451-1470) and logdet
+// (include/linespec.h:43-56).
+//
+// The search is a serial chain over matched lines (each line's search reads
+// invCov_sum after all earlier lines).  One 64-lane wave owns one sequence:
+//  phase A  all lanes: initial info matrices (r = 0,0) of lines and points;
+//  phase B  21 lanes: invCov_sum, one lower-triangle element per lane, summed
+//           sequentially in list order (bit-identical to the reference order);
+//  phase C  serial over lines; per greedy step lanes 0..7 evaluate the 8
+//           neighbour cut ratios (info + 6x6 LLT + 6 logs each) in parallel and
+//           the wave picks the first strict maximum (the reference's j-loop).
+// Only the lower triangle is carried: LLT reads nothing else (ledger Q11).
+#include "gfpl_kernels.hpp"
+
+namespace gfpl {
+
+struct LineCutData {
+    double sP[3], eP[3], covS[9], covE[9], Jl[2];
+};
+
+// projected residual variance of one cut endpoint (src/stereoFrameHandler.cpp:1356-1369)
+__device__ double endpointVar(const DevCam& cam, const double* DT_inv, const double* Jl, const double* Pt,
+                              const double* cov) {
+    double Jdt[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Jdt[i * 3 + j] = DT_inv[i * 4 + j];
+    double cur[3];
+    se3_apply(DT_inv, Pt, cur);
+    // getJacob3D_2D (src/stereoFrame.cpp:1394-1412)
+    const double f = cam.fx, pz = cur[2], pz_2 = pz * pz;
+    double Jp[9];
+    Jp[0] = f / pz; Jp[3] = 0.0; Jp[6] = 0.0;
+    Jp[1] = 0.0; Jp[4] = f / pz; Jp[7] = 0.0;
+    Jp[2] = ((-f) * cur[0]) / pz_2;
+    Jp[5] = ((-f) * cur[1]) / pz_2;
+    Jp[8] = ((-f) * cam.b) / pz_2;
+    double T1[6], T2[6], T3[6], M[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T1[i * 3 + j] = (Jp[i * 3 + 0] * Jdt[0 * 3 + j] + Jp[i * 3 + 1] * Jdt[1 * 3 + j]) + Jp[i * 3 + 2] * Jdt[2 * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T2[i * 3 + j] = (T1[i * 3 + 0] * cov[0 * 3 + j] + T1[i * 3 + 1] * cov[1 * 3 + j]) + T1[i * 3 + 2] * cov[2 * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T3[i * 3 + j] = (T2[i * 3 + 0] * Jdt[j * 3 + 0] + T2[i * 3 + 1] * Jdt[j * 3 + 1]) + T2[i * 3 + 2] * Jdt[j * 3 + 2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            M[i * 2 + j] = (T3[i * 3 + 0] * Jp[j * 3 + 0] + T3[i * 3 + 1] * Jp[j * 3 + 1]) + T3[i * 3 + 2] * Jp[j * 3 + 2];
+    const double r0 = Jl[0] * M[0] + Jl[1] * M[2];
+    const double r1 = Jl[0] * M[1] + Jl[1] * M[3];
+    return r0 * Jl[0] + r1 * Jl[1];
+}
+
+// getPoseInfoOnLine: FULL -> 36 entries row-major, else lower triangle (21)
+template <bool FULL>
+__device__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT_inv, const LineCutData& L,
+                               double c0, double c1, double* info) {
+    double sPt[3], ePt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        sPt[k] = (1 - c0) * L.sP[k] + c0 * L.eP[k];
+        ePt[k] = (1 - c1) * L.eP[k] + c1 * L.sP[k];
+    }
+    const double a0 = (1 - c0) * (1 - c0), q0 = c0 * c0;
+    const double a1 = (1 - c1) * (1 - c1), q1 = c1 * c1;
+    double covSt[9], covEt[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        covSt[i] = a0 * L.covS[i] + q0 * L.covE[i];
+        covEt[i] = a1 * L.covE[i] + q1 * L.covS[i];
+    }
+    const double vs = endpointVar(cam, DT_inv, L.Jl, sPt, covSt);
+    const double ve = endpointVar(cam, DT_inv, L.Jl, ePt, covEt);
+    // Eigen 2x2 inverse via invdet (ledger Q10)
+    const double det = vs * ve - 0.0 * 0.0;
+    const double invdet = 1.0 / det;
+    const double i00 = ve * invdet, i10 = -0.0 * invdet, i01 = -0.0 * invdet, i11 = vs * invdet;
+    double curS[3], curE[3];
+    se3_apply(DT_inv, sPt, curS);
+    se3_apply(DT_inv, ePt, curE);
+    double Js[6], Je[6];
+    poseJac(cam, homog, curS, L.Jl[0], L.Jl[1], Js);
+    poseJac(cam, homog, curE, L.Jl[0], L.Jl[1], Je);
+    double T0[6], T1[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        T0[i] = Js[i] * i00 + Je[i] * i10;
+        T1[i] = Js[i] * i01 + Je[i] * i11;
+    }
+    if (FULL) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) info[i * 6 + j] = T0[i] * Js[j] + T1[i] * Je[j];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) info[tri(i, j)] = T0[i] * Js[j] + T1[i] * Je[j];
+    }
+}
+
+__device__ void load_line(const DevLines& L, size_t q, LineCutData& d) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { d.sP[k] = L.sP[3 * q + k]; d.eP[k] = L.eP[3 * q + k]; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { d.covS[k] = L.covS[9 * q + k]; d.covE[k] = L.covE[9 * q + k]; }
+    d.Jl[0] = L.le_obs[3 * q];
+    d.Jl[1] = L.le_obs[3 * q + 1];
+}
+
+__global__ void __launch_bounds__(64) k_line_cut(KParams p) {
+    __shared__ double DT_inv[16];
+    __shared__ double sum[24];
+    __shared__ double cm[8];
+    __shared__ int cv[8];
+    __shared__ double fin[36];
+    __shared__ double mback[1];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    const int npt = p.tr.n_matched_pt[b];
+    if (nls == 0) return;
+    const DevCam& cam = p.cam;
+    const double homog = p.cfg.homog_th;
+    DevLines& L = p.prev.ls;
+    const DevPoints& P = p.prev.pt;
+    const size_t lb = (size_t)b * p.kl_cap, pbase = (size_t)b * p.kp_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
+    const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
+    double* scr_l = p.scr.cut_ls + (size_t)b * p.mls_cap * 21;
+    double* scr_p = p.scr.cut_pt + (size_t)b * p.mpt_cap * 21;
+    if (lane == 0) {
+        // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635)
+        double Tc[16], Tp[16], Ti[16], D[16];
+        for (int i = 0; i < 16; ++i) { Tc[i] = p.curr.pose.Tfw[16 * b + i]; Tp[i] = p.prev.pose.Tfw[16 * b + i]; }
+        mat4_inv(Tc, Ti);
+        mat4_mul(Ti, Tp, D);
+        for (int i = 0; i < 16; ++i) DT_inv[i] = D[i];
+    }
+    __syncthreads();
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = DT_inv[i];
+    // ---- phase A
+    for (int m = lane; m < nls; m += 64) {
+        const size_t q = lb + mls[m];
+        LineCutData d;
+        load_line(L, q, d);
+        double info[36];
+        poseInfoOnLine<true>(cam, homog, Dl, d, 0.0, 0.0, info);
+        for (int i = 0; i < 36; ++i) L.invcov[36 * q + i] = info[i];
+        L.cut[2 * q] = 0.0; L.cut[2 * q + 1] = 0.0;
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j <= i; ++j) scr_l[(size_t)m * 21 + tri(i, j)] = info[i * 6 + j];
+    }
+    for (int m = lane; m < npt; m += 64) {
+        const size_t q = pbase + mpt[m];
+        double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
+        double cur[3], uv[2];
+        se3_apply(Dl, Pp, cur);
+        projection(cam, cur, uv);
+        const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
+        double J[6];
+        poseJac(cam, homog, cur, dx, dy, J);
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j <= i; ++j) scr_p[(size_t)m * 21 + tri(i, j)] = J[i] * J[j];
+    }
+    __syncthreads();
+    // ---- phase B: invCov_sum, sequential per element (lines then points)
+    if (lane < 21) {
+        double s = 0.0;
+        for (int m = 0; m < nls; ++m) s = s + scr_l[(size_t)m * 21 + lane];
+        for (int m = 0; m < npt; ++m) s = s + scr_p[(size_t)m * 21 + lane];
+        sum[lane] = s;
+    }
+    __syncthreads();
+    // ---- phase C
+    const double st = p.cfg.cut_step;
+    const double nb0[8] = {st, -st, 0, 0, st, st, -st, -st};
+    const double nb1[8] = {0, 0, st, -st, st, -st, st, -st};
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    for (int m = 0; m < nls; ++m) {
+        const size_t q = lb + mls[m];
+        LineCutData d;
+        load_line(L, q, d);
+        if (lane == 0) {
+            double a[21];
+            for (int i = 0; i < 21; ++i) a[i] = sum[i];
+            mback[0] = logdet6_lower(a);
+        }
+        __syncthreads();
+        if (lane < 21) sum[lane] = sum[lane] - scr_l[(size_t)m * 21 + lane];
+        __syncthreads();
+        double r0 = 0.0, r1 = 0.0;
+        double metric_back = mback[0];
+        while (r0 + r1 <= 1.0) {
+            if (lane < 8) {
+                const double t0 = r0 + nb0[lane], t1 = r1 + nb1[lane];
+                int valid = 1;
+                if (t0 + t1 > 1.0) valid = 0;
+                if (t0 < rlo || t0 > rhi) valid = 0;
+                if (t1 < rlo || t1 > rhi) valid = 0;
+                double mval = 0.0;
+                if (valid) {
+                    double tmp[21];
+                    poseInfoOnLine<false>(cam, homog, Dl, d, t0, t1, tmp);
+#pragma unroll
+                    for (int i = 0; i < 21; ++i) tmp[i] = tmp[i] + sum[i];
+                    mval = logdet6_lower(tmp);
+                }
+                cm[lane] = mval;
+                cv[lane] = valid;
+            }
+            __syncthreads();
+            double mi = metric_back;
+            int best = -1;
+            for (int j = 0; j < 8; ++j)
+                if (cv[j] && cm[j] > mi) { mi = cm[j]; best = j; }
+            __syncthreads();
+            if (best < 0) break;
+            r0 = r0 + nb0[best];
+            r1 = r1 + nb1[best];
+            metric_back = mi;
+        }
+        if (lane == 0) {
+            double info[36];
+            poseInfoOnLine<true>(cam, homog, Dl, d, r0, r1, info);
+            for (int i = 0; i < 36; ++i) { fin[i] = info[i]; L.invcov[36 * q + i] = info[i]; }
+            L.cut[2 * q] = r0; L.cut[2 * q + 1] = r1;
+            // updateEndPointByRatio (ledger Q4: eP uses the updated sP)
+            if (!(fabs(r0) < 0.0001 && fabs(r1) < 0.0001)) {
+                double sP[3] = {d.sP[0], d.sP[1], d.sP[2]}, eP[3] = {d.eP[0], d.eP[1], d.eP[2]};
+                if (fabs(r0) > 0.0001) {
+                    double s[3];
+                    for (int k = 0; k < 3; ++k) s[k] = (1 - r0) * sP[k] + r0 * eP[k];
+                    for (int k = 0; k < 3; ++k) { sP[k] = s[k]; L.sP[3 * q + k] = s[k]; }
+                    double uv[2];
+                    projection(cam, sP, uv);
+                    L.spl[2 * q] = uv[0]; L.spl[2 * q + 1] = uv[1];
+                    L.sdisp[q] = (cam.fx * cam.b) / sP[2];
+                }
+                if (fabs(r1) > 0.0001) {
+                    double e[3];
+                    for (int k = 0; k < 3; ++k) e[k] = (1 - r1) * eP[k] + r1 * sP[k];
+                    for (int k = 0; k < 3; ++k) { eP[k] = e[k]; L.eP[3 * q + k] = e[k]; }
+                    double uv[2];
+                    projection(cam, eP, uv);
+                    L.epl[2 * q] = uv[0]; L.epl[2 * q + 1] = uv[1];
+                    L.edisp[q] = (cam.fx * cam.b) / eP[2];
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < 21) {
+            // lower-triangle index -> (row, col)
+            int r = 0;
+            while ((r + 1) * (r + 2) / 2 <= lane) ++r;
+            const int c = lane - r * (r + 1) / 2;
+            sum[lane] = sum[lane] + fin[r * 6 + c];
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_line_cut(const KParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_line_cut, dim3(p.B), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace gfpl

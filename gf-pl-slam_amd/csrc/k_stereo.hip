@@ -1,0 +1,618 @@
+// k_stereo.hip — stereo matching of one frame per sequence (gfx950).
+//
+//  k_stereo_points : extractStereoFeatures_ORBSLAM point branch
+//                    (src/stereoFrame.cpp:453-630) + subPixelStereoRefine_ORBSLAM (:340-404)
+//  k_stereo_lines  : extractStereoFeatures_ORBSLAM line branch (src/stereoFrame.cpp:633-767)
+//  k_knn2          : BFMatcher::knnMatch(k=2) NORM_HAMMING / NORM_HAMMING2 (batched)
+//  k_init_points / k_init_lines : extractInitialStereoFeatures (src/stereoFrame.cpp:173-336)
+//  k_line_uncertainty : estimateStereoUncertainty on a frame slot
+//
+// One workgroup owns one sequence's frame: the band search, the (dist,iL) sort,
+// the median gate and the order-preserving compaction are all block-local, so a
+// frame never crosses workgroups and B sequences fill the 256 CUs.
+#include "gfpl_kernels.hpp"
+
+namespace gfpl {
+
+// ---------------------------------------------------------------- helpers
+template <typename K>
+__device__ void bitonic_sort(K* a, int n) {   // n power of two, ascending
+    for (int k = 2; k <= n; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    bool up = ((i & k) == 0);
+                    K x = a[i], y = a[ixj];
+                    if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__device__ __forceinline__ int clamp_level(int o, int n) { return o < 0 ? 0 : (o >= n ? n - 1 : o); }
+
+// subPixelStereoRefine_ORBSLAM (src/stereoFrame.cpp:340-404); ledger Q1: both
+// patches come from the RIGHT pyramid.  SAD of integer-valued pixels is exact,
+// so int accumulation equals cv::norm(NORM_L1).  U8: out-of-image windows reject.
+__device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, const gfpl_keypoint& kpR,
+                         float& disparity, float& bestuR) {
+    disparity = -1;
+    bestuR = kpR.x;
+    const float uR0 = kpR.x;
+    const int o = clamp_level(kpL.octave, p.cam.n_levels);
+    const float sf = p.cam.inv_scale[o];
+    const float scaleduL = roundf(kpL.x * sf);
+    const float scaledvL = roundf(kpL.y * sf);
+    const float scaleduR0 = roundf(uR0 * sf);
+    const int cols = p.cam.lvl_cols[o], rows = p.cam.lvl_rows[o];
+    const float iniu = scaleduR0 + 5 - 5;
+    const float endu = scaleduR0 + 5 + 5 + 1;
+    if (iniu < 0 || endu >= cols) return;
+    const int vL = (int)scaledvL, uL = (int)scaleduL, uR = (int)scaleduR0;
+    if (vL - 5 < 0 || vL + 5 >= rows || uL - 5 < 0 || uL + 5 >= cols || uR - 10 < 0 || uR + 10 >= cols) return;
+    const uint8_t* img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[o];
+    const uint8_t* crow = img + (size_t)vL * cols;
+    const int cL = crow[uL];
+    int cR[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) cR[i] = crow[uR - 5 + i];
+    int acc[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) acc[i] = 0;
+    for (int r = 0; r < 11; ++r) {
+        const uint8_t* rowp = img + (size_t)(vL - 5 + r) * cols;
+        int il[11], ir[21];
+#pragma unroll
+        for (int c = 0; c < 11; ++c) il[c] = (int)rowp[uL - 5 + c] - cL;
+#pragma unroll
+        for (int c = 0; c < 21; ++c) ir[c] = rowp[uR - 10 + c];
+#pragma unroll
+        for (int s = 0; s < 11; ++s)
+#pragma unroll
+            for (int c = 0; c < 11; ++c) acc[s] += abs(il[c] - (ir[c + s] - cR[s]));
+    }
+    int bestDist = 2147483647;
+    int bestinc = 0;
+    float vD[11];
+#pragma unroll
+    for (int s = 0; s < 11; ++s) {
+        float dist = (float)acc[s];
+        if (dist < (float)bestDist) { bestDist = (int)dist; bestinc = s - 5; }
+        vD[s] = dist;
+    }
+    if (bestinc == -5 || bestinc == 5) return;
+    const float dist1 = vD[5 + bestinc - 1];
+    const float dist2 = vD[5 + bestinc];
+    const float dist3 = vD[5 + bestinc + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) return;
+    bestuR = p.cam.scale[o] * ((float)scaleduR0 + (float)bestinc + deltaR);
+    disparity = (kpL.x - bestuR);
+}
+
+// ------------------------------------------------------- stereo points --
+// dynamic LDS: rkey[KP2] u32 | pairs[KP2] u32 | depth[cap] f32 | rmaxr[cap] i32 | misc[64]
+__global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int b = blockIdx.x;
+    const int cap = p.kp_cap;
+    uint32_t* rkey = (uint32_t*)smem;
+    uint32_t* pairs = rkey + KP2;
+    float* depth = (float*)(pairs + KP2);
+    int* rmaxr = (int*)(depth + cap);
+    int* misc = rmaxr + cap;
+    const int tid = threadIdx.x;
+    const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
+    const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
+    const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
+    const uint8_t* DL = p.in.pdesc_l + (size_t)b * cap * 32;
+    const uint8_t* DR = p.in.pdesc_r + (size_t)b * cap * 32;
+    const int nRows = p.cam.height;
+    if (tid == 0) { misc[0] = 0; misc[1] = 0; misc[2] = 0; }
+    __syncthreads();
+    // vRowIndices (src/stereoFrame.cpp:459-485) as (minr, iR) keys sorted by minr
+    for (int iR = tid; iR < KP2; iR += blockDim.x) {
+        if (iR < Nr) {
+            gfpl_keypoint kp = KR[iR];
+            const float r = 2.0f * p.cam.scale[clamp_level(kp.octave, p.cam.n_levels)];
+            const int maxr = (int)ceilf(kp.y + r);
+            const int minr = (int)floorf(kp.y - r);
+            rkey[iR] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)iR;
+            rmaxr[iR] = maxr;
+            atomicMax(&misc[0], maxr - minr);
+        } else {
+            rkey[iR] = 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    bitonic_sort(rkey, KP2);
+    const int D = misc[0];
+    const float minD = 0;
+    const float maxD = (float)p.cam.fx;
+    const float mbf = (float)(p.cam.fx * p.cam.b);
+    // per left keypoint: band search + Hamming + sub-pixel (src/stereoFrame.cpp:502-583)
+    for (int iL = tid; iL < KP2; iL += blockDim.x) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (iL < N) {
+            const gfpl_keypoint kpL = KL[iL];
+            const int levelL = kpL.octave;
+            const float vL = kpL.y, uL = kpL.x;
+            const float minU = uL - maxD, maxU = uL - minD;
+            if (vL >= 0.0f && (unsigned)(int)vL < (unsigned)nRows && !(maxU < 0)) {
+                const int row = (int)vL;
+                uint32_t dl[8];
+                load_desc(DL + (size_t)iL * 32, dl);
+                // lower bound of minr >= row - D
+                const uint32_t lo_key = (uint32_t)(row - D + 32768) << 16;
+                int lo = 0, hi = Nr;
+                while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
+                int bestDist = 100, bestIdxR = 0x7FFFFFFF;
+                for (int j = lo; j < Nr; ++j) {
+                    const uint32_t k = rkey[j];
+                    const int minr = (int)(k >> 16) - 32768;
+                    if (minr > row) break;
+                    const int iR = (int)(k & 0xFFFFu);
+                    if (rmaxr[iR] < row) continue;
+                    const gfpl_keypoint kpR = KR[iR];
+                    if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+                    const float uR = kpR.x;
+                    if (uR >= minU && uR <= maxU) {
+                        uint32_t dr[8];
+                        load_desc(DR + (size_t)iR * 32, dr);
+                        const int dist = hamming8<1>(dl, dr);
+                        // scan order of the reference is ascending iR with strict '<':
+                        // lexicographic (dist, iR) minimum
+                        if (dist < bestDist || (dist == bestDist && iR < bestIdxR)) { bestDist = dist; bestIdxR = iR; }
+                    }
+                }
+                if (bestDist < 80) {
+                    atomicAdd(&misc[2], 1);
+                    float disparity, bestuR;
+                    subpixel(p, b, kpL, KR[bestIdxR], disparity, bestuR);
+                    if (disparity >= minD && disparity < maxD) {
+                        if (disparity <= 0) { disparity = 0.01f; bestuR = (float)((double)uL - 0.01); }
+                        depth[iL] = mbf / disparity;
+                        key = ((uint32_t)bestDist << 16) | (uint32_t)iL;
+                    }
+                }
+            }
+        }
+        pairs[iL] = key;
+    }
+    __syncthreads();
+    // sort(vDistIdx) (src/stereoFrame.cpp:585)
+    bitonic_sort(pairs, KP2);
+    for (int i = tid; i < KP2; i += blockDim.x) {
+        bool v = pairs[i] != 0xFFFFFFFFu;
+        bool vn = (i + 1 < KP2) ? (pairs[i + 1] != 0xFFFFFFFFu) : false;
+        if (v && !vn) misc[1] = i + 1;
+    }
+    __syncthreads();
+    const int nv = misc[1];
+    float thDist = 0.0f;
+    if (nv > 0) {
+        const float median = (float)(pairs[nv / 2] >> 16);
+        thDist = 1.5f * 1.4f * median;
+    }
+    // emission in sorted order while dist < thDist, skipping negative disparities
+    // (src/stereoFrame.cpp:600-626); U5: empty -> no points
+    DevPoints& C = p.curr.pt;
+    const size_t base = (size_t)b * cap;
+    int off = 0;
+    for (int c0 = 0; c0 < KP2; c0 += 512) {
+        const int i = c0 + tid;
+        int flag = 0;
+        float disparity = 0.0f;
+        int iL = 0;
+        if (i < nv) {
+            const uint32_t k = pairs[i];
+            const int dist = (int)(k >> 16);
+            iL = (int)(k & 0xFFFFu);
+            if ((float)dist < thDist) {
+                disparity = mbf / depth[iL];   // Q6: float round trip
+                flag = (disparity < 0) ? 0 : 1;
+            }
+        }
+        int tot;
+        const int pos = off + block_exclusive_scan<512>(flag, misc + 4, &tot);
+        if (flag) {
+            const gfpl_keypoint kp = KL[iL];
+            const size_t q = base + pos;
+            const double plx = kp.x, ply = kp.y, disp = (double)disparity;
+            double P[3];
+            backProjection(p.cam, plx, ply, disp, P);
+            C.pl[2 * q] = plx; C.pl[2 * q + 1] = ply;
+            C.disp[q] = disp;
+            C.P[3 * q] = P[0]; C.P[3 * q + 1] = P[1]; C.P[3 * q + 2] = P[2];
+            const int lv = clamp_level(kp.octave, p.cam.n_levels);
+            C.sigma2[q] = p.cam.sigma2_pt[lv];
+            C.idx[q] = pos;
+            C.level[q] = kp.octave;
+            C.inlier[q] = 1;
+            const uint4* s = reinterpret_cast<const uint4*>(DL + (size_t)iL * 32);
+            uint4* d = reinterpret_cast<uint4*>(C.desc + q * 32);
+            d[0] = s[0]; d[1] = s[1];
+        }
+        off += tot;
+    }
+    if (tid == 0) {
+        C.n[b] = off;
+        p.curr.pose.time_stamp[b] = p.in.time_stamp[b];
+        p.scr.n_subpix[b] = misc[2];
+    }
+}
+
+// ------------------------------------------------------- stereo lines --
+struct LineOut {
+    double spl[2], epl[2], sdisp, edisp, sP[3], eP[3], le[3], angle;
+    int level;
+};
+
+// Line triangulation: initial (src/stereoFrame.cpp:301-330) / per-frame (:684-760)
+__device__ bool triangulate(const KParams& p, const gfpl_keyline& a, const gfpl_keyline& c, bool initial,
+                            LineOut* L) {
+    const DevCam& cam = p.cam;
+    double sp_l[3] = {a.sx, a.sy, 1.0}, ep_l[3] = {a.ex, a.ey, 1.0};
+    double le_l[3] = {sp_l[1] * ep_l[2] - sp_l[2] * ep_l[1], sp_l[2] * ep_l[0] - sp_l[0] * ep_l[2],
+                      sp_l[0] * ep_l[1] - sp_l[1] * ep_l[0]};
+    double nrm = sqrt(le_l[0] * le_l[0] + le_l[1] * le_l[1]);
+    le_l[0] = le_l[0] / nrm; le_l[1] = le_l[1] / nrm; le_l[2] = le_l[2] / nrm;
+    double sp_r[3] = {c.sx, c.sy, 1.0}, ep_r[3] = {c.ex, c.ey, 1.0};
+    double le_r[3] = {sp_r[1] * ep_r[2] - sp_r[2] * ep_r[1], sp_r[2] * ep_r[0] - sp_r[0] * ep_r[2],
+                      sp_r[0] * ep_r[1] - sp_r[1] * ep_r[0]};
+    double overlap = overlapStereo(sp_l[1], ep_l[1], sp_r[1], ep_r[1]);
+    double spx = (-(le_r[2] + le_r[1] * (double)a.sy)) / le_r[0];
+    double epx = (-(le_r[2] + le_r[1] * (double)a.ey)) / le_r[0];
+    double disp_s = (double)a.sx - spx;
+    double disp_e = (double)a.ex - epx;
+    double horiz = initial ? (double)fabsf((float)le_r[0]) : (double)fabsf((float)le_l[0]);
+    if (!(disp_s >= p.cfg.min_disp && disp_e >= p.cfg.min_disp && horiz > p.cfg.line_horiz_th &&
+          overlap > p.cfg.stereo_overlap_th))
+        return false;
+    if (!initial) {
+        double cS[9], cE[9], wS[3], wE[3];
+        endpointCov(cam, sp_l[0], sp_l[1], disp_s, cS);
+        endpointCov(cam, ep_l[0], ep_l[1], disp_e, cE);
+        eig_sym<3>(cS, wS);
+        eig_sym<3>(cE, wE);
+        double max_eig = std_max(wS[2], wE[2]);
+        if (!(max_eig < p.cfg.line_cov_th)) return false;
+    }
+    L->spl[0] = sp_l[0]; L->spl[1] = sp_l[1];
+    L->epl[0] = ep_l[0]; L->epl[1] = ep_l[1];
+    L->sdisp = disp_s; L->edisp = disp_e;
+    backProjection(cam, sp_l[0], sp_l[1], disp_s, L->sP);
+    backProjection(cam, ep_l[0], ep_l[1], disp_e, L->eP);
+    L->le[0] = le_l[0]; L->le[1] = le_l[1]; L->le[2] = le_l[2];
+    L->angle = (double)a.angle;
+    L->level = a.octave;
+    return true;
+}
+
+// estimateStereoUncertainty for one line (src/stereoFrame.cpp:1453-1483)
+__device__ void line_uncertainty(const KParams& p, const double* spl, const double* epl, double sdisp,
+                                 double edisp, const double* le, double* covS, double* covE) {
+    double sdisp_std, edisp_std;
+    if (fabs(le[0]) > 0.15) {
+        sdisp_std = p.cfg.ratio_disp_std * sdisp;
+        edisp_std = p.cfg.ratio_disp_std * edisp;
+    } else {
+        sdisp_std = p.cfg.ratio_disp_std_hor * sdisp;
+        edisp_std = p.cfg.ratio_disp_std_hor * edisp;
+    }
+    covMat2D_3D(p.cam, spl[0], spl[1], 1.0, sdisp, sdisp_std, covS);
+    covMat2D_3D(p.cam, epl[0], epl[1], 1.0, edisp, edisp_std, covE);
+}
+
+__device__ void write_line(const KParams& p, DevLines& C, size_t q, const LineOut& L, int idx, const uint8_t* desc) {
+    C.spl[2 * q] = L.spl[0]; C.spl[2 * q + 1] = L.spl[1];
+    C.epl[2 * q] = L.epl[0]; C.epl[2 * q + 1] = L.epl[1];
+    C.sdisp[q] = L.sdisp; C.edisp[q] = L.edisp;
+    for (int k = 0; k < 3; ++k) { C.sP[3 * q + k] = L.sP[k]; C.eP[3 * q + k] = L.eP[k]; C.le[3 * q + k] = L.le[k]; }
+    C.angle[q] = L.angle;
+    C.level[q] = L.level;
+    C.sigma2[q] = p.cam.sigma2_ln[clamp_level(L.level, GFPL_MAX_LEVELS)];
+    C.idx[q] = idx;
+    C.inlier[q] = 1;
+    C.cut[2 * q] = 0.0; C.cut[2 * q + 1] = 0.0;
+    const uint4* s = reinterpret_cast<const uint4*>(desc);
+    uint4* d = reinterpret_cast<uint4*>(C.desc + q * 32);
+    d[0] = s[0]; d[1] = s[1];
+}
+
+// knn-2 of row i of Q against T (both in LDS or global), insertion rule of
+// cv::batchDistance (ledger T1): ties keep the lower train index.
+template <int CELL>
+__device__ __forceinline__ void knn2_row(const uint32_t* q, const uint32_t* T, int nt, int& i0, int& d0, int& d1) {
+    int dist0 = 2147483647, dist1 = 2147483647, idx0 = -1;
+    for (int j = 0; j < nt; ++j) {
+        const int d = hamming8<CELL>(q, T + 8 * j);
+        if (d < dist1) {
+            if (dist0 > d) { dist1 = dist0; dist0 = d; idx0 = j; }
+            else { dist1 = d; }
+        }
+    }
+    i0 = idx0; d0 = dist0; d1 = dist1;
+}
+
+// histogram median helper: value at rank r (0-based) of a histogram h[0..256]
+__device__ int hist_rank(const int* h, int r) {
+    int c = 0;
+    for (int v = 0; v <= 256; ++v) { c += h[v]; if (c > r) return v; }
+    return 256;
+}
+
+// dynamic LDS: dl[cap*8] | dr[cap*8] u32 | lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
+template <int CELL, bool INITIAL>
+__global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int b = blockIdx.x;
+    const int cap = p.kl_cap;
+    uint32_t* dl = (uint32_t*)smem;
+    uint32_t* dr = dl + cap * 8;
+    int* lr_i = (int*)(dr + cap * 8);
+    int* lr_d0 = lr_i + cap;
+    int* lr_d1 = lr_d0 + cap;
+    int* rl_i = lr_d1 + cap;
+    int* hist = rl_i + cap;
+    int* misc = hist + 260;
+    const int tid = threadIdx.x;
+    const int NL = min(p.in.n_kl_l[b], cap), NR = min(p.in.n_kl_r[b], cap);
+    DevLines& C = p.curr.ls;   // INITIAL writes the slot passed as curr
+    if (NL < 2 || NR < 2) {    // empty -> skipped by the reference; 1 row -> U4 guard
+        if (tid == 0) C.n[b] = 0;
+        return;
+    }
+    const uint8_t* DLg = p.in.ldesc_l + (size_t)b * cap * 32;
+    const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
+    for (int i = tid; i < NL * 2; i += blockDim.x) reinterpret_cast<uint4*>(dl)[i] = reinterpret_cast<const uint4*>(DLg)[i];
+    for (int i = tid; i < NR * 2; i += blockDim.x) reinterpret_cast<uint4*>(dr)[i] = reinterpret_cast<const uint4*>(DRg)[i];
+    for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < NL; i += blockDim.x) {
+        int i0, d0, d1;
+        knn2_row<CELL>(dl + 8 * i, dr, NR, i0, d0, d1);
+        lr_i[i] = i0; lr_d0[i] = d0; lr_d1[i] = d1;
+        atomicAdd(&hist[d1 - d0], 1);   // lineDescriptorMAD deviations |d1-d0| (U1 pin)
+    }
+    for (int j = tid; j < NR; j += blockDim.x) {
+        int i0, d0, d1;
+        knn2_row<CELL>(dr + 8 * j, dl, NL, i0, d0, d1);
+        rl_i[j] = i0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int v = hist_rank(hist, NL / 2);
+        double th = (1.4826 * (double)(float)v) * p.cfg.desc_th_l;
+        reinterpret_cast<double*>(misc + 8)[0] = th;
+    }
+    __syncthreads();
+    const double nn12_dist_th = reinterpret_cast<double*>(misc + 8)[0];
+    const int n_matches = min(NL, NR);   // Q5
+    const gfpl_keyline* KL = p.in.kl_l + (size_t)b * cap;
+    const gfpl_keyline* KR = p.in.kl_r + (size_t)b * cap;
+    const size_t base = (size_t)b * cap;
+    int off = 0;
+    for (int c0 = 0; c0 < n_matches; c0 += 512) {
+        const int i = c0 + tid;
+        int flag = 0;
+        LineOut L;
+        if (i < n_matches) {
+            const int lr_tdx = lr_i[i];
+            const int rl_tdx = rl_i[lr_tdx];
+            const double dist_12 = (double)((float)lr_d1[i] - (float)lr_d0[i]);
+            if (i == rl_tdx && dist_12 > nn12_dist_th)
+                flag = triangulate(p, KL[i], KR[lr_tdx], INITIAL, &L) ? 1 : 0;
+        }
+        int tot;
+        const int pos = off + block_exclusive_scan<512>(flag, misc + 16, &tot);
+        if (flag) write_line(p, C, base + pos, L, INITIAL ? pos : -1, DLg + (size_t)i * 32);
+        off += tot;
+    }
+    if (tid == 0) C.n[b] = off;
+}
+
+// ------------------------------------------------------- knn2 (global) --
+// rows of q / t of sequence b at q + b*qstride*32 (counts nq[b], nt[b] or fixed)
+template <int CELL>
+__global__ void __launch_bounds__(256) k_knn2(const uint8_t* q, const int* nq_arr, int nq_fixed, size_t q_stride,
+                                             const uint8_t* t, const int* nt_arr, int nt_fixed, size_t t_stride,
+                                             int cap_clamp, int32_t* out_idx, float* out_dist, int32_t* packed,
+                                             size_t out_stride) {
+    const int b = blockIdx.y;
+    const int nq = nq_arr ? min(nq_arr[b], cap_clamp) : nq_fixed;
+    const int nt = nt_arr ? min(nt_arr[b], cap_clamp) : nt_fixed;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const uint8_t* Q = q + (size_t)b * q_stride * 32;
+    const uint8_t* T = t + (size_t)b * t_stride * 32;
+    uint32_t qd[8];
+    load_desc(Q + (size_t)i * 32, qd);
+    int dist0 = 2147483647, dist1 = 2147483647, idx0 = -1, idx1 = -1;
+    for (int j = 0; j < nt; ++j) {
+        uint32_t td[8];
+        load_desc(T + (size_t)j * 32, td);
+        const int d = hamming8<CELL>(qd, td);
+        if (d < dist1) {
+            if (dist0 > d) { dist1 = dist0; idx1 = idx0; dist0 = d; idx0 = j; }
+            else { dist1 = d; idx1 = j; }
+        }
+    }
+    if (out_idx) {
+        out_idx[2 * i] = idx0; out_idx[2 * i + 1] = idx1;
+        out_dist[2 * i] = (float)dist0; out_dist[2 * i + 1] = (float)dist1;
+    }
+    if (packed) {
+        int32_t* o = packed + (size_t)b * out_stride * 3;
+        o[3 * i] = idx0; o[3 * i + 1] = dist0; o[3 * i + 2] = dist1;
+    }
+}
+
+// -------------------------------------------------- initial-frame points --
+// src/stereoFrame.cpp:206-245 on knn results in scratch:
+//   knn[b][0][i] = (idx0,d0,d1) of L->R, knn[b][1][j] of R->L
+__global__ void __launch_bounds__(512) k_init_points(KParams p) {
+    __shared__ int misc[32];
+    const int b = blockIdx.x;
+    const int cap = p.kp_cap;
+    const int tid = threadIdx.x;
+    DevPoints& C = p.curr.pt;
+    const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
+    if (N < 2 || Nr < 2) {   // U4 guard
+        if (tid == 0) { C.n[b] = 0; p.curr.pose.time_stamp[b] = p.in.time_stamp[b]; }
+        return;
+    }
+    const int32_t* lr = p.scr.knn + (size_t)b * 2 * cap * 3;
+    const int32_t* rl = lr + (size_t)cap * 3;
+    const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
+    const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
+    const uint8_t* DL = p.in.pdesc_l + (size_t)b * cap * 32;
+    const size_t base = (size_t)b * cap;
+    int off = 0;
+    for (int c0 = 0; c0 < N; c0 += 512) {
+        const int i = c0 + tid;
+        int flag = 0;
+        double disp_ = 0.0;
+        if (i < N) {
+            const int t = lr[3 * i];
+            const int rl_tdx = rl[3 * t];
+            const double dist_12 = (double)((float)lr[3 * i + 1] / (float)lr[3 * i + 2]);
+            if (i == rl_tdx && dist_12 <= p.cfg.max_ratio_12_p) {
+                const gfpl_keypoint kl = KL[i], kr = KR[t];
+                if ((double)fabsf(kl.y - kr.y) <= p.cfg.max_dist_epip) {
+                    disp_ = (double)(kl.x - kr.x);
+                    if (disp_ >= p.cfg.min_disp) flag = 1;
+                }
+            }
+        }
+        int tot;
+        const int pos = off + block_exclusive_scan<512>(flag, misc, &tot);
+        if (flag) {
+            const gfpl_keypoint kl = KL[i];
+            const size_t q = base + pos;
+            double P[3];
+            const double plx = kl.x, ply = kl.y;
+            backProjection(p.cam, plx, ply, disp_, P);
+            C.pl[2 * q] = plx; C.pl[2 * q + 1] = ply;
+            C.disp[q] = disp_;
+            C.P[3 * q] = P[0]; C.P[3 * q + 1] = P[1]; C.P[3 * q + 2] = P[2];
+            C.sigma2[q] = p.cam.sigma2_pt[clamp_level(kl.octave, p.cam.n_levels)];
+            C.idx[q] = pos;
+            C.level[q] = kl.octave;
+            C.inlier[q] = 1;
+            const uint4* s = reinterpret_cast<const uint4*>(DL + (size_t)i * 32);
+            uint4* d = reinterpret_cast<uint4*>(C.desc + q * 32);
+            d[0] = s[0]; d[1] = s[1];
+        }
+        off += tot;
+    }
+    if (tid == 0) {
+        C.n[b] = off;
+        p.curr.pose.time_stamp[b] = p.in.time_stamp[b];
+    }
+}
+
+// initial pose: Tfw = Tfw_cov = DT = I, DT_cov = 0 (src/stereoFrameHandler.cpp:50-52)
+__global__ void k_init_pose(KParams p) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    DevPose& P = p.curr.pose;
+    for (int i = 0; i < 16; ++i) { P.Tfw[16 * b + i] = (i % 5 == 0) ? 1.0 : 0.0; P.DT[16 * b + i] = (i % 5 == 0) ? 1.0 : 0.0; }
+    for (int i = 0; i < 36; ++i) { P.Tfw_cov[36 * b + i] = (i % 7 == 0) ? 1.0 : 0.0; P.DT_cov[36 * b + i] = 0.0; }
+    for (int i = 0; i < 6; ++i) P.DT_cov_eig[6 * b + i] = 0.0;
+    P.err_norm[b] = 0.0;
+    p.tr.num_frame_loss[b] = 0;
+    p.tr.n_matched_pt[b] = 0;
+    p.tr.n_matched_ls[b] = 0;
+    p.tr.n_inliers[b] = 0; p.tr.n_inliers_pt[b] = 0; p.tr.n_inliers_ls[b] = 0;
+}
+
+// estimateStereoUncertainty on the slot passed as `prev`
+__global__ void k_line_uncertainty(KParams p) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    DevLines& L = p.prev.ls;
+    if (i >= L.n[b]) return;
+    const size_t q = (size_t)b * p.kl_cap + i;
+    double spl[2] = {L.spl[2 * q], L.spl[2 * q + 1]}, epl[2] = {L.epl[2 * q], L.epl[2 * q + 1]};
+    double le[3] = {L.le[3 * q], L.le[3 * q + 1], L.le[3 * q + 2]};
+    double cS[9], cE[9];
+    line_uncertainty(p, spl, epl, L.sdisp[q], L.edisp[q], le, cS, cE);
+    for (int k = 0; k < 9; ++k) { L.covS[9 * q + k] = cS[k]; L.covE[9 * q + k] = cE[k]; }
+}
+
+// algorithmic HBM bytes of one step of one sequence:
+// inputs (descriptors, keypoints, keylines, 11x11 + 11x21 SAD windows per
+// sub-pixel candidate), prev state read, curr state written, match lists, pose.
+__global__ void k_step_bytes(KParams p) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    const int64_t No = (int64_t)p.in.n_kp_l[b] + p.in.n_kp_r[b];
+    const int64_t Nk = (int64_t)p.in.n_kl_l[b] + p.in.n_kl_r[b];
+    const int64_t Mo = p.scr.n_subpix[b];
+    const int64_t Sp = p.prev.pt.n[b], Sl = p.prev.ls.n[b];
+    const int64_t Sp2 = p.curr.pt.n[b], Sl2 = p.curr.ls.n[b];
+    const int64_t Mp = p.tr.n_matched_pt[b], Ml = p.tr.n_matched_ls[b];
+    p.scr.bytes[b] = 32 * (No + Nk) + 12 * No + 24 * Nk + (121 + 231) * Mo + 80 * (Sp + Sp2) + 248 * (Sl + Sl2) +
+                     4 * (Mp + Ml) + 16 * Ml + 416;
+}
+
+// ------------------------------------------------------------ launchers --
+static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p; }
+
+hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
+    const int KP2 = next_pow2(p.kp_cap);
+    const size_t lds = (size_t)KP2 * 8 + (size_t)p.kp_cap * 8 + 64 * 4;
+    hipLaunchKernelGGL(k_stereo_points, dim3(p.B), dim3(512), lds, s, p, KP2);
+    return hipGetLastError();
+}
+
+size_t stereo_lines_lds(int cap) { return (size_t)cap * 64 + (size_t)cap * 16 + 260 * 4 + 64 * 4; }
+
+hipError_t launch_stereo_lines(const KParams& p, hipStream_t s) {
+    hipLaunchKernelGGL((k_stereo_lines<2, false>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_line_uncertainty(const KParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_line_uncertainty, dim3((p.kl_cap + 255) / 256, p.B), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_init(const KParams& p, hipStream_t s) {
+    // points: knn-2 NORM_HAMMING L->R and R->L into scratch, then gates
+    const int cap = p.kp_cap;
+    int32_t* lr = p.scr.knn;
+    dim3 g((cap + 255) / 256, p.B);
+    hipLaunchKernelGGL((k_knn2<1>), g, dim3(256), 0, s, p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap,
+                       p.in.pdesc_r, p.in.n_kp_r, 0, (size_t)cap, cap, (int32_t*)nullptr, (float*)nullptr,
+                       lr, (size_t)cap * 2);
+    hipLaunchKernelGGL((k_knn2<1>), g, dim3(256), 0, s, p.in.pdesc_r, p.in.n_kp_r, 0, (size_t)cap,
+                       p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap, cap, (int32_t*)nullptr, (float*)nullptr,
+                       lr + (size_t)cap * 3, (size_t)cap * 2);
+    hipLaunchKernelGGL(k_init_points, dim3(p.B), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_stereo_lines<1, true>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
+    hipLaunchKernelGGL(k_init_pose, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_bytes(const KParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_step_bytes, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* idx, float* dist,
+                       hipStream_t s) {
+    dim3 g((nq + 255) / 256, 1);
+    if (cell == 2)
+        hipLaunchKernelGGL((k_knn2<2>), g, dim3(256), 0, s, q, (const int*)nullptr, nq, (size_t)0, t,
+                           (const int*)nullptr, nt, (size_t)0, 0, idx, dist, (int32_t*)nullptr, (size_t)0);
+    else
+        hipLaunchKernelGGL((k_knn2<1>), g, dim3(256), 0, s, q, (const int*)nullptr, nq, (size_t)0, t,
+                           (const int*)nullptr, nt, (size_t)0, 0, idx, dist, (int32_t*)nullptr, (size_t)0);
+    return hipGetLastError();
+}
+
+}  // namespace gfpl

@@ -1,0 +1,516 @@
+"""gfpl — Python host side of the MI355X-native GF-PL-SLAM tracking path.
+
+Thin ctypes mirror of ``include/gfpl.h``.  The compute path is the HIP library
+``gf-pl-slam_amd/lib/libgfpl_hip.so`` (hand-written gfx950 kernels); this module
+only marshals structs and (optionally) torch device buffers.  There is no CPU
+fallback: the product classes raise if the HIP library is missing.
+
+The class names mirror the reference's operator interface
+(``StVO::StereoFrameHandler`` — include/stereoFrameHandler.h:38-174) so the parity
+tests read like the reference's own call sequence (app/plslam_mod.cpp:375-477):
+``initialize`` -> ``insertStereoPair`` -> ``optimizePose`` -> ``updateFrame``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+REPO_DIR = os.path.dirname(PKG_DIR)
+
+DESC = 32
+MAX_LEVELS = 8
+MAX_MATCHED_PT = 2048
+MAX_MATCHED_LS = 1024
+PREV, CURR = 0, 1
+HAMMING, HAMMING2 = 1, 2
+
+ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "no HIP device",
+          -4: "knn-2 needs at least 2 train descriptors", -5: "capacity exceeded",
+          -6: "call order violated", -7: "unsupported config"}
+
+
+class GfplError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        super().__init__(f"{what}: gfpl error {code} ({ERRORS.get(code, '?')})")
+        self.code = code
+
+
+# --------------------------------------------------------------- structs --
+class Camera(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int),
+                ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("b", C.c_double), ("n_levels", C.c_int),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("lvl_cols", C.c_int * MAX_LEVELS), ("lvl_rows", C.c_int * MAX_LEVELS),
+                ("lvl_offset", C.c_int64 * MAX_LEVELS), ("pyr_bytes", C.c_int64),
+                ("sigma2_pt", C.c_double * MAX_LEVELS), ("sigma2_ln", C.c_double * MAX_LEVELS)]
+
+
+class Config(C.Structure):
+    _fields_ = [("best_lr_matches", C.c_int), ("lr_in_parallel", C.c_int),
+                ("use_line_conf_cut", C.c_int), ("cut_with_max_vol", C.c_int),
+                ("ratio_disp_std", C.c_double), ("ratio_disp_std_hor", C.c_double),
+                ("max_line_match_num", C.c_int), ("max_point_match_num", C.c_int),
+                ("max_dist_epip", C.c_double), ("min_disp", C.c_double),
+                ("max_ratio_12_p", C.c_double), ("point_match_radius", C.c_double),
+                ("stereo_overlap_th", C.c_double), ("line_horiz_th", C.c_double),
+                ("desc_th_l", C.c_double), ("line_cov_th", C.c_double),
+                ("homog_th", C.c_double), ("min_features", C.c_int),
+                ("max_iters", C.c_int), ("max_iters_ref", C.c_int),
+                ("min_error", C.c_double), ("min_error_change", C.c_double),
+                ("inlier_k", C.c_double), ("motion_step_th", C.c_double),
+                ("orb_scale_factor", C.c_double), ("orb_n_levels", C.c_int),
+                ("lsd_scale", C.c_double), ("cut_step", C.c_double),
+                ("cut_rng", C.c_double * 2), ("proj_gate_px", C.c_double)]
+
+
+KEYPOINT_DT = np.dtype([("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
+KEYLINE_DT = np.dtype([("sx", "<f4"), ("sy", "<f4"), ("ex", "<f4"), ("ey", "<f4"),
+                       ("angle", "<f4"), ("octave", "<i4")])
+
+_vp = C.c_void_p
+
+
+class Frames(C.Structure):
+    _fields_ = [("batch", C.c_int), ("kp_cap", C.c_int), ("kl_cap", C.c_int),
+                ("n_kp_l", _vp), ("n_kp_r", _vp), ("kp_l", _vp), ("kp_r", _vp),
+                ("pdesc_l", _vp), ("pdesc_r", _vp),
+                ("n_kl_l", _vp), ("n_kl_r", _vp), ("kl_l", _vp), ("kl_r", _vp),
+                ("ldesc_l", _vp), ("ldesc_r", _vp), ("pyr_r", _vp), ("time_stamp", _vp)]
+
+
+# (name, dtype, per-feature shape) of gfpl_frame_host arrays, in struct order
+PT_FIELDS = [("pt_pl", np.float64, (2,)), ("pt_pl_obs", np.float64, (2,)),
+             ("pt_disp", np.float64, ()), ("pt_P", np.float64, (3,)),
+             ("pt_sigma2", np.float64, ()), ("pt_idx", np.int32, ()),
+             ("pt_level", np.int32, ()), ("pt_inlier", np.uint8, ()),
+             ("pdesc", np.uint8, (DESC,))]
+LS_FIELDS = [("ls_spl", np.float64, (2,)), ("ls_epl", np.float64, (2,)),
+             ("ls_spl_obs", np.float64, (2,)), ("ls_epl_obs", np.float64, (2,)),
+             ("ls_sdisp", np.float64, ()), ("ls_edisp", np.float64, ()),
+             ("ls_sdisp_obs", np.float64, ()), ("ls_edisp_obs", np.float64, ()),
+             ("ls_angle", np.float64, ()), ("ls_sigma2", np.float64, ()),
+             ("ls_sP", np.float64, (3,)), ("ls_eP", np.float64, (3,)),
+             ("ls_le", np.float64, (3,)), ("ls_le_obs", np.float64, (3,)),
+             ("ls_covS", np.float64, (9,)), ("ls_covE", np.float64, (9,)),
+             ("ls_cut", np.float64, (2,)), ("ls_invcov", np.float64, (36,)),
+             ("ls_idx", np.int32, ()), ("ls_level", np.int32, ()),
+             ("ls_inlier", np.uint8, ()), ("ldesc", np.uint8, (DESC,))]
+POSE_FIELDS = [("Tfw", 16), ("DT", 16), ("DT_cov", 36), ("Tfw_cov", 36), ("DT_cov_eig", 6)]
+
+
+class FrameHostStruct(C.Structure):
+    _fields_ = ([("n_pt", C.c_int), ("n_ls", C.c_int)]
+                + [(n, _vp) for n, _, _ in PT_FIELDS]
+                + [(n, _vp) for n, _, _ in LS_FIELDS]
+                + [(n, C.c_double * k) for n, k in POSE_FIELDS]
+                + [("err_norm", C.c_double), ("time_stamp", C.c_double)])
+
+
+class TrackHost(C.Structure):
+    _fields_ = [("n_matched_pt", C.c_int), ("n_matched_ls", C.c_int),
+                ("matched_pt", C.c_int32 * MAX_MATCHED_PT),
+                ("matched_ls", C.c_int32 * MAX_MATCHED_LS),
+                ("n_inliers", C.c_int), ("n_inliers_pt", C.c_int), ("n_inliers_ls", C.c_int),
+                ("num_frame_loss", C.c_int)]
+
+    def as_dict(self) -> dict:
+        return {"matched_pt": np.array(self.matched_pt[: self.n_matched_pt], dtype=np.int32),
+                "matched_ls": np.array(self.matched_ls[: self.n_matched_ls], dtype=np.int32),
+                "n_inliers": self.n_inliers, "n_inliers_pt": self.n_inliers_pt,
+                "n_inliers_ls": self.n_inliers_ls, "num_frame_loss": self.num_frame_loss}
+
+
+class SynthParams(C.Structure):
+    _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
+                ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
+                ("yaw_rate", C.c_double), ("z_min", C.c_double), ("z_max", C.c_double),
+                ("px_noise", C.c_double), ("distractor_frac", C.c_double),
+                ("margin", C.c_int), ("seed", C.c_uint64),
+                ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp)]
+
+
+# ------------------------------------------------------------- libraries --
+_LIBS: dict = {}
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(LIB_DIR, name)
+
+
+def _load(name: str) -> C.CDLL:
+    if name not in _LIBS:
+        p = lib_path(name)
+        if not os.path.exists(p):
+            raise GfplError(-3, f"{p} is not built (run __graft_entry__.build())")
+        _LIBS[name] = C.CDLL(p)
+    return _LIBS[name]
+
+
+def hiplib() -> C.CDLL:
+    """The product library (HIP kernels + C ABI).  Raises if not built."""
+    L = _load("libgfpl_hip.so")
+    if not getattr(L, "_gfpl_typed", False):
+        P = C.c_void_p
+        sigs = {
+            "gfpl_abi_version": ([], C.c_int),
+            "gfpl_config_default": ([P], C.c_int),
+            "gfpl_camera_init": ([P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                  C.c_double, C.c_double, P], C.c_int),
+            "gfpl_create": ([C.c_int, P, C.POINTER(P)], C.c_int),
+            "gfpl_destroy": ([P], C.c_int),
+            "gfpl_set_camera": ([P, P], C.c_int),
+            "gfpl_set_config": ([P, P], C.c_int),
+            "gfpl_get_camera": ([P, P], C.c_int),
+            "gfpl_get_config": ([P, P], C.c_int),
+            "gfpl_synchronize": ([P], C.c_int),
+            "gfpl_seqbatch_create": ([P, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_seqbatch_destroy": ([P], C.c_int),
+            "gfpl_seqbatch_bytes": ([P], C.c_int64),
+            "gfpl_initialize": ([P, P], C.c_int),
+            "gfpl_insert_stereo_pair": ([P, P], C.c_int),
+            "gfpl_optimize_pose": ([P], C.c_int),
+            "gfpl_update_frame": ([P], C.c_int),
+            "gfpl_frame_step": ([P, P], C.c_int),
+            "gfpl_stereo_points": ([P, P], C.c_int),
+            "gfpl_stereo_lines": ([P, P], C.c_int),
+            "gfpl_line_uncertainty": ([P], C.c_int),
+            "gfpl_cross_points": ([P], C.c_int),
+            "gfpl_cross_lines": ([P], C.c_int),
+            "gfpl_line_cut": ([P], C.c_int),
+            "gfpl_knn2_hamming": ([P, P, C.c_int, P, C.c_int, C.c_int, P, P], C.c_int),
+            "gfpl_read_frame": ([P, C.c_int, C.c_int, P], C.c_int),
+            "gfpl_write_frame": ([P, C.c_int, C.c_int, P], C.c_int),
+            "gfpl_read_track": ([P, C.c_int, P], C.c_int),
+            "gfpl_write_track": ([P, C.c_int, P], C.c_int),
+            "gfpl_set_timing": ([P, C.c_int], C.c_int),
+            "gfpl_get_stage_times": ([P, P], C.c_int),
+            "gfpl_last_step_bytes": ([P, P], C.c_int),
+            "gfpl_strerror": ([C.c_int], C.c_char_p),
+        }
+        for n, (a, r) in sigs.items():
+            try:
+                f = getattr(L, n)
+            except AttributeError:   # partial builds: the missing entry point fails when called
+                continue
+            f.argtypes = a
+            f.restype = r
+        L._gfpl_typed = True
+    return L
+
+
+def synthlib() -> C.CDLL:
+    L = _load("libgfpl_synth.so")
+    if not getattr(L, "_gfpl_typed", False):
+        P = C.c_void_p
+        L.gfpl_synth_default.argtypes = [P]
+        L.gfpl_synth_default.restype = None
+        L.gfpl_synth_batch.argtypes = ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+                                       + [P] * 14 + [C.c_int])
+        L.gfpl_synth_batch.restype = C.c_int
+        L._gfpl_typed = True
+    return L
+
+
+def check(code: int, what: str = "") -> None:
+    if code != 0:
+        raise GfplError(code, what)
+
+
+# ------------------------------------------------------------ parameters --
+def default_config(**over) -> Config:
+    cfg = Config()
+    check(hiplib().gfpl_config_default(C.byref(cfg)), "config_default")
+    for k, v in over.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+# Cameras of the BASELINE configs (intrinsics from the reference's YAMLs).
+CAMERAS = {
+    # config/gazebo_params.yaml:2,8-11 — the reference's synthetic VGA rig (cfg 2)
+    "vga": dict(width=640, height=480, fx=554.25626, fy=554.25626, cx=320.0, cy=240.0, b=0.1),
+    # config/euroc_params.yaml:2,8-11 (raw left K; cfg 1 and 4)
+    "euroc": dict(width=752, height=480, fx=458.654, fy=457.296, cx=367.215, cy=248.375, b=0.110077842),
+    # config/kitti/kitti00-02.yaml:2-13 (cfg 3)
+    "kitti": dict(width=1241, height=376, fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, b=0.537165719),
+    # gazebo x3 (cfg 5 stress)
+    "stress": dict(width=1920, height=1080, fx=1662.76878, fy=1662.76878, cx=960.0, cy=540.0, b=0.1),
+}
+
+
+def make_camera(name: str = "vga", cfg: Optional[Config] = None, **over) -> Camera:
+    p = dict(CAMERAS[name])
+    p.update(over)
+    cfg = cfg or default_config()
+    cam = Camera()
+    check(hiplib().gfpl_camera_init(C.byref(cam), p["width"], p["height"], p["fx"], p["fy"],
+                                    p["cx"], p["cy"], p["b"], C.byref(cfg)), "camera_init")
+    return cam
+
+
+def synth_params(**over) -> SynthParams:
+    sp = SynthParams()
+    synthlib().gfpl_synth_default(C.byref(sp))
+    for k, v in over.items():
+        setattr(sp, k, v)
+    return sp
+
+
+def _ptr(a) -> int:
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())   # torch tensor
+
+
+# ----------------------------------------------------- synthetic batches --
+class HostFrames:
+    """Synthetic input frames on the host: arrays [F][B][cap] (numpy)."""
+
+    def __init__(self, cam: Camera, sp: SynthParams, n_seq: int, n_frames: int,
+                 kp_cap: int, kl_cap: int, seq0: int = 0, frame0: int = 0, threads: int = 0):
+        self.cam, self.sp = cam, sp
+        self.B, self.F, self.kp_cap, self.kl_cap = n_seq, n_frames, kp_cap, kl_cap
+        F, B = n_frames, n_seq
+        self.n_kp_l = np.zeros((F, B), np.int32)
+        self.n_kp_r = np.zeros((F, B), np.int32)
+        self.kp_l = np.zeros((F, B, kp_cap), KEYPOINT_DT)
+        self.kp_r = np.zeros((F, B, kp_cap), KEYPOINT_DT)
+        self.pdesc_l = np.zeros((F, B, kp_cap, DESC), np.uint8)
+        self.pdesc_r = np.zeros((F, B, kp_cap, DESC), np.uint8)
+        self.n_kl_l = np.zeros((F, B), np.int32)
+        self.n_kl_r = np.zeros((F, B), np.int32)
+        self.kl_l = np.zeros((F, B, kl_cap), KEYLINE_DT)
+        self.kl_r = np.zeros((F, B, kl_cap), KEYLINE_DT)
+        self.ldesc_l = np.zeros((F, B, kl_cap, DESC), np.uint8)
+        self.ldesc_r = np.zeros((F, B, kl_cap, DESC), np.uint8)
+        self.pyr_r = np.zeros((F, B, cam.pyr_bytes), np.uint8)
+        self.time_stamp = np.zeros((F, B), np.float64)
+        threads = threads or min(16, os.cpu_count() or 1)
+        check(synthlib().gfpl_synth_batch(
+            C.byref(sp), C.byref(cam), seq0, B, frame0, F, kp_cap, kl_cap,
+            *[_ptr(a) for a in self.arrays()], threads), "synth_batch")
+
+    def arrays(self):
+        return [self.n_kp_l, self.n_kp_r, self.kp_l, self.kp_r, self.pdesc_l, self.pdesc_r,
+                self.n_kl_l, self.n_kl_r, self.kl_l, self.kl_r, self.ldesc_l, self.ldesc_r,
+                self.pyr_r, self.time_stamp]
+
+    def frames(self, f: int) -> Frames:
+        """gfpl_frames with HOST pointers for frame f (what the oracle reads)."""
+        a = [x[f] for x in self.arrays()]
+        return make_frames(self.B, self.kp_cap, self.kl_cap, a)
+
+
+def make_frames(B: int, kp_cap: int, kl_cap: int, arrs) -> Frames:
+    fr = Frames()
+    fr.batch, fr.kp_cap, fr.kl_cap = B, kp_cap, kl_cap
+    names = ["n_kp_l", "n_kp_r", "kp_l", "kp_r", "pdesc_l", "pdesc_r", "n_kl_l", "n_kl_r",
+             "kl_l", "kl_r", "ldesc_l", "ldesc_r", "pyr_r", "time_stamp"]
+    for n, a in zip(names, arrs):
+        setattr(fr, n, _ptr(a))
+    fr._keep = list(arrs)   # keep buffers alive
+    return fr
+
+
+class DeviceFrames:
+    """Input frames resident in HBM (torch uint8 buffers), one gfpl_frames per frame."""
+
+    def __init__(self, host: HostFrames, device: str = "cuda"):
+        import torch
+        self.host = host
+        self.bufs = []
+        for a in host.arrays():
+            t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(a.shape[0], -1))
+            self.bufs.append(t.to(device))
+        self.sizes = [a[0].nbytes for a in host.arrays()]
+
+    def frames(self, f: int) -> Frames:
+        arrs = [b[f] for b in self.bufs]
+        return make_frames(self.host.B, self.host.kp_cap, self.host.kl_cap, arrs)
+
+    def nbytes(self) -> int:
+        return sum(b.numel() for b in self.bufs)
+
+
+# ----------------------------------------------------------- frame state --
+class FrameHost:
+    """numpy-backed gfpl_frame_host (one sequence's frame state)."""
+
+    def __init__(self, kp_cap: int, kl_cap: int):
+        self.kp_cap, self.kl_cap = kp_cap, kl_cap
+        self.s = FrameHostStruct()
+        self.arr = {}
+        for n, dt, sh in PT_FIELDS:
+            self.arr[n] = np.zeros((kp_cap,) + sh, dt)
+            setattr(self.s, n, self.arr[n].ctypes.data)
+        for n, dt, sh in LS_FIELDS:
+            self.arr[n] = np.zeros((kl_cap,) + sh, dt)
+            setattr(self.s, n, self.arr[n].ctypes.data)
+
+    @property
+    def n_pt(self) -> int:
+        return self.s.n_pt
+
+    @property
+    def n_ls(self) -> int:
+        return self.s.n_ls
+
+    def get(self, name: str) -> np.ndarray:
+        if name in self.arr:
+            n = self.s.n_pt if name.startswith("pt_") or name == "pdesc" else self.s.n_ls
+            return self.arr[name][:n]
+        if name in ("err_norm", "time_stamp"):
+            return np.array(getattr(self.s, name))
+        k = dict(POSE_FIELDS)[name]
+        v = np.ctypeslib.as_array(getattr(self.s, name))[:k].copy()
+        return v.reshape(4, 4) if k == 16 else v.reshape(6, 6) if k == 36 else v
+
+    def pose(self) -> dict:
+        return {n: self.get(n) for n, _ in POSE_FIELDS} | {"err_norm": float(self.s.err_norm)}
+
+    def ptr(self):
+        return C.byref(self.s)
+
+
+# ---------------------------------------------------------- GPU handles --
+class Context:
+    """gfpl_ctx: one HIP device + stream + camera + config."""
+
+    def __init__(self, cam: Camera, cfg: Config, device: int = 0, stream: int = 0):
+        self.L = hiplib()
+        h = C.c_void_p()
+        check(self.L.gfpl_create(device, C.c_void_p(stream), C.byref(h)), "gfpl_create")
+        self.h = h
+        check(self.L.gfpl_set_camera(h, C.byref(cam)), "set_camera")
+        check(self.L.gfpl_set_config(h, C.byref(cfg)), "set_config")
+        self.cam, self.cfg = cam, cfg
+
+    def synchronize(self):
+        check(self.L.gfpl_synchronize(self.h), "synchronize")
+
+    def set_timing(self, on: bool):
+        check(self.L.gfpl_set_timing(self.h, int(on)), "set_timing")
+
+    def stage_times(self) -> np.ndarray:
+        out = np.zeros(7, np.float32)
+        check(self.L.gfpl_get_stage_times(self.h, out.ctypes.data), "stage_times")
+        return out
+
+    def knn2(self, q_dev, nq: int, t_dev, nt: int, cell: int, idx_dev, dist_dev) -> int:
+        return self.L.gfpl_knn2_hamming(self.h, _ptr(q_dev), nq, _ptr(t_dev), nt, cell,
+                                        _ptr(idx_dev), _ptr(dist_dev))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StereoFrameHandler:
+    """B independent StVO::StereoFrameHandler objects resident on one GPU.
+
+    Method names follow include/stereoFrameHandler.h:38-174."""
+
+    def __init__(self, ctx: Context, batch: int, kp_cap: int, kl_cap: int):
+        self.ctx, self.L = ctx, ctx.L
+        h = C.c_void_p()
+        check(self.L.gfpl_seqbatch_create(ctx.h, batch, kp_cap, kl_cap, C.byref(h)), "seqbatch_create")
+        self.h = h
+        self.B, self.kp_cap, self.kl_cap = batch, kp_cap, kl_cap
+
+    def initialize(self, fr: Frames):
+        check(self.L.gfpl_initialize(self.h, C.byref(fr)), "initialize")
+
+    def insertStereoPair(self, fr: Frames):
+        check(self.L.gfpl_insert_stereo_pair(self.h, C.byref(fr)), "insert_stereo_pair")
+
+    def optimizePose(self):
+        check(self.L.gfpl_optimize_pose(self.h), "optimize_pose")
+
+    def updateFrame(self):
+        check(self.L.gfpl_update_frame(self.h), "update_frame")
+
+    def frameStep(self, fr: Frames):
+        check(self.L.gfpl_frame_step(self.h, C.byref(fr)), "frame_step")
+
+    # stage entry points
+    def stereoPoints(self, fr: Frames):
+        check(self.L.gfpl_stereo_points(self.h, C.byref(fr)), "stereo_points")
+
+    def stereoLines(self, fr: Frames):
+        check(self.L.gfpl_stereo_lines(self.h, C.byref(fr)), "stereo_lines")
+
+    def estimateStereoUncertainty(self):
+        check(self.L.gfpl_line_uncertainty(self.h), "line_uncertainty")
+
+    def crossFrameMatchingPoints(self):
+        check(self.L.gfpl_cross_points(self.h), "cross_points")
+
+    def crossFrameMatchingLines(self):
+        check(self.L.gfpl_cross_lines(self.h), "cross_lines")
+
+    def estimateProjUncertainty_submodular(self):
+        check(self.L.gfpl_line_cut(self.h), "line_cut")
+
+    # state transfer
+    def read_frame(self, which: int, seq: int) -> FrameHost:
+        fh = FrameHost(self.kp_cap, self.kl_cap)
+        check(self.L.gfpl_read_frame(self.h, which, seq, fh.ptr()), "read_frame")
+        return fh
+
+    def write_frame(self, which: int, seq: int, fh: FrameHost):
+        check(self.L.gfpl_write_frame(self.h, which, seq, fh.ptr()), "write_frame")
+
+    def read_track(self, seq: int) -> dict:
+        t = TrackHost()
+        check(self.L.gfpl_read_track(self.h, seq, C.byref(t)), "read_track")
+        return t.as_dict()
+
+    def write_track(self, seq: int, tr: TrackHost):
+        check(self.L.gfpl_write_track(self.h, seq, C.byref(tr)), "write_track")
+
+    def last_step_bytes(self) -> int:
+        v = C.c_int64()
+        check(self.L.gfpl_last_step_bytes(self.h, C.byref(v)), "last_step_bytes")
+        return v.value
+
+    def nbytes(self) -> int:
+        return int(self.L.gfpl_seqbatch_bytes(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_seqbatch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def track_from_dict(d: dict) -> TrackHost:
+    t = TrackHost()
+    t.n_matched_pt = len(d["matched_pt"])
+    t.n_matched_ls = len(d["matched_ls"])
+    for i, v in enumerate(d["matched_pt"]):
+        t.matched_pt[i] = int(v)
+    for i, v in enumerate(d["matched_ls"]):
+        t.matched_ls[i] = int(v)
+    t.n_inliers, t.n_inliers_pt, t.n_inliers_ls = d["n_inliers"], d["n_inliers_pt"], d["n_inliers_ls"]
+    t.num_frame_loss = d["num_frame_loss"]
+    return t

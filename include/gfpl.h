@@ -1,0 +1,292 @@
+/*
+ * gfpl.h — C ABI of the MI355X-native GF-PL-SLAM tracking hot path.
+ *
+ * The reference has no FFI: its hot path is the C++ member functions of
+ * StVO::StereoFrame / StVO::StereoFrameHandler (include/stereoFrame.h:89-260,
+ * include/stereoFrameHandler.h:38-174 of SimonsRoad/gf-pl-slam).  Each entry
+ * point below names the reference method it replaces; INTEGRATION.md shows the
+ * one-line call a maintainer puts into that method body.
+ *
+ * Conventions
+ *  - extern "C", plain pointers and sizes, no C++ / torch types.
+ *  - Every function returns int: 0 = GFPL_OK, negative = GFPL_E_*.
+ *  - A gfpl_ctx is bound to one HIP device and is not re-entrant; one context
+ *    per host thread.  Work is enqueued on the stream passed to gfpl_create
+ *    (hipStream_t as void*, NULL = default stream) and is asynchronous unless
+ *    the function says it synchronises.
+ *  - A gfpl_seqbatch holds B independent stereo sequences (one StereoFrameHandler
+ *    each) resident in HBM: prev/curr frame state, matched lists and pose.
+ *  - Input frames (gfpl_frames) are DEVICE pointers laid out [B][cap] per
+ *    sequence (counts per sequence in n_*).  The right image pyramid is packed
+ *    per sequence as consecutive levels of gfpl_camera.lvl_rows x lvl_cols bytes.
+ *  - Matrices are row-major double.
+ */
+#ifndef GFPL_H
+#define GFPL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GFPL_ABI_VERSION 1
+
+#define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
+#define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
+#define GFPL_MAX_MATCHED_PT 2048    /* capacity of matched_pt (cap from config)   */
+#define GFPL_MAX_MATCHED_LS 1024    /* capacity of matched_ls (cap from config)   */
+
+/* error codes */
+#define GFPL_OK                   0
+#define GFPL_E_INVALID          (-1)   /* bad argument / NULL pointer            */
+#define GFPL_E_HIP              (-2)   /* HIP runtime error                     */
+#define GFPL_E_NO_DEVICE        (-3)   /* no HIP device / extension not built   */
+#define GFPL_E_TOO_FEW_TRAIN    (-4)   /* knn-2 with < 2 train rows (ref UB, U4) */
+#define GFPL_E_CAPACITY         (-5)   /* counts exceed the seqbatch capacity    */
+#define GFPL_E_STATE            (-6)   /* call order violated (e.g. insert before initialize) */
+#define GFPL_E_UNSUPPORTED      (-7)   /* config flag combination not on the path */
+
+/* which frame of a sequence */
+#define GFPL_PREV 0
+#define GFPL_CURR 1
+
+/* Hamming cell size: 1 = cv::NORM_HAMMING, 2 = cv::NORM_HAMMING2 */
+#define GFPL_HAMMING  1
+#define GFPL_HAMMING2 2
+
+/* ------------------------------------------------------------------------ */
+/* Camera: PinholeStereoCamera (include/pinholeStereoCamera.h:37-103) plus the
+ * ORB scale tables of ORBextractor (src/ORBextractor.cc:410-431) and the
+ * right-pyramid geometry of ORBextractor::ComputePyramid (:1107-1132).     */
+typedef struct gfpl_camera {
+    int    width, height;
+    double fx, fy, cx, cy, b;
+    int    n_levels;                          /* Config::orbNLevels            */
+    float  scale[GFPL_MAX_LEVELS];            /* mvScaleFactors                */
+    float  inv_scale[GFPL_MAX_LEVELS];        /* mvInvScaleFactors             */
+    int    lvl_cols[GFPL_MAX_LEVELS];         /* cvRound(W * inv_scale)        */
+    int    lvl_rows[GFPL_MAX_LEVELS];         /* cvRound(H * inv_scale)        */
+    int64_t lvl_offset[GFPL_MAX_LEVELS];      /* byte offset of level in packed pyramid */
+    int64_t pyr_bytes;                        /* bytes of one packed pyramid   */
+    double sigma2_pt[GFPL_MAX_LEVELS];        /* PointFeature::sigma2 per level (src/stereoFeatures.cpp:41-47) */
+    double sigma2_ln[GFPL_MAX_LEVELS];        /* LineFeature::sigma2 per level  (src/stereoFeatures.cpp:96-101) */
+} gfpl_camera;
+
+/* Config values used by the path (src/config.cpp:77-153).  Mutable like the
+ * reference's Config::xxx() accessors: fill with gfpl_config_default() and
+ * override fields before gfpl_set_config.                                  */
+typedef struct gfpl_config {
+    int    best_lr_matches;      /* :81  true  (only true is implemented)      */
+    int    lr_in_parallel;       /* :79  true  (radius branch of cross points) */
+    int    use_line_conf_cut;    /* :83  true                                   */
+    int    cut_with_max_vol;     /* :86  true  (only true is implemented)      */
+    double ratio_disp_std;       /* :84  0.15                                   */
+    double ratio_disp_std_hor;   /* :85  0.9                                    */
+    int    max_line_match_num;   /* :94  300                                    */
+    int    max_point_match_num;  /* :95  500                                    */
+    double max_dist_epip;        /* :101 2.0                                    */
+    double min_disp;             /* :102 1.0                                    */
+    double max_ratio_12_p;       /* :103 0.9                                    */
+    double point_match_radius;   /* :104 50.0                                   */
+    double stereo_overlap_th;    /* :106 0.5                                    */
+    double line_horiz_th;        /* :108 0.1                                    */
+    double desc_th_l;            /* :109 0.1                                    */
+    double line_cov_th;          /* :110 10.0                                   */
+    double homog_th;             /* :121 1e-7                                   */
+    int    min_features;         /* :122 10                                     */
+    int    max_iters;            /* :124 5                                      */
+    int    max_iters_ref;        /* :125 10                                     */
+    double min_error;            /* :126 1e-7                                   */
+    double min_error_change;     /* :127 1e-7                                   */
+    double inlier_k;             /* :128 2.0                                    */
+    double motion_step_th;       /* :129 10                                     */
+    double orb_scale_factor;     /* :135 1.2                                    */
+    int    orb_n_levels;         /* :136 4                                      */
+    double lsd_scale;            /* :145 1                                      */
+    double cut_step;             /* stepCutRatio 0.05 (src/stereoFrameHandler.cpp:135) */
+    double cut_rng[2];           /* rngCutRatio {0,1} (src/stereoFrameHandler.cpp:134)  */
+    double proj_gate_px;         /* rng_included 10.0 (src/stereoFrameHandler.cpp:534)  */
+} gfpl_config;
+
+/* cv::KeyPoint subset used by the path */
+typedef struct gfpl_keypoint { float x, y; int octave; } gfpl_keypoint;
+/* line_descriptor::KeyLine subset (3rdparty/line_descriptor/include/line_descriptor/descriptor_custom.hpp:105-170) */
+typedef struct gfpl_keyline { float sx, sy, ex, ey, angle; int octave; } gfpl_keyline;
+
+/* One batch of input stereo frames (detections already done — detection is out
+ * of scope).  All pointers are DEVICE pointers.     */
+typedef struct gfpl_frames {
+    int batch;                         /* B                                   */
+    int kp_cap, kl_cap;                /* row capacity per sequence           */
+    const int*           n_kp_l;       /* [B]  points_l.size()                */
+    const int*           n_kp_r;       /* [B]  points_r.size()                */
+    const gfpl_keypoint* kp_l;         /* [B*kp_cap]                          */
+    const gfpl_keypoint* kp_r;         /* [B*kp_cap]                          */
+    const uint8_t*       pdesc_l;      /* [B*kp_cap*32]                       */
+    const uint8_t*       pdesc_r;      /* [B*kp_cap*32]                       */
+    const int*           n_kl_l;       /* [B]  lines_l.size()                 */
+    const int*           n_kl_r;       /* [B]                                 */
+    const gfpl_keyline*  kl_l;         /* [B*kl_cap]                          */
+    const gfpl_keyline*  kl_r;         /* [B*kl_cap]                          */
+    const uint8_t*       ldesc_l;      /* [B*kl_cap*32]                       */
+    const uint8_t*       ldesc_r;      /* [B*kl_cap*32]                       */
+    const uint8_t*       pyr_r;        /* [B*cam.pyr_bytes] right ORB pyramid */
+    const double*        time_stamp;   /* [B]                                 */
+} gfpl_frames;
+
+/* Host view of one frame's state (StereoFrame public members the path
+ * produces, include/stereoFrame.h:205-259; feature records
+ * include/stereoFeatures.h:36-124).  Arrays are caller-allocated with the
+ * capacity given to the seqbatch (points: kp_cap, lines: kl_cap).  The CPU
+ * oracle fills the same struct, so parity tests compare field by field.   */
+typedef struct gfpl_frame_host {
+    int n_pt, n_ls;
+    /* stereo_pt */
+    double*  pt_pl;        /* [cap*2]  pl                    */
+    double*  pt_pl_obs;    /* [cap*2]  pl_obs                */
+    double*  pt_disp;      /* [cap]                          */
+    double*  pt_P;         /* [cap*3]                        */
+    double*  pt_sigma2;    /* [cap]                          */
+    int32_t* pt_idx;       /* [cap]                          */
+    int32_t* pt_level;     /* [cap]                          */
+    uint8_t* pt_inlier;    /* [cap]                          */
+    uint8_t* pdesc;        /* [cap*32]  pdesc_l (reordered)  */
+    /* stereo_ls */
+    double*  ls_spl;       /* [cap*2] */
+    double*  ls_epl;       /* [cap*2] */
+    double*  ls_spl_obs;   /* [cap*2] */
+    double*  ls_epl_obs;   /* [cap*2] */
+    double*  ls_sdisp;     /* [cap]   */
+    double*  ls_edisp;     /* [cap]   */
+    double*  ls_sdisp_obs; /* [cap]   */
+    double*  ls_edisp_obs; /* [cap]   */
+    double*  ls_angle;     /* [cap]   */
+    double*  ls_sigma2;    /* [cap]   */
+    double*  ls_sP;        /* [cap*3] */
+    double*  ls_eP;        /* [cap*3] */
+    double*  ls_le;        /* [cap*3] */
+    double*  ls_le_obs;    /* [cap*3] */
+    double*  ls_covS;      /* [cap*9] covSpt3D */
+    double*  ls_covE;      /* [cap*9] covEpt3D */
+    double*  ls_cut;       /* [cap*2] cutRatio */
+    double*  ls_invcov;    /* [cap*36] invCovPose */
+    int32_t* ls_idx;       /* [cap] */
+    int32_t* ls_level;     /* [cap] */
+    uint8_t* ls_inlier;    /* [cap] */
+    uint8_t* ldesc;        /* [cap*32] ldesc_l (reordered) */
+    /* pose */
+    double Tfw[16], DT[16], DT_cov[36], Tfw_cov[36], DT_cov_eig[6];
+    double err_norm, time_stamp;
+} gfpl_frame_host;
+
+/* StereoFrameHandler tracking results of the last step
+ * (include/stereoFrameHandler.h:120-161). matched_* hold indices into
+ * prev_frame->stereo_pt / stereo_ls in list order (duplicates allowed for
+ * points).                                                */
+typedef struct gfpl_track_host {
+    int n_matched_pt;
+    int n_matched_ls;
+    int32_t matched_pt[GFPL_MAX_MATCHED_PT];
+    int32_t matched_ls[GFPL_MAX_MATCHED_LS];
+    int n_inliers, n_inliers_pt, n_inliers_ls;
+    int num_frame_loss;
+} gfpl_track_host;
+
+typedef struct gfpl_ctx gfpl_ctx;
+typedef struct gfpl_seqbatch gfpl_seqbatch;
+
+/* ---------------------------------------------------------------- setup -- */
+int  gfpl_abi_version(void);
+/* Config::Config() defaults (src/config.cpp:26-154). */
+int  gfpl_config_default(gfpl_config* cfg);
+/* Fill the derived tables of a camera (scale tables, pyramid geometry,
+ * sigma2 tables) from the intrinsics, image size and ORB pyramid params.   */
+int  gfpl_camera_init(gfpl_camera* cam, int width, int height, double fx, double fy,
+                      double cx, double cy, double b, const gfpl_config* cfg);
+
+/* context: device + stream + camera + config (replaces the Config singleton
+ * src/config.cpp:158-162 and the PinholeStereoCamera* each frame holds).   */
+int  gfpl_create(int device, void* hip_stream, gfpl_ctx** out);
+int  gfpl_destroy(gfpl_ctx* ctx);
+int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
+int  gfpl_set_config(gfpl_ctx* ctx, const gfpl_config* cfg);
+int  gfpl_get_camera(const gfpl_ctx* ctx, gfpl_camera* cam);
+int  gfpl_get_config(const gfpl_ctx* ctx, gfpl_config* cfg);
+int  gfpl_synchronize(gfpl_ctx* ctx);
+
+/* B independent sequences (B StereoFrameHandler objects) resident in HBM.  */
+int  gfpl_seqbatch_create(gfpl_ctx* ctx, int batch, int kp_cap, int kl_cap, gfpl_seqbatch** out);
+int  gfpl_seqbatch_destroy(gfpl_seqbatch* sb);
+/* bytes of device memory held by the seqbatch (state + workspace) */
+int64_t gfpl_seqbatch_bytes(const gfpl_seqbatch* sb);
+
+/* -------------------------------------------------- tracker entry points -- */
+/* StereoFrameHandler::initialize (src/stereoFrameHandler.cpp:45-81) with the
+ * detections injected: StereoFrame::extractInitialStereoFeatures matching part
+ * (src/stereoFrame.cpp:173-336); Tfw = Tfw_cov = DT = I.                      */
+int  gfpl_initialize(gfpl_seqbatch* sb, const gfpl_frames* in);
+/* StereoFrameHandler::insertStereoPair (src/stereoFrameHandler.cpp:83-151):
+ * stereo matching of the new frame, predictFramePose, prev-frame line
+ * uncertainty, crossFrameMatching_Hybrid, estimateProjUncertainty_submodular. */
+int  gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in);
+/* StereoFrameHandler::optimizePose(prev_frame->DT) (src/stereoFrameHandler.cpp:1939-2030,
+ * called as at app/plslam_mod.cpp:408).                                       */
+int  gfpl_optimize_pose(gfpl_seqbatch* sb);
+/* StereoFrameHandler::updateFrame_ECCV18 state swap (src/stereoFrameHandler.cpp:864-922):
+ * prev <- curr.  (FAST-threshold adaptation and T_base logging are out of scope.) */
+int  gfpl_update_frame(gfpl_seqbatch* sb);
+/* insert_stereo_pair + optimize_pose + update_frame, one batched step.       */
+int  gfpl_frame_step(gfpl_seqbatch* sb, const gfpl_frames* in);
+
+/* ------------------------------------------------------- stage entry points */
+/* StereoFrame::extractStereoFeatures_ORBSLAM point branch (src/stereoFrame.cpp:453-630)
+ * incl. subPixelStereoRefine_ORBSLAM (:340-404) -> curr stereo_pt, pdesc_l.   */
+int  gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in);
+/* ... line branch (src/stereoFrame.cpp:633-767) -> curr stereo_ls, ldesc_l,
+ * plus the covariances estimateStereoUncertainty (:1448-1484) will need.      */
+int  gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in);
+/* StereoFrame::estimateStereoUncertainty on the PREV frame (src/stereoFrame.cpp:1448-1484). */
+int  gfpl_line_uncertainty(gfpl_seqbatch* sb);
+/* predictFramePose + crossFrameMatching_Hybrid points (src/stereoFrameHandler.cpp:153-157,451-603) */
+int  gfpl_cross_points(gfpl_seqbatch* sb);
+/* crossFrameMatching_Hybrid lines (src/stereoFrameHandler.cpp:605-695)       */
+int  gfpl_cross_lines(gfpl_seqbatch* sb);
+/* estimateProjUncertainty_submodular(0.05,{0,1}) (src/stereoFrameHandler.cpp:1618-1764) */
+int  gfpl_line_cut(gfpl_seqbatch* sb);
+
+/* cv::BFMatcher::knnMatch(k=2) with NORM_HAMMING / NORM_HAMMING2 on device
+ * buffers (call sites src/stereoFrame.cpp:183-197,256-272,636-656;
+ * src/stereoFrameHandler.cpp:617-633).  q: nq x 32 B, t: nt x 32 B (device).
+ * out_idx[2*nq], out_dist[2*nq] (device; distance as float like cv::DMatch).
+ * Returns GFPL_E_TOO_FEW_TRAIN when nt < 2 (reference UB).        */
+int  gfpl_knn2_hamming(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                       int cell, int32_t* out_idx, float* out_dist);
+
+/* ----------------------------------------------------- state transfer ----- */
+/* Copy one sequence's frame state device -> host (synchronises).            */
+int  gfpl_read_frame(gfpl_seqbatch* sb, int which, int seq, gfpl_frame_host* out);
+/* Copy a host frame state into one sequence (synchronises).  Used to start a
+ * stage from a given state (e.g. the oracle's), like the reference's
+ * simulators build frames through the public members (src/simulate_line_cut.cpp:62-212). */
+int  gfpl_write_frame(gfpl_seqbatch* sb, int which, int seq, const gfpl_frame_host* in);
+int  gfpl_read_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* out);
+int  gfpl_write_track(gfpl_seqbatch* sb, int seq, const gfpl_track_host* in);
+
+/* ----------------------------------------------------- instrumentation ---- */
+/* Per-stage device time of the last gfpl_frame_step (HIP events on the
+ * context stream), ms: [stereo_points, stereo_lines, cross_points,
+ * cross_lines, line_cut, pose, total].  Enable with gfpl_set_timing(ctx,1). */
+int  gfpl_set_timing(gfpl_ctx* ctx, int enable);
+int  gfpl_get_stage_times(gfpl_ctx* ctx, float* ms7);
+/* Algorithmic bytes of the last step (SURVEY.md §8(d) formula, from runtime
+ * counts, summed over the batch).  Synchronises.                           */
+int  gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes);
+
+const char* gfpl_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GFPL_H */

@@ -1,0 +1,85 @@
+/*
+ * gfpl_oracle.h — CPU ORACLE for the GF-PL-SLAM tracking hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the timed CPU baseline).  The product path (libgfpl_hip.so) never links,
+ * loads or calls it.
+ *
+ * It is a plain C++ restatement of the reference's algorithm
+ * (SimonsRoad/gf-pl-slam; every function cites the file:line it follows) with
+ * the semantics ledger of SURVEY.md §8(c) pinned explicitly (U1-U7, Q1-Q15,
+ * T1) plus the numeric pins listed in DESIGN.md §"Oracle":
+ *   N1  all floating point without contraction (-ffp-contract=off);
+ *   N2  Eigen expression trees are evaluated in their left-to-right order,
+ *       inner products k-sequential, sums over lists sequential in list order;
+ *   N3  log / sin / cos are the fdlibm algorithms (e_log.c, k_sin.c, k_cos.c,
+ *       e_rem_pio2.c medium branch) evaluated with + - * / only, because the
+ *       reference's own values come from Eigen packet math / libm and are not
+ *       reproducible across machines;
+ *   N4  SelfAdjointEigenSolver -> cyclic Jacobi; LDLT -> Eigen 3.3
+ *       ldlt_inplace<Lower> with pivoting + pseudo-inverse D solve;
+ *       inverse() of 6x6 -> partial-pivot LU; of 4x4 -> cofactor expansion.
+ *
+ * Parity status: the reference cannot be compiled in this image (OpenCV 3.4.1,
+ * Eigen3, g2o, Boost, yaml-cpp absent) and has no Python
+ * implementation and no usable golden vectors.  This oracle is pinned by
+ * hand-derived known answers (tests/test_oracle_known_answers.py) and the
+ * golden fixtures it generated (tests/golden/, make_golden.py).
+ */
+#ifndef GFPL_ORACLE_H
+#define GFPL_ORACLE_H
+#include "../include/gfpl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gfplo_handler gfplo_handler;
+
+gfplo_handler* gfplo_create(const gfpl_camera* cam, const gfpl_config* cfg);
+void gfplo_destroy(gfplo_handler* h);
+
+/* StereoFrameHandler::initialize (src/stereoFrameHandler.cpp:45-81); in = host
+ * frames batch, row `seq` is used. */
+int gfplo_initialize(gfplo_handler* h, const gfpl_frames* in, int seq);
+/* insertStereoPair (src/stereoFrameHandler.cpp:83-151) */
+int gfplo_insert_stereo_pair(gfplo_handler* h, const gfpl_frames* in, int seq);
+/* optimizePose(prev_frame->DT) (src/stereoFrameHandler.cpp:1939-2030) */
+int gfplo_optimize_pose(gfplo_handler* h);
+/* updateFrame_ECCV18 swap (src/stereoFrameHandler.cpp:864-922) */
+int gfplo_update_frame(gfplo_handler* h);
+
+/* stage-level entry points (same split as include/gfpl.h) */
+int gfplo_begin_frame(gfplo_handler* h, const gfpl_frames* in, int seq);   /* new curr_frame */
+int gfplo_stereo_points(gfplo_handler* h);
+int gfplo_stereo_lines(gfplo_handler* h);
+int gfplo_line_uncertainty(gfplo_handler* h);
+int gfplo_cross_points(gfplo_handler* h);   /* includes predictFramePose */
+int gfplo_cross_lines(gfplo_handler* h);
+int gfplo_line_cut(gfplo_handler* h);
+
+int gfplo_read_frame(gfplo_handler* h, int which, gfpl_frame_host* out);
+int gfplo_write_frame(gfplo_handler* h, int which, const gfpl_frame_host* in);
+int gfplo_read_track(gfplo_handler* h, gfpl_track_host* out);
+int gfplo_write_track(gfplo_handler* h, const gfpl_track_host* in);
+
+/* primitives (known-answer tests) */
+int    gfplo_hamming(const uint8_t* a, const uint8_t* b, int cell);
+int    gfplo_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell,
+                  int32_t* out_idx, float* out_dist);
+double gfplo_log(double x);
+double gfplo_sin(double x);
+double gfplo_cos(double x);
+double gfplo_logdet6(const double* M36);
+int    gfplo_ldlt_solve6(const double* H36, const double* g6, double* x6);
+int    gfplo_inverse6(const double* A36, double* out36);
+int    gfplo_inverse4(const double* A16, double* out16);
+int    gfplo_eig_sym(const double* A, int n, double* w);
+int    gfplo_expmap_se3(const double* x6, double* T16);
+int    gfplo_inverse_se3(const double* T16, double* out16);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

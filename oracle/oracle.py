@@ -1,0 +1,175 @@
+"""ctypes binding of the CPU ORACLE (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker.  The product path never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "gf-pl-slam_amd"))
+import gfpl  # noqa: E402  (struct definitions only)
+
+_L = None
+
+
+def lib() -> C.CDLL:
+    global _L
+    if _L is None:
+        p = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(p):
+            raise RuntimeError(f"{p} not built (make oracle)")
+        L = C.CDLL(p)
+        P = C.c_void_p
+        L.gfplo_create.argtypes = [P, P]; L.gfplo_create.restype = P
+        L.gfplo_destroy.argtypes = [P]; L.gfplo_destroy.restype = None
+        for n in ["gfplo_initialize", "gfplo_insert_stereo_pair", "gfplo_begin_frame"]:
+            getattr(L, n).argtypes = [P, P, C.c_int]; getattr(L, n).restype = C.c_int
+        for n in ["gfplo_optimize_pose", "gfplo_update_frame", "gfplo_stereo_points",
+                  "gfplo_stereo_lines", "gfplo_line_uncertainty", "gfplo_cross_points",
+                  "gfplo_cross_lines", "gfplo_line_cut"]:
+            getattr(L, n).argtypes = [P]; getattr(L, n).restype = C.c_int
+        for n in ["gfplo_read_frame", "gfplo_write_frame"]:
+            getattr(L, n).argtypes = [P, C.c_int, P]; getattr(L, n).restype = C.c_int
+        for n in ["gfplo_read_track", "gfplo_write_track"]:
+            getattr(L, n).argtypes = [P, P]; getattr(L, n).restype = C.c_int
+        L.gfplo_hamming.argtypes = [P, P, C.c_int]; L.gfplo_hamming.restype = C.c_int
+        L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
+        for n in ["gfplo_log", "gfplo_sin", "gfplo_cos"]:
+            getattr(L, n).argtypes = [C.c_double]; getattr(L, n).restype = C.c_double
+        L.gfplo_logdet6.argtypes = [P]; L.gfplo_logdet6.restype = C.c_double
+        L.gfplo_ldlt_solve6.argtypes = [P, P, P]; L.gfplo_ldlt_solve6.restype = C.c_int
+        for n in ["gfplo_inverse6", "gfplo_inverse4", "gfplo_expmap_se3", "gfplo_inverse_se3"]:
+            getattr(L, n).argtypes = [P, P]; getattr(L, n).restype = C.c_int
+        L.gfplo_eig_sym.argtypes = [P, C.c_int, P]; L.gfplo_eig_sym.restype = C.c_int
+        _L = L
+    return _L
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class OracleHandler:
+    """One reference StereoFrameHandler restated on the CPU."""
+
+    def __init__(self, cam: gfpl.Camera, cfg: gfpl.Config, kp_cap: int, kl_cap: int):
+        self.L = lib()
+        self.h = self.L.gfplo_create(C.byref(cam), C.byref(cfg))
+        if not self.h:
+            raise RuntimeError("gfplo_create failed (camera tables disagree with the oracle's?)")
+        self.kp_cap, self.kl_cap = kp_cap, kl_cap
+
+    def _c(self, code, what):
+        if code != 0:
+            raise RuntimeError(f"oracle {what}: {code}")
+
+    def initialize(self, fr: gfpl.Frames, seq: int):
+        self._c(self.L.gfplo_initialize(self.h, C.byref(fr), seq), "initialize")
+
+    def insertStereoPair(self, fr: gfpl.Frames, seq: int):
+        self._c(self.L.gfplo_insert_stereo_pair(self.h, C.byref(fr), seq), "insert")
+
+    def optimizePose(self):
+        self._c(self.L.gfplo_optimize_pose(self.h), "optimize_pose")
+
+    def updateFrame(self):
+        self._c(self.L.gfplo_update_frame(self.h), "update_frame")
+
+    def begin_frame(self, fr: gfpl.Frames, seq: int):
+        self._c(self.L.gfplo_begin_frame(self.h, C.byref(fr), seq), "begin_frame")
+
+    def stereoPoints(self):
+        self._c(self.L.gfplo_stereo_points(self.h), "stereo_points")
+
+    def stereoLines(self):
+        self._c(self.L.gfplo_stereo_lines(self.h), "stereo_lines")
+
+    def estimateStereoUncertainty(self):
+        self._c(self.L.gfplo_line_uncertainty(self.h), "line_uncertainty")
+
+    def crossFrameMatchingPoints(self):
+        self._c(self.L.gfplo_cross_points(self.h), "cross_points")
+
+    def crossFrameMatchingLines(self):
+        self._c(self.L.gfplo_cross_lines(self.h), "cross_lines")
+
+    def estimateProjUncertainty_submodular(self):
+        self._c(self.L.gfplo_line_cut(self.h), "line_cut")
+
+    def read_frame(self, which: int) -> gfpl.FrameHost:
+        fh = gfpl.FrameHost(self.kp_cap, self.kl_cap)
+        self._c(self.L.gfplo_read_frame(self.h, which, fh.ptr()), "read_frame")
+        return fh
+
+    def write_frame(self, which: int, fh: gfpl.FrameHost):
+        self._c(self.L.gfplo_write_frame(self.h, which, fh.ptr()), "write_frame")
+
+    def read_track(self) -> dict:
+        t = gfpl.TrackHost()
+        self._c(self.L.gfplo_read_track(self.h, C.byref(t)), "read_track")
+        return t.as_dict()
+
+    def write_track(self, tr: gfpl.TrackHost):
+        self._c(self.L.gfplo_write_track(self.h, C.byref(tr)), "write_track")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.gfplo_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+# ---- primitives
+def hamming(a: np.ndarray, b: np.ndarray, cell: int = 1) -> int:
+    a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
+    return lib().gfplo_hamming(_p(a), _p(b), cell)
+
+
+def knn2(q: np.ndarray, t: np.ndarray, cell: int = 1):
+    q = np.ascontiguousarray(q, np.uint8); t = np.ascontiguousarray(t, np.uint8)
+    idx = np.zeros((len(q), 2), np.int32); dist = np.zeros((len(q), 2), np.float32)
+    rc = lib().gfplo_knn2(_p(q), len(q), _p(t), len(t), cell, _p(idx), _p(dist))
+    return rc, idx, dist
+
+
+def log(x: float) -> float: return lib().gfplo_log(x)
+def sin(x: float) -> float: return lib().gfplo_sin(x)
+def cos(x: float) -> float: return lib().gfplo_cos(x)
+
+
+def logdet6(M: np.ndarray) -> float:
+    return lib().gfplo_logdet6(_p(np.ascontiguousarray(M, np.float64)))
+
+
+def ldlt_solve6(H: np.ndarray, g: np.ndarray) -> np.ndarray:
+    x = np.zeros(6); H = np.ascontiguousarray(H, np.float64); g = np.ascontiguousarray(g, np.float64)
+    lib().gfplo_ldlt_solve6(_p(H), _p(g), _p(x)); return x
+
+
+def inverse6(A):
+    o = np.zeros((6, 6)); A = np.ascontiguousarray(A, np.float64); lib().gfplo_inverse6(_p(A), _p(o)); return o
+
+
+def inverse4(A):
+    o = np.zeros((4, 4)); A = np.ascontiguousarray(A, np.float64); lib().gfplo_inverse4(_p(A), _p(o)); return o
+
+
+def eig_sym(A):
+    A = np.ascontiguousarray(A, np.float64); n = A.shape[0]; w = np.zeros(n)
+    lib().gfplo_eig_sym(_p(A), n, _p(w)); return w
+
+
+def expmap_se3(x):
+    x = np.ascontiguousarray(x, np.float64); T = np.zeros((4, 4)); lib().gfplo_expmap_se3(_p(x), _p(T)); return T
+
+
+def inverse_se3(T):
+    T = np.ascontiguousarray(T, np.float64); o = np.zeros((4, 4)); lib().gfplo_inverse_se3(_p(T), _p(o)); return o
