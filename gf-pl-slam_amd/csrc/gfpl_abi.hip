@@ -94,7 +94,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
     sb->scr.cut_pt = c.take<double>(B * sb->mpt_cap * 21);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
-    sb->scr.bytes = c.take<int64_t>(B);
+    sb->scr.bytes = c.take<int64_t>(B * 8);
     sb->scr.n_subpix = c.take<int32_t>(B);
 }
 
@@ -539,14 +539,25 @@ int gfpl_get_stage_times(gfpl_ctx* c, float* ms7) {
     return GFPL_OK;
 }
 
-int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {
-    if (!sb || !bytes) return GFPL_E_INVALID;
-    std::vector<int64_t> v(sb->B);
+int gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7) {
+    if (!sb || !bytes7) return GFPL_E_INVALID;
+    std::vector<int64_t> v((size_t)sb->B * 8);
     HIPCHK(hipStreamSynchronize(sb->ctx->stream));
-    HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * sb->B, hipMemcpyDeviceToHost));
-    int64_t s = 0;
-    for (int64_t x : v) s += x;
-    *bytes = s;
+    HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost));
+    for (int s = 0; s < 7; ++s) {
+        int64_t t = 0;
+        for (int b = 0; b < sb->B; ++b) t += v[(size_t)b * 8 + s];
+        bytes7[s] = t;
+    }
+    return GFPL_OK;
+}
+
+int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {
+    if (!bytes) return GFPL_E_INVALID;
+    int64_t v[7];
+    int e = gfpl_last_step_stage_bytes(sb, v);
+    if (e) return e;
+    *bytes = v[6];
     return GFPL_OK;
 }
 

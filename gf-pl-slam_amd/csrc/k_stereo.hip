@@ -543,9 +543,11 @@ __global__ void k_line_uncertainty(KParams p) {
     for (int k = 0; k < 9; ++k) { L.covS[9 * q + k] = cS[k]; L.covE[9 * q + k] = cE[k]; }
 }
 
-// algorithmic HBM bytes of one step of one sequence:
-// inputs (descriptors, keypoints, keylines, 11x11 + 11x21 SAD windows per
-// sub-pixel candidate), prev state read, curr state written, match lists, pose.
+// Algorithmic HBM bytes of one step of one sequence, per stage (DESIGN.md
+// §Roofline): the bytes each stage must read or write at minimum, from the
+// runtime counts.  bytes[b*8 + s], s = 0 stereo_points, 1 stereo_lines,
+// 2 cross_points (+ prev line uncertainty), 3 cross_lines, 4 line_cut, 5 pose,
+// 6 total.
 __global__ void k_step_bytes(KParams p) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.B) return;
@@ -555,8 +557,16 @@ __global__ void k_step_bytes(KParams p) {
     const int64_t Sp = p.prev.pt.n[b], Sl = p.prev.ls.n[b];
     const int64_t Sp2 = p.curr.pt.n[b], Sl2 = p.curr.ls.n[b];
     const int64_t Mp = p.tr.n_matched_pt[b], Ml = p.tr.n_matched_ls[b];
-    p.scr.bytes[b] = 32 * (No + Nk) + 12 * No + 24 * Nk + (121 + 231) * Mo + 80 * (Sp + Sp2) + 248 * (Sl + Sl2) +
-                     4 * (Mp + Ml) + 16 * Ml + 416;
+    int64_t st[6];
+    st[0] = 44 * No + (121 + 231) * Mo + 97 * Sp2;          // kps+descs, SAD windows, curr points
+    st[1] = 56 * Nk + 193 * Sl2;                             // keylines+descs, curr lines
+    st[2] = 216 * Sl + 60 * Sp + 48 * Sp2 + 25 * Mp + 256;   // uncertainty, projections, radius/gate, lists
+    st[3] = 36 * Sl + 32 * Sl2 + 153 * Ml;                   // line knn both ways, obs copy, lists
+    st[4] = 608 * Ml + 44 * Mp;                              // cut: line/point info inputs, cut endpoints + invCov
+    st[5] = 54 * Mp + 86 * Ml + 1504;                        // GN inputs once, inlier flags, pose + covariances
+    int64_t tot = 0;
+    for (int i = 0; i < 6; ++i) { p.scr.bytes[8 * b + i] = st[i]; tot += st[i]; }
+    p.scr.bytes[8 * b + 6] = tot;
 }
 
 // ------------------------------------------------------------ launchers --

@@ -153,7 +153,17 @@ def _load(name: str) -> C.CDLL:
 
 
 def hiplib() -> C.CDLL:
-    """The product library (HIP kernels + C ABI).  Raises if not built."""
+    """The product library (HIP kernels + C ABI).  Raises if not built.
+
+    torch (when importable) is imported first so the process has ONE HIP
+    runtime: torch's libamdhip64 is then what libgfpl_hip.so's NEEDED
+    libamdhip64.so.7 resolves to (a second copy loaded under another file name
+    would see no devices)."""
+    if "libgfpl_hip.so" not in _LIBS:
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
     L = _load("libgfpl_hip.so")
     if not getattr(L, "_gfpl_typed", False):
         P = C.c_void_p
@@ -191,6 +201,7 @@ def hiplib() -> C.CDLL:
             "gfpl_set_timing": ([P, C.c_int], C.c_int),
             "gfpl_get_stage_times": ([P, P], C.c_int),
             "gfpl_last_step_bytes": ([P, P], C.c_int),
+            "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_strerror": ([C.c_int], C.c_char_p),
         }
         for n, (a, r) in sigs.items():
@@ -487,6 +498,11 @@ class StereoFrameHandler:
         v = C.c_int64()
         check(self.L.gfpl_last_step_bytes(self.h, C.byref(v)), "last_step_bytes")
         return v.value
+
+    def last_step_stage_bytes(self) -> np.ndarray:
+        v = np.zeros(7, np.int64)
+        check(self.L.gfpl_last_step_stage_bytes(self.h, v.ctypes.data), "last_step_stage_bytes")
+        return v
 
     def nbytes(self) -> int:
         return int(self.L.gfpl_seqbatch_bytes(self.h))

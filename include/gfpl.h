@@ -283,6 +283,9 @@ int  gfpl_get_stage_times(gfpl_ctx* ctx, float* ms7);
 /* Algorithmic bytes of the last step (SURVEY.md §8(d) formula, from runtime
  * counts, summed over the batch).  Synchronises.                           */
 int  gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes);
+/* ... per stage: [stereo_points, stereo_lines, cross_points, cross_lines,
+ * line_cut, pose, total] (DESIGN.md §Roofline gives each stage's formula). */
+int  gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7);
 
 const char* gfpl_strerror(int code);
 
