@@ -96,6 +96,12 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
     sb->scr.bytes = c.take<int64_t>(B * 8);
     sb->scr.n_subpix = c.take<int32_t>(B);
+    sb->scr.cut_sum = c.take<double>(B * 24);
+    sb->scr.cut_dtinv = c.take<double>(B * 16);
+    sb->scr.pose_DT = c.take<double>(B * 16);
+    sb->scr.pose_H = c.take<double>(B * 36);
+    sb->scr.pose_err = c.take<double>(B);
+    sb->scr.pose_ok = c.take<int32_t>(B);
 }
 
 DevCam devcam(const gfpl_camera& c) {

@@ -361,97 +361,155 @@ GFPL_DEV double logdet6_lower(double* a /* 21, destroyed */) {
     return 2.0 * s;
 }
 
+// The three small dense solvers below keep every matrix in registers: loops
+// are fully unrolled and pivot swaps are applied through compile-time-indexed
+// selects, so no runtime-indexed array spills to scratch.  The arithmetic is
+// the oracle's, operation for operation (pivot choice, swap, update order).
+template <typename T>
+GFPL_DEV void swap_v(T& a, T& b) { T t = a; a = b; b = t; }
+
 // LDLT solve, Eigen 3.3 semantics (see oracle ldlt_solve6)
 GFPL_DEV void ldlt_solve6(const double* H, const double* g, double* x) {
     double m[36];
+#pragma unroll
     for (int i = 0; i < 36; ++i) m[i] = H[i];
     int tr[6];
     double temp[6];
+    bool stop = false;
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
+        if (stop) { tr[k] = k; continue; }
         int big = k;
-        double bv = fabs(m[k * 6 + k]);
+        double bv = fabs(m[k * 7]);
+#pragma unroll
         for (int i = k + 1; i < 6; ++i) {
-            double v = fabs(m[i * 6 + i]);
+            const double v = fabs(m[i * 7]);
             if (v > bv) { bv = v; big = i; }
         }
         tr[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; ++j) { double t = m[k * 6 + j]; m[k * 6 + j] = m[big * 6 + j]; m[big * 6 + j] = t; }
-            for (int i = big + 1; i < 6; ++i) { double t = m[i * 6 + k]; m[i * 6 + k] = m[i * 6 + big]; m[i * 6 + big] = t; }
-            { double t = m[k * 6 + k]; m[k * 6 + k] = m[big * 6 + big]; m[big * 6 + big] = t; }
-            for (int i = k + 1; i < big; ++i) {
-                double tmp = m[i * 6 + k];
-                m[i * 6 + k] = m[big * 6 + i];
-                m[big * 6 + i] = tmp;
+#pragma unroll
+        for (int c = k + 1; c < 6; ++c) {
+            if (big == c) {
+#pragma unroll
+                for (int j = 0; j < k; ++j) swap_v(m[k * 6 + j], m[c * 6 + j]);
+#pragma unroll
+                for (int i = c + 1; i < 6; ++i) swap_v(m[i * 6 + k], m[i * 6 + c]);
+                swap_v(m[k * 7], m[c * 7]);
+#pragma unroll
+                for (int i = k + 1; i < c; ++i) {
+                    const double tmp = m[i * 6 + k];
+                    m[i * 6 + k] = m[c * 6 + i];
+                    m[c * 6 + i] = tmp;
+                }
             }
         }
         if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = m[j * 6 + j] * m[k * 6 + j];
+#pragma unroll
+            for (int j = 0; j < k; ++j) temp[j] = m[j * 7] * m[k * 6 + j];
             double dot = m[k * 6 + 0] * temp[0];
+#pragma unroll
             for (int j = 1; j < k; ++j) dot = dot + m[k * 6 + j] * temp[j];
-            m[k * 6 + k] = m[k * 6 + k] - dot;
+            m[k * 7] = m[k * 7] - dot;
+#pragma unroll
             for (int i = k + 1; i < 6; ++i) {
                 double v = m[i * 6 + k];
+#pragma unroll
                 for (int j = 0; j < k; ++j) v = v - m[i * 6 + j] * temp[j];
                 m[i * 6 + k] = v;
             }
         }
-        double akk = m[k * 6 + k];
-        bool valid = fabs(akk) > 0.0;
+        const double akk = m[k * 7];
+        const bool valid = fabs(akk) > 0.0;
         if (k == 0 && !valid) {
-            for (int j = 0; j < 6; ++j) tr[j] = j;
-            break;
+            tr[0] = 0;
+            stop = true;
+            continue;
         }
-        if (k < 5 && valid)
+        if (k < 5 && valid) {
+#pragma unroll
             for (int i = k + 1; i < 6; ++i) m[i * 6 + k] = m[i * 6 + k] / akk;
+        }
     }
     double d[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) d[i] = g[i];
-    for (int k = 0; k < 6; ++k) { double t = d[k]; d[k] = d[tr[k]]; d[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int c = k + 1; c < 6; ++c)
+            if (tr[k] == c) swap_v(d[k], d[c]);
+#pragma unroll
     for (int i = 0; i < 6; ++i)
+#pragma unroll
         for (int j = 0; j < i; ++j) d[i] = d[i] - m[i * 6 + j] * d[j];
     const double tol = 1.0 / 1.7976931348623157e308;
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
-        double di = m[i * 6 + i];
+        const double di = m[i * 7];
         if (fabs(di) > tol) d[i] = d[i] / di; else d[i] = 0.0;
     }
+#pragma unroll
     for (int i = 5; i >= 0; --i)
+#pragma unroll
         for (int j = i + 1; j < 6; ++j) d[i] = d[i] - m[j * 6 + i] * d[j];
-    for (int k = 5; k >= 0; --k) { double t = d[k]; d[k] = d[tr[k]]; d[tr[k]] = t; }
+#pragma unroll
+    for (int k = 5; k >= 0; --k)
+#pragma unroll
+        for (int c = k + 1; c < 6; ++c)
+            if (tr[k] == c) swap_v(d[k], d[c]);
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
 // PartialPivLU inverse (see oracle inverse6)
 GFPL_DEV void inverse6(const double* A, double* out) {
     double m[36];
+#pragma unroll
     for (int i = 0; i < 36; ++i) m[i] = A[i];
     int perm[6] = {0, 1, 2, 3, 4, 5};
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         int p = k;
         double pv = fabs(m[k * 6 + k]);
+#pragma unroll
         for (int i = k + 1; i < 6; ++i) {
-            double v = fabs(m[i * 6 + k]);
+            const double v = fabs(m[i * 6 + k]);
             if (v > pv) { pv = v; p = i; }
         }
-        if (p != k) {
-            for (int j = 0; j < 6; ++j) { double t = m[k * 6 + j]; m[k * 6 + j] = m[p * 6 + j]; m[p * 6 + j] = t; }
-            int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
+#pragma unroll
+        for (int c = k + 1; c < 6; ++c) {
+            if (p == c) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) swap_v(m[k * 6 + j], m[c * 6 + j]);
+                swap_v(perm[k], perm[c]);
+            }
         }
-        double piv = m[k * 6 + k];
-        if (piv != 0.0)
+        const double piv = m[k * 6 + k];
+        if (piv != 0.0) {
+#pragma unroll
             for (int i = k + 1; i < 6; ++i) m[i * 6 + k] = m[i * 6 + k] / piv;
+        }
+#pragma unroll
         for (int i = k + 1; i < 6; ++i)
+#pragma unroll
             for (int j = k + 1; j < 6; ++j) m[i * 6 + j] = m[i * 6 + j] - m[i * 6 + k] * m[k * 6 + j];
     }
+#pragma unroll
     for (int c = 0; c < 6; ++c) {
         double x[6];
+#pragma unroll
         for (int i = 0; i < 6; ++i) x[i] = (perm[i] == c) ? 1.0 : 0.0;
+#pragma unroll
         for (int i = 0; i < 6; ++i)
+#pragma unroll
             for (int j = 0; j < i; ++j) x[i] = x[i] - m[i * 6 + j] * x[j];
+#pragma unroll
         for (int i = 5; i >= 0; --i) {
+#pragma unroll
             for (int j = i + 1; j < 6; ++j) x[i] = x[i] - m[i * 6 + j] * x[j];
             x[i] = x[i] / m[i * 6 + i];
         }
+#pragma unroll
         for (int i = 0; i < 6; ++i) out[i * 6 + c] = x[i];
     }
 }
@@ -460,45 +518,61 @@ GFPL_DEV void inverse6(const double* A, double* out) {
 template <int N>
 GFPL_DEV void eig_sym(const double* A, double* w) {
     double a[N * N];
+#pragma unroll
     for (int i = 0; i < N * N; ++i) a[i] = A[i];
     for (int sweep = 0; sweep < 50; ++sweep) {
         double off = 0.0;
+#pragma unroll
         for (int p = 0; p < N; ++p)
+#pragma unroll
             for (int q = p + 1; q < N; ++q) off = off + a[p * N + q] * a[p * N + q];
         if (!(off > 0.0)) break;
+#pragma unroll
         for (int p = 0; p < N - 1; ++p)
+#pragma unroll
             for (int q = p + 1; q < N; ++q) {
-                double apq = a[p * N + q];
-                if (apq == 0.0) continue;
-                double app = a[p * N + p], aqq = a[q * N + q];
-                double theta = (aqq - app) / (2.0 * apq);
-                double t;
-                if (fabs(theta) > 1e150) t = 0.5 / theta;
-                else {
-                    t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    if (theta < 0.0) t = -t;
+                const double apq = a[p * N + q];
+                if (apq != 0.0) {
+                    const double app = a[p * N + p], aqq = a[q * N + q];
+                    const double theta = (aqq - app) / (2.0 * apq);
+                    double t;
+                    if (fabs(theta) > 1e150) t = 0.5 / theta;
+                    else {
+                        t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                        if (theta < 0.0) t = -t;
+                    }
+                    const double c = 1.0 / sqrt(t * t + 1.0);
+                    const double s = t * c;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        if (k == p || k == q) continue;
+                        const double akp = a[k * N + p], akq = a[k * N + q];
+                        const double nkp = c * akp - s * akq;
+                        const double nkq = s * akp + c * akq;
+                        a[k * N + p] = nkp; a[p * N + k] = nkp;
+                        a[k * N + q] = nkq; a[q * N + k] = nkq;
+                    }
+                    a[p * N + p] = app - t * apq;
+                    a[q * N + q] = aqq + t * apq;
+                    a[p * N + q] = 0.0; a[q * N + p] = 0.0;
                 }
-                double c = 1.0 / sqrt(t * t + 1.0);
-                double s = t * c;
-                for (int k = 0; k < N; ++k) {
-                    if (k == p || k == q) continue;
-                    double akp = a[k * N + p], akq = a[k * N + q];
-                    double nkp = c * akp - s * akq;
-                    double nkq = s * akp + c * akq;
-                    a[k * N + p] = nkp; a[p * N + k] = nkp;
-                    a[k * N + q] = nkq; a[q * N + k] = nkq;
-                }
-                a[p * N + p] = app - t * apq;
-                a[q * N + q] = aqq + t * apq;
-                a[p * N + q] = 0.0; a[q * N + p] = 0.0;
             }
     }
+#pragma unroll
     for (int i = 0; i < N; ++i) w[i] = a[i * N + i];
+    // insertion sort, unrolled with a "still moving" flag (same result as the oracle's)
+#pragma unroll
     for (int i = 1; i < N; ++i) {
-        double v = w[i];
-        int j = i - 1;
-        while (j >= 0 && w[j] > v) { w[j + 1] = w[j]; --j; }
-        w[j + 1] = v;
+        const double v = w[i];
+        bool moving = true;
+#pragma unroll
+        for (int j = i - 1; j >= 0; --j) {
+            if (moving) {
+                if (w[j] > v) w[j + 1] = w[j];
+                else { w[j + 1] = v; moving = false; }
+            }
+        }
+        if (moving) w[0] = v;
     }
 }
 

@@ -70,6 +70,12 @@ struct DevScratch {
     int32_t* knn;     // [B*4*kcap] initial-frame knn results (idx0, d0, d1, ...)
     int64_t* bytes;   // [B] algorithmic bytes of the last step
     int32_t* n_subpix; // [B] left keypoints that reached the sub-pixel SAD (M_o)
+    double* cut_sum;   // [B*24] invCov_sum (lower triangle) after the r=0 pass
+    double* cut_dtinv; // [B*16] DT_inv of the line cut
+    double* pose_DT;   // [B*16] GN result before the final bookkeeping
+    double* pose_H;    // [B*36] last evaluated H
+    double* pose_err;  // [B]
+    int32_t* pose_ok;  // [B] 1: stage-2 result usable
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

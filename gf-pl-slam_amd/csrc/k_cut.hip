@@ -3,15 +3,23 @@
 // getPoseInfoPoint (:1414-1447), updateEndPointByRatio (:1451-1470) and logdet
 // (include/linespec.h:43-56).
 //
-// The search is a serial chain over matched lines (each line's search reads
-// invCov_sum after all earlier lines).  One 64-lane wave owns one sequence:
-//  phase A  all lanes: initial info matrices (r = 0,0) of lines and points;
-//  phase B  21 lanes: invCov_sum, one lower-triangle element per lane, summed
-//           sequentially in list order (bit-identical to the reference order);
-//  phase C  serial over lines; per greedy step lanes 0..7 evaluate the 8
-//           neighbour cut ratios (info + 6x6 LLT + 6 logs each) in parallel and
-//           the wave picks the first strict maximum (the reference's j-loop).
-// Only the lower triangle is carried: LLT reads nothing else (ledger Q11).
+// The search is a serial chain over matched lines: each line's greedy search
+// reads invCov_sum after all earlier lines were cut.  Three kernels:
+//  k_cut_prep   (64 lanes / sequence, parallel) initial info matrices (r = 0,0)
+//               of lines and points and invCov_sum, summed per element in list
+//               order (21 lanes) — the reference's accumulation order;
+//  k_cut_search (8 lanes / sequence, 8 sequences per wave) the serial greedy
+//               search.  Each wave iteration every lane evaluates ONE 6x6
+//               logdet: lane j of a sequence's group tries neighbour j of the
+//               current cut ratio (or, at the start of a line, lane 0 scores
+//               invCov_sum itself); the group then takes the first strict
+//               maximum (the reference's j-loop).  Groups advance independently
+//               through lines with a branch-free evaluation body, so a wave
+//               carries 8 chains at once;
+//  k_cut_finish (parallel) full 6x6 info of the chosen ratio (invCovPose) and
+//               the cut endpoints of every matched line.
+// Only the lower triangle is carried through the search: LLT reads nothing
+// else (ledger Q11).
 #include "gfpl_kernels.hpp"
 
 namespace gfpl {
@@ -21,8 +29,8 @@ struct LineCutData {
 };
 
 // projected residual variance of one cut endpoint (src/stereoFrameHandler.cpp:1356-1369)
-__device__ double endpointVar(const DevCam& cam, const double* DT_inv, const double* Jl, const double* Pt,
-                              const double* cov) {
+__device__ __forceinline__ double endpointVar(const DevCam& cam, const double* DT_inv, const double* Jl,
+                                              const double* Pt, const double* cov) {
     double Jdt[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -66,8 +74,8 @@ __device__ double endpointVar(const DevCam& cam, const double* DT_inv, const dou
 
 // getPoseInfoOnLine: FULL -> 36 entries row-major, else lower triangle (21)
 template <bool FULL>
-__device__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT_inv, const LineCutData& L,
-                               double c0, double c1, double* info) {
+__device__ __forceinline__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT_inv,
+                                               const LineCutData& L, double c0, double c1, double* info) {
     double sPt[3], ePt[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -113,7 +121,7 @@ __device__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT
     }
 }
 
-__device__ void load_line(const DevLines& L, size_t q, LineCutData& d) {
+__device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutData& d) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) { d.sP[k] = L.sP[3 * q + k]; d.eP[k] = L.eP[3 * q + k]; }
 #pragma unroll
@@ -122,13 +130,8 @@ __device__ void load_line(const DevLines& L, size_t q, LineCutData& d) {
     d.Jl[1] = L.le_obs[3 * q + 1];
 }
 
-__global__ void __launch_bounds__(64) k_line_cut(KParams p) {
-    __shared__ double DT_inv[16];
-    __shared__ double sum[24];
-    __shared__ double cm[8];
-    __shared__ int cv[8];
-    __shared__ double fin[36];
-    __shared__ double mback[1];
+// ------------------------------------------------------------------ prep --
+__global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -143,29 +146,24 @@ __global__ void __launch_bounds__(64) k_line_cut(KParams p) {
     const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
     double* scr_l = p.scr.cut_ls + (size_t)b * p.mls_cap * 21;
     double* scr_p = p.scr.cut_pt + (size_t)b * p.mpt_cap * 21;
-    if (lane == 0) {
-        // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635)
-        double Tc[16], Tp[16], Ti[16], D[16];
+    // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635), every lane
+    double Dl[16];
+    {
+        double Tc[16], Tp[16], Ti[16];
+#pragma unroll
         for (int i = 0; i < 16; ++i) { Tc[i] = p.curr.pose.Tfw[16 * b + i]; Tp[i] = p.prev.pose.Tfw[16 * b + i]; }
         mat4_inv(Tc, Ti);
-        mat4_mul(Ti, Tp, D);
-        for (int i = 0; i < 16; ++i) DT_inv[i] = D[i];
+        mat4_mul(Ti, Tp, Dl);
     }
-    __syncthreads();
-    double Dl[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) Dl[i] = DT_inv[i];
-    // ---- phase A
+    if (lane < 16) p.scr.cut_dtinv[16 * b + lane] = Dl[lane];
     for (int m = lane; m < nls; m += 64) {
         const size_t q = lb + mls[m];
         LineCutData d;
         load_line(L, q, d);
-        double info[36];
-        poseInfoOnLine<true>(cam, homog, Dl, d, 0.0, 0.0, info);
-        for (int i = 0; i < 36; ++i) L.invcov[36 * q + i] = info[i];
-        L.cut[2 * q] = 0.0; L.cut[2 * q + 1] = 0.0;
-        for (int i = 0; i < 6; ++i)
-            for (int j = 0; j <= i; ++j) scr_l[(size_t)m * 21 + tri(i, j)] = info[i * 6 + j];
+        double info[21];
+        poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];
     }
     for (int m = lane; m < npt; m += 64) {
         const size_t q = pbase + mpt[m];
@@ -176,108 +174,183 @@ __global__ void __launch_bounds__(64) k_line_cut(KParams p) {
         const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
         double J[6];
         poseJac(cam, homog, cur, dx, dy, J);
+#pragma unroll
         for (int i = 0; i < 6; ++i)
+#pragma unroll
             for (int j = 0; j <= i; ++j) scr_p[(size_t)m * 21 + tri(i, j)] = J[i] * J[j];
     }
     __syncthreads();
-    // ---- phase B: invCov_sum, sequential per element (lines then points)
+    // invCov_sum, sequential per element (lines then points)
     if (lane < 21) {
         double s = 0.0;
         for (int m = 0; m < nls; ++m) s = s + scr_l[(size_t)m * 21 + lane];
         for (int m = 0; m < npt; ++m) s = s + scr_p[(size_t)m * 21 + lane];
-        sum[lane] = s;
+        p.scr.cut_sum[24 * b + lane] = s;
     }
-    __syncthreads();
-    // ---- phase C
-    const double st = p.cfg.cut_step;
-    const double nb0[8] = {st, -st, 0, 0, st, st, -st, -st};
-    const double nb1[8] = {0, 0, st, -st, st, -st, st, -st};
-    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    for (int m = 0; m < nls; ++m) {
-        const size_t q = lb + mls[m];
-        LineCutData d;
-        load_line(L, q, d);
-        if (lane == 0) {
-            double a[21];
-            for (int i = 0; i < 21; ++i) a[i] = sum[i];
-            mback[0] = logdet6_lower(a);
-        }
-        __syncthreads();
-        if (lane < 21) sum[lane] = sum[lane] - scr_l[(size_t)m * 21 + lane];
-        __syncthreads();
-        double r0 = 0.0, r1 = 0.0;
-        double metric_back = mback[0];
-        while (r0 + r1 <= 1.0) {
-            if (lane < 8) {
-                const double t0 = r0 + nb0[lane], t1 = r1 + nb1[lane];
-                int valid = 1;
-                if (t0 + t1 > 1.0) valid = 0;
-                if (t0 < rlo || t0 > rhi) valid = 0;
-                if (t1 < rlo || t1 > rhi) valid = 0;
-                double mval = 0.0;
-                if (valid) {
-                    double tmp[21];
-                    poseInfoOnLine<false>(cam, homog, Dl, d, t0, t1, tmp);
+}
+
+// ---------------------------------------------------------------- search --
+#define CUT_G 8   // sequences per wave (8 lanes each)
+
+__global__ void __launch_bounds__(64) k_cut_search(KParams p) {
+    __shared__ double sum[CUT_G][24];
+    __shared__ double chosen[CUT_G][24];
+    __shared__ double cand[CUT_G][8][22];
+    __shared__ double val[CUT_G][8];
+    __shared__ int vld[CUT_G][8];
+    const int lane = threadIdx.x;
+    const int g = lane >> 3, j = lane & 7;
+    const int b = blockIdx.x * CUT_G + g;
+    const bool live = b < p.B;
+    const int nls = live ? p.tr.n_matched_ls[b] : 0;
+    const DevCam& cam = p.cam;
+    const double homog = p.cfg.homog_th;
+    DevLines& L = p.prev.ls;
+    const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
+    const double* scr_l = p.scr.cut_ls + (size_t)(live ? b : 0) * p.mls_cap * 21;
+    double Dl[16];
 #pragma unroll
-                    for (int i = 0; i < 21; ++i) tmp[i] = tmp[i] + sum[i];
-                    mval = logdet6_lower(tmp);
-                }
-                cm[lane] = mval;
-                cv[lane] = valid;
+    for (int i = 0; i < 16; ++i) Dl[i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
+    for (int e = j; e < 21; e += 8) sum[g][e] = (live && nls > 0) ? p.scr.cut_sum[24 * b + e] : 0.0;
+    const double st = p.cfg.cut_step;
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
+    const double nb0 = (j == 0 || j == 4 || j == 5) ? st : ((j == 1 || j == 6 || j == 7) ? -st : 0.0);
+    const double nb1 = (j == 2 || j == 4 || j == 6) ? st : ((j == 3 || j == 5 || j == 7) ? -st : 0.0);
+    // group state (identical in the 8 lanes of a group)
+    int m = 0;            // current line (list position)
+    int setup = 1;        // 1: score invCov_sum for line m; 0: greedy step
+    double r0 = 0.0, r1 = 0.0, mb = 0.0;
+    LineCutData d;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { d.sP[k] = 0.0; d.eP[k] = 1.0; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { d.covS[k] = 0.0; d.covE[k] = 0.0; }
+    d.Jl[0] = 0.0; d.Jl[1] = 0.0;
+    if (m < nls) load_line(L, lb + mls[m], d);
+    __syncthreads();
+    while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
+        const bool act = m < nls;
+        // ---- evaluation: one logdet per lane, branch-free over setup/step
+        const double t0 = r0 + nb0, t1 = r1 + nb1;
+        int valid = 1;
+        if (t0 + t1 > 1.0) valid = 0;
+        if (t0 < rlo || t0 > rhi) valid = 0;
+        if (t1 < rlo || t1 > rhi) valid = 0;
+        double tmp[21];
+        poseInfoOnLine<false>(cam, homog, Dl, d, t0, t1, tmp);
+        double tot[21];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = setup ? sum[g][i] : tmp[i] + sum[g][i];
+        const double v = logdet6_lower(tot);
+        if (act) {
+            val[g][j] = v;
+            vld[g][j] = setup ? (j == 0) : valid;
+            if (!setup) {
+#pragma unroll
+                for (int i = 0; i < 21; ++i) cand[g][j][i] = tmp[i];
             }
-            __syncthreads();
-            double mi = metric_back;
-            int best = -1;
-            for (int j = 0; j < 8; ++j)
-                if (cv[j] && cm[j] > mi) { mi = cm[j]; best = j; }
-            __syncthreads();
-            if (best < 0) break;
-            r0 = r0 + nb0[best];
-            r1 = r1 + nb1[best];
-            metric_back = mi;
         }
-        if (lane == 0) {
-            double info[36];
-            poseInfoOnLine<true>(cam, homog, Dl, d, r0, r1, info);
-            for (int i = 0; i < 36; ++i) { fin[i] = info[i]; L.invcov[36 * q + i] = info[i]; }
-            L.cut[2 * q] = r0; L.cut[2 * q + 1] = r1;
-            // updateEndPointByRatio (ledger Q4: eP uses the updated sP)
-            if (!(fabs(r0) < 0.0001 && fabs(r1) < 0.0001)) {
-                double sP[3] = {d.sP[0], d.sP[1], d.sP[2]}, eP[3] = {d.eP[0], d.eP[1], d.eP[2]};
-                if (fabs(r0) > 0.0001) {
-                    double s[3];
-                    for (int k = 0; k < 3; ++k) s[k] = (1 - r0) * sP[k] + r0 * eP[k];
-                    for (int k = 0; k < 3; ++k) { sP[k] = s[k]; L.sP[3 * q + k] = s[k]; }
-                    double uv[2];
-                    projection(cam, sP, uv);
-                    L.spl[2 * q] = uv[0]; L.spl[2 * q + 1] = uv[1];
-                    L.sdisp[q] = (cam.fx * cam.b) / sP[2];
+        __syncthreads();
+        // ---- group decision (all 8 lanes compute it identically)
+        int finalize = 0;
+        if (act) {
+            if (setup) {
+                mb = val[g][0];
+                // invCov_sum -= invCovPose(line m) (r = 0,0); chosen starts as that info
+                for (int e = j; e < 21; e += 8) {
+                    const double li = scr_l[(size_t)m * 21 + e];
+                    sum[g][e] = sum[g][e] - li;
+                    chosen[g][e] = li;
                 }
-                if (fabs(r1) > 0.0001) {
-                    double e[3];
-                    for (int k = 0; k < 3; ++k) e[k] = (1 - r1) * eP[k] + r1 * sP[k];
-                    for (int k = 0; k < 3; ++k) { eP[k] = e[k]; L.eP[3 * q + k] = e[k]; }
-                    double uv[2];
-                    projection(cam, eP, uv);
-                    L.epl[2 * q] = uv[0]; L.epl[2 * q + 1] = uv[1];
-                    L.edisp[q] = (cam.fx * cam.b) / eP[2];
+                setup = 0;
+                r0 = 0.0; r1 = 0.0;
+            } else {
+                double mi = mb;
+                int best = -1;
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj)
+                    if (vld[g][jj] && val[g][jj] > mi) { mi = val[g][jj]; best = jj; }
+                if (best >= 0) {
+                    const double bb0 = (best == 0 || best == 4 || best == 5) ? st : ((best == 1 || best == 6 || best == 7) ? -st : 0.0);
+                    const double bb1 = (best == 2 || best == 4 || best == 6) ? st : ((best == 3 || best == 5 || best == 7) ? -st : 0.0);
+                    r0 = r0 + bb0;
+                    r1 = r1 + bb1;
+                    mb = mi;
+                    for (int e = j; e < 21; e += 8) chosen[g][e] = cand[g][best][e];
+                    if (!(r0 + r1 <= 1.0)) finalize = 1;   // while-condition
+                } else {
+                    finalize = 1;
                 }
             }
         }
         __syncthreads();
-        if (lane < 21) {
-            // lower-triangle index -> (row, col)
-            int r = 0;
-            while ((r + 1) * (r + 2) / 2 <= lane) ++r;
-            const int c = lane - r * (r + 1) / 2;
-            sum[lane] = sum[lane] + fin[r * 6 + c];
+        if (act && finalize) {
+            // invCov_sum += invCovPose(final); record the cut ratio
+            for (int e = j; e < 21; e += 8) sum[g][e] = sum[g][e] + chosen[g][e];
+            if (j == 0) {
+                const size_t q = lb + mls[m];
+                L.cut[2 * q] = r0;
+                L.cut[2 * q + 1] = r1;
+            }
+            ++m;
+            setup = 1;
+            if (m < nls) load_line(L, lb + mls[m], d);
         }
         __syncthreads();
     }
 }
 
+// ---------------------------------------------------------------- finish --
+// invCovPose of the chosen ratio + updateEndPointByRatio (ledger Q4)
+__global__ void __launch_bounds__(64) k_cut_finish(KParams p) {
+    const int b = blockIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    if (nls == 0) return;
+    const DevCam& cam = p.cam;
+    DevLines& L = p.prev.ls;
+    const size_t lb = (size_t)b * p.kl_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
+    for (int m = threadIdx.x; m < nls; m += blockDim.x) {
+        const size_t q = lb + mls[m];
+        LineCutData d;
+        load_line(L, q, d);
+        const double r0 = L.cut[2 * q], r1 = L.cut[2 * q + 1];
+        double info[36];
+        poseInfoOnLine<true>(cam, p.cfg.homog_th, Dl, d, r0, r1, info);
+        for (int i = 0; i < 36; ++i) L.invcov[36 * q + i] = info[i];
+        if (!(fabs(r0) < 0.0001 && fabs(r1) < 0.0001)) {
+            double sP[3] = {d.sP[0], d.sP[1], d.sP[2]}, eP[3] = {d.eP[0], d.eP[1], d.eP[2]};
+            if (fabs(r0) > 0.0001) {
+                double s[3];
+                for (int k = 0; k < 3; ++k) s[k] = (1 - r0) * sP[k] + r0 * eP[k];
+                for (int k = 0; k < 3; ++k) { sP[k] = s[k]; L.sP[3 * q + k] = s[k]; }
+                double uv[2];
+                projection(cam, sP, uv);
+                L.spl[2 * q] = uv[0]; L.spl[2 * q + 1] = uv[1];
+                L.sdisp[q] = (cam.fx * cam.b) / sP[2];
+            }
+            if (fabs(r1) > 0.0001) {
+                double e[3];
+                for (int k = 0; k < 3; ++k) e[k] = (1 - r1) * eP[k] + r1 * sP[k];
+                for (int k = 0; k < 3; ++k) { eP[k] = e[k]; L.eP[3 * q + k] = e[k]; }
+                double uv[2];
+                projection(cam, eP, uv);
+                L.epl[2 * q] = uv[0]; L.epl[2 * q + 1] = uv[1];
+                L.edisp[q] = (cam.fx * cam.b) / eP[2];
+            }
+        }
+    }
+}
+
 hipError_t launch_line_cut(const KParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_line_cut, dim3(p.B), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(k_cut_search, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(k_cut_finish, dim3(p.B), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

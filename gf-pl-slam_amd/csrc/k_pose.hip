@@ -109,10 +109,12 @@ __device__ void gauss_newton(const KParams& p, int b, PoseLDS& S, double* feat, 
             const int f0 = list == 0 ? 0 : npt, f1 = list == 0 ? npt : npt + nls;
             double s = 0.0;
             int cnt = 0;
+#pragma unroll 4
             for (int f = f0; f < f1; ++f) {
-                if (!act[f]) continue;
-                s = s + term(feat + (size_t)f * 8, e, ti, tj);
-                ++cnt;
+                const double t = term(feat + (size_t)f * 8, e, ti, tj);
+                const bool a = act[f] != 0;
+                s = a ? s + t : s;
+                cnt += a ? 1 : 0;
             }
             S.part[tid] = s;
             if (e == 0) S.npart[list] = cnt;
@@ -207,8 +209,6 @@ __global__ void __launch_bounds__(256) k_pose(KParams p, int NP2, int featN) {
     __syncthreads();
     int ok = 0;        // 1: stage-2 DT usable
     double err = 0.0;  // err of the last GN run (reference: uninitialised when no GN runs, pinned 0)
-    double DT_cov[36];
-    for (int i = 0; i < 36; ++i) DT_cov[i] = 0.0;
     if (S.ninl > p.cfg.min_features) {
         gauss_newton(p, b, S, feat, act, npt, nls, p.cfg.max_iters);
         err = S.err;
@@ -276,69 +276,111 @@ __global__ void __launch_bounds__(256) k_pose(KParams p, int NP2, int featN) {
             }
         }
     }
-    if (tid != 0) return;
-    double DT[16];
+    if (tid == 0) {
+        for (int i = 0; i < 16; ++i) p.scr.pose_DT[16 * b + i] = S.DT[i];
+        for (int i = 0; i < 36; ++i) p.scr.pose_H[36 * b + i] = S.H[i];
+        p.scr.pose_err[b] = err;
+        p.scr.pose_ok[b] = ok;
+    }
+}
+
+// Final bookkeeping of optimizePose (src/stereoFrameHandler.cpp:1983-2028), one
+// lane per sequence: inverse_se3, motion-step gate, Tfw, DT_cov = H^-1 (Q13),
+// its eigenvalues, Tfw_cov = unccomp_se3, err_norm, numFrameLoss.
+__global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    DevPose& CP = p.curr.pose;
+    const DevPose& PP = p.prev.pose;
+    const int ok = p.scr.pose_ok[b];
+    const double err = p.scr.pose_err[b];
+    double DT[16], DT_cov[36];
     if (ok) {
-        for (int i = 0; i < 16; ++i) DT[i] = S.DT[i];
-        inverse6(S.H, DT_cov);   // Q13: last evaluated H
+        double H[36];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) DT[i] = p.scr.pose_DT[16 * b + i];
+#pragma unroll
+        for (int i = 0; i < 36; ++i) H[i] = p.scr.pose_H[36 * b + i];
+        inverse6(H, DT_cov);
     } else {
+#pragma unroll
         for (int i = 0; i < 16; ++i) DT[i] = (i % 5 == 0) ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < 36; ++i) DT_cov[i] = 0.0;
     }
     bool fin = true;
+#pragma unroll
     for (int i = 0; i < 16; ++i) { double d = DT[i] - DT[i]; if (!(d == d)) fin = false; }
     double Tp[16], Tpc[36];
+#pragma unroll
     for (int i = 0; i < 16; ++i) Tp[i] = PP.Tfw[16 * b + i];
+#pragma unroll
     for (int i = 0; i < 36; ++i) Tpc[i] = PP.Tfw_cov[36 * b + i];
     double cDT[16], Tfw[16], Tcov[36], eig[6];
     double err_norm;
-    const double dts = PP.time_stamp[b];
+    bool moved = false;
     if (fin) {
         inverse_se3(DT, cDT);
         const double tn = sqrt((cDT[3] * cDT[3] + cDT[7] * cDT[7]) + cDT[11] * cDT[11]);
-        if (tn < p.cfg.motion_step_th * (CP.time_stamp[b] - dts)) {
-            mat4_mul(Tp, cDT, Tfw);
-            // unccomp_se3(prev.Tfw, prev.Tfw_cov, DT_cov) (src/auxiliar.cpp:216-238)
-            double Ad[36], R[9], t[3] = {Tp[3], Tp[7], Tp[11]}, Sk[9], SR[9];
-            for (int i = 0; i < 36; ++i) Ad[i] = 0.0;
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) R[i * 3 + j] = Tp[i * 4 + j];
-            skew3(t, Sk);
-            mat3_mul(Sk, R, SR);
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) {
-                    Ad[i * 6 + j] = R[i * 3 + j];
-                    Ad[i * 6 + 3 + j] = SR[i * 3 + j];
-                    Ad[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
-                }
-            double AS[36];
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 6; ++j) {
-                    double s = Ad[i * 6 + 0] * DT_cov[0 * 6 + j];
-                    for (int k = 1; k < 6; ++k) s = s + Ad[i * 6 + k] * DT_cov[k * 6 + j];
-                    AS[i * 6 + j] = s;
-                }
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 6; ++j) {
-                    double s = AS[i * 6 + 0] * Ad[j * 6 + 0];
-                    for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * Ad[j * 6 + k];
-                    Tcov[i * 6 + j] = Tpc[i * 6 + j] + s;
-                }
-            err_norm = err;
-        } else {
-            for (int i = 0; i < 16; ++i) { cDT[i] = (i % 5 == 0) ? 1.0 : 0.0; Tfw[i] = Tp[i]; }
-            for (int i = 0; i < 36; ++i) Tcov[i] = Tpc[i];
-            err_norm = -1.0;
-        }
+        moved = tn < p.cfg.motion_step_th * (CP.time_stamp[b] - PP.time_stamp[b]);
         p.tr.num_frame_loss[b] = 0;
     } else {
-        for (int i = 0; i < 16; ++i) { cDT[i] = (i % 5 == 0) ? 1.0 : 0.0; Tfw[i] = Tp[i]; }
-        for (int i = 0; i < 36; ++i) Tcov[i] = Tpc[i];
-        err_norm = -1.0;
         p.tr.num_frame_loss[b] = p.tr.num_frame_loss[b] + 1;
     }
+    if (moved) {
+        mat4_mul(Tp, cDT, Tfw);
+        // unccomp_se3(prev.Tfw, prev.Tfw_cov, DT_cov) (src/auxiliar.cpp:216-238)
+        double Ad[36], R[9], t[3] = {Tp[3], Tp[7], Tp[11]}, Sk[9], SR[9];
+#pragma unroll
+        for (int i = 0; i < 36; ++i) Ad[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) R[i * 3 + j] = Tp[i * 4 + j];
+        skew3(t, Sk);
+        mat3_mul(Sk, R, SR);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                Ad[i * 6 + j] = R[i * 3 + j];
+                Ad[i * 6 + 3 + j] = SR[i * 3 + j];
+                Ad[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
+            }
+        double AS[36];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double s = Ad[i * 6 + 0] * DT_cov[0 * 6 + j];
+#pragma unroll
+                for (int k = 1; k < 6; ++k) s = s + Ad[i * 6 + k] * DT_cov[k * 6 + j];
+                AS[i * 6 + j] = s;
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double s = AS[i * 6 + 0] * Ad[j * 6 + 0];
+#pragma unroll
+                for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * Ad[j * 6 + k];
+                Tcov[i * 6 + j] = Tpc[i * 6 + j] + s;
+            }
+        err_norm = err;
+    } else {
+        // rejected step or non-finite pose: identity, prev pose kept, err_norm = -1
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { cDT[i] = (i % 5 == 0) ? 1.0 : 0.0; Tfw[i] = Tp[i]; }
+#pragma unroll
+        for (int i = 0; i < 36; ++i) Tcov[i] = Tpc[i];
+        err_norm = -1.0;
+    }
     eig_sym<6>(DT_cov, eig);
+#pragma unroll
     for (int i = 0; i < 16; ++i) { CP.DT[16 * b + i] = cDT[i]; CP.Tfw[16 * b + i] = Tfw[i]; }
+#pragma unroll
     for (int i = 0; i < 36; ++i) { CP.DT_cov[36 * b + i] = DT_cov[i]; CP.Tfw_cov[36 * b + i] = Tcov[i]; }
+#pragma unroll
     for (int i = 0; i < 6; ++i) CP.DT_cov_eig[6 * b + i] = eig[i];
     CP.err_norm[b] = err_norm;
 }
@@ -350,6 +392,7 @@ hipError_t launch_pose(const KParams& p, hipStream_t s) {
     if (feat < (size_t)3 * NP2) feat = (size_t)3 * NP2;
     const size_t lds = feat * 8 + (size_t)(p.mpt_cap + p.mls_cap) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(256), lds, s, p, NP2, (int)feat);
+    hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 
