@@ -99,6 +99,33 @@ def cpu_baseline(cam, cfg, sp, n_threads, n_seqs, n_frames, kp_cap, kl_cap):
                       f"({dt:.1f} s wall, {os.cpu_count()} CPUs visible)"}
 
 
+def shard_first_seq(rank: int, batch: int) -> int:
+    """Sequences are partitioned across ranks: rank r owns [r*B, (r+1)*B)."""
+    return rank * batch
+
+
+def broadcast_setup(cam, cfg, dist, device):
+    """Broadcast rank 0's camera + config block to every rank (RCCL over xGMI
+    with the nccl backend; gloo on CPU in the tests) and load it in place."""
+    blob = bytes(cam) + bytes(cfg)
+    import torch
+    t = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
+    dist.broadcast(t, src=0)
+    raw = t.cpu().numpy().tobytes()
+    C.memmove(C.addressof(cam), raw[: C.sizeof(cam)], C.sizeof(cam))
+    C.memmove(C.addressof(cfg), raw[C.sizeof(cam):], C.sizeof(cfg))
+
+
+def reduce_job(elapsed: float, frames: int, dist, device):
+    """MAX over ranks of the timed region, SUM of processed frames."""
+    import torch
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    cnt = torch.tensor([frames], dtype=torch.int64, device=device)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    dist.all_reduce(cnt)
+    return float(el.item()), int(cnt.item())
+
+
 def load_pmc(path, kernel_name):
     try:
         with open(path) as f:
@@ -130,19 +157,14 @@ def main():
     if world > 1:
         # RCCL broadcast of the camera + config block; every rank
         # then runs with rank 0's bytes.
-        blob = bytes(cam) + bytes(cfg)
-        t = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
-        dist.broadcast(t, src=0)
-        raw = t.cpu().numpy().tobytes()
-        C.memmove(C.addressof(cam), raw[: C.sizeof(cam)], C.sizeof(cam))
-        C.memmove(C.addressof(cfg), raw[C.sizeof(cam):], C.sizeof(cfg))
+        broadcast_setup(cam, cfg, dist, dev)
 
     B, W, K = args.batch, args.warmup, args.steps
     KP, KL = 2048, 512
     sp = gfpl.synth_params(**synth_over)
     F = 1 + W + K
     t0 = time.perf_counter()
-    H = gfpl.HostFrames(cam, sp, B, F, KP, KL, seq0=rank * B, threads=16)
+    H = gfpl.HostFrames(cam, sp, B, F, KP, KL, seq0=shard_first_seq(rank, B), threads=16)
     t_gen = time.perf_counter() - t0
     D = gfpl.DeviceFrames(H, dev)
     in_bytes = D.nbytes()
@@ -168,15 +190,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        cnt = torch.tensor([B * K], dtype=torch.int64, device=dev)
-        dist.all_reduce(cnt)   # frame counter all-reduce
-        frames_total = int(cnt.item())
+        t_max, frames_total = reduce_job(elapsed, B * K, dist, dev)
     else:
-        frames_total = B * K
-    t_max = float(el.item())
+        t_max, frames_total = elapsed, B * K
     # tracking health: fraction of sequences still tracked
     lost = sum(h.read_track(b)["num_frame_loss"] > 0 for b in range(0, B, max(1, B // 16)))
 

@@ -85,3 +85,15 @@ def compare_pose(g, o, rtol=1e-6, atol=1e-12, what=""):
     if g.s.err_norm != o.s.err_norm:
         exact = False
     return bad, exact
+
+
+def make_ragged(H):
+    """Edge cases the reference guards (or would hit UB on): empty and tiny
+    detection sets.  Needs >= 5 sequences and >= 3 frames."""
+    assert H.B >= 5 and H.F >= 3
+    H.n_kp_l[2, 1] = 0                       # no left keypoints -> no stereo points
+    H.n_kl_r[1, 2] = 1                       # one right line (ledger U4) -> no stereo lines
+    H.n_kp_l[2, 3] = 0; H.n_kp_r[2, 3] = 0   # nothing at all -> pose skipped
+    H.n_kl_l[2, 3] = 0
+    H.n_kp_l[1, 4] = 30; H.n_kl_l[1, 4] = 3  # tiny sets
+    return H
