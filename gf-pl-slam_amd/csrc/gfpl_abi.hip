@@ -94,6 +94,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
     sb->scr.cut_pt = c.take<double>(B * sb->mpt_cap * 21);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
+    sb->scr.proj = reinterpret_cast<double*>(sb->scr.knn);
     sb->scr.bytes = c.take<int64_t>(B * 8);
     sb->scr.n_subpix = c.take<int32_t>(B);
     sb->scr.cut_sum = c.take<double>(B * 24);
@@ -217,7 +218,7 @@ int gfpl_synchronize(gfpl_ctx* c) {
 }
 
 int gfpl_seqbatch_create(gfpl_ctx* c, int batch, int kp_cap, int kl_cap, gfpl_seqbatch** out) {
-    if (!c || !out || batch < 1 || kp_cap < 2 || kl_cap < 2 || kp_cap > 16384 || kl_cap > 1536 || !c->has_cam)
+    if (!c || !out || batch < 1 || kp_cap < 2 || kl_cap < 2 || kp_cap > 8192 || kl_cap > 2048 || !c->has_cam)
         return GFPL_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
     gfpl_seqbatch* sb = new gfpl_seqbatch();

@@ -17,16 +17,40 @@
 
 namespace gfpl {
 
-// dynamic LDS: projx[cap] projy[cap] f64 | lastT[cap] i32 | Tinv[16] f64 | misc[64] i32
-__global__ void __launch_bounds__(1024) k_cross_points(KParams p) {
+// Exact spatial grid over the predicted projections of the previous points.
+// Cells are CS px squares (CS a power of two >= gate+0.5, so x*inv_cs is exact);
+// indices are clamped into the grid, which never separates two values whose
+// cells differ by <= 1, so the 3x3 neighbourhood of a current point's cell is a
+// superset of every q with |dx|,|dy| <= gate+0.5.  NaN projections (z = 0 or a
+// NaN P) pass the reference's `norm() > 10` test, so they sit in a "wild"
+// bucket every current point visits.  The visit order is irrelevant: the pick
+// is the lexicographic minimum (dist, q), exactly the multimap resolution.
+struct CrossGrid {
+    int gx, gy, ncell;   // ncell = gx*gy; bucket ncell = wild
+    double inv_cs;
+};
+
+__device__ __forceinline__ int grid_axis(double v, double inv_cs, int n) {
+    double c = floor(v * inv_cs);
+    c = c < 0.0 ? 0.0 : (c > (double)(n - 1) ? (double)(n - 1) : c);
+    return (int)c;
+}
+
+// dynamic LDS: cnt[ncell+2] start[ncell+2] i32 | sq[cap] i32 | spx[cap] spy[cap] f32 |
+//              lastT[cap] i32 | prevT[16] Tinv[16] f64 | misc[64] i32
+__global__ void __launch_bounds__(1024) k_cross_points(KParams p, CrossGrid G) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;
-    double* projx = (double*)smem;
-    double* projy = projx + cap;
-    double* Tinv = projy + cap;
-    double* prevT = Tinv + 16;
-    int* lastT = (int*)(prevT + 16);
+    const int NB = G.ncell + 1;   // buckets incl. wild
+    double* prevT = (double*)smem;
+    double* Tinv = prevT + 16;
+    int* cnt = (int*)(Tinv + 16);
+    int* start = cnt + NB + 1;
+    int* sq = start + NB + 1;
+    float* spx = (float*)(sq + cap);
+    float* spy = spx + cap;
+    int* lastT = (int*)(spy + cap);
     int* misc = lastT + cap;
     const int tid = threadIdx.x;
     const int Sp = p.prev.pt.n[b], Sc = p.curr.pt.n[b];
@@ -38,25 +62,58 @@ __global__ void __launch_bounds__(1024) k_cross_points(KParams p) {
         for (int i = 0; i < 16; ++i) { p.curr.pose.Tfw[16 * b + i] = T[i]; prevT[i] = A[i]; }
         mat4_inv(T, Tinv);
     }
+    for (int i = tid; i < NB; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     int total = 0;
     if (Sp > 0 && Sc > 0) {
         const DevPoints& P = p.prev.pt;
         const DevPoints& Cc = p.curr.pt;
         const size_t pb = (size_t)b * cap;
+        double* proj = p.scr.proj + pb * 2;   // exact projections (L2-resident)
+        // 1. projectPrev3DPoint (src/stereoFrame.cpp:1550-1570) + bucket histogram
         for (int q = tid; q < Sp; q += blockDim.x) {
             double v[4] = {P.P[3 * (pb + q)], P.P[3 * (pb + q) + 1], P.P[3 * (pb + q) + 2], 1.0};
             mat4_vec(prevT, v, v);
             mat4_vec(Tinv, v, v);
             double uv[2];
             projection(p.cam, v, uv);
-            projx[q] = uv[0];
-            projy[q] = uv[1];
+            proj[2 * q] = uv[0];
+            proj[2 * q + 1] = uv[1];
+            int cell = G.ncell;
+            if (uv[0] == uv[0] && uv[1] == uv[1])
+                cell = grid_axis(uv[1], G.inv_cs, G.gy) * G.gx + grid_axis(uv[0], G.inv_cs, G.gx);
+            lastT[q] = cell;
+            atomicAdd(&cnt[cell], 1);
+        }
+        __syncthreads();
+        // 2. bucket offsets (exclusive scan over NB counts, chunked by the block)
+        int base = 0;
+        for (int c0 = 0; c0 < NB; c0 += blockDim.x) {
+            const int i = c0 + tid;
+            const int v = i < NB ? cnt[i] : 0;
+            int tot;
+            const int r = base + block_exclusive_scan<1024>(v, misc, &tot);
+            if (i < NB) start[i] = r;
+            base += tot;
+        }
+        if (tid == 0) start[NB] = base;
+        __syncthreads();
+        for (int i = tid; i < NB; i += blockDim.x) cnt[i] = 0;
+        __syncthreads();
+        // 3. scatter (order inside a bucket is irrelevant, see above)
+        for (int q = tid; q < Sp; q += blockDim.x) {
+            const int cell = lastT[q];
+            const int pos = start[cell] + atomicAdd(&cnt[cell], 1);
+            sq[pos] = q;
+            spx[pos] = (float)proj[2 * q];
+            spy[pos] = (float)proj[2 * q + 1];
             lastT[q] = -1;
         }
         __syncthreads();
         const double gate = p.cfg.proj_gate_px;
-        const double pre = gate + 0.5;   // exact pre-filter: |dx| > gate+0.5 implies norm > gate
+        // float pre-filter margin: for |pl| < 1e6 and |proj - pl| <= gate+0.5 the float
+        // difference is within 0.2 of the exact one, so gate+1.5 rejects no true candidate.
+        const float fpre = (float)(gate + 1.5);
         const float radius = (float)p.cfg.point_match_radius;
         const int cap_m = p.cfg.max_point_match_num;
         const uint8_t* PD = P.desc + pb * 32;
@@ -69,14 +126,29 @@ __global__ void __launch_bounds__(1024) k_cross_points(KParams p) {
                 uint32_t dt[8];
                 load_desc(Cc.desc + (pb + t) * 32, dt);
                 int bestd = 0x7FFFFFFF;
-                for (int q = 0; q < Sp; ++q) {
-                    const double dx = projx[q] - plx, dy = projy[q] - ply;
-                    if (fabs(dx) > pre || fabs(dy) > pre) continue;
-                    if (sqrt(dx * dx + dy * dy) > gate) continue;
+                auto consider = [&](int q) {
+                    const double dx = proj[2 * q] - plx, dy = proj[2 * q + 1] - ply;
+                    if (sqrt(dx * dx + dy * dy) > gate) return;   // :536 (NaN passes, as in the reference)
                     uint32_t dq[8];
                     load_desc(PD + (size_t)q * 32, dq);
                     const int d = hamming8<1>(dq, dt);
-                    if ((float)d <= radius && d < bestd) { bestd = d; bestq = q; }
+                    if ((float)d <= radius && (d < bestd || (d == bestd && q < bestq))) { bestd = d; bestq = q; }
+                };
+                const bool normal = fabs(plx) < 1e6 && fabs(ply) < 1e6;   // false for NaN too
+                if (normal) {
+                    const float fx = (float)plx, fy = (float)ply;
+                    const int cx = grid_axis(plx, G.inv_cs, G.gx), cy = grid_axis(ply, G.inv_cs, G.gy);
+                    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, G.gx - 1);
+                    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, G.gy - 1); ++yy) {
+                        const int k1 = start[yy * G.gx + x1 + 1];
+                        for (int k = start[yy * G.gx + x0]; k < k1; ++k) {
+                            if (fabsf(spx[k] - fx) > fpre || fabsf(spy[k] - fy) > fpre) continue;
+                            consider(sq[k]);
+                        }
+                    }
+                    for (int k = start[G.ncell]; k < start[NB]; ++k) consider(sq[k]);   // wild bucket
+                } else {
+                    for (int q = 0; q < Sp; ++q) consider(q);   // exact slow path (NaN / huge pl)
                 }
             }
             const int has = bestq >= 0 ? 1 : 0;
@@ -104,6 +176,7 @@ __global__ void __launch_bounds__(1024) k_cross_points(KParams p) {
     if (tid == 0) {
         p.tr.n_matched_pt[b] = total;
         p.tr.n_inliers_pt[b] = total;
+        p.tr.n_inliers[b] = total + p.tr.n_matched_ls[b];   // counts = list sizes (:700-702)
     }
 }
 
@@ -126,14 +199,14 @@ __device__ int hist_rank_c(const int* h, int r) {
     return 256;
 }
 
-// dynamic LDS: dp[cap*8] dc[cap*8] u32 | i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
+// dynamic LDS: tb[cap*8] u32 (train rows: curr for 12, then prev for 21) |
+//              i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
 __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
-    uint32_t* dp = (uint32_t*)smem;
-    uint32_t* dc = dp + cap * 8;
-    int* i12 = (int*)(dc + cap * 8);
+    uint32_t* tb = (uint32_t*)smem;
+    int* i12 = (int*)(tb + cap * 8);
     int* d012 = i12 + cap;
     int* d112 = d012 + cap;
     int* i21 = d112 + cap;
@@ -147,20 +220,28 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
         DevLines& P = p.prev.ls;
         DevLines& Cc = p.curr.ls;
         const size_t pb = (size_t)b * cap;
-        for (int i = tid; i < Sl * 2; i += blockDim.x) reinterpret_cast<uint4*>(dp)[i] = reinterpret_cast<const uint4*>(P.desc + pb * 32)[i];
-        for (int i = tid; i < Sc * 2; i += blockDim.x) reinterpret_cast<uint4*>(dc)[i] = reinterpret_cast<const uint4*>(Cc.desc + pb * 32)[i];
+        const uint8_t* DP = P.desc + pb * 32;
+        const uint8_t* DC = Cc.desc + pb * 32;
+        for (int i = tid; i < Sc * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DC)[i];
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
         __syncthreads();
         for (int i = tid; i < Sl; i += blockDim.x) {
+            uint32_t qd[8];
+            load_desc(DP + (size_t)i * 32, qd);
             int a, d0, d1;
-            knn2_lds<1>(dp + 8 * i, dc, Sc, a, d0, d1);
+            knn2_lds<1>(qd, tb, Sc, a, d0, d1);
             i12[i] = a; d012[i] = d0; d112[i] = d1;
             atomicAdd(&h12[d1 - d0], 1);
             atomicAdd(&h0[d0], 1);
         }
+        __syncthreads();
+        for (int i = tid; i < Sl * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DP)[i];
+        __syncthreads();
         for (int j = tid; j < Sc; j += blockDim.x) {
+            uint32_t qd[8];
+            load_desc(DC + (size_t)j * 32, qd);
             int a, d0, d1;
-            knn2_lds<1>(dc + 8 * j, dp, Sl, a, d0, d1);
+            knn2_lds<1>(qd, tb, Sl, a, d0, d1);
             i21[j] = a;
         }
         __syncthreads();
@@ -210,14 +291,33 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
     }
 }
 
+CrossGrid cross_grid(const KParams& p) {
+    const double pre = p.cfg.proj_gate_px + 0.5;
+    int cs = 16;
+    CrossGrid G;
+    for (;;) {
+        G.gx = (p.cam.width + cs - 1) / cs;
+        G.gy = (p.cam.height + cs - 1) / cs;
+        if ((double)cs >= pre && G.gx * G.gy <= 2048) break;
+        cs *= 2;
+    }
+    G.ncell = G.gx * G.gy;
+    G.inv_cs = 1.0 / cs;
+    return G;
+}
+
+size_t cross_points_lds(const KParams& p, const CrossGrid& G) {
+    return 32 * 8 + (size_t)(G.ncell + 2) * 8 + (size_t)p.kp_cap * 16 + 64 * 4;
+}
+
 hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
-    const size_t lds = (size_t)p.kp_cap * 16 + 32 * 8 + (size_t)p.kp_cap * 4 + 64 * 4;
-    hipLaunchKernelGGL(k_cross_points, dim3(p.B), dim3(1024), lds, s, p);
+    const CrossGrid G = cross_grid(p);
+    hipLaunchKernelGGL(k_cross_points, dim3(p.B), dim3(1024), cross_points_lds(p, G), s, p, G);
     return hipGetLastError();
 }
 
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s) {
-    const size_t lds = (size_t)p.kl_cap * 64 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4;
+    const size_t lds = (size_t)p.kl_cap * 32 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4;
     hipLaunchKernelGGL(k_cross_lines, dim3(p.B), dim3(512), lds, s, p);
     return hipGetLastError();
 }

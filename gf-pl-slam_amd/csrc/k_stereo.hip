@@ -344,15 +344,17 @@ __device__ int hist_rank(const int* h, int r) {
     return 256;
 }
 
-// dynamic LDS: dl[cap*8] | dr[cap*8] u32 | lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
+// dynamic LDS: tb[cap*8] u32 (train rows: R for L->R, then L for R->L) |
+//              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
+// Query rows stream from HBM into registers; only the train set sits in LDS, so
+// 2000 lines per side (config 5) fit.
 template <int CELL, bool INITIAL>
 __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
-    uint32_t* dl = (uint32_t*)smem;
-    uint32_t* dr = dl + cap * 8;
-    int* lr_i = (int*)(dr + cap * 8);
+    uint32_t* tb = (uint32_t*)smem;
+    int* lr_i = (int*)(tb + cap * 8);
     int* lr_d0 = lr_i + cap;
     int* lr_d1 = lr_d0 + cap;
     int* rl_i = lr_d1 + cap;
@@ -367,19 +369,25 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     }
     const uint8_t* DLg = p.in.ldesc_l + (size_t)b * cap * 32;
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
-    for (int i = tid; i < NL * 2; i += blockDim.x) reinterpret_cast<uint4*>(dl)[i] = reinterpret_cast<const uint4*>(DLg)[i];
-    for (int i = tid; i < NR * 2; i += blockDim.x) reinterpret_cast<uint4*>(dr)[i] = reinterpret_cast<const uint4*>(DRg)[i];
+    for (int i = tid; i < NR * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DRg)[i];
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     for (int i = tid; i < NL; i += blockDim.x) {
+        uint32_t qd[8];
+        load_desc(DLg + (size_t)i * 32, qd);
         int i0, d0, d1;
-        knn2_row<CELL>(dl + 8 * i, dr, NR, i0, d0, d1);
+        knn2_row<CELL>(qd, tb, NR, i0, d0, d1);
         lr_i[i] = i0; lr_d0[i] = d0; lr_d1[i] = d1;
         atomicAdd(&hist[d1 - d0], 1);   // lineDescriptorMAD deviations |d1-d0| (U1 pin)
     }
+    __syncthreads();
+    for (int i = tid; i < NL * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DLg)[i];
+    __syncthreads();
     for (int j = tid; j < NR; j += blockDim.x) {
+        uint32_t qd[8];
+        load_desc(DRg + (size_t)j * 32, qd);
         int i0, d0, d1;
-        knn2_row<CELL>(dr + 8 * j, dl, NL, i0, d0, d1);
+        knn2_row<CELL>(qd, tb, NL, i0, d0, d1);
         rl_i[j] = i0;
     }
     __syncthreads();
@@ -579,7 +587,7 @@ hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
-size_t stereo_lines_lds(int cap) { return (size_t)cap * 64 + (size_t)cap * 16 + 260 * 4 + 64 * 4; }
+size_t stereo_lines_lds(int cap) { return (size_t)cap * 32 + (size_t)cap * 16 + 260 * 4 + 64 * 4; }
 
 hipError_t launch_stereo_lines(const KParams& p, hipStream_t s) {
     hipLaunchKernelGGL((k_stereo_lines<2, false>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);

@@ -216,7 +216,9 @@ int  gfpl_get_camera(const gfpl_ctx* ctx, gfpl_camera* cam);
 int  gfpl_get_config(const gfpl_ctx* ctx, gfpl_config* cfg);
 int  gfpl_synchronize(gfpl_ctx* ctx);
 
-/* B independent sequences (B StereoFrameHandler objects) resident in HBM.  */
+/* B independent sequences (B StereoFrameHandler objects) resident in HBM.
+ * kp_cap <= 8192 keypoints and kl_cap <= 2048 keylines per side (config 5:
+ * 8000 ORB + 2000 LBD); larger values return GFPL_E_INVALID.               */
 int  gfpl_seqbatch_create(gfpl_ctx* ctx, int batch, int kp_cap, int kl_cap, gfpl_seqbatch** out);
 int  gfpl_seqbatch_destroy(gfpl_seqbatch* sb);
 /* bytes of device memory held by the seqbatch (state + workspace) */

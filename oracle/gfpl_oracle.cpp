@@ -629,6 +629,7 @@ struct Frame {
     std::vector<Desc> pdesc, ldesc;
     // injected detections (views into the caller's host batch)
     const gfpl_frames* in = nullptr;
+    gfpl_frames in_store{};   // begin_frame keeps a copy: the caller's struct may be a temporary
     int seq = 0;
     Frame() {
         for (int i = 0; i < 16; ++i) Tfw[i] = DT[i] = (i % 5 == 0) ? 1.0 : 0.0;
@@ -1597,7 +1598,8 @@ int gfplo_begin_frame(gfplo_handler* h, const gfpl_frames* in, int seq) {
     if (!h->prev) return GFPL_E_STATE;
     delete h->curr;
     h->curr = new Frame();
-    h->curr->in = in; h->curr->seq = seq;
+    h->curr->in_store = *in;
+    h->curr->in = &h->curr->in_store; h->curr->seq = seq;
     h->curr->time_stamp = in->time_stamp[seq];
     return 0;
 }

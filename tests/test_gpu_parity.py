@@ -191,3 +191,54 @@ def test_pose_only_noise_free_parity():
         bad, exact = compare_pose(g.read_frame(gfpl.CURR, 0), o.read_frame(gfpl.CURR))
         assert not bad and exact, bad
         assert compare_track(g.read_track(0), o.read_track()) == []
+
+
+def test_stress_config_parity():
+    """BASELINE configs[4]: 1920x1080 stereo, 8000 ORB + 2000 LBD per side, line cut on."""
+    rep = _run_sequence("stress", {}, n_seq=1, n_frames=3, kp_cap=8192, kl_cap=2048,
+                        synth_over=dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=2800,
+                                        z_max=12.0), seed=19)
+    _check(rep)
+    assert rep["counts"][0][0] > 3000 and rep["counts"][0][1] > 500, rep["counts"]
+
+
+def test_cross_points_nan_and_far_projections():
+    """Cross-frame point matching on hostile state (written through gfpl_write_frame):
+    NaN / infinite / far projections of previous points and NaN / far current
+    observations.  The reference's `norm() > 10` gate lets NaN through
+    (src/stereoFrameHandler.cpp:536); the GPU grid must keep exactly that."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    KP, KL = 2048, 512
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=23), 1, 3, KP, KL)
+    o = O.OracleHandler(cam, cfg, KP, KL)
+    o.initialize(H.frames(0), 0)
+    o.insertStereoPair(H.frames(1), 0)
+    o.optimizePose()
+    o.updateFrame()
+    o.begin_frame(H.frames(2), 0)
+    o.stereoPoints(); o.stereoLines(); o.estimateStereoUncertainty()
+    prev, curr = o.read_frame(gfpl.PREV), o.read_frame(gfpl.CURR)
+    P = prev.get("pt_P")
+    pl = curr.get("pt_pl")
+    assert len(P) > 40 and len(pl) > 40
+    P[5] = np.nan                     # NaN projection -> passes the gate in the reference
+    P[7] = (0.0, 0.0, 0.0)            # 0/0 -> NaN
+    P[9] = (1e12, 0.0, 1.0)           # far off-image
+    P[11] = (np.inf, 0.0, 1.0)
+    P[13] = (-3.0, 1.0, -2.0)         # behind the camera, finite projection
+    pl[3] = np.nan                    # NaN observation -> every prev point passes the gate
+    pl[4] = (1e7, 1e7)
+    pl[6] = (-1e9, 5.0)
+    ctx = gfpl.Context(cam, cfg)
+    g = gfpl.StereoFrameHandler(ctx, 1, KP, KL)
+    for w, f in ((gfpl.PREV, prev), (gfpl.CURR, curr)):
+        o.write_frame(w, f)
+        g.write_frame(w, 0, f)
+    g.crossFrameMatchingPoints(); o.crossFrameMatchingPoints()
+    tg, to = g.read_track(0), o.read_track()
+    bad = compare_track(tg, to, "cross ")
+    bad += compare_prev_matched(g.read_frame(gfpl.PREV, 0), o.read_frame(gfpl.PREV), to, "cross ")
+    bad += compare_core(g.read_frame(gfpl.CURR, 0), o.read_frame(gfpl.CURR), "cross curr ")
+    assert not bad, "\n".join(bad[:30])
+    assert len(to["matched_pt"]) > 100
