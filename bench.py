@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seqs", type=int, default=16)
     ap.add_argument("--cpu-frames", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--input-mem-frac", type=float, default=0.6,
+                    help="max fraction of free HBM used by the staged input frames")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_summary.py (optional)")
     return ap.parse_args()
@@ -163,12 +165,18 @@ def main():
     KP, KL = 2048, 512
     sp = gfpl.synth_params(**synth_over)
     F = 1 + W + K
+    # all F input frames of the B sequences are staged in HBM before timing; bound
+    # them to a fraction of device memory (inputs resident)
+    free, total = torch.cuda.mem_get_info(dev)
+    per_seq_frame = gfpl.input_bytes_per_frame(cam, KP, KL)
+    b_fit = int(args.input_mem_frac * free // (per_seq_frame * F)) // 64 * 64
+    if b_fit < B:
+        print(f"note: --batch {B} x {F} frames does not fit; using {b_fit} sequences", file=sys.stderr)
+        B = max(64, b_fit)
     t0 = time.perf_counter()
-    H = gfpl.HostFrames(cam, sp, B, F, KP, KL, seq0=shard_first_seq(rank, B), threads=16)
+    D = gfpl.DeviceFrames.generate(cam, sp, B, F, KP, KL, seq0=shard_first_seq(rank, B), device=dev, threads=16)
     t_gen = time.perf_counter() - t0
-    D = gfpl.DeviceFrames(H, dev)
     in_bytes = D.nbytes()
-    del H
     stream = torch.cuda.current_stream(dev).cuda_stream
     ctx = gfpl.Context(cam, cfg, device=local, stream=stream)
     h = gfpl.StereoFrameHandler(ctx, B, KP, KL)

@@ -103,6 +103,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_H = c.take<double>(B * 36);
     sb->scr.pose_err = c.take<double>(B);
     sb->scr.pose_ok = c.take<int32_t>(B);
+    sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
 }
 
 DevCam devcam(const gfpl_camera& c) {

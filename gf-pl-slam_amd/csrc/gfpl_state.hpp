@@ -77,6 +77,7 @@ struct DevScratch {
     double* pose_H;    // [B*36] last evaluated H
     double* pose_err;  // [B]
     int32_t* pose_ok;  // [B] 1: stage-2 result usable
+    double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

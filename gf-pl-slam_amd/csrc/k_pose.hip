@@ -3,13 +3,18 @@
 // optimizeFunctions (:2118-2245), removeOutliers (:2058-2116) and
 // vector_stdv_mad (src/auxiliar.cpp:521-537).
 //
-// One 256-thread workgroup owns one sequence for the whole two-stage solve:
-//  * every GN iteration all threads evaluate the per-feature Jacobian rows
-//    (J[6], |e|, Cauchy weight) of the matched list into LDS;
-//  * 56 threads then form the 6x6 J^T W J reduction (21 unique H entries + 6 g
-//    + 1 e, separately for points and lines), each summing one entry over the
-//    list in list order — the reference's accumulation order, so H is bit-identical;
-//  * thread 0 solves the 6x6 LDLT, applies the SE(3) update and tests convergence.
+// One 64-lane wave owns one sequence for the whole two-stage solve:
+//  * the matched list's inputs (P, pl_obs, sigma2 / sP, eP, le_obs, sigma2) are
+//    gathered once into a per-sequence SoA scratch (coalesced re-reads, L2/MALL
+//    resident) — lane l owns list positions l, l+64, ... for gather, evaluation
+//    and residuals, so it only ever reads back its own stores;
+//  * every GN iteration walks the lists in chunks of 64: each lane evaluates one
+//    point and one line (J[6], |e|, Cauchy weight; inactive or past-the-end
+//    entries are zero rows) into LDS, then lanes 0-27 (points) and 28-55 (lines)
+//    each add one of the 28 reduction entries (21 H + 6 g + 1 e) over the chunk
+//    in list order — the reference's accumulation order, so H is bit-identical
+//    (a zero row adds +0.0, which leaves a sum that started at +0.0 unchanged);
+//  * lane 0 solves the 6x6 LDLT, applies the SE(3) update and tests convergence.
 // The outlier pass sorts residuals in LDS (bitonic) for the MAD medians.
 #include "gfpl_kernels.hpp"
 
@@ -19,108 +24,117 @@ struct PoseLDS {
     double DT[16];
     double DTini[16];
     double H[36];
-    double part[56];
-    int npart[2];
+    double part[64];
     int brk;
     int ninl;
+    int cnt[2];
     double err;
 };
 
-// feature rows: feat[f*8 + 0..5] = J, [6] = |e|, [7] = w;  act[f] = inlier
-__device__ void eval_features(const KParams& p, int b, const double* DT, double* feat, uint8_t* act, int npt,
-                              int nls) {
+#define PT_K 6    // X Y Z ox oy sigma2
+#define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
+
+// evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w
+__device__ __forceinline__ void eval_point(const DevCam& cam, double homog, const double* DT, const double* in,
+                                           size_t stride, double* o) {
+    const double Pp[3] = {in[0], in[stride], in[2 * stride]};
+    double Pc[3], uv[2];
+    se3_apply(DT, Pp, Pc);
+    projection(cam, Pc, uv);
+    const double ex = uv[0] - in[3 * stride], ey = uv[1] - in[4 * stride];
+    const double n = sqrt(ex * ex + ey * ey);
+    double J[6];
+    poseJac(cam, homog, Pc, ex, ey, J);
+    const double m = ref_max(homog, n);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] = J[i] / m;
+    o[6] = n;
+    o[7] = 1.0 / (1.0 + (n * n) * in[5 * stride]);
+}
+
+// evaluate one line row (src/stereoFrameHandler.cpp:2175-2235)
+__device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const double* DT, const double* in,
+                                          size_t stride, double* o) {
+    const double sP[3] = {in[0], in[stride], in[2 * stride]};
+    const double eP[3] = {in[3 * stride], in[4 * stride], in[5 * stride]};
+    double sc[3], ec[3], su[2], eu[2];
+    se3_apply(DT, sP, sc);
+    projection(cam, sc, su);
+    se3_apply(DT, eP, ec);
+    projection(cam, ec, eu);
+    const double l0 = in[6 * stride], l1 = in[7 * stride], l2 = in[8 * stride];
+    const double ds = (l0 * su[0] + l1 * su[1]) + l2;
+    const double de = (l0 * eu[0] + l1 * eu[1]) + l2;
+    const double n = sqrt(ds * ds + de * de);
+    double Js[6], Je[6];
+    poseJac(cam, homog, sc, l0, l1, Js);
+    poseJac(cam, homog, ec, l0, l1, Je);
+    const double m = ref_max(homog, n);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] = (Js[i] * ds + Je[i] * de) / m;
+    o[6] = n;
+    o[7] = 1.0 / (1.0 + (n * n) * in[9 * stride]);
+}
+
+struct PoseCtx {
+    const double* pin;   // [PT_K][mpt_cap] of this sequence
+    const double* lin;   // [LS_K][mls_cap]
+    size_t mpt_cap, mls_cap;
+    const uint8_t* act;  // LDS [npt + nls] list-position inlier flags
+    int npt, nls;
+};
+
+// gaussNewtonOptimization (:2032-2056): DT updated in place in S, H = last evaluated
+__device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl,
+                             int max_iters) {
+    const int lane = threadIdx.x;
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
-    const DevPoints& P = p.prev.pt;
-    const DevLines& L = p.prev.ls;
-    const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
-    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
-    const size_t pb = (size_t)b * p.kp_cap, lb = (size_t)b * p.kl_cap;
-    for (int f = threadIdx.x; f < npt + nls; f += blockDim.x) {
-        double J[6], n, w;
-        if (f < npt) {
-            const size_t q = pb + mpt[f];
-            if (!P.inlier[q]) { act[f] = 0; continue; }
-            double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
-            double Pc[3], uv[2];
-            se3_apply(DT, Pp, Pc);
-            projection(cam, Pc, uv);
-            const double ex = uv[0] - P.pl_obs[2 * q], ey = uv[1] - P.pl_obs[2 * q + 1];
-            n = sqrt(ex * ex + ey * ey);
-            poseJac(cam, homog, Pc, ex, ey, J);
-            const double m = ref_max(homog, n);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) J[i] = J[i] / m;
-            w = 1.0 / (1.0 + (n * n) * P.sigma2[q]);
-        } else {
-            const size_t q = lb + mls[f - npt];
-            if (!L.inlier[q]) { act[f] = 0; continue; }
-            double sP[3] = {L.sP[3 * q], L.sP[3 * q + 1], L.sP[3 * q + 2]};
-            double eP[3] = {L.eP[3 * q], L.eP[3 * q + 1], L.eP[3 * q + 2]};
-            double sc[3], ec[3], su[2], eu[2];
-            se3_apply(DT, sP, sc);
-            projection(cam, sc, su);
-            se3_apply(DT, eP, ec);
-            projection(cam, ec, eu);
-            const double l0 = L.le_obs[3 * q], l1 = L.le_obs[3 * q + 1], l2 = L.le_obs[3 * q + 2];
-            const double ds = (l0 * su[0] + l1 * su[1]) + l2;
-            const double de = (l0 * eu[0] + l1 * eu[1]) + l2;
-            n = sqrt(ds * ds + de * de);
-            double Js[6], Je[6];
-            poseJac(cam, homog, sc, l0, l1, Js);
-            poseJac(cam, homog, ec, l0, l1, Je);
-            const double m = ref_max(homog, n);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) J[i] = (Js[i] * ds + Je[i] * de) / m;
-            w = 1.0 / (1.0 + (n * n) * L.sigma2[q]);
-        }
-        act[f] = 1;
-        double* o = feat + (size_t)f * 8;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) o[i] = J[i];
-        o[6] = n;
-        o[7] = w;
-    }
-}
-
-// one reduction entry e in [0,28): H lower (i,j), g_i, e
-__device__ __forceinline__ double term(const double* o, int e, int ti, int tj) {
-    if (e < 21) return (o[ti] * o[tj]) * o[7];
-    if (e < 27) return (o[e - 21] * o[6]) * o[7];
-    return (o[6] * o[6]) * o[7];
-}
-
-// gaussNewtonOptimization; returns via S: DT updated in place, H (last evaluated), err
-__device__ void gauss_newton(const KParams& p, int b, PoseLDS& S, double* feat, uint8_t* act, int npt, int nls,
-                             int max_iters) {
-    const int tid = threadIdx.x;
-    double err_prev = 999999999.9;   // thread 0 only
-    if (tid == 0) S.err = 0.0;
+    double err_prev = 999999999.9;   // lane 0 only
+    if (lane == 0) S.err = 0.0;
+    // reduction role: lanes 0-27 points, 28-55 lines; entry e: H lower (ti,tj), g_i, e
+    const int list = lane / 28, e = lane % 28;
+    int ia, ib;
+    if (e < 21) { int ti = 0; while ((ti + 1) * (ti + 2) / 2 <= e) ++ti; ia = ti; ib = e - ti * (ti + 1) / 2; }
+    else if (e < 27) { ia = e - 21; ib = 6; }
+    else { ia = 6; ib = 6; }
+    const double* buf = list == 0 ? cp : cl;
+    const int nch = (max(X.npt, X.nls) + 63) >> 6;
+    const uint8_t* actp = X.act;
+    const uint8_t* actl = X.act + X.npt;
     for (int it = 0; it < max_iters; ++it) {
         double DT[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) DT[i] = S.DT[i];
-        eval_features(p, b, DT, feat, act, npt, nls);
-        __syncthreads();
-        if (tid < 56) {
-            const int list = tid / 28, e = tid % 28;
-            int ti = 0, tj = 0;
-            if (e < 21) { ti = 0; while ((ti + 1) * (ti + 2) / 2 <= e) ++ti; tj = e - ti * (ti + 1) / 2; }
-            const int f0 = list == 0 ? 0 : npt, f1 = list == 0 ? npt : npt + nls;
-            double s = 0.0;
-            int cnt = 0;
-#pragma unroll 4
-            for (int f = f0; f < f1; ++f) {
-                const double t = term(feat + (size_t)f * 8, e, ti, tj);
-                const bool a = act[f] != 0;
-                s = a ? s + t : s;
-                cnt += a ? 1 : 0;
+        double s = 0.0;
+        for (int c = 0; c < nch; ++c) {
+            const int f = (c << 6) + lane;
+            double o[8];
+            if (f < X.npt && actp[f]) eval_point(cam, homog, DT, X.pin + f, X.mpt_cap, o);
+            else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
-            S.part[tid] = s;
-            if (e == 0) S.npart[list] = cnt;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cp[i * 64 + lane] = o[i];
+            if (f < X.nls && actl[f]) eval_line(cam, homog, DT, X.lin + f, X.mls_cap, o);
+            else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cl[i * 64 + lane] = o[i];
+            __syncthreads();
+            const double* A = buf + ia * 64;
+            const double* Bv = buf + ib * 64;
+            const double* W = buf + 7 * 64;
+#pragma unroll 16
+            for (int k = 0; k < 64; ++k) s = s + (A[k] * Bv[k]) * W[k];
+            __syncthreads();
         }
+        S.part[lane] = s;
         __syncthreads();
-        if (tid == 0) {
+        if (lane == 0) {
             double H[36], g[6];
             for (int i = 0; i < 6; ++i)
                 for (int j = 0; j <= i; ++j) {
@@ -128,12 +142,12 @@ __device__ void gauss_newton(const KParams& p, int b, PoseLDS& S, double* feat, 
                     H[i * 6 + j] = v; H[j * 6 + i] = v;
                 }
             for (int i = 0; i < 6; ++i) g[i] = S.part[21 + i] + S.part[28 + 21 + i];
-            double e = S.part[27] + S.part[28 + 27];
-            e = e / (double)(S.npart[1] + S.npart[0]);
+            double ee = S.part[27] + S.part[28 + 27];
+            ee = ee / (double)(S.cnt[1] + S.cnt[0]);
             for (int i = 0; i < 36; ++i) S.H[i] = H[i];
-            S.err = e;
+            S.err = ee;
             int brk = 0;
-            if ((fabs(e - err_prev) < p.cfg.min_error_change) || (e < p.cfg.min_error)) {
+            if ((fabs(ee - err_prev) < p.cfg.min_error_change) || (ee < p.cfg.min_error)) {
                 brk = 1;
             } else {
                 double inc[6], E[16], Ei[16], Dn[16];
@@ -145,7 +159,7 @@ __device__ void gauss_newton(const KParams& p, int b, PoseLDS& S, double* feat, 
                 const double nrm = sqrt(((((inc[0] * inc[0] + inc[1] * inc[1]) + inc[2] * inc[2]) + inc[3] * inc[3]) +
                                          inc[4] * inc[4]) + inc[5] * inc[5]);
                 if (nrm < 2.220446049250313e-16) brk = 1;
-                err_prev = e;
+                err_prev = ee;
             }
             S.brk = brk;
         }
@@ -154,7 +168,7 @@ __device__ void gauss_newton(const KParams& p, int b, PoseLDS& S, double* feat, 
     }
 }
 
-// vector_stdv_mad on res[0..n) (LDS, destroyed); scratch buf has NP2 entries
+// vector_stdv_mad on buf[0..n) (LDS, destroyed); buf has NP2 entries
 __device__ double stdv_mad(double* buf, int n, int NP2) {
     if (n == 0) return 0.0;   // uniform
     for (int i = threadIdx.x + n; i < NP2; i += blockDim.x) buf[i] = __builtin_inf();
@@ -192,91 +206,142 @@ __device__ double stdv_mad(double* buf, int n, int NP2) {
     return 1.4826 * mad;
 }
 
-// dynamic LDS: feat[(mpt+mls)*8] f64 (reused for residual sorts) | act[mpt+mls] u8
-__global__ void __launch_bounds__(256) k_pose(KParams p, int NP2, int featN) {
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// dynamic LDS: {cp[8*64] cl[8*64] | rp[mpt_cap] rl[mls_cap]} f64 | buf[NP2] f64 | act[mpt+mls] u8
+__global__ void __launch_bounds__(64) k_pose(KParams p, int NP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ PoseLDS S;
-    __shared__ int cnt[4];
     const int b = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     const int npt = p.tr.n_matched_pt[b], nls = p.tr.n_matched_ls[b];
-    double* feat = (double*)smem;
-    uint8_t* act = (uint8_t*)(feat + featN);
-    DevPose& CP = p.curr.pose;
+    // the GN chunk rows and the outlier residuals are never live together
+    const int region = max(16 * 64, p.mpt_cap + p.mls_cap);
+    double* cp = (double*)smem;
+    double* cl = cp + 8 * 64;
+    double* rp = cp;
+    double* rl = rp + p.mpt_cap;
+    double* buf = cp + region;
+    uint8_t* act = (uint8_t*)(buf + NP2);
     const DevPose& PP = p.prev.pose;
-    if (tid < 16) { S.DTini[tid] = PP.DT[16 * b + tid]; S.DT[tid] = S.DTini[tid]; }   // Q2
-    if (tid == 0) { S.ninl = p.tr.n_inliers[b]; cnt[0] = cnt[1] = 0; }
+    const DevPoints& P = p.prev.pt;
+    const DevLines& L = p.prev.ls;
+    const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
+    const size_t pb = (size_t)b * p.kp_cap, lb = (size_t)b * p.kl_cap;
+    PoseCtx X;
+    X.mpt_cap = p.mpt_cap; X.mls_cap = p.mls_cap;
+    double* pin = p.scr.pose_in + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
+    double* lin = pin + PT_K * p.mpt_cap;
+    X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
+    if (lane < 16) { S.DTini[lane] = PP.DT[16 * b + lane]; S.DT[lane] = S.DTini[lane]; }   // Q2
+    if (lane == 0) S.ninl = p.tr.n_inliers[b];
+    // gather the matched lists once (lane l owns positions l, l+64, ...)
+    int cpn = 0, cln = 0;
+    for (int f = lane; f < npt; f += 64) {
+        const size_t q = pb + mpt[f];
+        pin[f] = P.P[3 * q]; pin[p.mpt_cap + f] = P.P[3 * q + 1]; pin[2 * p.mpt_cap + f] = P.P[3 * q + 2];
+        pin[3 * p.mpt_cap + f] = P.pl_obs[2 * q]; pin[4 * p.mpt_cap + f] = P.pl_obs[2 * q + 1];
+        pin[5 * p.mpt_cap + f] = P.sigma2[q];
+        act[f] = P.inlier[q] ? 1 : 0;
+        cpn += act[f];
+    }
+    for (int f = lane; f < nls; f += 64) {
+        const size_t q = lb + mls[f];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lin[k * p.mls_cap + f] = L.sP[3 * q + k];
+            lin[(3 + k) * p.mls_cap + f] = L.eP[3 * q + k];
+            lin[(6 + k) * p.mls_cap + f] = L.le_obs[3 * q + k];
+        }
+        lin[9 * p.mls_cap + f] = L.sigma2[q];
+        act[npt + f] = L.inlier[q] ? 1 : 0;
+        cln += act[npt + f];
+    }
+    cpn = wave_sum(cpn);
+    cln = wave_sum(cln);
+    if (lane == 0) { S.cnt[0] = cpn; S.cnt[1] = cln; }
     __syncthreads();
     int ok = 0;        // 1: stage-2 DT usable
     double err = 0.0;  // err of the last GN run (reference: uninitialised when no GN runs, pinned 0)
     if (S.ninl > p.cfg.min_features) {
-        gauss_newton(p, b, S, feat, act, npt, nls, p.cfg.max_iters);
+        gauss_newton(p, X, S, cp, cl, p.cfg.max_iters);
         err = S.err;
         double DTs[16];
         for (int i = 0; i < 16; ++i) DTs[i] = S.DT[i];
         bool fin = true;
         for (int i = 0; i < 16; ++i) { double d = DTs[i] - DTs[i]; if (!(d == d)) fin = false; }
         if (fin) {
-            // removeOutliers(DT_): residuals of every list entry
-            const DevPoints& P = p.prev.pt;
-            const DevLines& L = p.prev.ls;
-            const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
-            const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
-            const size_t pb = (size_t)b * p.kp_cap, lb = (size_t)b * p.kl_cap;
-            double* rp = feat;                 // [npt] residuals (kept)
-            double* rl = feat + NP2;           // [nls]
-            double* buf = feat + 2 * NP2;      // sort scratch [NP2]
-            for (int k = tid; k < npt; k += blockDim.x) {
-                const size_t q = pb + mpt[k];
-                double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]}, Pc[3], uv[2];
+            // removeOutliers(DT_) (:2058-2116): residuals of every list entry
+            for (int k = lane; k < npt; k += 64) {
+                const double* in = pin + k;
+                const double Pp[3] = {in[0], in[p.mpt_cap], in[2 * p.mpt_cap]};
+                double Pc[3], uv[2];
                 se3_apply(DTs, Pp, Pc);
                 projection(p.cam, Pc, uv);
-                const double ex = uv[0] - P.pl_obs[2 * q], ey = uv[1] - P.pl_obs[2 * q + 1];
-                rp[k] = sqrt(ex * ex + ey * ey) * sqrt(P.sigma2[q]);
+                const double ex = uv[0] - in[3 * p.mpt_cap], ey = uv[1] - in[4 * p.mpt_cap];
+                rp[k] = sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
             }
-            for (int k = tid; k < nls; k += blockDim.x) {
-                const size_t q = lb + mls[k];
-                double sP[3] = {L.sP[3 * q], L.sP[3 * q + 1], L.sP[3 * q + 2]};
-                double eP[3] = {L.eP[3 * q], L.eP[3 * q + 1], L.eP[3 * q + 2]};
+            for (int k = lane; k < nls; k += 64) {
+                const double* in = lin + k;
+                const size_t st = p.mls_cap;
+                const double sP[3] = {in[0], in[st], in[2 * st]};
+                const double eP[3] = {in[3 * st], in[4 * st], in[5 * st]};
                 double sc[3], ec[3], su[2], eu[2];
                 se3_apply(DTs, sP, sc);
                 se3_apply(DTs, eP, ec);
                 projection(p.cam, sc, su);
                 projection(p.cam, ec, eu);
-                const double l0 = L.le_obs[3 * q], l1 = L.le_obs[3 * q + 1], l2 = L.le_obs[3 * q + 2];
+                const double l0 = in[6 * st], l1 = in[7 * st], l2 = in[8 * st];
                 const double e0 = (l0 * su[0] + l1 * su[1]) + l2;
                 const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
-                rl[k] = sqrt(e0 * e0 + e1 * e1) * sqrt(L.sigma2[q]);
+                rl[k] = sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
             }
             __syncthreads();
-            for (int k = tid; k < npt; k += blockDim.x) buf[k] = rp[k];
+            for (int k = lane; k < npt; k += 64) buf[k] = rp[k];
             __syncthreads();
             const double th_p = p.cfg.inlier_k * stdv_mad(buf, npt, NP2);
-            for (int k = tid; k < nls; k += blockDim.x) buf[k] = rl[k];
+            for (int k = lane; k < nls; k += 64) buf[k] = rl[k];
             __syncthreads();
             const double th_l = p.cfg.inlier_k * stdv_mad(buf, nls, NP2);
-            for (int k = tid; k < npt; k += blockDim.x)
-                if (rp[k] > th_p) { p.prev.pt.inlier[pb + mpt[k]] = 0; atomicAdd(&cnt[0], 1); }
-            for (int k = tid; k < nls; k += blockDim.x)
-                if (rl[k] > th_l) { p.prev.ls.inlier[lb + mls[k]] = 0; atomicAdd(&cnt[1], 1); }
+            // duplicates of one prev point share P, pl_obs and sigma2, hence the residual:
+            // flagging per list position equals the reference's per-feature flag
+            int op = 0, ol = 0;
+            for (int k = lane; k < npt; k += 64)
+                if (rp[k] > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
+            for (int k = lane; k < nls; k += 64)
+                if (rl[k] > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+            op = wave_sum(op);
+            ol = wave_sum(ol);
+            // active counts for stage 2
+            int ap = 0, al = 0;
             __syncthreads();
-            if (tid == 0) {
-                S.ninl = S.ninl - cnt[0] - cnt[1];
+            for (int k = lane; k < npt; k += 64) ap += act[k];
+            for (int k = lane; k < nls; k += 64) al += act[npt + k];
+            ap = wave_sum(ap);
+            al = wave_sum(al);
+            if (lane == 0) {
+                S.ninl = S.ninl - op - ol;
                 p.tr.n_inliers[b] = S.ninl;
-                p.tr.n_inliers_pt[b] -= cnt[0];
-                p.tr.n_inliers_ls[b] -= cnt[1];
+                p.tr.n_inliers_pt[b] -= op;
+                p.tr.n_inliers_ls[b] -= ol;
+                S.cnt[0] = ap; S.cnt[1] = al;
             }
             __syncthreads();
             if (S.ninl > p.cfg.min_features) {
-                if (tid < 16) S.DT[tid] = S.DTini[tid];   // Q3: stage 2 restarts from DT_ini
+                if (lane < 16) S.DT[lane] = S.DTini[lane];   // Q3: stage 2 restarts from DT_ini
                 __syncthreads();
-                gauss_newton(p, b, S, feat, act, npt, nls, p.cfg.max_iters_ref);
+                gauss_newton(p, X, S, cp, cl, p.cfg.max_iters_ref);
                 err = S.err;
                 ok = 1;
             }
         }
     }
-    if (tid == 0) {
+    if (lane == 0) {
         for (int i = 0; i < 16; ++i) p.scr.pose_DT[16 * b + i] = S.DT[i];
         for (int i = 0; i < 36; ++i) p.scr.pose_H[36 * b + i] = S.H[i];
         p.scr.pose_err[b] = err;
@@ -388,10 +453,9 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
 hipError_t launch_pose(const KParams& p, hipStream_t s) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
-    size_t feat = (size_t)(p.mpt_cap + p.mls_cap) * 8;
-    if (feat < (size_t)3 * NP2) feat = (size_t)3 * NP2;
-    const size_t lds = feat * 8 + (size_t)(p.mpt_cap + p.mls_cap) + 16;
-    hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(256), lds, s, p, NP2, (int)feat);
+    const size_t region = (size_t)std::max(16 * 64, p.mpt_cap + p.mls_cap);
+    const size_t lds = (region + NP2) * 8 + (p.mpt_cap + p.mls_cap) + 16;
+    hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     return hipGetLastError();
 }

@@ -331,21 +331,47 @@ def make_frames(B: int, kp_cap: int, kl_cap: int, arrs) -> Frames:
     return fr
 
 
+def input_bytes_per_frame(cam: Camera, kp_cap: int, kl_cap: int) -> int:
+    """Bytes of one sequence's input frame in the [B][cap] layout."""
+    return (2 * 4 + 2 * kp_cap * (KEYPOINT_DT.itemsize + DESC) + 2 * 4 + 2 * kl_cap * (KEYLINE_DT.itemsize + DESC)
+            + cam.pyr_bytes + 8)
+
+
 class DeviceFrames:
     """Input frames resident in HBM (torch uint8 buffers), one gfpl_frames per frame."""
 
-    def __init__(self, host: HostFrames, device: str = "cuda"):
-        import torch
-        self.host = host
+    def __init__(self, host: HostFrames = None, device: str = "cuda"):
         self.bufs = []
+        if host is None:
+            return
+        import torch
+        self.B, self.kp_cap, self.kl_cap = host.B, host.kp_cap, host.kl_cap
         for a in host.arrays():
             t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(a.shape[0], -1))
             self.bufs.append(t.to(device))
-        self.sizes = [a[0].nbytes for a in host.arrays()]
+
+    @classmethod
+    def generate(cls, cam: Camera, sp: SynthParams, n_seq: int, n_frames: int, kp_cap: int, kl_cap: int,
+                 seq0: int = 0, device="cuda", threads: int = 0) -> "DeviceFrames":
+        """Generate frame by frame on the host and stage each into HBM, so host memory
+        holds one frame of the batch at a time (frames are independent given the
+        sequence seed, gfpl_synth)."""
+        import torch
+        d = cls(None)
+        d.B, d.kp_cap, d.kl_cap = n_seq, kp_cap, kl_cap
+        for f in range(n_frames):
+            h = HostFrames(cam, sp, n_seq, 1, kp_cap, kl_cap, seq0=seq0, frame0=f, threads=threads)
+            arrs = h.arrays()
+            if not d.bufs:
+                d.bufs = [torch.empty((n_frames, a[0].nbytes), dtype=torch.uint8, device=device) for a in arrs]
+            for buf, a in zip(d.bufs, arrs):
+                buf[f].copy_(torch.from_numpy(np.ascontiguousarray(a[0]).view(np.uint8).reshape(-1)))
+            del h
+        return d
 
     def frames(self, f: int) -> Frames:
         arrs = [b[f] for b in self.bufs]
-        return make_frames(self.host.B, self.host.kp_cap, self.host.kl_cap, arrs)
+        return make_frames(self.B, self.kp_cap, self.kl_cap, arrs)
 
     def nbytes(self) -> int:
         return sum(b.numel() for b in self.bufs)

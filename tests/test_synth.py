@@ -37,3 +37,16 @@ def test_seq_offset_equals_global_id():
     B = gfpl.HostFrames(cam, sp, 1, 2, 512, 128, seq0=2)
     for a, b in zip(A.arrays(), B.arrays()):
         assert np.array_equal(a[:, 2], b[:, 0])
+
+
+def test_frames_independent_of_chunking():
+    """bench.py stages inputs frame by frame (DeviceFrames.generate): a frame must
+    not depend on which other frames were generated with it."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    sp = gfpl.synth_params(seed=3, n_kp=300, n_kl=60, n_world_pts=400, n_world_lines=90)
+    whole = gfpl.HostFrames(cam, sp, 3, 4, 512, 128, seq0=5)
+    one = gfpl.HostFrames(cam, sp, 3, 1, 512, 128, seq0=5, frame0=2)
+    for a, b in zip(whole.arrays(), one.arrays()):
+        assert np.array_equal(a[2], b[0])
+    assert gfpl.input_bytes_per_frame(cam, 512, 128) == sum(a[0].nbytes for a in one.arrays()) // 3
