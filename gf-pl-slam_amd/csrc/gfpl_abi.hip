@@ -2,6 +2,7 @@
 // sequence batches, stage/step entry points and state transfer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -186,6 +187,12 @@ int gfpl_destroy(gfpl_ctx* c) {
 
 int gfpl_set_camera(gfpl_ctx* c, const gfpl_camera* cam) {
     if (!c || !cam || cam->n_levels < 1 || cam->n_levels > GFPL_MAX_LEVELS) return GFPL_E_INVALID;
+    int64_t need = 0;
+    for (int i = 0; i < cam->n_levels; ++i) {
+        if (cam->lvl_cols[i] < 1 || cam->lvl_rows[i] < 1 || cam->lvl_offset[i] < 0) return GFPL_E_INVALID;
+        need = std::max<int64_t>(need, cam->lvl_offset[i] + (int64_t)cam->lvl_cols[i] * cam->lvl_rows[i]);
+    }
+    if (cam->pyr_bytes < need + GFPL_PYR_TAIL) return GFPL_E_INVALID;   // window loads read past the last row
     c->cam = *cam;
     c->has_cam = true;
     return GFPL_OK;

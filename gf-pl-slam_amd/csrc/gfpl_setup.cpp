@@ -68,8 +68,9 @@ extern "C" int gfpl_camera_init(gfpl_camera* cam, int width, int height, double 
         cam->lvl_offset[i] = off;
         off += (int64_t)cam->lvl_cols[i] * cam->lvl_rows[i];
     }
-    // keep every sequence's pyramid 256-byte aligned inside a batch
-    cam->pyr_bytes = (off + 255) & ~(int64_t)255;
+    // keep every sequence's pyramid 256-byte aligned inside a batch, with a tail of
+    // at least GFPL_PYR_TAIL bytes (the SAD window rows are read as aligned dwords)
+    cam->pyr_bytes = (off + GFPL_PYR_TAIL + 255) & ~(int64_t)255;
     for (int l = 0; l < GFPL_MAX_LEVELS; ++l) {
         double s = 1.0;
         for (int i = 0; i < l + 1; ++i) s *= cfg->orb_scale_factor;

@@ -31,6 +31,25 @@ __device__ void bitonic_sort(K* a, int n) {   // n power of two, ascending
         }
 }
 
+// two independent arrays through one bitonic network (shared barriers)
+template <typename K>
+__device__ void bitonic_sort2(K* a, K* c, int n) {
+    for (int k = 2; k <= n; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    bool up = ((i & k) == 0);
+                    K x = a[i], y = a[ixj];
+                    if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+                    K u = c[i], v = c[ixj];
+                    if ((u > v) == up) { c[i] = v; c[ixj] = u; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
 __device__ __forceinline__ int clamp_level(int o, int n) { return o < 0 ? 0 : (o >= n ? n - 1 : o); }
 
 // subPixelStereoRefine_ORBSLAM (src/stereoFrame.cpp:340-404); ledger Q1: both
@@ -53,21 +72,47 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
     const int vL = (int)scaledvL, uL = (int)scaleduL, uR = (int)scaleduR0;
     if (vL - 5 < 0 || vL + 5 >= rows || uL - 5 < 0 || uL + 5 >= cols || uR - 10 < 0 || uR + 10 >= cols) return;
     const uint8_t* img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[o];
-    const uint8_t* crow = img + (size_t)vL * cols;
-    const int cL = crow[uL];
-    int cR[11];
+    // Each window row is read as aligned dwords and re-aligned with v_alignbyte:
+    // 4 loads for the 11-byte IL row and 6 for the 21-byte IR row instead of 32
+    // byte loads (the camera's pyramid tail keeps the last dword in bounds).
+    const size_t aL = (size_t)(uL - 5), aR = (size_t)(uR - 10);
+    auto load_row = [&](int y, uint32_t* il4, uint32_t* ir6) {
+        const uint8_t* rowp = img + (size_t)y * cols;
+        const uintptr_t pl = (uintptr_t)(rowp + aL), pr = (uintptr_t)(rowp + aR);
+        const uint32_t* wl = reinterpret_cast<const uint32_t*>(pl & ~(uintptr_t)3);
+        const uint32_t* wr = reinterpret_cast<const uint32_t*>(pr & ~(uintptr_t)3);
+        const uint32_t shl = (uint32_t)(pl & 3u), shr = (uint32_t)(pr & 3u);
+        uint32_t a[4], c[6];
 #pragma unroll
-    for (int i = 0; i < 11; ++i) cR[i] = crow[uR - 5 + i];
+        for (int i = 0; i < 4; ++i) a[i] = wl[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c[i] = wr[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) il4[i] = __builtin_amdgcn_alignbyte(a[i + 1], a[i], shl);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) ir6[i] = __builtin_amdgcn_alignbyte(c[i + 1], c[i], shr);
+        ir6[5] = __builtin_amdgcn_alignbyte(c[5], c[5], shr);
+    };
+    auto byte_at = [](const uint32_t* w, int k) -> int { return (int)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu); };
+    int cL, cR[11];
+    {
+        uint32_t il4[3], ir6[6];
+        load_row(vL, il4, ir6);
+        cL = byte_at(il4, 5);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) cR[i] = byte_at(ir6, 5 + i);
+    }
     int acc[11];
 #pragma unroll
     for (int i = 0; i < 11; ++i) acc[i] = 0;
     for (int r = 0; r < 11; ++r) {
-        const uint8_t* rowp = img + (size_t)(vL - 5 + r) * cols;
+        uint32_t il4[3], ir6[6];
+        load_row(vL - 5 + r, il4, ir6);
         int il[11], ir[21];
 #pragma unroll
-        for (int c = 0; c < 11; ++c) il[c] = (int)rowp[uL - 5 + c] - cL;
+        for (int c = 0; c < 11; ++c) il[c] = byte_at(il4, c) - cL;
 #pragma unroll
-        for (int c = 0; c < 21; ++c) ir[c] = rowp[uR - 10 + c];
+        for (int c = 0; c < 21; ++c) ir[c] = byte_at(ir6, c);
 #pragma unroll
         for (int s = 0; s < 11; ++s)
 #pragma unroll
@@ -93,16 +138,21 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
 }
 
 // ------------------------------------------------------- stereo points --
-// dynamic LDS: rkey[KP2] u32 | pairs[KP2] u32 | depth[cap] f32 | rmaxr[cap] i32 | misc[64]
+// dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | rmaxr[cap] i32 | misc[64]
+// Left keypoints are processed in row order (a row-sorted permutation, order[]),
+// so the lanes of a wave touch the same right-keypoint band and overlapping SAD
+// window rows: the gathers hit L1/L2 instead of HBM.  Results are keyed by iL,
+// so the processing order has no effect on the output.
 __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;
     uint32_t* rkey = (uint32_t*)smem;
-    uint32_t* pairs = rkey + KP2;
-    float* depth = (float*)(pairs + KP2);
-    int* rmaxr = (int*)(depth + cap);
+    uint32_t* order = rkey + KP2;
+    uint32_t* pairs = order + KP2;
+    int* rmaxr = (int*)(pairs + KP2);
     int* misc = rmaxr + cap;
+    float* depth = reinterpret_cast<float*>(p.scr.knn) + (size_t)b * cap;   // scratch (cross points reuses it later)
     const int tid = threadIdx.x;
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
     const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
@@ -112,30 +162,40 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     const int nRows = p.cam.height;
     if (tid == 0) { misc[0] = 0; misc[1] = 0; misc[2] = 0; }
     __syncthreads();
-    // vRowIndices (src/stereoFrame.cpp:459-485) as (minr, iR) keys sorted by minr
-    for (int iR = tid; iR < KP2; iR += blockDim.x) {
-        if (iR < Nr) {
-            gfpl_keypoint kp = KR[iR];
+    // vRowIndices (src/stereoFrame.cpp:459-485) as (minr, iR) keys sorted by minr;
+    // left keypoints as (row, iL) keys
+    for (int i = tid; i < KP2; i += blockDim.x) {
+        if (i < Nr) {
+            gfpl_keypoint kp = KR[i];
             const float r = 2.0f * p.cam.scale[clamp_level(kp.octave, p.cam.n_levels)];
             const int maxr = (int)ceilf(kp.y + r);
             const int minr = (int)floorf(kp.y - r);
-            rkey[iR] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)iR;
-            rmaxr[iR] = maxr;
+            rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
+            rmaxr[i] = maxr;
             atomicMax(&misc[0], maxr - minr);
         } else {
-            rkey[iR] = 0xFFFFFFFFu;
+            rkey[i] = 0xFFFFFFFFu;
         }
+        if (i < N) {
+            const float y = KL[i].y;
+            const int row = (y >= 0.0f && y < 65534.0f) ? (int)y + 1 : 0;
+            order[i] = ((uint32_t)row << 16) | (uint32_t)i;
+        } else {
+            order[i] = 0xFFFFFFFFu;
+        }
+        pairs[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    bitonic_sort(rkey, KP2);
+    bitonic_sort2(rkey, order, KP2);
     const int D = misc[0];
     const float minD = 0;
     const float maxD = (float)p.cam.fx;
     const float mbf = (float)(p.cam.fx * p.cam.b);
     // per left keypoint: band search + Hamming + sub-pixel (src/stereoFrame.cpp:502-583)
-    for (int iL = tid; iL < KP2; iL += blockDim.x) {
+    for (int t = tid; t < N; t += blockDim.x) {
+        const int iL = (int)(order[t] & 0xFFFFu);
         uint32_t key = 0xFFFFFFFFu;
-        if (iL < N) {
+        {
             const gfpl_keypoint kpL = KL[iL];
             const int levelL = kpL.octave;
             const float vL = kpL.y, uL = kpL.x;
@@ -582,7 +642,7 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
-    const size_t lds = (size_t)KP2 * 8 + (size_t)p.kp_cap * 8 + 64 * 4;
+    const size_t lds = (size_t)KP2 * 12 + (size_t)p.kp_cap * 4 + 64 * 4;
     hipLaunchKernelGGL(k_stereo_points, dim3(p.B), dim3(512), lds, s, p, KP2);
     return hipGetLastError();
 }

@@ -37,6 +37,7 @@ extern "C" {
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
 #define GFPL_MAX_MATCHED_PT 2048    /* capacity of matched_pt (cap from config)   */
 #define GFPL_MAX_MATCHED_LS 1024    /* capacity of matched_ls (cap from config)   */
+#define GFPL_PYR_TAIL 64            /* slack after each packed pyramid (bytes)    */
 
 /* error codes */
 #define GFPL_OK                   0
@@ -69,7 +70,8 @@ typedef struct gfpl_camera {
     int    lvl_cols[GFPL_MAX_LEVELS];         /* cvRound(W * inv_scale)        */
     int    lvl_rows[GFPL_MAX_LEVELS];         /* cvRound(H * inv_scale)        */
     int64_t lvl_offset[GFPL_MAX_LEVELS];      /* byte offset of level in packed pyramid */
-    int64_t pyr_bytes;                        /* bytes of one packed pyramid   */
+    int64_t pyr_bytes;                        /* bytes of one packed pyramid: sum of the
+                                                 levels + >= GFPL_PYR_TAIL, 256-aligned   */
     double sigma2_pt[GFPL_MAX_LEVELS];        /* PointFeature::sigma2 per level (src/stereoFeatures.cpp:41-47) */
     double sigma2_ln[GFPL_MAX_LEVELS];        /* LineFeature::sigma2 per level  (src/stereoFeatures.cpp:96-101) */
 } gfpl_camera;

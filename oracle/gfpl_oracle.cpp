@@ -658,6 +658,8 @@ std::vector<Desc> collect(const uint8_t* (Frame::*f)(int) const, const Frame& fr
 
 }  // namespace
 
+static int64_t g_cut_stats[8];   // line-cut work counters (analysis only)
+
 struct gfplo_handler {
     Cam cam;
     gfpl_config cfg;
@@ -1223,21 +1225,39 @@ struct gfplo_handler {
             poseInfoPoint(DT_inv, prev->pt[pi], tmp);
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] + tmp[i];
         }
+        bool prev_moved = true;
+        double sum_before[36];
         for (int li : matched_ls) {
             LineF& L = prev->ls[li];
             double Jl[2] = {L.le_obs[0], L.le_obs[1]};
             double metric_back = logdet6(sum);
+            g_cut_stats[0]++;   // lines
+            if (!prev_moved) {
+                bool same = true;
+                for (int i = 0; i < 36; ++i) same = same && (sum[i] == sum_before[i]);
+                if (!same) g_cut_stats[5]++;   // setup logdet really needed
+            }
+            std::memcpy(sum_before, sum, sizeof sum);
+            std::vector<std::pair<uint64_t, uint64_t>> seen;
+            bool moved = false;
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] - L.invCov[i];
             while (L.cut[0] + L.cut[1] <= 1.0) {
                 bool hit = false;
                 double cand[2] = {0, 0};
                 double cand_info[36];
                 double metric_init = metric_back;
+                g_cut_stats[1]++;   // steps
                 for (int j = 0; j < 8; ++j) {
                     double rt[2] = {L.cut[0] + nb[j][0], L.cut[1] + nb[j][1]};
                     if (rt[0] + rt[1] > 1.0) continue;
                     if (rt[0] < cfg.cut_rng[0] || rt[0] > cfg.cut_rng[1]) continue;
                     if (rt[1] < cfg.cut_rng[0] || rt[1] > cfg.cut_rng[1]) continue;
+                    g_cut_stats[2]++;   // valid evaluations
+                    uint64_t k0, k1;
+                    std::memcpy(&k0, &rt[0], 8); std::memcpy(&k1, &rt[1], 8);
+                    bool dup = false;
+                    for (auto& pr : seen) dup = dup || (pr.first == k0 && pr.second == k1);
+                    if (!dup) { seen.push_back({k0, k1}); g_cut_stats[3]++; }   // distinct evaluations
                     double tmp[36], tot[36];
                     poseInfoOnLine(DT_inv, Jl, L, rt, tmp);
                     for (int i = 0; i < 36; ++i) tot[i] = tmp[i] + sum[i];
@@ -1253,8 +1273,11 @@ struct gfplo_handler {
                     L.cut[0] = cand[0]; L.cut[1] = cand[1];
                     std::memcpy(L.invCov, cand_info, sizeof cand_info);
                     metric_back = metric_init;
+                    moved = true;
                 } else break;
             }
+            if (!moved) g_cut_stats[4]++;   // lines that never moved
+            prev_moved = moved;
             updateEndPointByRatio(L);
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] + L.invCov[i];
         }
@@ -1711,3 +1734,10 @@ int gfplo_expmap_se3(const double* x, double* T) { expmap_se3(x, T); return 0; }
 int gfplo_inverse_se3(const double* T, double* out) { inverse_se3(T, out); return 0; }
 
 }  // extern "C"
+
+/* line-cut work counters since the last call (analysis of the search shape):
+ * lines, steps, valid evaluations, bit-distinct evaluations per line,
+ * lines that never moved, setup logdets not implied by the previous line */
+extern "C" void gfplo_cut_stats(int64_t* out8) {
+    for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
+}
