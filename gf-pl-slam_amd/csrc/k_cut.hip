@@ -72,36 +72,38 @@ __device__ __forceinline__ double endpointVar(const DevCam& cam, const double* D
     return r0 * Jl[0] + r1 * Jl[1];
 }
 
-// getPoseInfoOnLine: FULL -> 36 entries row-major, else lower triangle (21)
+// One cut endpoint of getPoseInfoOnLine (src/stereoFrameHandler.cpp:1350-1388):
+// P = (1-c)*P0 + c*P1 with its covariance blend (1-c)^2*C0 + c^2*C1, the
+// projected residual variance v and the pose Jacobian J of that endpoint.
+// Start endpoint: (sP, eP, covS, covE, c0); end endpoint: (eP, sP, covE, covS, c1).
+// The start terms depend on c0 only and the end terms on c1 only, which the
+// search exploits.
+__device__ __forceinline__ void cut_endpoint(const DevCam& cam, double homog, const double* DT_inv, const double* Jl,
+                                             const double* P0, const double* P1, const double* C0, const double* C1,
+                                             double c, double* out7) {
+    double Pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Pt[k] = (1 - c) * P0[k] + c * P1[k];
+    const double a = (1 - c) * (1 - c), q = c * c;
+    double cov[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
+    out7[0] = endpointVar(cam, DT_inv, Jl, Pt, cov);
+    double cur[3];
+    se3_apply(DT_inv, Pt, cur);
+    poseJac(cam, homog, cur, Jl[0], Jl[1], out7 + 1);
+}
+
+// info = [Js Je] inv(diag(vs, ve)) [Js Je]^T, Eigen 2x2 inverse via invdet (ledger Q10)
+// FULL -> 36 entries row-major, else lower triangle (21)
 template <bool FULL>
-__device__ __forceinline__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT_inv,
-                                               const LineCutData& L, double c0, double c1, double* info) {
-    double sPt[3], ePt[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        sPt[k] = (1 - c0) * L.sP[k] + c0 * L.eP[k];
-        ePt[k] = (1 - c1) * L.eP[k] + c1 * L.sP[k];
-    }
-    const double a0 = (1 - c0) * (1 - c0), q0 = c0 * c0;
-    const double a1 = (1 - c1) * (1 - c1), q1 = c1 * c1;
-    double covSt[9], covEt[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        covSt[i] = a0 * L.covS[i] + q0 * L.covE[i];
-        covEt[i] = a1 * L.covE[i] + q1 * L.covS[i];
-    }
-    const double vs = endpointVar(cam, DT_inv, L.Jl, sPt, covSt);
-    const double ve = endpointVar(cam, DT_inv, L.Jl, ePt, covEt);
-    // Eigen 2x2 inverse via invdet (ledger Q10)
+__device__ __forceinline__ void cut_assemble(const double* S7, const double* E7, double* info) {
+    const double vs = S7[0], ve = E7[0];
+    const double* Js = S7 + 1;
+    const double* Je = E7 + 1;
     const double det = vs * ve - 0.0 * 0.0;
     const double invdet = 1.0 / det;
     const double i00 = ve * invdet, i10 = -0.0 * invdet, i01 = -0.0 * invdet, i11 = vs * invdet;
-    double curS[3], curE[3];
-    se3_apply(DT_inv, sPt, curS);
-    se3_apply(DT_inv, ePt, curE);
-    double Js[6], Je[6];
-    poseJac(cam, homog, curS, L.Jl[0], L.Jl[1], Js);
-    poseJac(cam, homog, curE, L.Jl[0], L.Jl[1], Je);
     double T0[6], T1[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
@@ -119,6 +121,16 @@ __device__ __forceinline__ void poseInfoOnLine(const DevCam& cam, double homog, 
 #pragma unroll
             for (int j = 0; j <= i; ++j) info[tri(i, j)] = T0[i] * Js[j] + T1[i] * Je[j];
     }
+}
+
+// getPoseInfoOnLine (src/stereoFrameHandler.cpp:1342-1411)
+template <bool FULL>
+__device__ __forceinline__ void poseInfoOnLine(const DevCam& cam, double homog, const double* DT_inv,
+                                               const LineCutData& L, double c0, double c1, double* info) {
+    double S7[7], E7[7];
+    cut_endpoint(cam, homog, DT_inv, L.Jl, L.sP, L.eP, L.covS, L.covE, c0, S7);
+    cut_endpoint(cam, homog, DT_inv, L.Jl, L.eP, L.sP, L.covE, L.covS, c1, E7);
+    cut_assemble<FULL>(S7, E7, info);
 }
 
 __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutData& d) {
@@ -187,15 +199,54 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         for (int m = 0; m < npt; ++m) s = s + scr_p[(size_t)m * 21 + lane];
         p.scr.cut_sum[24 * b + lane] = s;
     }
+    __syncthreads();
+    if (lane == 0) {   // metric of the first line's search: logdet(invCov_sum) (:1671)
+        double a[21];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) a[i] = p.scr.cut_sum[24 * b + i];
+        p.scr.cut_sum[24 * b + 21] = logdet6_lower(a);
+    }
 }
 
 // ---------------------------------------------------------------- search --
+// 8 sequences per wave, 8 lanes each; every wave iteration is one greedy step
+// of each of its 8 chains, in three phases separated by wave barriers:
+//   E  lanes 0-2 of a group compute the start endpoint at t0 = r0 + {-s, 0, +s},
+//      lanes 3-5 the end endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint: blend,
+//      projected variance, pose Jacobian).  A neighbour's start terms depend on
+//      t0 only and its end terms on t1 only, so the 8 neighbours share these 6;
+//   C  lane j assembles neighbour j's info from its two endpoints, adds
+//      invCov_sum and takes the logdet (first failing LLT pivot kept, Q11);
+//   D  the group takes the first strict maximum over the valid neighbours (the
+//      reference's j-loop); no improvement finalises the line: invCov_sum +=
+//      info of the chosen ratio (re-assembled from the middle endpoints, the
+//      same arithmetic as the chosen candidate's), the cut ratio is stored and
+//      the next line opens at (0, 0).
+// The metric that opens line m+1, logdet(invCov_sum), equals line m's final
+// metric whenever line m moved: invCov_sum' = (sum - info_m) + chosen has the
+// bits of the chosen candidate's own total chosen + (sum - info_m).  Only when a
+// line never moved and the sum did not come back bit-identical is it evaluated
+// (one extra "setup" iteration, lane 0 of the group).
 #define CUT_G 8   // sequences per wave (8 lanes each)
+
+__device__ __forceinline__ double nb_step(int j, int side, double st) {
+    // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
+    const int a = side == 0 ? ((j == 0 || j == 4 || j == 5) ? 1 : ((j == 1 || j == 6 || j == 7) ? -1 : 0))
+                            : ((j == 2 || j == 4 || j == 6) ? 1 : ((j == 3 || j == 5 || j == 7) ? -1 : 0));
+    return a > 0 ? st : (a < 0 ? -st : 0.0);
+}
+__device__ __forceinline__ int nb_slot(int j, int side) {   // endpoint slot: 0: -s, 1: 0, 2: +s
+    if (side == 0) return (j == 0 || j == 4 || j == 5) ? 2 : ((j == 1 || j == 6 || j == 7) ? 0 : 1);
+    return (j == 2 || j == 4 || j == 6) ? 2 : ((j == 3 || j == 5 || j == 7) ? 0 : 1);
+}
+__device__ __forceinline__ bool same_bits(double a, double b) {
+    return __double_as_longlong(a) == __double_as_longlong(b);
+}
 
 __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     __shared__ double sum[CUT_G][24];
-    __shared__ double chosen[CUT_G][24];
-    __shared__ double cand[CUT_G][8][22];
+    __shared__ double sumb[CUT_G][24];
+    __shared__ double ep[CUT_G][6][8];
     __shared__ double val[CUT_G][8];
     __shared__ int vld[CUT_G][8];
     const int lane = threadIdx.x;
@@ -209,63 +260,83 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
     const double* scr_l = p.scr.cut_ls + (size_t)(live ? b : 0) * p.mls_cap * 21;
-    double Dl[16];
+    double Dl[12];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) Dl[i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
-    for (int e = j; e < 21; e += 8) sum[g][e] = (live && nls > 0) ? p.scr.cut_sum[24 * b + e] : 0.0;
+    for (int i = 0; i < 12; ++i) Dl[i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
-    const double nb0 = (j == 0 || j == 4 || j == 5) ? st : ((j == 1 || j == 6 || j == 7) ? -st : 0.0);
-    const double nb1 = (j == 2 || j == 4 || j == 6) ? st : ((j == 3 || j == 5 || j == 7) ? -st : 0.0);
+    // E role of this lane
+    const int eside = j < 3 ? 0 : 1;
+    const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
+    // C role: neighbour j
+    const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
+    const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
     // group state (identical in the 8 lanes of a group)
-    int m = 0;            // current line (list position)
-    int setup = 1;        // 1: score invCov_sum for line m; 0: greedy step
-    double r0 = 0.0, r1 = 0.0, mb = 0.0;
+    int m = 0;
+    int setup = 0;       // 1: this iteration evaluates logdet(invCov_sum) only
+    int moved = 0;
+    double r0 = 0.0, r1 = 0.0, mb = 0.0, mb_init = 0.0;
     LineCutData d;
+    if (m < nls) {
+        load_line(L, lb + mls[m], d);
+        for (int e = j; e < 21; e += 8) {
+            const double s0 = p.scr.cut_sum[24 * b + e];
+            sumb[g][e] = s0;
+            sum[g][e] = s0 - scr_l[e];
+        }
+        mb = p.scr.cut_sum[24 * b + 21];   // logdet(invCov_sum) from k_cut_prep
+        mb_init = mb;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { d.sP[k] = 0.0; d.eP[k] = 1.0; }
+        for (int k = 0; k < 3; ++k) { d.sP[k] = 0.0; d.eP[k] = 1.0; }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) { d.covS[k] = 0.0; d.covE[k] = 0.0; }
-    d.Jl[0] = 0.0; d.Jl[1] = 0.0;
-    if (m < nls) load_line(L, lb + mls[m], d);
+        for (int k = 0; k < 9; ++k) { d.covS[k] = 0.0; d.covE[k] = 0.0; }
+        d.Jl[0] = 0.0; d.Jl[1] = 0.0;
+    }
     __syncthreads();
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- evaluation: one logdet per lane, branch-free over setup/step
-        const double t0 = r0 + nb0, t1 = r1 + nb1;
-        int valid = 1;
-        if (t0 + t1 > 1.0) valid = 0;
-        if (t0 < rlo || t0 > rhi) valid = 0;
-        if (t1 < rlo || t1 > rhi) valid = 0;
-        double tmp[21];
-        poseInfoOnLine<false>(cam, homog, Dl, d, t0, t1, tmp);
-        double tot[21];
+        // ---- E: the six endpoints of this step
+        if (j < 6) {
+            const double t = (eside == 0 ? r0 : r1) + eoff;
+            double out[7];
+            if (eside == 0) cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, t, out);
+            else cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, t, out);
 #pragma unroll
-        for (int i = 0; i < 21; ++i) tot[i] = setup ? sum[g][i] : tmp[i] + sum[g][i];
-        const double v = logdet6_lower(tot);
-        if (act) {
-            val[g][j] = v;
-            vld[g][j] = setup ? (j == 0) : valid;
-            if (!setup) {
+            for (int i = 0; i < 7; ++i) ep[g][j][i] = out[i];
+        }
+        __syncthreads();
+        // ---- C: neighbour j (or the setup logdet)
+        {
+            const double t0 = r0 + nb0, t1 = r1 + nb1;
+            int valid = 1;
+            if (t0 + t1 > 1.0) valid = 0;
+            if (t0 < rlo || t0 > rhi) valid = 0;
+            if (t1 < rlo || t1 > rhi) valid = 0;
+            double tot[21];
+            if (setup) {
 #pragma unroll
-                for (int i = 0; i < 21; ++i) cand[g][j][i] = tmp[i];
+                for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
+            } else {
+                double tmp[21];
+                cut_assemble<false>(ep[g][cs], ep[g][ce], tmp);
+#pragma unroll
+                for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
+            }
+            const double v = logdet6_lower(tot);
+            if (act) {
+                val[g][j] = v;
+                vld[g][j] = setup ? 0 : valid;
             }
         }
         __syncthreads();
-        // ---- group decision (all 8 lanes compute it identically)
-        int finalize = 0;
+        // ---- D: group decision (all 8 lanes compute it identically)
+        int finalize = 0, stale_mid = 0;
         if (act) {
             if (setup) {
                 mb = val[g][0];
-                // invCov_sum -= invCovPose(line m) (r = 0,0); chosen starts as that info
-                for (int e = j; e < 21; e += 8) {
-                    const double li = scr_l[(size_t)m * 21 + e];
-                    sum[g][e] = sum[g][e] - li;
-                    chosen[g][e] = li;
-                }
+                mb_init = mb;
                 setup = 0;
-                r0 = 0.0; r1 = 0.0;
             } else {
                 double mi = mb;
                 int best = -1;
@@ -273,30 +344,63 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 for (int jj = 0; jj < 8; ++jj)
                     if (vld[g][jj] && val[g][jj] > mi) { mi = val[g][jj]; best = jj; }
                 if (best >= 0) {
-                    const double bb0 = (best == 0 || best == 4 || best == 5) ? st : ((best == 1 || best == 6 || best == 7) ? -st : 0.0);
-                    const double bb1 = (best == 2 || best == 4 || best == 6) ? st : ((best == 3 || best == 5 || best == 7) ? -st : 0.0);
-                    r0 = r0 + bb0;
-                    r1 = r1 + bb1;
+                    r0 = r0 + nb_step(best, 0, st);
+                    r1 = r1 + nb_step(best, 1, st);
                     mb = mi;
-                    for (int e = j; e < 21; e += 8) chosen[g][e] = cand[g][best][e];
-                    if (!(r0 + r1 <= 1.0)) finalize = 1;   // while-condition
+                    moved = 1;
+                    if (!(r0 + r1 <= 1.0)) { finalize = 1; stale_mid = 1; }   // while-condition
                 } else {
-                    finalize = 1;
+                    finalize = 1;   // the middle endpoints of this step are (r0 + 0, r1 + 0) = (r0, r1)
                 }
             }
         }
-        __syncthreads();
         if (act && finalize) {
-            // invCov_sum += invCovPose(final); record the cut ratio
-            for (int e = j; e < 21; e += 8) sum[g][e] = sum[g][e] + chosen[g][e];
+            // invCov_sum += info of the chosen ratio
+            double S7[7], E7[7];
+            if (!stale_mid) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) { S7[i] = ep[g][1][i]; E7[i] = ep[g][4][i]; }
+            } else {
+                cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, r0, S7);
+                cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, r1, E7);
+            }
+            double info[21];
+            cut_assemble<false>(S7, E7, info);
+            int differs = 0;
+#pragma unroll
+            for (int e = 0; e < 21; ++e) {   // lane j owns entries j, j+8, j+16 (compile-time register index)
+                if ((e & 7) == j) {
+                    const double ns = sum[g][e] + info[e];
+                    differs |= same_bits(ns, sumb[g][e]) ? 0 : 1;
+                    sum[g][e] = ns;
+                }
+            }
+            // group-level "the sum came back bit-identical" (consulted only if the line never moved)
+            const unsigned long long bad = __ballot(differs);
+            const bool same = ((bad >> (8 * g)) & 0xFFull) == 0;
             if (j == 0) {
                 const size_t q = lb + mls[m];
                 L.cut[2 * q] = r0;
                 L.cut[2 * q + 1] = r1;
             }
             ++m;
-            setup = 1;
-            if (m < nls) load_line(L, lb + mls[m], d);
+            if (m < nls) {
+                if (!moved) {
+                    if (same) mb = mb_init;   // logdet of a bit-identical sum
+                    else setup = 1;           // evaluated next iteration
+                }
+                moved = 0;
+                r0 = 0.0;
+                r1 = 0.0;
+                load_line(L, lb + mls[m], d);
+                // open line m: sumb = invCov_sum, sum = invCov_sum - info(line m, r = 0)
+                for (int e = j; e < 21; e += 8) {
+                    const double s0 = sum[g][e];
+                    sumb[g][e] = s0;
+                    sum[g][e] = s0 - scr_l[(size_t)m * 21 + e];
+                }
+                if (!setup) mb_init = mb;
+            }
         }
         __syncthreads();
     }

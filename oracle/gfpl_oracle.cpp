@@ -1238,7 +1238,7 @@ struct gfplo_handler {
                 if (!same) g_cut_stats[5]++;   // setup logdet really needed
             }
             std::memcpy(sum_before, sum, sizeof sum);
-            std::vector<std::pair<uint64_t, uint64_t>> seen;
+            std::vector<std::pair<uint64_t, uint64_t>> seen, last_step, this_step;
             bool moved = false;
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] - L.invCov[i];
             while (L.cut[0] + L.cut[1] <= 1.0) {
@@ -1247,6 +1247,7 @@ struct gfplo_handler {
                 double cand_info[36];
                 double metric_init = metric_back;
                 g_cut_stats[1]++;   // steps
+                this_step.clear();
                 for (int j = 0; j < 8; ++j) {
                     double rt[2] = {L.cut[0] + nb[j][0], L.cut[1] + nb[j][1]};
                     if (rt[0] + rt[1] > 1.0) continue;
@@ -1258,6 +1259,11 @@ struct gfplo_handler {
                     bool dup = false;
                     for (auto& pr : seen) dup = dup || (pr.first == k0 && pr.second == k1);
                     if (!dup) { seen.push_back({k0, k1}); g_cut_stats[3]++; }   // distinct evaluations
+                    // history limited to the previous step's evaluations
+                    bool dup1 = false;
+                    for (auto& pr : last_step) dup1 = dup1 || (pr.first == k0 && pr.second == k1);
+                    if (!dup1) g_cut_stats[6]++;
+                    this_step.push_back({k0, k1});
                     double tmp[36], tot[36];
                     poseInfoOnLine(DT_inv, Jl, L, rt, tmp);
                     for (int i = 0; i < 36; ++i) tot[i] = tmp[i] + sum[i];
@@ -1269,6 +1275,7 @@ struct gfplo_handler {
                         hit = true;
                     }
                 }
+                last_step = this_step;
                 if (hit) {
                     L.cut[0] = cand[0]; L.cut[1] = cand[1];
                     std::memcpy(L.invCov, cand_info, sizeof cand_info);
