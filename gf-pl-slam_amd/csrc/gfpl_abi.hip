@@ -12,6 +12,8 @@
 
 using namespace gfpl;
 
+#define GFPL_NEV 10   // timing marks: 0-6 stages, 7 after k_cut_prep, 8 after k_cut_search, 9 after k_pose
+
 struct gfpl_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -19,7 +21,7 @@ struct gfpl_ctx {
     gfpl_config cfg{};
     bool has_cam = false, has_cfg = false;
     bool timing = false;
-    hipEvent_t ev[8]{};
+    hipEvent_t ev[GFPL_NEV]{};
     float stage_ms[7]{};
 };
 
@@ -171,7 +173,7 @@ int gfpl_create(int device, void* stream, gfpl_ctx** out) {
     c->stream = (hipStream_t)stream;
     gfpl_config_default(&c->cfg);
     c->has_cfg = true;
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < GFPL_NEV; ++i)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) { delete c; return GFPL_E_HIP; }
     *out = c;
     return GFPL_OK;
@@ -179,7 +181,7 @@ int gfpl_create(int device, void* stream, gfpl_ctx** out) {
 
 int gfpl_destroy(gfpl_ctx* c) {
     if (!c) return GFPL_E_INVALID;
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < GFPL_NEV; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
     return GFPL_OK;
@@ -317,7 +319,7 @@ int gfpl_cross_lines(gfpl_seqbatch* sb) {
 int gfpl_line_cut(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
-    HIPCHK(launch_line_cut(params(sb, nullptr), sb->ctx->stream));
+    HIPCHK(launch_line_cut(params(sb, nullptr), sb->ctx->stream, nullptr));
     return GFPL_OK;
 }
 
@@ -339,9 +341,10 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
     tmark(c, 3);
     HIPCHK(launch_cross_lines(p, c->stream));
     tmark(c, 4);
-    if (c->cfg.use_line_conf_cut) HIPCHK(launch_line_cut(p, c->stream));
-    tmark(c, 5);
+    if (c->cfg.use_line_conf_cut)
+        HIPCHK(launch_line_cut(p, c->stream, c->timing ? &c->ev[7] : nullptr));
     HIPCHK(launch_step_bytes(p, c->stream));
+    tmark(c, 5);
     sb->has_curr = true;
     return GFPL_OK;
 }
@@ -349,7 +352,7 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
 int gfpl_optimize_pose(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
-    HIPCHK(launch_pose(params(sb, nullptr), sb->ctx->stream));
+    HIPCHK(launch_pose(params(sb, nullptr), sb->ctx->stream, sb->ctx->timing ? sb->ctx->ev[9] : nullptr));
     tmark(sb->ctx, 6);
     return GFPL_OK;
 }
@@ -551,6 +554,36 @@ int gfpl_get_stage_times(gfpl_ctx* c, float* ms7) {
     HIPCHK(hipEventSynchronize(c->ev[6]));
     for (int i = 0; i < 6; ++i) HIPCHK(hipEventElapsedTime(&ms7[i], c->ev[i], c->ev[i + 1]));
     HIPCHK(hipEventElapsedTime(&ms7[6], c->ev[0], c->ev[6]));
+    return GFPL_OK;
+}
+
+int gfpl_get_kernel_times(gfpl_ctx* c, float* ms4) {
+    if (!c || !ms4) return GFPL_E_INVALID;
+    if (!c->timing) return GFPL_E_STATE;
+    if (!c->cfg.use_line_conf_cut) return GFPL_E_STATE;   // no cut kernels were marked
+    HIPCHK(hipEventSynchronize(c->ev[6]));
+    HIPCHK(hipEventElapsedTime(&ms4[0], c->ev[4], c->ev[7]));   // k_cut_prep
+    HIPCHK(hipEventElapsedTime(&ms4[1], c->ev[7], c->ev[8]));   // k_cut_search
+    HIPCHK(hipEventElapsedTime(&ms4[2], c->ev[8], c->ev[5]));   // k_cut_finish (+ k_step_bytes)
+    HIPCHK(hipEventElapsedTime(&ms4[3], c->ev[5], c->ev[9]));   // k_pose
+    return GFPL_OK;
+}
+
+int gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4) {
+    if (!sb || !bytes4) return GFPL_E_INVALID;
+    std::vector<int64_t> v((size_t)sb->B * 8);
+    HIPCHK(hipStreamSynchronize(sb->ctx->stream));
+    HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost));
+    int64_t t = 0;
+    for (int b = 0; b < sb->B; ++b) t += v[(size_t)b * 8 + 7];
+    // k_cut_search bytes are recorded per sequence; the other three are the
+    // stage bytes split as documented in k_step_bytes
+    bytes4[1] = t;
+    int64_t st[7];
+    int e = gfpl_last_step_stage_bytes(sb, st);
+    if (e) return e;
+    bytes4[0] = bytes4[2] = -1;   // not split out
+    bytes4[3] = st[5];
     return GFPL_OK;
 }
 

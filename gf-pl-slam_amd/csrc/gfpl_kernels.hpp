@@ -12,8 +12,8 @@ hipError_t launch_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int c
                        hipStream_t s);
 hipError_t launch_cross_points(const KParams& p, hipStream_t s);
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s);
-hipError_t launch_line_cut(const KParams& p, hipStream_t s);
-hipError_t launch_pose(const KParams& p, hipStream_t s);
+hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks /* [2] or null */);
+hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark /* or null */);
 hipError_t launch_step_bytes(const KParams& p, hipStream_t s);
 
 size_t stereo_lines_lds(int cap);

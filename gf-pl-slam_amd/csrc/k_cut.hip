@@ -451,9 +451,11 @@ __global__ void __launch_bounds__(64) k_cut_finish(KParams p) {
     }
 }
 
-hipError_t launch_line_cut(const KParams& p, hipStream_t s) {
+hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
     hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
+    if (marks) (void)hipEventRecord(marks[0], s);
     hipLaunchKernelGGL(k_cut_search, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+    if (marks) (void)hipEventRecord(marks[1], s);
     hipLaunchKernelGGL(k_cut_finish, dim3(p.B), dim3(64), 0, s, p);
     return hipGetLastError();
 }

@@ -450,12 +450,13 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
     CP.err_norm[b] = err_norm;
 }
 
-hipError_t launch_pose(const KParams& p, hipStream_t s) {
+hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
     const size_t region = (size_t)std::max(16 * 64, p.mpt_cap + p.mls_cap);
     const size_t lds = (region + NP2) * 8 + (p.mpt_cap + p.mls_cap) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
+    if (mark) (void)hipEventRecord(mark, s);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     return hipGetLastError();
 }

@@ -635,6 +635,10 @@ __global__ void k_step_bytes(KParams p) {
     int64_t tot = 0;
     for (int i = 0; i < 6; ++i) { p.scr.bytes[8 * b + i] = st[i]; tot += st[i]; }
     p.scr.bytes[8 * b + 6] = tot;
+    // k_cut_search alone: per matched line its cut inputs (sP eP covS covE le_obs
+    // 208 B + index 4 B), its r = 0 info from k_cut_prep (168 B), the cut ratio
+    // written (16 B); per sequence invCov_sum + metric + DT_inv (272 B)
+    p.scr.bytes[8 * b + 7] = (p.cfg.use_line_conf_cut && Ml > 0) ? 396 * Ml + 272 : 0;
 }
 
 // ------------------------------------------------------------ launchers --

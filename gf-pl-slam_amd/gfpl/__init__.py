@@ -200,6 +200,8 @@ def hiplib() -> C.CDLL:
             "gfpl_write_track": ([P, C.c_int, P], C.c_int),
             "gfpl_set_timing": ([P, C.c_int], C.c_int),
             "gfpl_get_stage_times": ([P, P], C.c_int),
+            "gfpl_get_kernel_times": ([P, P], C.c_int),
+            "gfpl_last_step_kernel_bytes": ([P, P], C.c_int),
             "gfpl_last_step_bytes": ([P, P], C.c_int),
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_strerror": ([C.c_int], C.c_char_p),
@@ -441,6 +443,12 @@ class Context:
         check(self.L.gfpl_get_stage_times(self.h, out.ctypes.data), "stage_times")
         return out
 
+    def kernel_times(self) -> np.ndarray:
+        """[k_cut_prep, k_cut_search, k_cut_finish, k_pose] device ms of the last step."""
+        out = np.zeros(4, np.float32)
+        check(self.L.gfpl_get_kernel_times(self.h, out.ctypes.data), "kernel_times")
+        return out
+
     def knn2(self, q_dev, nq: int, t_dev, nt: int, cell: int, idx_dev, dist_dev) -> int:
         return self.L.gfpl_knn2_hamming(self.h, _ptr(q_dev), nq, _ptr(t_dev), nt, cell,
                                         _ptr(idx_dev), _ptr(dist_dev))
@@ -528,6 +536,11 @@ class StereoFrameHandler:
     def last_step_stage_bytes(self) -> np.ndarray:
         v = np.zeros(7, np.int64)
         check(self.L.gfpl_last_step_stage_bytes(self.h, v.ctypes.data), "last_step_stage_bytes")
+        return v
+
+    def last_step_kernel_bytes(self) -> np.ndarray:
+        v = np.zeros(4, np.int64)
+        check(self.L.gfpl_last_step_kernel_bytes(self.h, v.ctypes.data), "last_step_kernel_bytes")
         return v
 
     def nbytes(self) -> int:

@@ -290,6 +290,12 @@ int  gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes);
 /* ... per stage: [stereo_points, stereo_lines, cross_points, cross_lines,
  * line_cut, pose, total] (DESIGN.md §Roofline gives each stage's formula). */
 int  gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7);
+/* Per-kernel view of the dominant stages (timing enabled, line cut on):
+ * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
+ * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same
+ * kernels (-1 where not split out: DESIGN.md §4).                              */
+int  gfpl_get_kernel_times(gfpl_ctx* ctx, float* ms4);
+int  gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4);
 
 const char* gfpl_strerror(int code);
 
