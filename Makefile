@@ -18,7 +18,9 @@ ORACLEFLAGS := $(CXXFLAGS) -march=x86-64-v3
 HIP_SRC  := $(wildcard $(PKG)/csrc/*.hip) $(wildcard $(PKG)/csrc/*.cpp)
 HIP_HDR  := $(wildcard $(PKG)/csrc/*.hpp) include/gfpl.h
 
-all: $(LIBDIR)/libgfpl_hip.so $(LIBDIR)/libgfpl_synth.so oracle/liboracle.so
+BINDIR   := $(PKG)/bin
+
+all: $(LIBDIR)/libgfpl_hip.so $(LIBDIR)/libgfpl_synth.so oracle/liboracle.so $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu
 
 $(LIBDIR)/libgfpl_hip.so: $(HIP_SRC) $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
@@ -28,14 +30,25 @@ $(LIBDIR)/libgfpl_synth.so: $(PKG)/synth/gfpl_synth.cpp $(PKG)/synth/gfpl_synth.
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(CXXFLAGS) -march=x86-64-v3 $< -o $@ -lpthread
 
+# C++ host mirror of the reference's StVO classes over the C ABI, and the
+# app/plslam_mod.cpp-style driver (both plain g++; no HIP headers needed)
+$(LIBDIR)/libgfpl_stvo.so: $(PKG)/host/stvo.cpp $(PKG)/host/stvo.h include/gfpl.h $(LIBDIR)/libgfpl_hip.so
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lgfpl_hip -Wl,-rpath,'$$ORIGIN'
+
+$(BINDIR)/plslam_gpu: $(PKG)/host/plslam_gpu.cpp $(LIBDIR)/libgfpl_stvo.so $(LIBDIR)/libgfpl_synth.so
+	@mkdir -p $(BINDIR)
+	$(CXX) -O2 -std=c++17 -ffp-contract=off -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lgfpl_stvo -lgfpl_hip -l:libgfpl_synth.so -lpthread \
+	    -Wl,-rpath,'$$ORIGIN/../lib'
+
 oracle/liboracle.so: oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h include/gfpl.h
 	$(CXX) $(ORACLEFLAGS) $< -o $@
 
 oracle: oracle/liboracle.so
 synth: $(LIBDIR)/libgfpl_synth.so
 hip: $(LIBDIR)/libgfpl_hip.so
+host: $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu
 
 clean:
-	rm -f $(LIBDIR)/*.so oracle/liboracle.so
+	rm -f $(LIBDIR)/*.so oracle/liboracle.so $(BINDIR)/plslam_gpu
 
-.PHONY: all clean oracle synth hip
+.PHONY: all clean oracle synth hip host

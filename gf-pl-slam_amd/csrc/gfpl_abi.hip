@@ -36,6 +36,8 @@ struct gfpl_seqbatch {
     bool has_curr = false;
     DevTrack tr{};
     DevScratch scr{};
+    void* stage = nullptr;   // device staging of one uploaded input batch (gfpl_upload_frames)
+    size_t stage_bytes = 0;
 };
 
 namespace {
@@ -107,6 +109,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_err = c.take<double>(B);
     sb->scr.pose_ok = c.take<int32_t>(B);
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
+    sb->scr.pose_dtini = c.take<double>(B * 16);
 }
 
 DevCam devcam(const gfpl_camera& c) {
@@ -257,6 +260,7 @@ int gfpl_seqbatch_destroy(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     (void)hipStreamSynchronize(sb->ctx->stream);
     if (sb->base) (void)hipFree(sb->base);
+    if (sb->stage) (void)hipFree(sb->stage);
     delete sb;
     return GFPL_OK;
 }
@@ -357,9 +361,65 @@ int gfpl_optimize_pose(gfpl_seqbatch* sb) {
     return GFPL_OK;
 }
 
+int gfpl_optimize_pose_ini(gfpl_seqbatch* sb, const double* dt_ini) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!dt_ini) return gfpl_optimize_pose(sb);
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(hipMemcpyAsync(sb->scr.pose_dtini, dt_ini, sizeof(double) * 16 * (size_t)sb->B, hipMemcpyHostToDevice,
+                          sb->ctx->stream));
+    KParams p = params(sb, nullptr);
+    p.dt_ini = sb->scr.pose_dtini;
+    HIPCHK(launch_pose(p, sb->ctx->stream, sb->ctx->timing ? sb->ctx->ev[9] : nullptr));
+    tmark(sb->ctx, 6);
+    HIPCHK(hipStreamSynchronize(sb->ctx->stream));   // the caller's buffer may be reused on return
+    return GFPL_OK;
+}
+
+int gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* dev) {
+    if (!sb || !host || !dev) return GFPL_E_INVALID;
+    if (host->batch != sb->B || host->kp_cap != sb->kp_cap || host->kl_cap != sb->kl_cap) return GFPL_E_INVALID;
+    const size_t B = sb->B, P = B * sb->kp_cap, L = B * sb->kl_cap;
+    const size_t pyr = B * (size_t)sb->ctx->cam.pyr_bytes;
+    Carver c;
+    auto layout = [&](gfpl_frames& f) {
+        f.batch = host->batch; f.kp_cap = host->kp_cap; f.kl_cap = host->kl_cap;
+        f.n_kp_l = c.take<int>(B); f.n_kp_r = c.take<int>(B);
+        f.kp_l = c.take<gfpl_keypoint>(P); f.kp_r = c.take<gfpl_keypoint>(P);
+        f.pdesc_l = c.take<uint8_t>(P * 32); f.pdesc_r = c.take<uint8_t>(P * 32);
+        f.n_kl_l = c.take<int>(B); f.n_kl_r = c.take<int>(B);
+        f.kl_l = c.take<gfpl_keyline>(L); f.kl_r = c.take<gfpl_keyline>(L);
+        f.ldesc_l = c.take<uint8_t>(L * 32); f.ldesc_r = c.take<uint8_t>(L * 32);
+        f.pyr_r = c.take<uint8_t>(pyr); f.time_stamp = c.take<double>(B);
+    };
+    gfpl_frames d{};
+    layout(d);   // sizing pass (base == nullptr)
+    if (sb->stage_bytes < c.off) {
+        if (sb->stage) (void)hipFree(sb->stage);
+        sb->stage = nullptr;
+        sb->stage_bytes = 0;
+        HIPCHK(hipMalloc(&sb->stage, c.off));
+        sb->stage_bytes = c.off;
+    }
+    c.off = 0;
+    c.base = (char*)sb->stage;
+    layout(d);
+    hipStream_t s = sb->ctx->stream;
+#define UP(field, n) HIPCHK(hipMemcpyAsync((void*)d.field, host->field, sizeof(*d.field) * (n), hipMemcpyHostToDevice, s))
+    UP(n_kp_l, B); UP(n_kp_r, B); UP(kp_l, P); UP(kp_r, P); UP(pdesc_l, P * 32); UP(pdesc_r, P * 32);
+    UP(n_kl_l, B); UP(n_kl_r, B); UP(kl_l, L); UP(kl_r, L); UP(ldesc_l, L * 32); UP(ldesc_r, L * 32);
+    UP(pyr_r, pyr); UP(time_stamp, B);
+#undef UP
+    HIPCHK(hipStreamSynchronize(s));
+    *dev = d;
+    return GFPL_OK;
+}
+
 int gfpl_update_frame(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    // matched_pt.clear(); matched_ls.clear() (src/stereoFrameHandler.cpp:889-890)
+    HIPCHK(hipMemsetAsync(sb->tr.n_matched_pt, 0, sizeof(int32_t) * sb->B, sb->ctx->stream));
+    HIPCHK(hipMemsetAsync(sb->tr.n_matched_ls, 0, sizeof(int32_t) * sb->B, sb->ctx->stream));
     sb->prev_slot = 1 - sb->prev_slot;
     sb->has_curr = false;
     return GFPL_OK;

@@ -78,6 +78,7 @@ struct DevScratch {
     double* pose_err;  // [B]
     int32_t* pose_ok;  // [B] 1: stage-2 result usable
     double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
+    double* pose_dtini; // [B*16] staging of gfpl_optimize_pose_ini's DT_ini
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).
@@ -89,6 +90,7 @@ struct KParams {
     DevScratch scr;
     gfpl_frames in;       // device pointers of the current input batch
     int B, kp_cap, kl_cap, mpt_cap, mls_cap;
+    const double* dt_ini; // [B*16] explicit GN initial guesses (optimizePose(DT_ini)); null: prev.DT
 };
 
 }  // namespace gfpl

@@ -238,7 +238,10 @@ __global__ void __launch_bounds__(64) k_pose(KParams p, int NP2) {
     double* pin = p.scr.pose_in + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
     double* lin = pin + PT_K * p.mpt_cap;
     X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
-    if (lane < 16) { S.DTini[lane] = PP.DT[16 * b + lane]; S.DT[lane] = S.DTini[lane]; }   // Q2
+    if (lane < 16) {   // Q2: the app passes prev_frame->DT (app/plslam_mod.cpp:408)
+        S.DTini[lane] = p.dt_ini ? p.dt_ini[16 * b + lane] : PP.DT[16 * b + lane];
+        S.DT[lane] = S.DTini[lane];
+    }
     if (lane == 0) S.ninl = p.tr.n_inliers[b];
     // gather the matched lists once (lane l owns positions l, l+64, ...)
     int cpn = 0, cln = 0;

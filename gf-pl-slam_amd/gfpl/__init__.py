@@ -185,6 +185,7 @@ def hiplib() -> C.CDLL:
             "gfpl_initialize": ([P, P], C.c_int),
             "gfpl_insert_stereo_pair": ([P, P], C.c_int),
             "gfpl_optimize_pose": ([P], C.c_int),
+            "gfpl_optimize_pose_ini": ([P, P], C.c_int),
             "gfpl_update_frame": ([P], C.c_int),
             "gfpl_frame_step": ([P, P], C.c_int),
             "gfpl_stereo_points": ([P, P], C.c_int),
@@ -483,8 +484,15 @@ class StereoFrameHandler:
     def insertStereoPair(self, fr: Frames):
         check(self.L.gfpl_insert_stereo_pair(self.h, C.byref(fr)), "insert_stereo_pair")
 
-    def optimizePose(self):
-        check(self.L.gfpl_optimize_pose(self.h), "optimize_pose")
+    def optimizePose(self, DT_ini=None):
+        """optimizePose(prev_frame->DT) (the app's call, Q2), or optimizePose(Matrix4d DT_ini)
+        with DT_ini a 4x4 (all sequences) or [B,4,4] host array."""
+        if DT_ini is None:
+            check(self.L.gfpl_optimize_pose(self.h), "optimize_pose")
+            return
+        d = np.asarray(DT_ini, dtype=np.float64)
+        d = np.ascontiguousarray(np.broadcast_to(d.reshape(-1, 4, 4), (self.B, 4, 4)))
+        check(self.L.gfpl_optimize_pose_ini(self.h, d.ctypes.data), "optimize_pose_ini")
 
     def updateFrame(self):
         check(self.L.gfpl_update_frame(self.h), "update_frame")

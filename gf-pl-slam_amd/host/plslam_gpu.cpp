@@ -1,0 +1,171 @@
+// plslam_gpu.cpp — the per-frame loop of app/plslam_mod.cpp:318-515 over the
+// StVO host mirror, on synthetic stereo detections (gfpl_synth), GPU only.
+//
+//   plslam_gpu [--camera vga|euroc|kitti|stress] [--frames N] [--seq S] [--out PREFIX] [--json]
+//
+// Per frame: initialize (frame 0) or insertStereoPair -> optimizePose(prev_frame->DT)
+// -> numFrameLoss check -> updateFrame_ECCV18(T_base), then the trajectory line of
+// PREFIX_AllFrameTrajectory.txt in the reference's format (app/plslam_mod.cpp:288-293,
+// 480-493: fixed, setprecision(7), " tx ty tz qx qy qz qw" of R^T).  Mapping / keyframes
+// are out of scope.  --json prints one line per frame with the pose bits, for the
+// parity test that compares this binary against the CPU oracle.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../synth/gfpl_synth.h"
+#include "stvo.h"
+
+using namespace StVO;
+
+// Eigen::Quaterniond(const Matrix3d&) (Eigen/src/Geometry/Quaternion.h, quaternionbase_assign_impl)
+// as used by toQuaternion (src/auxiliar.cpp:38-50): x, y, z, w
+static std::vector<float> toQuaternion(const Matrix3d& M) {
+    double q[4];   // x y z w
+    const double t = (M(0, 0) + M(1, 1)) + M(2, 2);
+    if (t > 0.0) {
+        double s = std::sqrt(t + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (M(2, 1) - M(1, 2)) * s;
+        q[1] = (M(0, 2) - M(2, 0)) * s;
+        q[2] = (M(1, 0) - M(0, 1)) * s;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(((M(i, i) - M(j, j)) - M(k, k)) + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (M(k, j) - M(j, k)) * s;
+        q[j] = (M(j, i) + M(i, j)) * s;
+        q[k] = (M(k, i) + M(i, k)) * s;
+    }
+    return {(float)q[0], (float)q[1], (float)q[2], (float)q[3]};
+}
+
+struct CamDef { const char* name; int w, h; double fx, fy, cx, cy, b; };
+static const CamDef kCams[] = {
+    {"vga", 640, 480, 554.25626, 554.25626, 320.0, 240.0, 0.1},                       // config/gazebo_params.yaml
+    {"euroc", 752, 480, 458.654, 457.296, 367.215, 248.375, 0.110077842},             // config/euroc_params.yaml
+    {"kitti", 1241, 376, 718.856, 718.856, 607.1928, 185.2157, 0.537165719},          // config/kitti/kitti00-02.yaml
+    {"stress", 1920, 1080, 1662.76878, 1662.76878, 960.0, 540.0, 0.1},                // gazebo x3
+};
+
+static StereoFrame* make_frame(const gfpl_synth_params& sp, PinholeStereoCamera* cam, int seq, int k, int kp_cap,
+                               int kl_cap) {
+    int nkl, nkr, nll, nlr;
+    double ts;
+    std::vector<gfpl_keypoint> kl(kp_cap), kr(kp_cap);
+    std::vector<gfpl_keyline> ll(kl_cap), lr(kl_cap);
+    std::vector<uint8_t> pdl(32 * (size_t)kp_cap), pdr(32 * (size_t)kp_cap), ldl(32 * (size_t)kl_cap),
+        ldr(32 * (size_t)kl_cap), pyr((size_t)cam->pyramidBytes());
+    if (gfpl_synth_frame(&sp, &cam->abi(), seq, k, kp_cap, kl_cap, &nkl, &nkr, kl.data(), kr.data(), pdl.data(),
+                         pdr.data(), &nll, &nlr, ll.data(), lr.data(), ldl.data(), ldr.data(), pyr.data(), &ts,
+                         nullptr) != 0)
+        throw std::runtime_error("gfpl_synth_frame failed");
+    auto kps = [](const std::vector<gfpl_keypoint>& v, int n) {
+        std::vector<KeyPoint> o(n);
+        for (int i = 0; i < n; ++i) o[i] = {v[i].x, v[i].y, v[i].octave};
+        return o;
+    };
+    auto kls = [](const std::vector<gfpl_keyline>& v, int n) {
+        std::vector<KeyLine> o(n);
+        for (int i = 0; i < n; ++i) o[i] = {v[i].sx, v[i].sy, v[i].ex, v[i].ey, v[i].angle, v[i].octave};
+        return o;
+    };
+    auto rows = [](const std::vector<uint8_t>& v, int n) {
+        std::vector<Descriptor> o(n);
+        for (int i = 0; i < n; ++i) std::memcpy(o[i].data(), &v[32 * (size_t)i], 32);
+        return o;
+    };
+    return new StereoFrame(k, cam, ts, kps(kl, nkl), kps(kr, nkr), rows(pdl, nkl), rows(pdr, nkr), kls(ll, nll),
+                           kls(lr, nlr), rows(ldl, nll), rows(ldr, nlr), std::move(pyr));
+}
+
+static int run(int argc, char** argv) {
+    std::string camname = "vga", out;
+    int frames = 10, seq = 0;
+    bool json = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> std::string {
+            if (i + 1 >= argc) throw std::invalid_argument("missing value for " + a);
+            return argv[++i];
+        };
+        if (a == "--camera") camname = next();
+        else if (a == "--frames") frames = std::stoi(next());
+        else if (a == "--seq") seq = std::stoi(next());
+        else if (a == "--out") out = next();
+        else if (a == "--json") json = true;
+        else { std::cerr << "unknown option " << a << "\n"; return 2; }
+    }
+    const CamDef* cd = nullptr;
+    for (const auto& c : kCams)
+        if (camname == c.name) cd = &c;
+    if (!cd) { std::cerr << "unknown camera " << camname << "\n"; return 2; }
+    PinholeStereoCamera cam(cd->w, cd->h, cd->fx, cd->fy, cd->cx, cd->cy, cd->b);
+    gfpl_synth_params sp;
+    gfpl_synth_default(&sp);
+    if (camname == "kitti") { sp.dt = 0.1; sp.v_fwd = 8.0; sp.z_min = 4.0; sp.z_max = 40.0; }
+    const int kp_cap = 2048, kl_cap = 512;
+
+    std::ofstream fAllFrameTrack;
+    if (!out.empty()) {
+        fAllFrameTrack.open(out + "_AllFrameTrajectory.txt");
+        fAllFrameTrack << std::fixed;
+        fAllFrameTrack << "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" << std::endl;
+    }
+    StereoFrameHandler* StVO = new StereoFrameHandler(&cam, 0, kp_cap, kl_cap);
+    const Matrix4d T_base = Matrix4d::Identity();
+    for (int k = 0; k < frames; ++k) {
+        StereoFrame* f = make_frame(sp, &cam, seq, k, kp_cap, kl_cap);
+        if (k == 0) {
+            StVO->initialize(f);
+            continue;
+        }
+        StVO->insertStereoPair(f);
+        const int mpt = (int)StVO->matched_pt.size(), mls = (int)StVO->matched_ls.size();
+        StVO->optimizePose(StVO->prev_frame->DT);
+        if (json) {
+            const StereoFrame* c = StVO->curr_frame;
+            std::printf("{\"frame\": %d, \"n_pt\": %zu, \"n_ls\": %zu, \"matched_pt\": %d, \"matched_ls\": %d, "
+                        "\"n_inliers\": %d, \"num_frame_loss\": %d, \"err_norm\": %.17g, \"Tfw\": [",
+                        k, c->stereo_pt.size(), c->stereo_ls.size(), mpt, mls, StVO->n_inliers, StVO->numFrameLoss,
+                        c->err_norm);
+            for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->Tfw.v[i]);
+            std::printf("]}\n");
+        }
+        if (StVO->numFrameLoss > 10) {   // Config::maxNumFrameLoss() (src/config.cpp)
+            std::cerr << "Early termination due to track loss!" << std::endl;
+            break;
+        }
+        StVO->updateFrame_ECCV18(T_base);
+        if (!out.empty() && !StVO->vec_all_frame_pose.empty()) {
+            const Matrix4d& Tfw = StVO->vec_all_frame_pose.back();
+            Matrix3d R;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) R(i, j) = Tfw(j, i);   // Tfw.block(0,0,3,3).transpose()
+            const std::vector<float> q = toQuaternion(R);
+            fAllFrameTrack << std::setprecision(7) << " " << Tfw(0, 3) << " " << Tfw(1, 3) << " " << Tfw(2, 3) << " "
+                           << q[0] << " " << q[1] << " " << q[2] << " " << q[3] << std::endl;
+        }
+    }
+    delete StVO;
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    try {
+        return run(argc, argv);
+    } catch (const std::exception& e) {
+        std::cerr << "plslam_gpu: " << e.what() << std::endl;
+        return 1;
+    }
+}

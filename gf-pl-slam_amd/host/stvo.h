@@ -1,0 +1,258 @@
+// stvo.h — C++ host mirror of the reference's tracking API (namespace StVO) over
+// the MI355X C ABI (include/gfpl.h).
+//
+// The reference's per-frame path lives behind StVO::StereoFrame and
+// StVO::StereoFrameHandler (include/stereoFrame.h:89-260,
+// include/stereoFrameHandler.h:38-174 of SimonsRoad/gf-pl-slam).  This header
+// keeps the names, public members and call order a caller such as
+// app/plslam_mod.cpp:375-477, KeyFrame (src/keyFrame.cpp:26-58) or MapHandler
+// relies on, with these deliberate differences:
+//  * detection is out of scope: a StereoFrame is built from injected keypoints,
+//    keylines, descriptors and the right ORB pyramid (the reference's own
+//    simulator does the same through public members, src/simulate_line_cut.cpp:62-212);
+//  * Eigen / OpenCV are not available: Vector*/Matrix* are small row-major value
+//    types with the same element access (operator()), KeyPoint/KeyLine carry the
+//    fields the path reads;
+//  * the handler owns its frames and features (the reference leaks features);
+//  * every compute call runs on the GPU through the C ABI; there is no CPU path.
+//    After each call the host objects are refreshed from HBM so the public
+//    members read exactly like the reference's (matched_pt / matched_ls point into
+//    prev_frame->stereo_pt / stereo_ls, mutated in place).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <list>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/gfpl.h"
+
+namespace StVO {
+
+// ------------------------------------------------------------ value types --
+template <int R, int C>
+struct Mat {
+    double v[R * C] = {};
+    double& operator()(int i, int j) { return v[i * C + j]; }
+    double operator()(int i, int j) const { return v[i * C + j]; }
+    double& operator()(int i) { return v[i]; }
+    double operator()(int i) const { return v[i]; }
+    double* data() { return v; }
+    const double* data() const { return v; }
+    static Mat Identity() {
+        Mat m;
+        for (int i = 0; i < (R < C ? R : C); ++i) m(i, i) = 1.0;
+        return m;
+    }
+    static Mat Zero() { return Mat(); }
+    bool operator==(const Mat& o) const {
+        for (int i = 0; i < R * C; ++i)
+            if (v[i] != o.v[i]) return false;
+        return true;
+    }
+};
+using Vector2d = Mat<2, 1>;
+using Vector3d = Mat<3, 1>;
+using Vector6d = Mat<6, 1>;
+using Matrix3d = Mat<3, 3>;
+using Matrix4d = Mat<4, 4>;
+using Matrix6d = Mat<6, 6>;
+Matrix4d operator*(const Matrix4d& a, const Matrix4d& b);
+
+// cv::KeyPoint / line_descriptor::KeyLine subsets read by the path
+struct KeyPoint {
+    float x = 0, y = 0;   // pt
+    int octave = 0;
+};
+struct KeyLine {
+    float startPointX = 0, startPointY = 0, endPointX = 0, endPointY = 0, angle = 0;
+    int octave = 0;
+};
+using Descriptor = std::array<uint8_t, GFPL_DESC_BYTES>;   // one row of pdesc_* / ldesc_*
+
+// ---------------------------------------------------------------- Config --
+// The path's subset of Config (include/config.h:28-141, defaults src/config.cpp:26-154),
+// same static accessor names.  Changes take effect at the next handler call.
+class Config {
+public:
+    static Config& getInstance();
+    static bool& bestLRMatches() { return getInstance().best_lr_matches; }
+    static bool& lrInParallel() { return getInstance().lr_in_parallel; }
+    static bool& useLineConfCut() { return getInstance().use_line_conf_cut; }
+    static bool& cutWithMaxVol() { return getInstance().max_vol_line_cut; }
+    static double& ratioDispSTD() { return getInstance().c.ratio_disp_std; }
+    static double& ratioDispSTDHor() { return getInstance().c.ratio_disp_std_hor; }
+    static int& maxLineMatchNum() { return getInstance().c.max_line_match_num; }
+    static int& maxPointMatchNum() { return getInstance().c.max_point_match_num; }
+    static double& maxDistEpip() { return getInstance().c.max_dist_epip; }
+    static double& minDisp() { return getInstance().c.min_disp; }
+    static double& maxRatio12P() { return getInstance().c.max_ratio_12_p; }
+    static double& pointMatchRadius() { return getInstance().c.point_match_radius; }
+    static double& stereoOverlapTh() { return getInstance().c.stereo_overlap_th; }
+    static double& lineHorizTh() { return getInstance().c.line_horiz_th; }
+    static double& descThL() { return getInstance().c.desc_th_l; }
+    static double& lineCovTh() { return getInstance().c.line_cov_th; }
+    static double& homogTh() { return getInstance().c.homog_th; }
+    static int& minFeatures() { return getInstance().c.min_features; }
+    static int& maxIters() { return getInstance().c.max_iters; }
+    static int& maxItersRef() { return getInstance().c.max_iters_ref; }
+    static double& minError() { return getInstance().c.min_error; }
+    static double& minErrorChange() { return getInstance().c.min_error_change; }
+    static double& inlierK() { return getInstance().c.inlier_k; }
+    static double& motionStepThres() { return getInstance().c.motion_step_th; }
+    static double& orbScaleFactor() { return getInstance().c.orb_scale_factor; }
+    static int& orbNLevels() { return getInstance().c.orb_n_levels; }
+    static double& lsdScale() { return getInstance().c.lsd_scale; }
+    // the C-ABI view (bools folded in)
+    static gfpl_config abi();
+
+private:
+    Config();
+    gfpl_config c{};
+    bool best_lr_matches = true, lr_in_parallel = true, use_line_conf_cut = true, max_vol_line_cut = true;
+};
+
+// ---------------------------------------------------- PinholeStereoCamera --
+// include/pinholeStereoCamera.h:37-103 (rectified, distortion-free subset).
+class PinholeStereoCamera {
+public:
+    PinholeStereoCamera(int width, int height, double fx, double fy, double cx, double cy, double b);
+    int getWidth() const { return cam_.width; }
+    int getHeight() const { return cam_.height; }
+    double getFx() const { return cam_.fx; }
+    double getFy() const { return cam_.fy; }
+    double getCx() const { return cam_.cx; }
+    double getCy() const { return cam_.cy; }
+    double getB() const { return cam_.b; }
+    // ORB pyramid geometry the right pyramid must follow (levels consecutive)
+    int64_t pyramidBytes() const { return cam_.pyr_bytes; }
+    const gfpl_camera& abi() const { return cam_; }
+
+private:
+    gfpl_camera cam_{};
+};
+
+// -------------------------------------------------------------- features --
+// include/stereoFeatures.h:36-124
+class PointFeature {
+public:
+    int idx = -1;
+    Vector2d pl, pl_obs;
+    double disp = 0;
+    Vector3d P;
+    bool inlier = true;
+    int level = 0;
+    double sigma2 = 1.0;
+    bool frame_matched = false;
+};
+
+class LineFeature {
+public:
+    int idx = -1;
+    Vector2d spl, epl, spl_obs, epl_obs;
+    double sdisp = 0, edisp = 0, angle = 0, sdisp_obs = 0, edisp_obs = 0;
+    Vector3d sP, eP;
+    Vector3d le, le_obs;
+    bool inlier = true;
+    int level = 0;
+    double sigma2 = 1.0;
+    bool frame_matched = false;
+    Matrix3d covSpt3D, covEpt3D;
+    double cutRatio[2] = {0, 0};
+    Matrix6d invCovPose;
+};
+
+// ----------------------------------------------------------- StereoFrame --
+// include/stereoFrame.h:89-260.  Built from injected detections; after the
+// handler matched it, stereo_pt / stereo_ls and the reordered pdesc_l / ldesc_l
+// hold the stereo features exactly as extractStereoFeatures_ORBSLAM leaves them.
+class StereoFrame {
+public:
+    StereoFrame(const int& idx_, PinholeStereoCamera* cam_, const double& time_stamp_,
+                std::vector<KeyPoint> points_l_, std::vector<KeyPoint> points_r_,
+                std::vector<Descriptor> pdesc_l_, std::vector<Descriptor> pdesc_r_,
+                std::vector<KeyLine> lines_l_, std::vector<KeyLine> lines_r_,
+                std::vector<Descriptor> ldesc_l_, std::vector<Descriptor> ldesc_r_,
+                std::vector<uint8_t> pyramid_r_);
+    ~StereoFrame();
+    StereoFrame(const StereoFrame&) = delete;
+    StereoFrame& operator=(const StereoFrame&) = delete;
+
+    double time_stamp;
+    int frame_idx;
+    Matrix4d Tfw = Matrix4d::Identity();
+    Matrix4d DT = Matrix4d::Identity();
+    Matrix6d Tfw_cov = Matrix6d::Identity();
+    Vector6d Tfw_cov_eig;
+    Matrix6d DT_cov;
+    Vector6d DT_cov_eig;
+    double err_norm = 0;
+
+    std::vector<PointFeature*> stereo_pt;
+    std::vector<LineFeature*> stereo_ls;
+
+    std::vector<KeyPoint> points_l, points_r;
+    std::vector<KeyLine> lines_l, lines_r;
+    std::vector<Descriptor> pdesc_l, pdesc_r, ldesc_l, ldesc_r;
+    std::vector<uint8_t> pyramid_r;   // right ORB pyramid, levels packed (cam->pyramidBytes())
+
+    PinholeStereoCamera* cam;
+
+    // Hamming distance of two 32-byte rows (include/stereoFrame.h:185-201)
+    static int descriptorDistance(const Descriptor& a, const Descriptor& b);
+};
+
+// ---------------------------------------------------- StereoFrameHandler --
+// include/stereoFrameHandler.h:38-174; one handler = one sequence.
+class StereoFrameHandler {
+public:
+    explicit StereoFrameHandler(PinholeStereoCamera* cam_, int device = 0, int kp_cap = 8192, int kl_cap = 2048);
+    ~StereoFrameHandler();
+    StereoFrameHandler(const StereoFrameHandler&) = delete;
+    StereoFrameHandler& operator=(const StereoFrameHandler&) = delete;
+
+    // src/stereoFrameHandler.cpp:45-81 (takes ownership of the frame)
+    void initialize(StereoFrame* frame);
+    // src/stereoFrameHandler.cpp:83-151 (takes ownership of the frame)
+    void insertStereoPair(StereoFrame* frame);
+    // src/stereoFrameHandler.cpp:1939-2030; the app calls optimizePose(prev_frame->DT)
+    void optimizePose(Matrix4d DT_ini);
+    // src/stereoFrameHandler.cpp:864-922 (prev <- curr; logs T_base * old prev Tfw)
+    void updateFrame_ECCV18(const Matrix4d T_base);
+    void updateFrame();
+
+    // stage entry points of insertStereoPair, for callers that drive them one by one
+    void stereoMatching(StereoFrame* frame);                     // extractStereoFeatures_ORBSLAM minus detection
+    void estimateStereoUncertainty();                             // prev_frame->estimateStereoUncertainty()
+    void crossFrameMatching_Hybrid();                             // includes predictFramePose()
+    void estimateProjUncertainty_submodular(const double stepCutRatio, const double rngCutRatio[2]);
+
+    // write host-side edits of prev_frame / curr_frame / matched lists back to HBM
+    void pushState();
+
+    std::list<PointFeature*> matched_pt;
+    std::list<LineFeature*> matched_ls;
+    StereoFrame* prev_frame = nullptr;
+    StereoFrame* curr_frame = nullptr;
+    PinholeStereoCamera* cam;
+    int n_inliers = 0, n_inliers_pt = 0, n_inliers_ls = 0;
+    int numFrameLoss = 0;
+    std::vector<Matrix4d> vec_all_frame_pose;
+
+private:
+    void sync_config();
+    void upload(StereoFrame* f, gfpl_frames* dev);
+    void pull(int which, StereoFrame* f, bool features, bool pose);
+    void pull_track();
+    void check(int rc, const char* what) const;
+
+    gfpl_ctx* ctx_ = nullptr;
+    gfpl_seqbatch* sb_ = nullptr;
+    int kp_cap_, kl_cap_;
+    gfpl_config cfg_{};
+    struct HostBuf;   // gfpl_frame_host backing store
+    HostBuf* buf_ = nullptr;
+};
+
+}  // namespace StVO

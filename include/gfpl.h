@@ -238,8 +238,17 @@ int  gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in);
 /* StereoFrameHandler::optimizePose(prev_frame->DT) (src/stereoFrameHandler.cpp:1939-2030,
  * called as at app/plslam_mod.cpp:408).                                       */
 int  gfpl_optimize_pose(gfpl_seqbatch* sb);
+/* StereoFrameHandler::optimizePose(Matrix4d DT_ini) with an explicit initial guess per
+ * sequence: dt_ini = HOST array [B*16] row-major (NULL = prev_frame->DT).  Synchronises. */
+int  gfpl_optimize_pose_ini(gfpl_seqbatch* sb, const double* dt_ini);
+/* Copy one batch of HOST input frames (host->* are host pointers, same layout)
+ * into a device staging area owned by the seqbatch and return its device view
+ * in *dev (valid until the next upload).  Synchronous; for FFI callers without a
+ * HIP runtime of their own.  The rate through this path includes PCIe.        */
+int  gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* dev);
 /* StereoFrameHandler::updateFrame_ECCV18 state swap (src/stereoFrameHandler.cpp:864-922):
- * prev <- curr.  (FAST-threshold adaptation and T_base logging are out of scope.) */
+ * prev <- curr, matched lists cleared.  (FAST-threshold adaptation is out of scope;
+ * the T_base trajectory log lives in the host mirror, gf-pl-slam_amd/host/stvo.h.) */
 int  gfpl_update_frame(gfpl_seqbatch* sb);
 /* insert_stereo_pair + optimize_pose + update_frame, one batched step.       */
 int  gfpl_frame_step(gfpl_seqbatch* sb, const gfpl_frames* in);

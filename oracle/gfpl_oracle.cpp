@@ -1673,6 +1673,14 @@ int gfplo_optimize_pose(gfplo_handler* h) {
     h->optimizePose(DT_ini);
     return 0;
 }
+/* optimizePose(Matrix4d DT_ini) with an explicit initial guess (row-major 4x4) */
+int gfplo_optimize_pose_ini(gfplo_handler* h, const double* DT_ini) {
+    if (!h->prev || !h->curr || !DT_ini) return GFPL_E_STATE;
+    double D[16];
+    std::memcpy(D, DT_ini, sizeof D);
+    h->optimizePose(D);
+    return 0;
+}
 
 int gfplo_update_frame(gfplo_handler* h) {
     if (!h->prev || !h->curr) return GFPL_E_STATE;

@@ -47,6 +47,7 @@ int gfplo_initialize(gfplo_handler* h, const gfpl_frames* in, int seq);
 int gfplo_insert_stereo_pair(gfplo_handler* h, const gfpl_frames* in, int seq);
 /* optimizePose(prev_frame->DT) (src/stereoFrameHandler.cpp:1939-2030) */
 int gfplo_optimize_pose(gfplo_handler* h);
+int gfplo_optimize_pose_ini(gfplo_handler* h, const double* DT_ini);
 /* updateFrame_ECCV18 swap (src/stereoFrameHandler.cpp:864-922) */
 int gfplo_update_frame(gfplo_handler* h);
 

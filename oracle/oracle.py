@@ -38,6 +38,7 @@ def lib() -> C.CDLL:
             getattr(L, n).argtypes = [P, C.c_int, P]; getattr(L, n).restype = C.c_int
         for n in ["gfplo_read_track", "gfplo_write_track"]:
             getattr(L, n).argtypes = [P, P]; getattr(L, n).restype = C.c_int
+        L.gfplo_optimize_pose_ini.argtypes = [P, P]; L.gfplo_optimize_pose_ini.restype = C.c_int
         L.gfplo_hamming.argtypes = [P, P, C.c_int]; L.gfplo_hamming.restype = C.c_int
         L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
         for n in ["gfplo_log", "gfplo_sin", "gfplo_cos"]:
@@ -75,8 +76,13 @@ class OracleHandler:
     def insertStereoPair(self, fr: gfpl.Frames, seq: int):
         self._c(self.L.gfplo_insert_stereo_pair(self.h, C.byref(fr), seq), "insert")
 
-    def optimizePose(self):
-        self._c(self.L.gfplo_optimize_pose(self.h), "optimize_pose")
+    def optimizePose(self, DT_ini=None):
+        """optimizePose(prev_frame->DT) (Q2), or optimizePose(Matrix4d DT_ini)."""
+        if DT_ini is None:
+            self._c(self.L.gfplo_optimize_pose(self.h), "optimize_pose")
+        else:
+            d = np.ascontiguousarray(DT_ini, dtype=np.float64).reshape(16)
+            self._c(self.L.gfplo_optimize_pose_ini(self.h, d.ctypes.data), "optimize_pose_ini")
 
     def updateFrame(self):
         self._c(self.L.gfplo_update_frame(self.h), "update_frame")

@@ -242,3 +242,31 @@ def test_cross_points_nan_and_far_projections():
     bad += compare_core(g.read_frame(gfpl.CURR, 0), o.read_frame(gfpl.CURR), "cross curr ")
     assert not bad, "\n".join(bad[:30])
     assert len(to["matched_pt"]) > 100
+
+
+def test_optimize_pose_explicit_initial_guess():
+    """optimizePose(Matrix4d DT_ini) with a guess other than prev_frame->DT (per sequence)."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    KP, KL = 2048, 512
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=29), 2, 3, KP, KL)
+    D = gfpl.DeviceFrames(H)
+    ctx = gfpl.Context(cam, cfg)
+    g = gfpl.StereoFrameHandler(ctx, 2, KP, KL)
+    orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(2)]
+    g.initialize(D.frames(0))
+    for b, o in enumerate(orc):
+        o.initialize(H.frames(0), b)
+    guesses = np.stack([np.eye(4), O.expmap_se3(np.array([0.01, 0.0, -0.02, 0.0, 0.01, 0.0]))])
+    for k in (1, 2):
+        g.insertStereoPair(D.frames(k))
+        g.optimizePose(guesses)
+        for b, o in enumerate(orc):
+            o.insertStereoPair(H.frames(k), b)
+            o.optimizePose(guesses[b])
+            bad, exact = compare_pose(g.read_frame(gfpl.CURR, b), o.read_frame(gfpl.CURR), what=f"f{k} s{b} ")
+            assert not bad and exact, bad
+            assert compare_track(g.read_track(b), o.read_track()) == []
+        g.updateFrame()
+        for o in orc:
+            o.updateFrame()
