@@ -97,7 +97,6 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->tr.n_inliers_ls = c.take<int32_t>(B);
     sb->tr.num_frame_loss = c.take<int32_t>(B);
     sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
-    sb->scr.cut_pt = c.take<double>(B * sb->mpt_cap * 21);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
     sb->scr.proj = reinterpret_cast<double*>(sb->scr.knn);
     sb->scr.bytes = c.take<int64_t>(B * 8);

@@ -66,7 +66,6 @@ struct DevTrack {
 
 struct DevScratch {
     double* cut_ls;   // [B*mls_cap*21] lower-triangle info of matched lines
-    double* cut_pt;   // [B*mpt_cap*21] lower-triangle info of matched points
     int32_t* knn;     // [B*6*kcap] initial-frame knn results (idx0, d0, d1, ...)
     double* proj;     // [B*kcap*2] cross-points projections (aliases knn: init never overlaps)
     int64_t* bytes;   // [B] algorithmic bytes of the last step

@@ -5,17 +5,12 @@
 //
 // The search is a serial chain over matched lines: each line's greedy search
 // reads invCov_sum after all earlier lines were cut.  Three kernels:
-//  k_cut_prep   (64 lanes / sequence, parallel) initial info matrices (r = 0,0)
-//               of lines and points and invCov_sum, summed per element in list
-//               order (21 lanes) — the reference's accumulation order;
-//  k_cut_search (8 lanes / sequence, 8 sequences per wave) the serial greedy
-//               search.  Each wave iteration every lane evaluates ONE 6x6
-//               logdet: lane j of a sequence's group tries neighbour j of the
-//               current cut ratio (or, at the start of a line, lane 0 scores
-//               invCov_sum itself); the group then takes the first strict
-//               maximum (the reference's j-loop).  Groups advance independently
-//               through lines with a branch-free evaluation body, so a wave
-//               carries 8 chains at once;
+//  k_cut_prep   (one wave / sequence) r = (0,0) infos of lines and points and
+//               invCov_sum, each entry summed in list order (lines, then points)
+//               by one lane over 64-entry chunks staged in LDS, plus the metric
+//               logdet(invCov_sum) that opens the first line;
+//  k_cut_search (8 sequences per wave, 8 lanes each) the greedy search, one step
+//               of every chain per wave iteration (see the comment at the kernel);
 //  k_cut_finish (parallel) full 6x6 info of the chosen ratio (invCovPose) and
 //               the cut endpoints of every matched line.
 // Only the lower triangle is carried through the search: LLT reads nothing
@@ -144,6 +139,7 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
 
 // ------------------------------------------------------------------ prep --
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
+    __shared__ double chunk[21][64];   // lower-triangle infos of 64 list entries
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -157,7 +153,6 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
     const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
     double* scr_l = p.scr.cut_ls + (size_t)b * p.mls_cap * 21;
-    double* scr_p = p.scr.cut_pt + (size_t)b * p.mpt_cap * 21;
     // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635), every lane
     double Dl[16];
     {
@@ -168,37 +163,45 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         mat4_mul(Ti, Tp, Dl);
     }
     if (lane < 16) p.scr.cut_dtinv[16 * b + lane] = Dl[lane];
-    for (int m = lane; m < nls; m += 64) {
-        const size_t q = lb + mls[m];
-        LineCutData d;
-        load_line(L, q, d);
+    // invCov_sum: lines then points, each entry summed in list order by lane e < 21,
+    // 64 list entries at a time staged through LDS (src/stereoFrameHandler.cpp:1640-1657)
+    double s = 0.0;
+    const int nl_ch = (nls + 63) >> 6, np_ch = (npt + 63) >> 6;
+    for (int c = 0; c < nl_ch + np_ch; ++c) {
+        const bool lines = c < nl_ch;
+        const int m = ((lines ? c : c - nl_ch) << 6) + lane;
+        const int cnt = min(64, (lines ? nls : npt) - (((lines ? c : c - nl_ch)) << 6));
         double info[21];
-        poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
+        if (lane < cnt) {
+            if (lines) {
+                LineCutData d;
+                load_line(L, lb + mls[m], d);
+                poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
 #pragma unroll
-        for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];
-    }
-    for (int m = lane; m < npt; m += 64) {
-        const size_t q = pbase + mpt[m];
-        double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
-        double cur[3], uv[2];
-        se3_apply(Dl, Pp, cur);
-        projection(cam, cur, uv);
-        const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
-        double J[6];
-        poseJac(cam, homog, cur, dx, dy, J);
+                for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];   // k_cut_search subtracts it
+            } else {
+                const size_t q = pbase + mpt[m];
+                double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
+                double cur[3], uv[2];
+                se3_apply(Dl, Pp, cur);
+                projection(cam, cur, uv);
+                const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
+                double J[6];
+                poseJac(cam, homog, cur, dx, dy, J);   // getPoseInfoPoint (:1414-1447)
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
+                for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int j = 0; j <= i; ++j) scr_p[(size_t)m * 21 + tri(i, j)] = J[i] * J[j];
+                    for (int j = 0; j <= i; ++j) info[tri(i, j)] = J[i] * J[j];
+            }
+#pragma unroll
+            for (int i = 0; i < 21; ++i) chunk[i][lane] = info[i];
+        }
+        __syncthreads();
+        if (lane < 21)
+            for (int k = 0; k < cnt; ++k) s = s + chunk[lane][k];
+        __syncthreads();
     }
-    __syncthreads();
-    // invCov_sum, sequential per element (lines then points)
-    if (lane < 21) {
-        double s = 0.0;
-        for (int m = 0; m < nls; ++m) s = s + scr_l[(size_t)m * 21 + lane];
-        for (int m = 0; m < npt; ++m) s = s + scr_p[(size_t)m * 21 + lane];
-        p.scr.cut_sum[24 * b + lane] = s;
-    }
+    if (lane < 21) p.scr.cut_sum[24 * b + lane] = s;
     __syncthreads();
     if (lane == 0) {   // metric of the first line's search: logdet(invCov_sum) (:1671)
         double a[21];

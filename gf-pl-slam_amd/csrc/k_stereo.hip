@@ -59,6 +59,9 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
                          float& disparity, float& bestuR) {
     disparity = -1;
     bestuR = kpR.x;
+#ifdef GFPL_EXP_NO_SAD
+    return;
+#endif
     const float uR0 = kpR.x;
     const int o = clamp_level(kpL.octave, p.cam.n_levels);
     const float sf = p.cam.inv_scale[o];
@@ -102,28 +105,43 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
 #pragma unroll
         for (int i = 0; i < 11; ++i) cR[i] = byte_at(ir6, 5 + i);
     }
-    int acc[11];
+    // SAD = sum |(IL - cL) - (IR_s - cR[s])| = sum |(IL + cR[s]) - (IR_s + cL)|, both
+    // sides <= 510: two columns per v_sad_u16 (16-bit lanes of one register)
+    uint32_t cRR[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) cRR[i] = (uint32_t)cR[i] * 0x10001u;
+    const uint32_t cLL = (uint32_t)cL * 0x10001u;
+    uint32_t acc[11];
 #pragma unroll
     for (int i = 0; i < 11; ++i) acc[i] = 0;
     for (int r = 0; r < 11; ++r) {
         uint32_t il4[3], ir6[6];
         load_row(vL - 5 + r, il4, ir6);
-        int il[11], ir[21];
+        uint32_t ILp[5], IRe[10], IRo[10];
 #pragma unroll
-        for (int c = 0; c < 11; ++c) il[c] = byte_at(il4, c) - cL;
+        for (int k = 0; k < 5; ++k) ILp[k] = (uint32_t)byte_at(il4, 2 * k) | ((uint32_t)byte_at(il4, 2 * k + 1) << 16);
+        const int il10 = byte_at(il4, 10);
 #pragma unroll
-        for (int c = 0; c < 21; ++c) ir[c] = byte_at(ir6, c);
+        for (int m = 0; m < 10; ++m) {
+            IRe[m] = ((uint32_t)byte_at(ir6, 2 * m) | ((uint32_t)byte_at(ir6, 2 * m + 1) << 16)) + cLL;
+            IRo[m] = ((uint32_t)byte_at(ir6, 2 * m + 1) | ((uint32_t)byte_at(ir6, 2 * m + 2) << 16)) + cLL;
+        }
 #pragma unroll
-        for (int s = 0; s < 11; ++s)
+        for (int s = 0; s < 11; ++s) {
+            uint32_t a = acc[s];
 #pragma unroll
-            for (int c = 0; c < 11; ++c) acc[s] += abs(il[c] - (ir[c + s] - cR[s]));
+            for (int k = 0; k < 5; ++k)
+                a = __builtin_amdgcn_sad_u16(ILp[k] + cRR[s], (s & 1) ? IRo[k + (s >> 1)] : IRe[k + (s >> 1)], a);
+            a += (uint32_t)abs((il10 + cR[s]) - (byte_at(ir6, 10 + s) + cL));
+            acc[s] = a;
+        }
     }
     int bestDist = 2147483647;
     int bestinc = 0;
     float vD[11];
 #pragma unroll
     for (int s = 0; s < 11; ++s) {
-        float dist = (float)acc[s];
+        float dist = (float)(int)acc[s];
         if (dist < (float)bestDist) { bestDist = (int)dist; bestinc = s - 5; }
         vD[s] = dist;
     }
@@ -138,20 +156,27 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
 }
 
 // ------------------------------------------------------- stereo points --
-// dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | rmaxr[cap] i32 | misc[64]
-// Left keypoints are processed in row order (a row-sorted permutation, order[]),
-// so the lanes of a wave touch the same right-keypoint band and overlapping SAD
-// window rows: the gathers hit L1/L2 instead of HBM.  Results are keyed by iL,
-// so the processing order has no effect on the output.
+// dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | recx[KP2] f32 |
+//              recm[KP2] u16 | rowlo[nRows] u16 | misc[64] i32
+// Right keypoints are sorted by their row band start (the reference's
+// vRowIndices buckets, src/stereoFrame.cpp:459-485) and their x, octave and band
+// height are copied next to the sorted keys, so the band scan of a left keypoint
+// reads LDS only (its first candidate comes from a per-row table).  Left
+// keypoints are processed in row order (order[]), so the lanes of a wave touch the
+// same descriptors and overlapping SAD window rows.  Results are keyed by iL: the
+// processing order has no effect on the output.
 __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;
+    const int nRows = p.cam.height;
     uint32_t* rkey = (uint32_t*)smem;
     uint32_t* order = rkey + KP2;
     uint32_t* pairs = order + KP2;
-    int* rmaxr = (int*)(pairs + KP2);
-    int* misc = rmaxr + cap;
+    float* recx = (float*)(pairs + KP2);
+    uint16_t* recm = (uint16_t*)(recx + KP2);
+    uint16_t* rowlo = recm + KP2;
+    int* misc = (int*)(rowlo + ((nRows + 1) & ~1));
     float* depth = reinterpret_cast<float*>(p.scr.knn) + (size_t)b * cap;   // scratch (cross points reuses it later)
     const int tid = threadIdx.x;
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
@@ -159,11 +184,9 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
     const uint8_t* DL = p.in.pdesc_l + (size_t)b * cap * 32;
     const uint8_t* DR = p.in.pdesc_r + (size_t)b * cap * 32;
-    const int nRows = p.cam.height;
     if (tid == 0) { misc[0] = 0; misc[1] = 0; misc[2] = 0; }
     __syncthreads();
-    // vRowIndices (src/stereoFrame.cpp:459-485) as (minr, iR) keys sorted by minr;
-    // left keypoints as (row, iL) keys
+    // vRowIndices as (minr, iR) keys; left keypoints as (row, iL) keys
     for (int i = tid; i < KP2; i += blockDim.x) {
         if (i < Nr) {
             gfpl_keypoint kp = KR[i];
@@ -171,7 +194,6 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
             const int maxr = (int)ceilf(kp.y + r);
             const int minr = (int)floorf(kp.y - r);
             rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
-            rmaxr[i] = maxr;
             atomicMax(&misc[0], maxr - minr);
         } else {
             rkey[i] = 0xFFFFFFFFu;
@@ -188,6 +210,25 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     __syncthreads();
     bitonic_sort2(rkey, order, KP2);
     const int D = misc[0];
+    // records in sorted order: x, band height maxr - minr (<= 16), octave (int8;
+    // -128 = out of range, read from HBM)
+    for (int j = tid; j < Nr; j += blockDim.x) {
+        const int iR = (int)(rkey[j] & 0xFFFFu);
+        const gfpl_keypoint kp = KR[iR];
+        const float r = 2.0f * p.cam.scale[clamp_level(kp.octave, p.cam.n_levels)];
+        const int band = (int)ceilf(kp.y + r) - (int)floorf(kp.y - r);
+        const int oc = (kp.octave >= -127 && kp.octave <= 127) ? kp.octave : -128;
+        recx[j] = kp.x;
+        recm[j] = (uint16_t)(((uint32_t)band << 8) | ((uint32_t)oc & 0xFFu));
+    }
+    // first candidate of each row: lower bound of minr >= row - D
+    for (int row = tid; row < nRows; row += blockDim.x) {
+        const uint32_t lo_key = (uint32_t)(row - D + 32768) << 16;
+        int lo = 0, hi = Nr;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
+        rowlo[row] = (uint16_t)lo;
+    }
+    __syncthreads();
     const float minD = 0;
     const float maxD = (float)p.cam.fx;
     const float mbf = (float)(p.cam.fx * p.cam.b);
@@ -204,20 +245,22 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
                 const int row = (int)vL;
                 uint32_t dl[8];
                 load_desc(DL + (size_t)iL * 32, dl);
-                // lower bound of minr >= row - D
-                const uint32_t lo_key = (uint32_t)(row - D + 32768) << 16;
-                int lo = 0, hi = Nr;
-                while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
                 int bestDist = 100, bestIdxR = 0x7FFFFFFF;
-                for (int j = lo; j < Nr; ++j) {
+                int j0 = rowlo[row];
+#ifdef GFPL_EXP_NO_BAND
+                j0 = Nr;
+#endif
+                for (int j = j0; j < Nr; ++j) {
                     const uint32_t k = rkey[j];
                     const int minr = (int)(k >> 16) - 32768;
                     if (minr > row) break;
+                    const uint32_t m = recm[j];
+                    if (minr + (int)(m >> 8) < row) continue;   // maxr < row
                     const int iR = (int)(k & 0xFFFFu);
-                    if (rmaxr[iR] < row) continue;
-                    const gfpl_keypoint kpR = KR[iR];
-                    if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-                    const float uR = kpR.x;
+                    int octR = (int)(int8_t)(uint8_t)(m & 0xFFu);
+                    if (octR == -128) octR = KR[iR].octave;
+                    if (octR < levelL - 1 || octR > levelL + 1) continue;
+                    const float uR = recx[j];
                     if (uR >= minU && uR <= maxU) {
                         uint32_t dr[8];
                         load_desc(DR + (size_t)iR * 32, dr);
@@ -646,7 +689,7 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
-    const size_t lds = (size_t)KP2 * 12 + (size_t)p.kp_cap * 4 + 64 * 4;
+    const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
     hipLaunchKernelGGL(k_stereo_points, dim3(p.B), dim3(512), lds, s, p, KP2);
     return hipGetLastError();
 }

@@ -140,7 +140,8 @@ _LIBS: dict = {}
 
 
 def lib_path(name: str) -> str:
-    return os.path.join(LIB_DIR, name)
+    # GFPL_LIB_DIR: load an alternative in-tree build (kernel experiments in tools/)
+    return os.path.join(os.environ.get("GFPL_LIB_DIR", LIB_DIR), name)
 
 
 def _load(name: str) -> C.CDLL:
