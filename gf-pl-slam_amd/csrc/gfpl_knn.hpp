@@ -1,0 +1,126 @@
+// gfpl_knn.hpp — knn-2 Hamming matching on the matrix cores (gfx950 i8 MFMA).
+//
+// BFMatcher::knnMatch(k = 2) with NORM_HAMMING / NORM_HAMMING2 (OpenCV 3.4.1
+// batchDistance; ledger T1) restated as an exact integer GEMM:
+//   HAMMING  : dist(t, q) = popc(t) + popc(q) - 2 <t_bits, q_bits>
+//              = <t_bits, 1 - 2 q_bits> + popc(q)            (K = 256, one i8 per bit)
+//   HAMMING2 : dist(t, q) = 128 - <onehot(t), onehot(q)>     (K = 512, each 2-bit
+//              cell one-hot over its 4 values: equal cells contribute 1)
+// v_mfma_i32_32x32x32_i8 takes a 32x32 tile of (train row t) x (query column q)
+// per wave; the C layout puts one query column on each lane (col = lane & 31) and
+// 16 train rows in its registers (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)), so
+// the per-query top-2 is lane-local.  The top-2 is the lexicographic minimum of
+// the packed key (dist << 16 | t) — the OpenCV insertion rule (strict '<', ties
+// keep the lower train index) is exactly that, independent of visiting order.
+// The k-index each (lane half, element) holds is the same for A and B, so the
+// dot products are exact whatever the hardware's k permutation inside a step.
+#pragma once
+#include "gfpl_device.hpp"
+
+namespace gfpl {
+
+typedef int mfma_v4i __attribute__((ext_vector_type(4)));
+typedef int mfma_v16i __attribute__((ext_vector_type(16)));
+
+// 4 bits -> 4 bytes of 0 / 1
+__device__ __forceinline__ uint32_t spread4(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
+
+// operand fragment of k-step ks for a 32-byte descriptor held as 8 dwords.
+// CELL 2 (one-hot): lane half h takes descriptor byte 2 ks + h (4 cells -> 16 i8)
+// CELL 1 (bits)   : lane half h takes bytes 4 ks + 2 h, +1 (16 bits -> 16 i8);
+//                   SIGNED (query side) maps bit b to 1 - 2 b.
+template <int CELL, bool SIGNED>
+__device__ __forceinline__ mfma_v4i knn_frag(const uint32_t* d, int ks, int h) {
+    mfma_v4i f;
+    if (CELL == 2) {   // byte 2 ks + h lives in dword ks >> 1 (compile-time index)
+        const uint32_t v = (d[ks >> 1] >> (8u * (2u * (ks & 1) + (uint32_t)h))) & 0xFFu;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = (int)(1u << (8u * ((v >> (2 * i)) & 3u)));
+    } else {           // bytes 4 ks + 2 h, +1 live in dword ks
+        const uint32_t v = (d[ks] >> (16u * (uint32_t)h)) & 0xFFFFu;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t x = spread4((v >> (4 * i)) & 0xFu);
+            f[i] = SIGNED ? (int)((x * 0xFEu) | 0x01010101u) : (int)x;
+        }
+    }
+    return f;
+}
+
+__device__ __forceinline__ int popc8(const uint32_t* d) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += __popc(d[i]);
+    return s;
+}
+
+// One knn pass of a workgroup: every query q < nq against the train rows of T
+// (LDS, nt rows of 8 dwords).  Queries are read from Q (global or LDS, 32-byte
+// rows).  Writes out_k0[q] = lexicographic minimum key (dist << 16 | t) and, when
+// TOP2, out_k1[q] = the second one.  Waves split the query column tiles.
+template <int CELL, bool TOP2>
+__device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, uint32_t* out_k0, uint32_t* out_k1) {
+    constexpr int KS = CELL == 2 ? 16 : 8;   // k-steps of 32
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const int h = lane >> 5, c = lane & 31;
+    const int nct = (nq + 31) >> 5, nrt = (nt + 31) >> 5;
+    for (int ct = wave; ct < nct; ct += nwave) {
+        const int q = ct * 32 + c;
+        uint32_t qd[8];
+        if (q < nq) load_desc(Q + (size_t)q * 32, qd);
+        else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) qd[i] = 0;
+        }
+        mfma_v4i bq[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bq[ks] = knn_frag<CELL, true>(qd, ks, h);
+        const int pq = CELL == 2 ? 0 : popc8(qd);
+        uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+        for (int rt = 0; rt < nrt; ++rt) {
+            const int t = rt * 32 + c;
+            uint32_t td[8];
+            if (t < nt) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) td[i] = T[8 * t + i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) td[i] = 0;
+            }
+            mfma_v16i acc = {};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(knn_frag<CELL, false>(td, ks, h), bq[ks], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int tr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int d = CELL == 2 ? 128 - acc[r] : acc[r] + pq;
+                const uint32_t key = tr < nt ? (((uint32_t)d << 16) | (uint32_t)tr) : 0xFFFFFFFFu;
+                if (TOP2) {
+                    const uint32_t hi = max(k0, key);
+                    k0 = min(k0, key);
+                    k1 = min(k1, hi);
+                } else {
+                    k0 = min(k0, key);
+                }
+            }
+        }
+        // the two lane halves hold disjoint train rows of the same query column
+        const uint32_t o0 = __shfl_xor(k0, 32, 64);
+        if (TOP2) {
+            const uint32_t o1 = __shfl_xor(k1, 32, 64);
+            const uint32_t lo = min(k0, o0), hi0 = max(k0, o0);
+            k1 = min(hi0, min(k1, o1));
+            k0 = lo;
+        } else {
+            k0 = min(k0, o0);
+        }
+        if (h == 0 && q < nq) {
+            out_k0[q] = k0;
+            if (TOP2) out_k1[q] = k1;
+        }
+    }
+}
+
+}  // namespace gfpl

@@ -14,6 +14,7 @@
 //                   histograms (the medians are order statistics of small integers),
 //                   mutual check, first max_line_match_num accepted in prev order.
 #include "gfpl_kernels.hpp"
+#include "gfpl_knn.hpp"
 
 namespace gfpl {
 
@@ -225,25 +226,22 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
         for (int i = tid; i < Sc * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DC)[i];
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
         __syncthreads();
+        // 12: prev queries against curr trains, knn-2 on the matrix cores (gfpl_knn.hpp)
+        knn2_mfma<1, true>(tb, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112);
+        __syncthreads();
         for (int i = tid; i < Sl; i += blockDim.x) {
-            uint32_t qd[8];
-            load_desc(DP + (size_t)i * 32, qd);
-            int a, d0, d1;
-            knn2_lds<1>(qd, tb, Sc, a, d0, d1);
-            i12[i] = a; d012[i] = d0; d112[i] = d1;
+            const uint32_t k0 = (uint32_t)i12[i], k1 = (uint32_t)d112[i];
+            const int d0 = (int)(k0 >> 16), d1 = (int)(k1 >> 16);
+            i12[i] = (int)(k0 & 0xFFFFu); d012[i] = d0; d112[i] = d1;
             atomicAdd(&h12[d1 - d0], 1);
             atomicAdd(&h0[d0], 1);
         }
-        __syncthreads();
         for (int i = tid; i < Sl * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DP)[i];
         __syncthreads();
-        for (int j = tid; j < Sc; j += blockDim.x) {
-            uint32_t qd[8];
-            load_desc(DC + (size_t)j * 32, qd);
-            int a, d0, d1;
-            knn2_lds<1>(qd, tb, Sl, a, d0, d1);
-            i21[j] = a;
-        }
+        // 21: curr queries against prev trains (best index only)
+        knn2_mfma<1, false>(tb, Sl, DC, Sc, (uint32_t*)i21, nullptr);
+        __syncthreads();
+        for (int j = tid; j < Sc; j += blockDim.x) i21[j] = (int)((uint32_t)i21[j] & 0xFFFFu);
         __syncthreads();
         if (tid == 0) {
             const int v = hist_rank_c(h12, Sl / 2);

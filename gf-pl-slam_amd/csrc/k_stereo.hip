@@ -11,6 +11,7 @@
 // the median gate and the order-preserving compaction are all block-local, so a
 // frame never crosses workgroups and B sequences fill the 256 CUs.
 #include "gfpl_kernels.hpp"
+#include "gfpl_knn.hpp"
 
 namespace gfpl {
 
@@ -475,24 +476,21 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     for (int i = tid; i < NR * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DRg)[i];
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
     __syncthreads();
+    // L->R knn-2 on the matrix cores (gfpl_knn.hpp): keys (dist << 16 | iR)
+    knn2_mfma<CELL, true>(tb, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1);
+    __syncthreads();
     for (int i = tid; i < NL; i += blockDim.x) {
-        uint32_t qd[8];
-        load_desc(DLg + (size_t)i * 32, qd);
-        int i0, d0, d1;
-        knn2_row<CELL>(qd, tb, NR, i0, d0, d1);
-        lr_i[i] = i0; lr_d0[i] = d0; lr_d1[i] = d1;
+        const uint32_t k0 = (uint32_t)lr_i[i], k1 = (uint32_t)lr_d1[i];
+        const int d0 = (int)(k0 >> 16), d1 = (int)(k1 >> 16);
+        lr_i[i] = (int)(k0 & 0xFFFFu); lr_d0[i] = d0; lr_d1[i] = d1;
         atomicAdd(&hist[d1 - d0], 1);   // lineDescriptorMAD deviations |d1-d0| (U1 pin)
     }
-    __syncthreads();
     for (int i = tid; i < NL * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DLg)[i];
     __syncthreads();
-    for (int j = tid; j < NR; j += blockDim.x) {
-        uint32_t qd[8];
-        load_desc(DRg + (size_t)j * 32, qd);
-        int i0, d0, d1;
-        knn2_row<CELL>(qd, tb, NL, i0, d0, d1);
-        rl_i[j] = i0;
-    }
+    // R->L knn (only the best index is used)
+    knn2_mfma<CELL, false>(tb, NL, DRg, NR, (uint32_t*)rl_i, nullptr);
+    __syncthreads();
+    for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = (int)((uint32_t)rl_i[j] & 0xFFFFu);
     __syncthreads();
     if (tid == 0) {
         const int v = hist_rank(hist, NL / 2);
