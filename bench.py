@@ -41,6 +41,11 @@ WORKLOADS = {
     "cfg2": ("vga", {}, "cfg2: synthetic VGA 640x480 stereo (gazebo rig), 2000 ORB + 500 LBD per side, 10+10 GN iters"),
     "cfg3": ("kitti", dict(dt=0.1, v_fwd=8.0, z_min=4.0, z_max=40.0),
              "cfg3: KITTI-00 1241x376 stream (synthetic detections), 2000 ORB + 500 LBD, 10+10 GN iters"),
+    # BASELINE configs[3]: the EuRoC rig following the ground-truth motion of the 8 EuRoC
+    # sequences (config/asl/gt-ass/*), sequence (rank mod 8) on rank r
+    "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0),
+             "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
+             "2000 ORB + 500 LBD, 10+10 GN iters"),
 }
 
 
@@ -163,8 +168,16 @@ def main():
 
     B, W, K = args.batch, args.warmup, args.steps
     KP, KL = 2048, 512
-    sp = gfpl.synth_params(**synth_over)
     F = 1 + W + K
+    keep = []
+    if args.workload == "cfg4":
+        T, t = gfpl.euroc_traj(gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)], 64)
+        keep += [T, t]   # the generator reads them through raw pointers
+        if F > len(t):
+            print(f"note: {F} frames > {len(t)} ground-truth poses; the trajectory wraps", file=sys.stderr)
+        synth_over = dict(synth_over, traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data)
+        desc = desc + f" [this rank: {gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)]}]"
+    sp = gfpl.synth_params(**synth_over)
     # all F input frames of the B sequences are staged in HBM before timing; bound
     # them to a fraction of device memory (inputs resident)
     free, total = torch.cuda.mem_get_info(dev)

@@ -13,6 +13,7 @@ tests read like the reference's own call sequence (app/plslam_mod.cpp:375-477):
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 from typing import Optional
 
@@ -257,6 +258,19 @@ CAMERAS = {
     # gazebo x3 (cfg 5 stress)
     "stress": dict(width=1920, height=1080, fx=1662.76878, fy=1662.76878, cx=960.0, cy=540.0, b=0.1),
 }
+
+
+EUROC_SEQS = ["mh_01", "mh_02", "mh_03", "mh_04", "mh_05", "v1_01", "v1_02", "v1_03"]
+
+
+def euroc_traj(seq: str = "mh_01", n: int = 64):
+    """First n ground-truth camera poses (3x4 row-major T_w<-c) and timestamps [s] of a
+    EuRoC sequence, from the reference's config/asl/gt-ass/<seq> files (data/euroc_gt.json)."""
+    with open(os.path.join(os.path.dirname(LIB_DIR), "data", "euroc_gt.json")) as f:
+        d = json.load(f)["seqs"][seq]
+    T = np.ascontiguousarray(np.array(d["T_wc_3x4"][:n], np.float64))
+    t = np.ascontiguousarray(np.array(d["t"][:n], np.float64))
+    return T, t
 
 
 def make_camera(name: str = "vga", cfg: Optional[Config] = None, **over) -> Camera:

@@ -1,6 +1,7 @@
 """Extract the first N ground-truth poses + timestamps of the EuRoC sequences
 the BASELINE configs 1 and 4 name (config/asl/gt-ass/{mh_01..mh_05,v1_01..v1_03})
-from the reference's data files into tests/golden/euroc_gt.json.
+from the reference's data files into gf-pl-slam_amd/data/euroc_gt.json (used by the
+golden fixtures, the EuRoC parity tests and bench.py's cfg4 workload).
 
 Run in the build container (the reference is not on the GPU box):
     python tests/golden/make_euroc_fixture.py /root/reference
@@ -24,7 +25,8 @@ def main(ref):
             ts = [int(ln.split()[0]) / 1e9 for ln in f if ln.strip()][:N]
         assert all(len(r) == 12 for r in rows)
         out["seqs"][s] = {"T_wc_3x4": rows, "t": ts}
-    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "euroc_gt.json")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    dst = os.path.join(root, "gf-pl-slam_amd", "data", "euroc_gt.json")
     with open(dst, "w") as f:
         json.dump(out, f)
     print("wrote", dst)

@@ -32,10 +32,7 @@ def digest(*arrays) -> str:
 
 
 def euroc_traj(seq="mh_01", n=2):
-    d = json.load(open(os.path.join(HERE, "euroc_gt.json")))["seqs"][seq]
-    T = np.ascontiguousarray(np.array(d["T_wc_3x4"][:n], np.float64))
-    t = np.ascontiguousarray(np.array(d["t"][:n], np.float64))
-    return T, t
+    return gfpl.euroc_traj(seq, n)
 
 
 CASES = {

@@ -270,3 +270,13 @@ def test_optimize_pose_explicit_initial_guess():
         g.updateFrame()
         for o in orc:
             o.updateFrame()
+
+
+def test_euroc_ground_truth_trajectory_parity():
+    """BASELINE configs[3] shape: the EuRoC rig on a ground-truth trajectory (MH_03)."""
+    T, t = gfpl.euroc_traj("mh_03", 6)
+    rep = _run_sequence("euroc", {}, n_seq=2, n_frames=6, kp_cap=2048, kl_cap=512,
+                        synth_over=dict(z_min=2.0, z_max=12.0, traj=T.ctypes.data, n_traj=len(t),
+                                        traj_t=t.ctypes.data), seed=31)
+    _check(rep)
+    assert all(rep["pose_exact"])
