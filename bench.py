@@ -43,6 +43,10 @@ WORKLOADS = {
              "cfg3: KITTI-00 1241x376 stream (synthetic detections), 2000 ORB + 500 LBD, 10+10 GN iters"),
     # BASELINE configs[3]: the EuRoC rig following the ground-truth motion of the 8 EuRoC
     # sequences (config/asl/gt-ass/*), sequence (rank mod 8) on rank r
+    # BASELINE configs[4]: stress, 8000 ORB + 2000 LBD per 1920x1080 frame, line cut on
+    "cfg5": ("stress", dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=2800, z_max=12.0),
+             "cfg5: stress 1920x1080 stereo (gazebo x3), 8000 ORB + 2000 LBD per side, good-line-cut on, "
+             "10+10 GN iters"),
     "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0),
              "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
              "2000 ORB + 500 LBD, 10+10 GN iters"),
@@ -133,12 +137,15 @@ def reduce_job(elapsed: float, frames: int, dist, device):
     return float(el.item()), int(cnt.item())
 
 
-def load_pmc(path, kernel_name):
+def load_pmc(path, kernel_name, batch, workload):
+    """HBM bytes per launch of a kernel from the PMC summary (tools/pmc_summary.py),
+    only when it was collected on this workload and batch size."""
     try:
         with open(path) as f:
             d = json.load(f)
-        k = d["kernels"][kernel_name]
-        return float(k["hbm_bytes_per_launch"])
+        if d.get("batch") != batch or d.get("workload", "cfg2") != workload:
+            return None
+        return float(d["kernels"][kernel_name]["hbm_bytes_per_launch"])
     except Exception:
         return None
 
@@ -167,7 +174,7 @@ def main():
         broadcast_setup(cam, cfg, dist, dev)
 
     B, W, K = args.batch, args.warmup, args.steps
-    KP, KL = 2048, 512
+    KP, KL = (8192, 2048) if args.workload == "cfg5" else (2048, 512)
     F = 1 + W + K
     keep = []
     if args.workload == "cfg4":
@@ -236,7 +243,7 @@ def main():
         step_bytes = float(np.mean(np.array(stage_bytes)[:, 6]))
         ms_step = t_max / K * 1e3
         value = frames_total / t_max
-        traffic = load_pmc(args.pmc, kname)
+        traffic = load_pmc(args.pmc, kname, B, args.workload)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(cam, cfg, sp, args.cpu_threads, args.cpu_seqs, args.cpu_frames, KP, KL)
@@ -253,7 +260,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth)",
-            "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": 2000, "kl_per_side": 500,
+            "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": int(sp.n_kp), "kl_per_side": int(sp.n_kl),
                        "gn_iters": "10+10", "parallelism": f"sequences sharded 1/{world} per GPU"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": float(achieved), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": float(achieved / HBM_PEAK_GBS), "traffic": traffic,

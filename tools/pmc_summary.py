@@ -27,6 +27,7 @@ def short(name: str) -> str:
 def main():
     d = sys.argv[1]
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    workload = sys.argv[4] if len(sys.argv) > 4 else "cfg2"
     vals = defaultdict(lambda: defaultdict(dict))   # kernel -> counter -> {dispatch: value}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -36,7 +37,7 @@ def main():
                 v = float(row.get("Counter_Value", 0) or 0)
                 disp = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 vals[k][c][disp] = vals[k][c].get(disp, 0.0) + v
-    out = {"batch": batch, "kernels": {}}
+    out = {"batch": batch, "workload": workload, "kernels": {}}
     for k in sorted(vals):
         row = {c: sum(v.values()) / max(1, len(v)) for c, v in vals[k].items()}
         row["dispatches"] = max(len(v) for v in vals[k].values())

@@ -17,7 +17,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d $OUT/pmc/$c -o $c -f csv -- \
       python3 bench.py --no-cpu --steps 2 --warmup 1 $BENCH_ARGS > $OUT/pmc/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $OUT/pmc/$c.log; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT/pmc 0 profiles/pmc_latest.json > $OUT/pmc/summary.txt && cp profiles/pmc_latest.json $OUT/pmc_latest.json || exit 1
+python3 tools/pmc_summary.py $OUT/pmc ${PMC_BATCH:-16384} profiles/pmc_latest.json ${PMC_WORKLOAD:-cfg2} > $OUT/pmc/summary.txt && cp profiles/pmc_latest.json $OUT/pmc_latest.json || exit 1
 timeout -k 10 600 python3 bench.py $BENCH_ARGS > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 || { echo "rocprof failed"; tail -5 $OUT/bench_rocprof.log; exit 1; }
