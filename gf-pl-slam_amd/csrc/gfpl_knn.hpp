@@ -5,7 +5,8 @@
 //   HAMMING  : dist(t, q) = popc(t) + popc(q) - 2 <t_bits, q_bits>
 //              = <t_bits, 1 - 2 q_bits> + popc(q)            (K = 256, one i8 per bit)
 //   HAMMING2 : dist(t, q) = 128 - <onehot(t), onehot(q)>     (K = 512, each 2-bit
-//              cell one-hot over its 4 values: equal cells contribute 1)
+//              cell one-hot over its 4 values: equal cells contribute 1; the query
+//              side is negated and the accumulator starts at 128)
 // v_mfma_i32_32x32x32_i8 takes a 32x32 tile of (train row t) x (query column q)
 // per wave; the C layout puts one query column on each lane (col = lane & 31) and
 // 16 train rows in its registers (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)), so
@@ -27,15 +28,16 @@ __device__ __forceinline__ uint32_t spread4(uint32_t nib) { return (nib * 0x0020
 
 // operand fragment of k-step ks for a 32-byte descriptor held as 8 dwords.
 // CELL 2 (one-hot): lane half h takes descriptor byte 2 ks + h (4 cells -> 16 i8)
-// CELL 1 (bits)   : lane half h takes bytes 4 ks + 2 h, +1 (16 bits -> 16 i8);
-//                   SIGNED (query side) maps bit b to 1 - 2 b.
+// CELL 1 (bits)   : lane half h takes bytes 4 ks + 2 h, +1 (16 bits -> 16 i8).
+// SIGNED (query side): CELL 1 maps bit b to 1 - 2 b, CELL 2 makes the one-hot -1.
 template <int CELL, bool SIGNED>
 __device__ __forceinline__ mfma_v4i knn_frag(const uint32_t* d, int ks, int h) {
     mfma_v4i f;
     if (CELL == 2) {   // byte 2 ks + h lives in dword ks >> 1 (compile-time index)
         const uint32_t v = (d[ks >> 1] >> (8u * (2u * (ks & 1) + (uint32_t)h))) & 0xFFu;
+        const uint32_t one = SIGNED ? 0xFFu : 0x01u;   // SIGNED: the one-hot byte is -1
 #pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = (int)(1u << (8u * ((v >> (2 * i)) & 3u)));
+        for (int i = 0; i < 4; ++i) f[i] = (int)(one << (8u * ((v >> (2 * i)) & 3u)));
     } else {           // bytes 4 ks + 2 h, +1 live in dword ks
         const uint32_t v = (d[ks] >> (16u * (uint32_t)h)) & 0xFFFFu;
 #pragma unroll
@@ -54,12 +56,50 @@ __device__ __forceinline__ int popc8(const uint32_t* d) {
     return s;
 }
 
+// Expansion table for the train (A) side, filled once per workgroup in LDS:
+// CELL 2: byte -> 4 dwords of one-hot cells (16 i8); CELL 1: byte -> 2 dwords of bits (8 i8).
+template <int CELL>
+__device__ void knn_lut_fill(uint32_t* lut) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+        if (CELL == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lut[4 * b + i] = 1u << (8u * ((b >> (2 * i)) & 3u));
+        } else {
+            lut[2 * b] = spread4(b & 0xFu);
+            lut[2 * b + 1] = spread4((uint32_t)b >> 4);
+        }
+    }
+}
+template <int CELL>
+constexpr int knn_lut_dwords() { return CELL == 2 ? 1024 : 512; }
+
+// A fragment of k-step ks from the LUT (same element order as knn_frag)
+template <int CELL>
+__device__ __forceinline__ mfma_v4i knn_frag_lut(const uint32_t* lut, const uint32_t* d, int ks, int h) {
+    mfma_v4i f;
+    if (CELL == 2) {
+        const uint32_t v = (d[ks >> 1] >> (8u * (2u * (ks & 1) + (uint32_t)h))) & 0xFFu;
+        const uint4 e = *reinterpret_cast<const uint4*>(lut + 4 * v);
+        f[0] = (int)e.x; f[1] = (int)e.y; f[2] = (int)e.z; f[3] = (int)e.w;
+    } else {
+        const uint32_t v = (d[ks] >> (16u * (uint32_t)h)) & 0xFFFFu;
+        const uint2 lo = *reinterpret_cast<const uint2*>(lut + 2 * (v & 0xFFu));
+        const uint2 hi = *reinterpret_cast<const uint2*>(lut + 2 * (v >> 8));
+        f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)hi.x; f[3] = (int)hi.y;
+    }
+    return f;
+}
+
 // One knn pass of a workgroup: every query q < nq against the train rows of T
 // (LDS, nt rows of 8 dwords).  Queries are read from Q (global or LDS, 32-byte
 // rows).  Writes out_k0[q] = lexicographic minimum key (dist << 16 | t) and, when
 // TOP2, out_k1[q] = the second one.  Waves split the query column tiles.
+// The accumulator starts at the distance offset (128 for HAMMING2 with the query
+// one-hot negated, popc(q) for HAMMING), so the MFMA result IS the distance.
+// lut: knn_lut_fill<CELL> table in LDS.
 template <int CELL, bool TOP2>
-__device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, uint32_t* out_k0, uint32_t* out_k1) {
+__device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, uint32_t* out_k0, uint32_t* out_k1,
+                          const uint32_t* lut) {
     constexpr int KS = CELL == 2 ? 16 : 8;   // k-steps of 32
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
@@ -75,8 +115,10 @@ __device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, u
         }
         mfma_v4i bq[KS];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bq[ks] = knn_frag<CELL, true>(qd, ks, h);
-        const int pq = CELL == 2 ? 0 : popc8(qd);
+        for (int ks = 0; ks < KS; ++ks) {
+            bq[ks] = knn_frag<CELL, true>(qd, ks, h);
+        }
+        const int off = CELL == 2 ? 128 : popc8(qd);
         uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
         for (int rt = 0; rt < nrt; ++rt) {
             const int t = rt * 32 + c;
@@ -88,15 +130,19 @@ __device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, u
 #pragma unroll
                 for (int i = 0; i < 8; ++i) td[i] = 0;
             }
-            mfma_v16i acc = {};
+            mfma_v16i acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = off;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(knn_frag<CELL, false>(td, ks, h), bq[ks], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(knn_frag_lut<CELL>(lut, td, ks, h), bq[ks], acc, 0, 0, 0);
+            const uint32_t tb = (uint32_t)(rt * 32 + 4 * h);
+            const bool full = rt * 32 + 32 <= nt;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int tr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int d = CELL == 2 ? 128 - acc[r] : acc[r] + pq;
-                const uint32_t key = tr < nt ? (((uint32_t)d << 16) | (uint32_t)tr) : 0xFFFFFFFFu;
+                const uint32_t tr = tb + (uint32_t)((r & 3) + 8 * (r >> 2));
+                uint32_t key = ((uint32_t)acc[r] << 16) + tr;
+                if (!full && (int)tr >= nt) key = 0xFFFFFFFFu;
                 if (TOP2) {
                     const uint32_t hi = max(k0, key);
                     k0 = min(k0, key);

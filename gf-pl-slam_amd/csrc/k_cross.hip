@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
     int* h12 = i21 + cap;
     int* h0 = h12 + 260;
     int* misc = h0 + 260;
+    uint32_t* lut = (uint32_t*)(misc + 64);
     const int tid = threadIdx.x;
     const int Sl = p.prev.ls.n[b], Sc = p.curr.ls.n[b];
     int total = 0;
@@ -225,9 +226,10 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
         const uint8_t* DC = Cc.desc + pb * 32;
         for (int i = tid; i < Sc * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DC)[i];
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
+        knn_lut_fill<1>(lut);
         __syncthreads();
         // 12: prev queries against curr trains, knn-2 on the matrix cores (gfpl_knn.hpp)
-        knn2_mfma<1, true>(tb, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112);
+        knn2_mfma<1, true>(tb, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112, lut);
         __syncthreads();
         for (int i = tid; i < Sl; i += blockDim.x) {
             const uint32_t k0 = (uint32_t)i12[i], k1 = (uint32_t)d112[i];
@@ -239,7 +241,7 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
         for (int i = tid; i < Sl * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DP)[i];
         __syncthreads();
         // 21: curr queries against prev trains (best index only)
-        knn2_mfma<1, false>(tb, Sl, DC, Sc, (uint32_t*)i21, nullptr);
+        knn2_mfma<1, false>(tb, Sl, DC, Sc, (uint32_t*)i21, nullptr, lut);
         __syncthreads();
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = (int)((uint32_t)i21[j] & 0xFFFFu);
         __syncthreads();
@@ -315,7 +317,7 @@ hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
 }
 
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s) {
-    const size_t lds = (size_t)p.kl_cap * 32 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4;
+    const size_t lds = (size_t)p.kl_cap * 32 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4 + 512 * 4;
     hipLaunchKernelGGL(k_cross_lines, dim3(p.B), dim3(512), lds, s, p);
     return hipGetLastError();
 }

@@ -449,7 +449,7 @@ __device__ int hist_rank(const int* h, int r) {
 }
 
 // dynamic LDS: tb[cap*8] u32 (train rows: R for L->R, then L for R->L) |
-//              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
+//              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64] | knn LUT
 // Query rows stream from HBM into registers; only the train set sits in LDS, so
 // 2000 lines per side (config 5) fit.
 template <int CELL, bool INITIAL>
@@ -464,6 +464,7 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     int* rl_i = lr_d1 + cap;
     int* hist = rl_i + cap;
     int* misc = hist + 260;
+    uint32_t* lut = (uint32_t*)(misc + 64);
     const int tid = threadIdx.x;
     const int NL = min(p.in.n_kl_l[b], cap), NR = min(p.in.n_kl_r[b], cap);
     DevLines& C = p.curr.ls;   // INITIAL writes the slot passed as curr
@@ -475,9 +476,10 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
     for (int i = tid; i < NR * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DRg)[i];
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
+    knn_lut_fill<CELL>(lut);
     __syncthreads();
     // L->R knn-2 on the matrix cores (gfpl_knn.hpp): keys (dist << 16 | iR)
-    knn2_mfma<CELL, true>(tb, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1);
+    knn2_mfma<CELL, true>(tb, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1, lut);
     __syncthreads();
     for (int i = tid; i < NL; i += blockDim.x) {
         const uint32_t k0 = (uint32_t)lr_i[i], k1 = (uint32_t)lr_d1[i];
@@ -488,7 +490,7 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     for (int i = tid; i < NL * 2; i += blockDim.x) reinterpret_cast<uint4*>(tb)[i] = reinterpret_cast<const uint4*>(DLg)[i];
     __syncthreads();
     // R->L knn (only the best index is used)
-    knn2_mfma<CELL, false>(tb, NL, DRg, NR, (uint32_t*)rl_i, nullptr);
+    knn2_mfma<CELL, false>(tb, NL, DRg, NR, (uint32_t*)rl_i, nullptr, lut);
     __syncthreads();
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = (int)((uint32_t)rl_i[j] & 0xFFFFu);
     __syncthreads();
@@ -692,7 +694,7 @@ hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
-size_t stereo_lines_lds(int cap) { return (size_t)cap * 32 + (size_t)cap * 16 + 260 * 4 + 64 * 4; }
+size_t stereo_lines_lds(int cap) { return (size_t)cap * 32 + (size_t)cap * 16 + 260 * 4 + 64 * 4 + 1024 * 4; }
 
 hipError_t launch_stereo_lines(const KParams& p, hipStream_t s) {
     hipLaunchKernelGGL((k_stereo_lines<2, false>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
