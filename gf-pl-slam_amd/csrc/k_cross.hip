@@ -202,7 +202,8 @@ __device__ int hist_rank_c(const int* h, int r) {
 
 // dynamic LDS: tb[cap*8] u32 (train rows: curr for 12, then prev for 21) |
 //              i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
-__global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_cross_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
@@ -256,7 +257,7 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
         const double budget = reinterpret_cast<double*>(misc + 16)[1];
         const int cap_m = p.cfg.max_line_match_num;
         int off = 0;
-        for (int c0 = 0; c0 < Sl; c0 += 512) {
+        for (int c0 = 0; c0 < Sl; c0 += BLOCK) {
             const int i = c0 + tid;
             int acc = 0, t = 0;
             if (i < Sl) {
@@ -267,7 +268,7 @@ __global__ void __launch_bounds__(512) k_cross_lines(KParams p) {
                 acc = (!over && i == rl && dist_12 > nn12) ? 1 : 0;
             }
             int tot;
-            const int rank = off + block_exclusive_scan<512>(acc, misc, &tot);
+            const int rank = off + block_exclusive_scan<BLOCK>(acc, misc, &tot);
             if (acc && rank < cap_m) {
                 const size_t qi = pb + i, qt = pb + t;
                 P.sdisp_obs[qi] = Cc.sdisp[qt];
@@ -318,7 +319,10 @@ hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
 
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s) {
     const size_t lds = (size_t)p.kl_cap * 32 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4 + 512 * 4;
-    hipLaunchKernelGGL(k_cross_lines, dim3(p.B), dim3(512), lds, s, p);
+    if (p.kl_cap > 1024)   // large-capacity LDS layout: one workgroup per CU, 16 waves
+        hipLaunchKernelGGL(k_cross_lines<1024>, dim3(p.B), dim3(1024), lds, s, p);
+    else
+        hipLaunchKernelGGL(k_cross_lines<512>, dim3(p.B), dim3(512), lds, s, p);
     return hipGetLastError();
 }
 

@@ -166,7 +166,8 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
 // keypoints are processed in row order (order[]), so the lanes of a wave touch the
 // same descriptors and overlapping SAD window rows.  Results are keyed by iL: the
 // processing order has no effect on the output.
-__global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
     DevPoints& C = p.curr.pt;
     const size_t base = (size_t)b * cap;
     int off = 0;
-    for (int c0 = 0; c0 < KP2; c0 += 512) {
+    for (int c0 = 0; c0 < KP2; c0 += BLOCK) {
         const int i = c0 + tid;
         int flag = 0;
         float disparity = 0.0f;
@@ -320,7 +321,7 @@ __global__ void __launch_bounds__(512) k_stereo_points(KParams p, int KP2) {
             }
         }
         int tot;
-        const int pos = off + block_exclusive_scan<512>(flag, misc + 4, &tot);
+        const int pos = off + block_exclusive_scan<BLOCK>(flag, misc + 4, &tot);
         if (flag) {
             const gfpl_keypoint kp = KL[iL];
             const size_t q = base + pos;
@@ -452,8 +453,8 @@ __device__ int hist_rank(const int* h, int r) {
 //              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64] | knn LUT
 // Query rows stream from HBM into registers; only the train set sits in LDS, so
 // 2000 lines per side (config 5) fit.
-template <int CELL, bool INITIAL>
-__global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
+template <int CELL, bool INITIAL, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_stereo_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
@@ -506,7 +507,7 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
     const gfpl_keyline* KR = p.in.kl_r + (size_t)b * cap;
     const size_t base = (size_t)b * cap;
     int off = 0;
-    for (int c0 = 0; c0 < n_matches; c0 += 512) {
+    for (int c0 = 0; c0 < n_matches; c0 += BLOCK) {
         const int i = c0 + tid;
         int flag = 0;
         LineOut L;
@@ -518,7 +519,7 @@ __global__ void __launch_bounds__(512) k_stereo_lines(KParams p) {
                 flag = triangulate(p, KL[i], KR[lr_tdx], INITIAL, &L) ? 1 : 0;
         }
         int tot;
-        const int pos = off + block_exclusive_scan<512>(flag, misc + 16, &tot);
+        const int pos = off + block_exclusive_scan<BLOCK>(flag, misc + 16, &tot);
         if (flag) write_line(p, C, base + pos, L, INITIAL ? pos : -1, DLg + (size_t)i * 32);
         off += tot;
     }
@@ -690,14 +691,21 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
-    hipLaunchKernelGGL(k_stereo_points, dim3(p.B), dim3(512), lds, s, p, KP2);
+    // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
+    if (p.kp_cap > 2048)
+        hipLaunchKernelGGL(k_stereo_points<1024>, dim3(p.B), dim3(1024), lds, s, p, KP2);
+    else
+        hipLaunchKernelGGL(k_stereo_points<512>, dim3(p.B), dim3(512), lds, s, p, KP2);
     return hipGetLastError();
 }
 
 size_t stereo_lines_lds(int cap) { return (size_t)cap * 32 + (size_t)cap * 16 + 260 * 4 + 64 * 4 + 1024 * 4; }
 
 hipError_t launch_stereo_lines(const KParams& p, hipStream_t s) {
-    hipLaunchKernelGGL((k_stereo_lines<2, false>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
+    if (p.kl_cap > 1024)   // large-capacity LDS layout: one workgroup per CU, 16 waves
+        hipLaunchKernelGGL((k_stereo_lines<2, false, 1024>), dim3(p.B), dim3(1024), stereo_lines_lds(p.kl_cap), s, p);
+    else
+        hipLaunchKernelGGL((k_stereo_lines<2, false, 512>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
     return hipGetLastError();
 }
 
@@ -718,7 +726,10 @@ hipError_t launch_init(const KParams& p, hipStream_t s) {
                        p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap, cap, (int32_t*)nullptr, (float*)nullptr,
                        lr + (size_t)cap * 3, (size_t)cap * 2);
     hipLaunchKernelGGL(k_init_points, dim3(p.B), dim3(512), 0, s, p);
-    hipLaunchKernelGGL((k_stereo_lines<1, true>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
+    if (p.kl_cap > 1024)
+        hipLaunchKernelGGL((k_stereo_lines<1, true, 1024>), dim3(p.B), dim3(1024), stereo_lines_lds(p.kl_cap), s, p);
+    else
+        hipLaunchKernelGGL((k_stereo_lines<1, true, 512>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);
     hipLaunchKernelGGL(k_init_pose, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     return hipGetLastError();
 }
