@@ -169,4 +169,92 @@ __device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, u
     }
 }
 
+// Batched knn-2 over global descriptor sets (BFMatcher::knnMatch for the initial
+// frame, src/stereoFrame.cpp:183-197, and gfpl_knn2_hamming): grid (query tiles of
+// 128, sequences); each wave keeps one 32-query column tile in registers while the
+// train rows stream through LDS in chunks of KNN_CHUNK; train index < 65536.
+#define KNN_CHUNK 1024
+template <int CELL>
+__global__ void __launch_bounds__(256) k_knn2m(const uint8_t* q, const int* nq_arr, int nq_fixed, size_t q_stride,
+                                              const uint8_t* t, const int* nt_arr, int nt_fixed, size_t t_stride,
+                                              int cap_clamp, int32_t* out_idx, float* out_dist, int32_t* packed,
+                                              size_t out_stride) {
+    __shared__ __align__(16) uint32_t T[KNN_CHUNK * 8];
+    __shared__ __align__(16) uint32_t lut[knn_lut_dwords<CELL>()];
+    constexpr int KS = CELL == 2 ? 16 : 8;
+    const int b = blockIdx.y;
+    const int nq = nq_arr ? min(nq_arr[b], cap_clamp) : nq_fixed;
+    const int nt = nt_arr ? min(nt_arr[b], cap_clamp) : nt_fixed;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, c = lane & 31;
+    const int qi = (blockIdx.x * 4 + wave) * 32 + c;
+    if (blockIdx.x * 128 >= nq) return;   // uniform per workgroup
+    const uint8_t* Q = q + (size_t)b * q_stride * 32;
+    const uint8_t* Tg = t + (size_t)b * t_stride * 32;
+    knn_lut_fill<CELL>(lut);
+    uint32_t qd[8];
+    if (qi < nq) load_desc(Q + (size_t)qi * 32, qd);
+    else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qd[i] = 0;
+    }
+    mfma_v4i bq[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) bq[ks] = knn_frag<CELL, true>(qd, ks, h);
+    const int off = CELL == 2 ? 128 : popc8(qd);
+    uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+    for (int c0 = 0; c0 < nt; c0 += KNN_CHUNK) {
+        const int nc = min(KNN_CHUNK, nt - c0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nc * 2; i += blockDim.x)
+            reinterpret_cast<uint4*>(T)[i] = reinterpret_cast<const uint4*>(Tg + (size_t)c0 * 32)[i];
+        __syncthreads();
+        const int nrt = (nc + 31) >> 5;
+        for (int rt = 0; rt < nrt; ++rt) {
+            const int tl = rt * 32 + c;
+            uint32_t td[8];
+            if (tl < nc) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) td[i] = T[8 * tl + i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) td[i] = 0;
+            }
+            mfma_v16i acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = off;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(knn_frag_lut<CELL>(lut, td, ks, h), bq[ks], acc, 0, 0, 0);
+            const uint32_t tb = (uint32_t)(c0 + rt * 32 + 4 * h);
+            const bool full = rt * 32 + 32 <= nc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t tr = tb + (uint32_t)((r & 3) + 8 * (r >> 2));
+                uint32_t key = ((uint32_t)acc[r] << 16) + tr;
+                if (!full && (int)(tr - (uint32_t)c0) >= nc) key = 0xFFFFFFFFu;
+                const uint32_t hi = max(k0, key);
+                k0 = min(k0, key);
+                k1 = min(k1, hi);
+            }
+        }
+    }
+    const uint32_t o0 = __shfl_xor(k0, 32, 64), o1 = __shfl_xor(k1, 32, 64);
+    const uint32_t lo = min(k0, o0), hi0 = max(k0, o0);
+    k1 = min(hi0, min(k1, o1));
+    k0 = lo;
+    if (h == 0 && qi < nq) {
+        const int i0 = k0 == 0xFFFFFFFFu ? -1 : (int)(k0 & 0xFFFFu), i1 = k1 == 0xFFFFFFFFu ? -1 : (int)(k1 & 0xFFFFu);
+        const int d0 = k0 == 0xFFFFFFFFu ? 2147483647 : (int)(k0 >> 16), d1 = k1 == 0xFFFFFFFFu ? 2147483647 : (int)(k1 >> 16);
+        if (out_idx) {
+            out_idx[2 * qi] = i0; out_idx[2 * qi + 1] = i1;
+            out_dist[2 * qi] = (float)d0; out_dist[2 * qi + 1] = (float)d1;
+        }
+        if (packed) {
+            int32_t* o = packed + (size_t)b * out_stride * 3;
+            o[3 * qi] = i0; o[3 * qi + 1] = d0; o[3 * qi + 2] = d1;
+        }
+    }
+}
+
 }  // namespace gfpl

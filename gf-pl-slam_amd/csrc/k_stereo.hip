@@ -718,11 +718,12 @@ hipError_t launch_init(const KParams& p, hipStream_t s) {
     // points: knn-2 NORM_HAMMING L->R and R->L into scratch, then gates
     const int cap = p.kp_cap;
     int32_t* lr = p.scr.knn;
-    dim3 g((cap + 255) / 256, p.B);
-    hipLaunchKernelGGL((k_knn2<1>), g, dim3(256), 0, s, p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap,
+    // MFMA knn (gfpl_knn.hpp): 128 queries per workgroup, train rows streamed through LDS
+    const dim3 gm((cap + 127) / 128, p.B);
+    hipLaunchKernelGGL((k_knn2m<1>), gm, dim3(256), 0, s, p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap,
                        p.in.pdesc_r, p.in.n_kp_r, 0, (size_t)cap, cap, (int32_t*)nullptr, (float*)nullptr,
                        lr, (size_t)cap * 2);
-    hipLaunchKernelGGL((k_knn2<1>), g, dim3(256), 0, s, p.in.pdesc_r, p.in.n_kp_r, 0, (size_t)cap,
+    hipLaunchKernelGGL((k_knn2m<1>), gm, dim3(256), 0, s, p.in.pdesc_r, p.in.n_kp_r, 0, (size_t)cap,
                        p.in.pdesc_l, p.in.n_kp_l, 0, (size_t)cap, cap, (int32_t*)nullptr, (float*)nullptr,
                        lr + (size_t)cap * 3, (size_t)cap * 2);
     hipLaunchKernelGGL(k_init_points, dim3(p.B), dim3(512), 0, s, p);
@@ -741,6 +742,16 @@ hipError_t launch_step_bytes(const KParams& p, hipStream_t s) {
 
 hipError_t launch_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* idx, float* dist,
                        hipStream_t s) {
+    if (nt <= 65536) {   // MFMA path: the packed key holds a 16-bit train index
+        const dim3 g((nq + 127) / 128, 1);
+        if (cell == 2)
+            hipLaunchKernelGGL((k_knn2m<2>), g, dim3(256), 0, s, q, (const int*)nullptr, nq, (size_t)0, t,
+                               (const int*)nullptr, nt, (size_t)0, 0, idx, dist, (int32_t*)nullptr, (size_t)0);
+        else
+            hipLaunchKernelGGL((k_knn2m<1>), g, dim3(256), 0, s, q, (const int*)nullptr, nq, (size_t)0, t,
+                               (const int*)nullptr, nt, (size_t)0, 0, idx, dist, (int32_t*)nullptr, (size_t)0);
+        return hipGetLastError();
+    }
     dim3 g((nq + 255) / 256, 1);
     if (cell == 2)
         hipLaunchKernelGGL((k_knn2<2>), g, dim3(256), 0, s, q, (const int*)nullptr, nq, (size_t)0, t,

@@ -104,6 +104,30 @@ def test_small_counts_parity():
     _check(rep)
 
 
+@pytest.mark.parametrize("nq,nt", [(33, 2), (5, 2049), (1000, 3000), (64, 31)])
+def test_knn2_hamming_shapes(nq, nt):
+    """gfpl_knn2_hamming (MFMA path) on ragged tile shapes and a train set that spans
+    several LDS chunks, with planted ties, against the oracle's BFMatcher restatement."""
+    import torch
+    rng = np.random.default_rng(nq * 7 + nt)
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    t[nt - 1] = t[0]                 # a tie across the whole train range
+    q[nq // 2] = t[nt // 2]          # an exact match
+    cfg = gfpl.default_config()
+    ctx = gfpl.Context(gfpl.make_camera("vga", cfg), cfg)
+    qd, td = torch.from_numpy(q).cuda(), torch.from_numpy(t).cuda()
+    for cell in (1, 2):
+        idx = torch.zeros((nq, 2), dtype=torch.int32, device="cuda")
+        dist = torch.zeros((nq, 2), dtype=torch.float32, device="cuda")
+        assert ctx.knn2(qd, nq, td, nt, cell, idx, dist) == 0
+        ctx.synchronize()
+        rc, oi, od = O.knn2(q, t, cell)
+        assert rc == 0
+        assert np.array_equal(idx.cpu().numpy(), oi), cell
+        assert np.array_equal(dist.cpu().numpy(), od), cell
+
+
 def test_knn2_hamming_parity():
     import torch
     rng = np.random.default_rng(5)
