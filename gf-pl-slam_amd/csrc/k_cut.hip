@@ -247,10 +247,12 @@ __device__ __forceinline__ bool same_bits(double a, double b) {
 }
 
 __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
-    __shared__ double sum[CUT_G][24];
-    __shared__ double sumb[CUT_G][24];
-    __shared__ double ep[CUT_G][6][8];
-    __shared__ double val[CUT_G][8];
+    // per-group rows padded by one double so the 8 groups of a wave sit in
+    // different LDS banks when their lanes read the same entry
+    __shared__ double sum[CUT_G][25];
+    __shared__ double sumb[CUT_G][25];
+    __shared__ double epf[CUT_G * 49];   // group g, slot j: epf + 49 g + 8 j (v, J[6])
+    __shared__ double val[CUT_G][9];
     __shared__ int vld[CUT_G][8];
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
@@ -306,7 +308,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             if (eside == 0) cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, t, out);
             else cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, t, out);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) ep[g][j][i] = out[i];
+            for (int i = 0; i < 7; ++i) epf[49 * g + 8 * j + i] = out[i];
         }
         __syncthreads();
         // ---- C: neighbour j (or the setup logdet)
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
             } else {
                 double tmp[21];
-                cut_assemble<false>(ep[g][cs], ep[g][ce], tmp);
+                cut_assemble<false>(epf + 49 * g + 8 * cs, epf + 49 * g + 8 * ce, tmp);
 #pragma unroll
                 for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
             }
@@ -362,7 +364,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             double S7[7], E7[7];
             if (!stale_mid) {
 #pragma unroll
-                for (int i = 0; i < 7; ++i) { S7[i] = ep[g][1][i]; E7[i] = ep[g][4][i]; }
+                for (int i = 0; i < 7; ++i) { S7[i] = epf[49 * g + 8 + i]; E7[i] = epf[49 * g + 32 + i]; }
             } else {
                 cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, r0, S7);
                 cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, r1, E7);

@@ -32,6 +32,9 @@ struct PoseLDS {
 };
 
 #define PT_K 6    // X Y Z ox oy sigma2
+// chunk rows are 65 doubles apart: the reduction lanes read rows ia, ib of the
+// same column k, and a 64-double stride would put every row in the same LDS bank
+#define CH_STRIDE 65
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
 // evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w
@@ -116,18 +119,18 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cp[i * 64 + lane] = o[i];
+            for (int i = 0; i < 8; ++i) cp[i * CH_STRIDE + lane] = o[i];
             if (f < X.nls && actl[f]) eval_line(cam, homog, DT, X.lin + f, X.mls_cap, o);
             else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cl[i * 64 + lane] = o[i];
+            for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
             __syncthreads();
-            const double* A = buf + ia * 64;
-            const double* Bv = buf + ib * 64;
-            const double* W = buf + 7 * 64;
+            const double* A = buf + ia * CH_STRIDE;
+            const double* Bv = buf + ib * CH_STRIDE;
+            const double* W = buf + 7 * CH_STRIDE;
 #pragma unroll 16
             for (int k = 0; k < 64; ++k) s = s + (A[k] * Bv[k]) * W[k];
             __syncthreads();
@@ -212,7 +215,7 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// dynamic LDS: {cp[8*64] cl[8*64] | rp[mpt_cap] rl[mls_cap]} f64 | buf[NP2] f64 | act[mpt+mls] u8
+// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | rp[mpt_cap] rl[mls_cap]} f64 | buf[NP2] f64 | act[mpt+mls] u8
 __global__ void __launch_bounds__(64) k_pose(KParams p, int NP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ PoseLDS S;
@@ -220,9 +223,9 @@ __global__ void __launch_bounds__(64) k_pose(KParams p, int NP2) {
     const int lane = threadIdx.x;
     const int npt = p.tr.n_matched_pt[b], nls = p.tr.n_matched_ls[b];
     // the GN chunk rows and the outlier residuals are never live together
-    const int region = max(16 * 64, p.mpt_cap + p.mls_cap);
+    const int region = max(16 * CH_STRIDE, p.mpt_cap + p.mls_cap);
     double* cp = (double*)smem;
-    double* cl = cp + 8 * 64;
+    double* cl = cp + 8 * CH_STRIDE;
     double* rp = cp;
     double* rl = rp + p.mpt_cap;
     double* buf = cp + region;
@@ -456,7 +459,7 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
-    const size_t region = (size_t)std::max(16 * 64, p.mpt_cap + p.mls_cap);
+    const size_t region = (size_t)std::max(16 * CH_STRIDE, p.mpt_cap + p.mls_cap);
     const size_t lds = (region + NP2) * 8 + (p.mpt_cap + p.mls_cap) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
