@@ -90,16 +90,31 @@ __device__ __forceinline__ mfma_v4i knn_frag_lut(const uint32_t* lut, const uint
     return f;
 }
 
+// Stage nt descriptor rows (32 B each, global) into LDS as structure-of-arrays:
+// dword i of row t at T[i * stride + t], so a wave reading 32 consecutive rows
+// touches consecutive banks.
+__device__ __forceinline__ void knn_stage_soa(uint32_t* T, int stride, const uint8_t* src, int nt) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    for (int k = threadIdx.x; k < nt * 2; k += blockDim.x) {   // coalesced 16-B reads
+        const uint4 v = s4[k];
+        const int t = k >> 1, i0 = (k & 1) * 4;
+        T[(i0 + 0) * stride + t] = v.x;
+        T[(i0 + 1) * stride + t] = v.y;
+        T[(i0 + 2) * stride + t] = v.z;
+        T[(i0 + 3) * stride + t] = v.w;
+    }
+}
+
 // One knn pass of a workgroup: every query q < nq against the train rows of T
-// (LDS, nt rows of 8 dwords).  Queries are read from Q (global or LDS, 32-byte
-// rows).  Writes out_k0[q] = lexicographic minimum key (dist << 16 | t) and, when
+// (LDS, structure-of-arrays, knn_stage_soa).  Queries are read from Q (global,
+// 32-byte rows).  Writes out_k0[q] = lexicographic minimum key (dist << 16 | t) and, when
 // TOP2, out_k1[q] = the second one.  Waves split the query column tiles.
 // The accumulator starts at the distance offset (128 for HAMMING2 with the query
 // one-hot negated, popc(q) for HAMMING), so the MFMA result IS the distance.
 // lut: knn_lut_fill<CELL> table in LDS.
 template <int CELL, bool TOP2>
-__device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, uint32_t* out_k0, uint32_t* out_k1,
-                          const uint32_t* lut) {
+__device__ void knn2_mfma(const uint32_t* T, int tstride, int nt, const uint8_t* Q, int nq, uint32_t* out_k0,
+                          uint32_t* out_k1, const uint32_t* lut) {
     constexpr int KS = CELL == 2 ? 16 : 8;   // k-steps of 32
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
@@ -125,7 +140,7 @@ __device__ void knn2_mfma(const uint32_t* T, int nt, const uint8_t* Q, int nq, u
             uint32_t td[8];
             if (t < nt) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) td[i] = T[8 * t + i];
+                for (int i = 0; i < 8; ++i) td[i] = T[i * tstride + t];
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) td[i] = 0;
@@ -206,8 +221,7 @@ __global__ void __launch_bounds__(256) k_knn2m(const uint8_t* q, const int* nq_a
     for (int c0 = 0; c0 < nt; c0 += KNN_CHUNK) {
         const int nc = min(KNN_CHUNK, nt - c0);
         __syncthreads();
-        for (int i = threadIdx.x; i < nc * 2; i += blockDim.x)
-            reinterpret_cast<uint4*>(T)[i] = reinterpret_cast<const uint4*>(Tg + (size_t)c0 * 32)[i];
+        knn_stage_soa(T, KNN_CHUNK, Tg + (size_t)c0 * 32, nc);
         __syncthreads();
         const int nrt = (nc + 31) >> 5;
         for (int rt = 0; rt < nrt; ++rt) {
@@ -215,7 +229,7 @@ __global__ void __launch_bounds__(256) k_knn2m(const uint8_t* q, const int* nq_a
             uint32_t td[8];
             if (tl < nc) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) td[i] = T[8 * tl + i];
+                for (int i = 0; i < 8; ++i) td[i] = T[i * KNN_CHUNK + tl];
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) td[i] = 0;

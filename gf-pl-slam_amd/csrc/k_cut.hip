@@ -139,7 +139,7 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
 
 // ------------------------------------------------------------------ prep --
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
-    __shared__ double chunk[21][64];   // lower-triangle infos of 64 list entries
+    __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     const int nls = p.tr.n_matched_ls[b];
