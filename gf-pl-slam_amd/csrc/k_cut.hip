@@ -254,6 +254,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     __shared__ double epf[CUT_G * 49];   // group g, slot j: epf + 49 g + 8 j (v, J[6])
     __shared__ double val[CUT_G][9];
     __shared__ int vld[CUT_G][8];
+    __shared__ double nxt[CUT_G][49];    // prefetched next line: sP eP covS covE Jl (26) | r=0 info (21)
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -282,6 +283,28 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     int moved = 0;
     double r0 = 0.0, r1 = 0.0, mb = 0.0, mb_init = 0.0;
     LineCutData d;
+    // Next-line prefetch: lane j loads elements j, j+8, ... of the 47-element vector
+    // [line data | r = 0 info] of the group's next line right after a line opens;
+    // the values land in LDS one iteration later, so opening a line never waits on HBM.
+    double pf[6];
+    int pending = 0;
+    auto pf_issue = [&](int mm) {
+        const size_t q = lb + mls[mm];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int e = j + 8 * k;
+            const double* src;
+            size_t off;
+            if (e < 3) { src = L.sP; off = 3 * q + e; }
+            else if (e < 6) { src = L.eP; off = 3 * q + (e - 3); }
+            else if (e < 15) { src = L.covS; off = 9 * q + (e - 6); }
+            else if (e < 24) { src = L.covE; off = 9 * q + (e - 15); }
+            else if (e < 26) { src = L.le_obs; off = 3 * q + (e - 24); }
+            else { src = scr_l; off = (size_t)mm * 21 + (size_t)(e < 47 ? e - 26 : 0); }
+            pf[k] = src[off];
+        }
+        pending = 1;
+    };
     if (m < nls) {
         load_line(L, lb + mls[m], d);
         for (int e = j; e < 21; e += 8) {
@@ -291,6 +314,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         }
         mb = p.scr.cut_sum[24 * b + 21];   // logdet(invCov_sum) from k_cut_prep
         mb_init = mb;
+        if (nls > 1) pf_issue(1);
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) { d.sP[k] = 0.0; d.eP[k] = 1.0; }
@@ -333,6 +357,14 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 val[g][j] = v;
                 vld[g][j] = setup ? 0 : valid;
             }
+        }
+        __syncthreads();
+        // ---- land the prefetched next line in LDS (its loads were issued >= 1 iteration ago)
+        if (pending) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (j + 8 * k < 47) nxt[g][j + 8 * k] = pf[k];
+            pending = 0;
         }
         __syncthreads();
         // ---- D: group decision (all 8 lanes compute it identically)
@@ -397,14 +429,21 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 moved = 0;
                 r0 = 0.0;
                 r1 = 0.0;
-                load_line(L, lb + mls[m], d);
+                // line m from the prefetch buffer (same values load_line would read)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { d.sP[k] = nxt[g][k]; d.eP[k] = nxt[g][3 + k]; }
+#pragma unroll
+                for (int k = 0; k < 9; ++k) { d.covS[k] = nxt[g][6 + k]; d.covE[k] = nxt[g][15 + k]; }
+                d.Jl[0] = nxt[g][24];
+                d.Jl[1] = nxt[g][25];
                 // open line m: sumb = invCov_sum, sum = invCov_sum - info(line m, r = 0)
                 for (int e = j; e < 21; e += 8) {
                     const double s0 = sum[g][e];
                     sumb[g][e] = s0;
-                    sum[g][e] = s0 - scr_l[(size_t)m * 21 + e];
+                    sum[g][e] = s0 - nxt[g][26 + e];
                 }
                 if (!setup) mb_init = mb;
+                if (m + 1 < nls) pf_issue(m + 1);
             }
         }
         __syncthreads();
