@@ -153,6 +153,8 @@ int cfg_supported(const gfpl_config& c) {
     if (!c.best_lr_matches || !c.lr_in_parallel || !c.cut_with_max_vol) return GFPL_E_UNSUPPORTED;
     if (c.max_point_match_num < 1 || c.max_point_match_num > GFPL_MAX_MATCHED_PT) return GFPL_E_INVALID;
     if (c.max_line_match_num < 1 || c.max_line_match_num > GFPL_MAX_MATCHED_LS) return GFPL_E_INVALID;
+    // the certified cut search needs a margin far above its ~1e-13 error
+    if (!(c.cut_certify == 0.0 || (c.cut_certify >= 1e-10 && c.cut_certify < 1.0))) return GFPL_E_INVALID;
     return GFPL_OK;
 }
 

@@ -41,6 +41,7 @@ extern "C" int gfpl_config_default(gfpl_config* c) {
     c->cut_rng[0] = 0.0;
     c->cut_rng[1] = 1.0;
     c->proj_gate_px = 10.0;
+    c->cut_certify = 1e-9;
     return GFPL_OK;
 }
 

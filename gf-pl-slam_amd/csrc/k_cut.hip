@@ -7,8 +7,7 @@
 // reads invCov_sum after all earlier lines were cut.  Three kernels:
 //  k_cut_prep   (one wave / sequence) r = (0,0) infos of lines and points and
 //               invCov_sum, each entry summed in list order (lines, then points)
-//               by one lane over 64-entry chunks staged in LDS, plus the metric
-//               logdet(invCov_sum) that opens the first line;
+//               by one lane over 64-entry chunks staged in LDS;
 //  k_cut_search (8 sequences per wave, 8 lanes each) the greedy search, one step
 //               of every chain per wave iteration (see the comment at the kernel);
 //  k_cut_finish (parallel) full 6x6 info of the chosen ratio (invCovPose) and
@@ -202,35 +201,46 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         __syncthreads();
     }
     if (lane < 21) p.scr.cut_sum[24 * b + lane] = s;
-    __syncthreads();
-    if (lane == 0) {   // metric of the first line's search: logdet(invCov_sum) (:1671)
-        double a[21];
-#pragma unroll
-        for (int i = 0; i < 21; ++i) a[i] = p.scr.cut_sum[24 * b + i];
-        p.scr.cut_sum[24 * b + 21] = logdet6_lower(a);
-    }
 }
 
 // ---------------------------------------------------------------- search --
 // 8 sequences per wave, 8 lanes each; every wave iteration is one greedy step
-// of each of its 8 chains, in three phases separated by wave barriers:
-//   E  lanes 0-2 of a group compute the start endpoint at t0 = r0 + {-s, 0, +s},
-//      lanes 3-5 the end endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint: blend,
-//      projected variance, pose Jacobian).  A neighbour's start terms depend on
-//      t0 only and its end terms on t1 only, so the 8 neighbours share these 6;
-//   C  lane j assembles neighbour j's info from its two endpoints, adds
-//      invCov_sum and takes the logdet (first failing LLT pivot kept, Q11);
-//   D  the group takes the first strict maximum over the valid neighbours (the
-//      reference's j-loop); no improvement finalises the line: invCov_sum +=
-//      info of the chosen ratio (re-assembled from the middle endpoints, the
-//      same arithmetic as the chosen candidate's), the cut ratio is stored and
-//      the next line opens at (0, 0).
-// The metric that opens line m+1, logdet(invCov_sum), equals line m's final
-// metric whenever line m moved: invCov_sum' = (sum - info_m) + chosen has the
-// bits of the chosen candidate's own total chosen + (sum - info_m).  Only when a
-// line never moved and the sum did not come back bit-identical is it evaluated
-// (one extra "setup" iteration, lane 0 of the group).
-#define CUT_G 8   // sequences per wave (8 lanes each)
+// of each of its 8 chains.
+//
+// Certified comparisons.  Within line m the search compares
+// logdet(S + info(t0, t1)) over neighbours, S = invCov_sum - info_m(0, 0) fixed
+// for the line, and info = Js Js^T / vs + Je Je^T / ve (rank 2, ledger Q10).  By
+// the matrix determinant lemma logdet(S + info) = logdet(S) + log d with
+//   d = (1 + as)(1 + ae) - c^2 / (vs ve),  as = |ws|^2 / vs, ae = |we|^2 / ve,
+//   c = ws . we,  ws = L^-1 Js, we = L^-1 Je,  S = L L^T,
+// so the step's decision (the reference's first strict maximum over the valid
+// neighbours, starting from the centre's metric) only needs the d values: ws and
+// as depend on t0 only, we and ae on t1 only, and a neighbour costs one 6-term
+// dot product instead of a 6x6 LLT and six logs.  The decision is accepted when
+// every comparison it rests on is separated by more than cfg.cut_certify
+// (relative, 1e-9) — four orders of magnitude above the measured disagreement
+// between d and the reference's own LLT arithmetic (<= 1e-13).
+// Otherwise (and whenever S or an endpoint is not healthy) the group evaluates
+// that step exactly as the reference does: neighbour j's info assembled from its
+// endpoints, + S, LLT, six fdlibm logs, against the exact centre metric.  Either
+// way the chosen ratios are the reference's; the metric values themselves are
+// never output.
+//
+// Phases (wave barriers between them):
+//   E1  lanes 0-2 compute the start endpoint at t0 = r0 + {-s, 0, +s}, lanes 3-5
+//       the end endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint); lane 6 factors
+//       S when the line just opened;
+//   E2  lanes 0-5: w = L^-1 J and a = |w|^2 / v of their endpoint;
+//   C   lane j: d of neighbour j; every lane: d of the centre;
+//   D   certified decision, or the exact evaluation of the step (X) when any
+//       group of the wave needs it; no improvement finalises the line:
+//       invCov_sum += info of the chosen ratio (re-assembled from the middle
+//       endpoints, the same arithmetic as the chosen candidate's), the cut
+//       ratio is stored and the next line opens at (0, 0).
+#define CUT_G 8          // sequences per wave (8 lanes each)
+#define CUT_SL 15        // endpoint slot: v, J[6], w[6], a, (pad)
+#define CUT_EP 91        // per-group endpoint block: 6 slots + 1 (odd stride)
+#define CUT_CH 29        // per-group factor of S: L (21), 1/L_kk (6), ok, (pad)
 
 __device__ __forceinline__ double nb_step(int j, int side, double st) {
     // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
@@ -242,17 +252,57 @@ __device__ __forceinline__ int nb_slot(int j, int side) {   // endpoint slot: 0:
     if (side == 0) return (j == 0 || j == 4 || j == 5) ? 2 : ((j == 1 || j == 6 || j == 7) ? 0 : 1);
     return (j == 2 || j == 4 || j == 6) ? 2 : ((j == 3 || j == 5 || j == 7) ? 0 : 1);
 }
-__device__ __forceinline__ bool same_bits(double a, double b) {
-    return __double_as_longlong(a) == __double_as_longlong(b);
+
+// S = L L^T for the certified comparisons (out: L lower 21, 1/L_kk 6, ok).  ok = 0
+// unless every pivot keeps at least 1e-6 of its diagonal (the synthetic and EuRoC
+// workloads stay above 0.1); the line is then searched with exact steps only.
+__device__ __forceinline__ void chol_s(const double* a, double* out) {
+    double L[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) L[i] = a[i];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double akk = L[tri(k, k)];
+        double x = akk;
+#pragma unroll
+        for (int j = 0; j < k; ++j) x = x - L[tri(k, j)] * L[tri(k, j)];
+        if (!(x > 1e-6 * akk && akk < 1e300)) { ok = false; x = 1.0; }
+        const double dk = sqrt(x), r = 1.0 / dk;
+        L[tri(k, k)] = dk;
+        out[21 + k] = r;
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            double v = L[tri(i, k)];
+#pragma unroll
+            for (int j = 0; j < k; ++j) v = v - L[tri(i, j)] * L[tri(k, j)];
+            L[tri(i, k)] = v * r;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 21; ++i) out[i] = L[i];
+    out[27] = ok ? 1.0 : 0.0;
+}
+
+// d of the neighbour whose endpoints sit in slots S, E (NaN when not usable)
+__device__ __forceinline__ double cut_d(const double* S, const double* E) {
+    double c = S[7] * E[7];
+#pragma unroll
+    for (int i = 1; i < 6; ++i) c = c + S[7 + i] * E[7 + i];
+    const double vs = S[0], ve = E[0];
+    const double d = (1.0 + S[13]) * (1.0 + E[13]) - (c * c) / (vs * ve);
+    return (vs > 0.0 && ve > 0.0 && d > 0.0 && d < 1e300) ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
 
 __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
-    // per-group rows padded by one double so the 8 groups of a wave sit in
+    // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
-    __shared__ double sum[CUT_G][25];
-    __shared__ double sumb[CUT_G][25];
-    __shared__ double epf[CUT_G * 49];   // group g, slot j: epf + 49 g + 8 j (v, J[6])
-    __shared__ double val[CUT_G][9];
+    __shared__ double sum[CUT_G][25];    // S
+    __shared__ double sumb[CUT_G][25];   // invCov_sum when the line opened
+    __shared__ double chol[CUT_G][CUT_CH];
+    __shared__ double epf[CUT_G][CUT_EP];
+    __shared__ double val[CUT_G][9];     // d of neighbours 0-7, centre
+    __shared__ double vx[CUT_G][9];      // exact metrics of an exact step
     __shared__ int vld[CUT_G][8];
     __shared__ double nxt[CUT_G][49];    // prefetched next line: sP eP covS covE Jl (26) | r=0 info (21)
     const int lane = threadIdx.x;
@@ -262,6 +312,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     const int nls = live ? p.tr.n_matched_ls[b] : 0;
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
+    const double tau = p.cfg.cut_certify;
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
@@ -274,14 +325,15 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     // E role of this lane
     const int eside = j < 3 ? 0 : 1;
     const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
+    double* my_slot = &epf[g][CUT_SL * (j < 6 ? j : 0)];
     // C role: neighbour j
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
     // group state (identical in the 8 lanes of a group)
     int m = 0;
-    int setup = 0;       // 1: this iteration evaluates logdet(invCov_sum) only
-    int moved = 0;
-    double r0 = 0.0, r1 = 0.0, mb = 0.0, mb_init = 0.0;
+    int first = 1;       // first step of the line: the exact centre metric is logdet(sumb)
+    int need_chol = 1;   // S changed: lane 6 factors it in the next E1
+    double r0 = 0.0, r1 = 0.0;
     LineCutData d;
     // Next-line prefetch: lane j loads elements j, j+8, ... of the 47-element vector
     // [line data | r = 0 info] of the group's next line right after a line opens;
@@ -312,8 +364,6 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             sumb[g][e] = s0;
             sum[g][e] = s0 - scr_l[e];
         }
-        mb = p.scr.cut_sum[24 * b + 21];   // logdet(invCov_sum) from k_cut_prep
-        mb_init = mb;
         if (nls > 1) pf_issue(1);
     } else {
 #pragma unroll
@@ -321,44 +371,62 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) { d.covS[k] = 0.0; d.covE[k] = 0.0; }
         d.Jl[0] = 0.0; d.Jl[1] = 0.0;
+        need_chol = 0;
     }
     __syncthreads();
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- E: the six endpoints of this step
+        // ---- E1: the six endpoints of this step; the factor of a new line's S
         if (j < 6) {
             const double t = (eside == 0 ? r0 : r1) + eoff;
             double out[7];
             if (eside == 0) cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, t, out);
             else cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, t, out);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) epf[49 * g + 8 * j + i] = out[i];
+            for (int i = 0; i < 7; ++i) my_slot[i] = out[i];
+        } else if (j == 6 && need_chol) {
+            double a[21];
+#pragma unroll
+            for (int i = 0; i < 21; ++i) a[i] = sum[g][i];
+            double o[28];
+            chol_s(a, o);
+#pragma unroll
+            for (int i = 0; i < 28; ++i) chol[g][i] = o[i];
+        }
+        need_chol = 0;
+        __syncthreads();
+        // ---- E2: w = L^-1 J, a = |w|^2 / v
+        if (j < 6) {
+            double w[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double u = my_slot[1 + i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) u = u - chol[g][tri(i, k)] * w[k];
+                w[i] = u * chol[g][21 + i];
+            }
+            double a = w[0] * w[0];
+#pragma unroll
+            for (int i = 1; i < 6; ++i) a = a + w[i] * w[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) my_slot[7 + i] = w[i];
+            my_slot[13] = a / my_slot[0];
         }
         __syncthreads();
-        // ---- C: neighbour j (or the setup logdet)
+        // ---- C: d of neighbour j and of the centre
+        const double t0 = r0 + nb0, t1 = r1 + nb1;
+        int valid = 1;
+        if (t0 + t1 > 1.0) valid = 0;
+        if (t0 < rlo || t0 > rhi) valid = 0;
+        if (t1 < rlo || t1 > rhi) valid = 0;
         {
-            const double t0 = r0 + nb0, t1 = r1 + nb1;
-            int valid = 1;
-            if (t0 + t1 > 1.0) valid = 0;
-            if (t0 < rlo || t0 > rhi) valid = 0;
-            if (t1 < rlo || t1 > rhi) valid = 0;
-            double tot[21];
-            if (setup) {
-#pragma unroll
-                for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
-            } else {
-                double tmp[21];
-                cut_assemble<false>(epf + 49 * g + 8 * cs, epf + 49 * g + 8 * ce, tmp);
-#pragma unroll
-                for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
-            }
-            const double v = logdet6_lower(tot);
+            const double dj = cut_d(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce]);
             if (act) {
-                val[g][j] = v;
-                vld[g][j] = setup ? 0 : valid;
+                val[g][j] = dj;
+                vld[g][j] = valid;
+                if (j == 0) val[g][8] = cut_d(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4]);
             }
         }
-        __syncthreads();
         // ---- land the prefetched next line in LDS (its loads were issued >= 1 iteration ago)
         if (pending) {
 #pragma unroll
@@ -367,28 +435,66 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             pending = 0;
         }
         __syncthreads();
-        // ---- D: group decision (all 8 lanes compute it identically)
-        int finalize = 0, stale_mid = 0;
+        // ---- D: certified decision (all 8 lanes of a group compute it identically)
+        int best = -1;
+        int exact = 0;
         if (act) {
-            if (setup) {
-                mb = val[g][0];
-                mb_init = mb;
-                setup = 0;
-            } else {
-                double mi = mb;
-                int best = -1;
+            const double dc = val[g][8];
+            double mi = dc;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                if (vld[g][jj] && val[g][jj] > mi) { mi = val[g][jj]; best = jj; }
+            // every comparison the decision rests on must clear the margin; NaN
+            // (unhealthy) values fail every test
+            bool cert = tau > 0.0 && chol[g][27] != 0.0 && dc == dc;
+            const double top = best >= 0 ? mi : dc;
+            if (best >= 0 && !(top - dc > tau * top)) cert = false;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                if (vld[g][jj] && jj != best && !(top - val[g][jj] > tau * top)) cert = false;
+            exact = cert ? 0 : 1;
+        }
+        if (__any(exact)) {
+            // ---- X: the reference's evaluation of this step for the groups that need it
+            if (exact) {
+                double tot[21];
+                double tmp[21];
+                cut_assemble<false>(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], tmp);
+#pragma unroll
+                for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
+                vx[g][j] = logdet6_lower(tot);
+                if (j == 0) {
+                    // centre metric: logdet(invCov_sum) on a line's first step (:1671),
+                    // else the previous step's chosen candidate, re-evaluated (same bits)
+                    if (first) {
+#pragma unroll
+                        for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
+                    } else {
+                        cut_assemble<false>(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4], tmp);
+#pragma unroll
+                        for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
+                    }
+                    vx[g][8] = logdet6_lower(tot);
+                }
+            }
+            __syncthreads();
+            if (exact) {
+                double mi = vx[g][8];
+                best = -1;
 #pragma unroll
                 for (int jj = 0; jj < 8; ++jj)
-                    if (vld[g][jj] && val[g][jj] > mi) { mi = val[g][jj]; best = jj; }
-                if (best >= 0) {
-                    r0 = r0 + nb_step(best, 0, st);
-                    r1 = r1 + nb_step(best, 1, st);
-                    mb = mi;
-                    moved = 1;
-                    if (!(r0 + r1 <= 1.0)) { finalize = 1; stale_mid = 1; }   // while-condition
-                } else {
-                    finalize = 1;   // the middle endpoints of this step are (r0 + 0, r1 + 0) = (r0, r1)
-                }
+                    if (vld[g][jj] && vx[g][jj] > mi) { mi = vx[g][jj]; best = jj; }
+            }
+        }
+        int finalize = 0, stale_mid = 0;
+        if (act) {
+            first = 0;
+            if (best >= 0) {
+                r0 = r0 + nb_step(best, 0, st);
+                r1 = r1 + nb_step(best, 1, st);
+                if (!(r0 + r1 <= 1.0)) { finalize = 1; stale_mid = 1; }   // while-condition
+            } else {
+                finalize = 1;   // the middle endpoints of this step are (r0 + 0, r1 + 0) = (r0, r1)
             }
         }
         if (act && finalize) {
@@ -396,25 +502,16 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             double S7[7], E7[7];
             if (!stale_mid) {
 #pragma unroll
-                for (int i = 0; i < 7; ++i) { S7[i] = epf[49 * g + 8 + i]; E7[i] = epf[49 * g + 32 + i]; }
+                for (int i = 0; i < 7; ++i) { S7[i] = epf[g][CUT_SL * 1 + i]; E7[i] = epf[g][CUT_SL * 4 + i]; }
             } else {
                 cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, r0, S7);
                 cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, r1, E7);
             }
             double info[21];
             cut_assemble<false>(S7, E7, info);
-            int differs = 0;
 #pragma unroll
-            for (int e = 0; e < 21; ++e) {   // lane j owns entries j, j+8, j+16 (compile-time register index)
-                if ((e & 7) == j) {
-                    const double ns = sum[g][e] + info[e];
-                    differs |= same_bits(ns, sumb[g][e]) ? 0 : 1;
-                    sum[g][e] = ns;
-                }
-            }
-            // group-level "the sum came back bit-identical" (consulted only if the line never moved)
-            const unsigned long long bad = __ballot(differs);
-            const bool same = ((bad >> (8 * g)) & 0xFFull) == 0;
+            for (int e = 0; e < 21; ++e)   // lane j owns entries j, j+8, j+16 (compile-time register index)
+                if ((e & 7) == j) sum[g][e] = sum[g][e] + info[e];
             if (j == 0) {
                 const size_t q = lb + mls[m];
                 L.cut[2 * q] = r0;
@@ -422,11 +519,8 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             }
             ++m;
             if (m < nls) {
-                if (!moved) {
-                    if (same) mb = mb_init;   // logdet of a bit-identical sum
-                    else setup = 1;           // evaluated next iteration
-                }
-                moved = 0;
+                first = 1;
+                need_chol = 1;
                 r0 = 0.0;
                 r1 = 0.0;
                 // line m from the prefetch buffer (same values load_line would read)
@@ -436,13 +530,12 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 for (int k = 0; k < 9; ++k) { d.covS[k] = nxt[g][6 + k]; d.covE[k] = nxt[g][15 + k]; }
                 d.Jl[0] = nxt[g][24];
                 d.Jl[1] = nxt[g][25];
-                // open line m: sumb = invCov_sum, sum = invCov_sum - info(line m, r = 0)
+                // open line m: sumb = invCov_sum, S = invCov_sum - info(line m, r = 0)
                 for (int e = j; e < 21; e += 8) {
                     const double s0 = sum[g][e];
                     sumb[g][e] = s0;
                     sum[g][e] = s0 - nxt[g][26 + e];
                 }
-                if (!setup) mb_init = mb;
                 if (m + 1 < nls) pf_issue(m + 1);
             }
         }

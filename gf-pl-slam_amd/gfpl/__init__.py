@@ -67,7 +67,8 @@ class Config(C.Structure):
                 ("inlier_k", C.c_double), ("motion_step_th", C.c_double),
                 ("orb_scale_factor", C.c_double), ("orb_n_levels", C.c_int),
                 ("lsd_scale", C.c_double), ("cut_step", C.c_double),
-                ("cut_rng", C.c_double * 2), ("proj_gate_px", C.c_double)]
+                ("cut_rng", C.c_double * 2), ("proj_gate_px", C.c_double),
+                ("cut_certify", C.c_double)]
 
 
 KEYPOINT_DT = np.dtype([("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
@@ -390,6 +391,13 @@ class DeviceFrames:
     def frames(self, f: int) -> Frames:
         arrs = [b[f] for b in self.bufs]
         return make_frames(self.B, self.kp_cap, self.kl_cap, arrs)
+
+    def frames_slice(self, f: int, s0: int, n: int) -> Frames:
+        """Frame f of sequences [s0, s0 + n) (a view: every field is [B][...] row-major)."""
+        if s0 < 0 or n <= 0 or s0 + n > self.B:
+            raise ValueError(f"sequence slice [{s0}, {s0 + n}) outside [0, {self.B})")
+        arrs = [b[f].view(self.B, -1)[s0:s0 + n] for b in self.bufs]
+        return make_frames(n, self.kp_cap, self.kl_cap, arrs)
 
     def nbytes(self) -> int:
         return sum(b.numel() for b in self.bufs)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GFPL_ABI_VERSION 1
+#define GFPL_ABI_VERSION 2
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
@@ -110,6 +110,9 @@ typedef struct gfpl_config {
     double cut_step;             /* stepCutRatio 0.05 (src/stereoFrameHandler.cpp:135) */
     double cut_rng[2];           /* rngCutRatio {0,1} (src/stereoFrameHandler.cpp:134)  */
     double proj_gate_px;         /* rng_included 10.0 (src/stereoFrameHandler.cpp:534)  */
+    double cut_certify;          /* (new) 1e-9: relative margin of the certified line-cut
+                                    search; 0 = every neighbour evaluated with
+                                    the reference's LLT; nonzero values below 1e-10 are rejected */
 } gfpl_config;
 
 /* cv::KeyPoint subset used by the path */

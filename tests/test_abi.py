@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = gfpl.hiplib()
-    assert L.gfpl_abi_version() == 1
+    assert L.gfpl_abi_version() == 2
     assert L.gfpl_strerror(-4) == b"knn-2 needs at least 2 train descriptors"
 
 
@@ -55,6 +55,7 @@ def test_config_defaults_match_reference():
     assert (c.min_error, c.min_error_change, c.inlier_k, c.motion_step_th) == (1e-7, 1e-7, 2.0, 10.0)
     assert (c.ratio_disp_std, c.ratio_disp_std_hor, c.orb_scale_factor, c.orb_n_levels) == (0.15, 0.9, 1.2, 4)
     assert (c.cut_step, list(c.cut_rng), c.proj_gate_px) == (0.05, [0.0, 1.0], 10.0)
+    assert c.cut_certify == 1e-9   # (new) certified line-cut margin; 0 = exact steps only
 
 
 def test_camera_tables_match_orbextractor():

@@ -304,3 +304,55 @@ def test_euroc_ground_truth_trajectory_parity():
                                         traj_t=t.ctypes.data), seed=31)
     _check(rep)
     assert all(rep["pose_exact"])
+
+
+# ---- certified line-cut search: the chosen ratios are the reference's
+@pytest.mark.parametrize("margin", [0.0, 1e-3])
+def test_line_cut_exact_and_mixed_steps_parity(margin):
+    # 0: every step evaluated with the reference's LLT; 1e-3: a large share of the
+    # steps fall back to it, mixed with certified steps inside the same lines
+    rep = _run_sequence("vga", dict(cut_certify=margin, max_iters=10, max_iters_ref=10, min_error=0.0,
+                                    min_error_change=0.0), n_seq=2, n_frames=3, kp_cap=2048, kl_cap=512, seed=11)
+    _check(rep)
+
+
+def test_cut_certify_margin_validated():
+    cam = gfpl.make_camera("vga", gfpl.default_config())
+    for bad in (1e-12, -1.0, 1.0):
+        with pytest.raises(gfpl.GfplError):
+            gfpl.Context(cam, gfpl.default_config(cut_certify=bad))
+
+
+def test_line_cut_certified_matches_exact_at_scale():
+    """512 sequences x 3 frames on the GPU twice — certified search and exact steps
+    only — cut ratios, invCovPose of every matched line and the poses bit-identical."""
+    n, F, KP, KL = 512, 3, 2048, 512
+    base = dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
+    cam = gfpl.make_camera("vga", gfpl.default_config(**base))
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=21), n, F, KP, KL)
+    D = gfpl.DeviceFrames(H)
+    out = []
+    for margin in (1e-9, 0.0):
+        ctx = gfpl.Context(cam, gfpl.default_config(cut_certify=margin, **base))
+        h = gfpl.StereoFrameHandler(ctx, n, KP, KL)
+        h.initialize(D.frames(0))
+        res = []
+        for k in range(1, F):
+            h.insertStereoPair(D.frames(k))
+            h.optimizePose()
+            for b in range(n):
+                tr = h.read_track(b)
+                pf = h.read_frame(gfpl.PREV, b)
+                ml = tr["matched_ls"]
+                res.append((ml.copy(), pf.get("ls_cut")[ml].copy(), pf.get("ls_invcov")[ml].copy(),
+                            h.read_frame(gfpl.CURR, b).get("Tfw")))
+            h.updateFrame()
+        out.append(res)
+    n_lines = 0
+    for (ma, ca, ia, ta), (mb, cb, ib, tb) in zip(*out):
+        assert np.array_equal(ma, mb)
+        assert np.array_equal(ca.view(np.uint64), cb.view(np.uint64))
+        assert np.array_equal(ia.view(np.uint64), ib.view(np.uint64))
+        assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64))
+        n_lines += len(ma)
+    assert n_lines > 100 * n
