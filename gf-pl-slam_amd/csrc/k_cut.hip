@@ -253,7 +253,7 @@ __device__ __forceinline__ int nb_slot(int j, int side) {   // endpoint slot: 0:
     return (j == 2 || j == 4 || j == 6) ? 2 : ((j == 3 || j == 5 || j == 7) ? 0 : 1);
 }
 
-// S = L L^T for the certified comparisons (out: L lower 21, 1/L_kk 6, ok).  ok = 0
+// S = L L^T for the certified comparisons (out: L strictly lower 21, 1/L_kk 6, ok).  ok = 0
 // unless every pivot keeps at least 1e-6 of its diagonal (the synthetic and EuRoC
 // workloads stay above 0.1); the line is then searched with exact steps only.
 __device__ __forceinline__ void chol_s(const double* a, double* out) {
@@ -268,8 +268,11 @@ __device__ __forceinline__ void chol_s(const double* a, double* out) {
 #pragma unroll
         for (int j = 0; j < k; ++j) x = x - L[tri(k, j)] * L[tri(k, j)];
         if (!(x > 1e-6 * akk && akk < 1e300)) { ok = false; x = 1.0; }
-        const double dk = sqrt(x), r = 1.0 / dk;
-        L[tri(k, k)] = dk;
+        // 1 / L_kk (the only use of the pivot): hardware rsq + two Newton steps
+        double r = __builtin_amdgcn_rsq(x);
+        r = r * (1.5 - (0.5 * x) * (r * r));
+        r = r * (1.5 - (0.5 * x) * (r * r));
+        L[tri(k, k)] = 0.0;
         out[21 + k] = r;
 #pragma unroll
         for (int i = k + 1; i < 6; ++i) {
@@ -294,6 +297,54 @@ __device__ __forceinline__ double cut_d(const double* S, const double* E) {
     return (vs > 0.0 && ve > 0.0 && d > 0.0 && d < 1e300) ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
 
+// Group-of-8 exchange on the DPP crossbar (no LDS): xor 1, xor 2 (quad_perm) and
+// the half-row mirror (lane i <-> 7 - i) pair every lane of a group in 3 steps.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+#define DPP_XOR1 0xB1
+#define DPP_XOR2 0x4E
+#define DPP_HALF_MIRROR 0x141
+
+// The reference's j-loop "if (m > metric_init)" over the group's 8 lanes: the
+// largest value, ties to the lowest j, NaN / invalid never chosen; -1 unless it
+// beats the centre metric mc.  (v, j) ends up identical in all 8 lanes.
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(double& v, int& k) {
+    const double ov = dpp_f64<CTRL>(v);
+    const int ok = dpp_i32<CTRL>(k);
+    if (ov > v || (ov == v && ok < k)) { v = ov; k = ok; }
+}
+__device__ __forceinline__ int group_first_max(double v, int valid, int j, double mc, double& top) {
+    double x = (valid && v == v) ? v : -__builtin_inf();
+    int k = valid && v == v ? j : 8;
+    argmax_step<DPP_XOR1>(x, k);
+    argmax_step<DPP_XOR2>(x, k);
+    argmax_step<DPP_HALF_MIRROR>(x, k);
+    top = x;
+    return (k < 8 && x > mc) ? k : -1;
+}
+
+// The search block is one wave: LDS accesses of a wave execute in order, so a
+// phase boundary only has to keep the compiler from moving LDS accesses across
+// it and drain the wave's LDS queue — unlike __syncthreads it does not wait for
+// the in-flight global prefetch loads.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Per iteration (one LDS sync between the halves, one at the end):
+//   A  lanes 0-2: the start endpoint at t0 = r0 + {-s, 0, +s}, lanes 3-5: the end
+//      endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint), then w = L^-1 J and
+//      a = |w|^2 / v of that endpoint; prefetched line data lands in LDS;
+//   B  lane j: d of neighbour j and of the centre, the group decision by DPP
+//      reduction, its certification by ballot; the exact step (X) when any
+//      group of the wave needs it; a move, or the line's finalisation.
 __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
@@ -301,10 +352,9 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     __shared__ double sumb[CUT_G][25];   // invCov_sum when the line opened
     __shared__ double chol[CUT_G][CUT_CH];
     __shared__ double epf[CUT_G][CUT_EP];
-    __shared__ double val[CUT_G][9];     // d of neighbours 0-7, centre
-    __shared__ double vx[CUT_G][9];      // exact metrics of an exact step
-    __shared__ int vld[CUT_G][8];
     __shared__ double nxt[CUT_G][49];    // prefetched next line: sP eP covS covE Jl (26) | r=0 info (21)
+    __shared__ double lin[CUT_G][27];    // current line: sP eP covS covE Jl
+    __shared__ double dtl[CUT_G][13];    // DT_inv rows 0-2
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -317,31 +367,50 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
     const double* scr_l = p.scr.cut_ls + (size_t)(live ? b : 0) * p.mls_cap * 21;
-    double Dl[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) Dl[i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
+    for (int i = j; i < 12; i += 8) dtl[g][i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
+    const double* Dl = dtl[g];
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     // E role of this lane
     const int eside = j < 3 ? 0 : 1;
     const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
     double* my_slot = &epf[g][CUT_SL * (j < 6 ? j : 0)];
+    // the line as this lane's E role sees it (LDS): start endpoints blend (sP, eP,
+    // covS, covE), end endpoints (eP, sP, covE, covS) — one cut_endpoint call per
+    // lane instead of two divergent ones
+    const double* P0 = &lin[g][eside ? 3 : 0];
+    const double* P1 = &lin[g][eside ? 0 : 3];
+    const double* C0 = &lin[g][eside ? 15 : 6];
+    const double* C1 = &lin[g][eside ? 6 : 15];
+    const double* Jl = &lin[g][24];
     // C role: neighbour j
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
+    const unsigned long long gmask = 0xFFull << (8 * g);
     // group state (identical in the 8 lanes of a group)
     int m = 0;
     int first = 1;       // first step of the line: the exact centre metric is logdet(sumb)
-    int need_chol = 1;   // S changed: lane 6 factors it in the next E1
     double r0 = 0.0, r1 = 0.0;
-    LineCutData d;
+    // factor of S for the certified comparisons, written by the group's lanes
+    // (lane j owns entries j, j+8, j+16, j+24: compile-time register indices)
+    auto put_chol = [&](const double* s21) {
+        double o[28];
+        chol_s(s21, o);
+#pragma unroll
+        for (int e = 0; e < 28; ++e)
+            if ((e & 7) == j) chol[g][e] = o[e];
+    };
     // Next-line prefetch: lane j loads elements j, j+8, ... of the 47-element vector
     // [line data | r = 0 info] of the group's next line right after a line opens;
     // the values land in LDS one iteration later, so opening a line never waits on HBM.
     double pf[6];
     int pending = 0;
-    auto pf_issue = [&](int mm) {
-        const size_t q = lb + mls[mm];
+    // mls indices run one line ahead of the data prefetch, so no HBM latency is
+    // exposed when a line opens: q_cur (line m), q_nx (line m + 1), ix_n2 (m + 2)
+    size_t q_cur = 0, q_nx = 0;
+    int ix_n2 = 0;
+    auto pf_issue = [&](int mm) {   // data of line mm = m + 1 (q_nx)
+        const size_t q = q_nx;
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int e = j + 8 * k;
@@ -358,49 +427,45 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         pending = 1;
     };
     if (m < nls) {
-        load_line(L, lb + mls[m], d);
-        for (int e = j; e < 21; e += 8) {
-            const double s0 = p.scr.cut_sum[24 * b + e];
-            sumb[g][e] = s0;
-            sum[g][e] = s0 - scr_l[e];
+        q_cur = lb + mls[0];
+        if (nls > 1) q_nx = lb + mls[1];
+        if (nls > 2) ix_n2 = mls[2];
+        {
+            const size_t q = q_cur;
+            for (int e = j; e < 26; e += 8)
+                lin[g][e] = e < 3 ? L.sP[3 * q + e] : e < 6 ? L.eP[3 * q + e - 3] : e < 15 ? L.covS[9 * q + e - 6]
+                          : e < 24 ? L.covE[9 * q + e - 15] : L.le_obs[3 * q + e - 24];
         }
+        double s21[21];
+#pragma unroll
+        for (int e = 0; e < 21; ++e) {
+            const double s0 = p.scr.cut_sum[24 * b + e];
+            s21[e] = s0 - scr_l[e];
+            if ((e & 7) == j) { sumb[g][e] = s0; sum[g][e] = s21[e]; }
+        }
+        put_chol(s21);
         if (nls > 1) pf_issue(1);
     } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { d.sP[k] = 0.0; d.eP[k] = 1.0; }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) { d.covS[k] = 0.0; d.covE[k] = 0.0; }
-        d.Jl[0] = 0.0; d.Jl[1] = 0.0;
-        need_chol = 0;
+        for (int e = j; e < 26; e += 8) lin[g][e] = (e >= 3 && e < 6) ? 1.0 : 0.0;
     }
     __syncthreads();
+#ifdef GFPL_CUT_PROF
+    unsigned long long cp_acc[6] = {0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0;
+#define CUT_PROF(k) { const unsigned long long _t = clock64(); cp_acc[k] += _t - cp_last; cp_last = _t; }
+#else
+#define CUT_PROF(k)
+#endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- E1: the six endpoints of this step; the factor of a new line's S
+        // ---- A: this lane's endpoint of the step and its certified-comparison terms
         if (j < 6) {
             const double t = (eside == 0 ? r0 : r1) + eoff;
             double out[7];
-            if (eside == 0) cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, t, out);
-            else cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, t, out);
-#pragma unroll
-            for (int i = 0; i < 7; ++i) my_slot[i] = out[i];
-        } else if (j == 6 && need_chol) {
-            double a[21];
-#pragma unroll
-            for (int i = 0; i < 21; ++i) a[i] = sum[g][i];
-            double o[28];
-            chol_s(a, o);
-#pragma unroll
-            for (int i = 0; i < 28; ++i) chol[g][i] = o[i];
-        }
-        need_chol = 0;
-        __syncthreads();
-        // ---- E2: w = L^-1 J, a = |w|^2 / v
-        if (j < 6) {
+            cut_endpoint(cam, homog, Dl, Jl, P0, P1, C0, C1, t, out);
             double w[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                double u = my_slot[1 + i];
+                double u = out[1 + i];
 #pragma unroll
                 for (int k = 0; k < i; ++k) u = u - chol[g][tri(i, k)] * w[k];
                 w[i] = u * chol[g][21 + i];
@@ -409,83 +474,65 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #pragma unroll
             for (int i = 1; i < 6; ++i) a = a + w[i] * w[i];
 #pragma unroll
+            for (int i = 0; i < 7; ++i) my_slot[i] = out[i];
+#pragma unroll
             for (int i = 0; i < 6; ++i) my_slot[7 + i] = w[i];
-            my_slot[13] = a / my_slot[0];
+            my_slot[13] = a / out[0];
         }
-        __syncthreads();
-        // ---- C: d of neighbour j and of the centre
-        const double t0 = r0 + nb0, t1 = r1 + nb1;
-        int valid = 1;
-        if (t0 + t1 > 1.0) valid = 0;
-        if (t0 < rlo || t0 > rhi) valid = 0;
-        if (t1 < rlo || t1 > rhi) valid = 0;
-        {
-            const double dj = cut_d(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce]);
-            if (act) {
-                val[g][j] = dj;
-                vld[g][j] = valid;
-                if (j == 0) val[g][8] = cut_d(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4]);
-            }
-        }
-        // ---- land the prefetched next line in LDS (its loads were issued >= 1 iteration ago)
+        // the prefetched next line lands in LDS (its loads were issued >= 1 iteration ago)
         if (pending) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
                 if (j + 8 * k < 47) nxt[g][j + 8 * k] = pf[k];
             pending = 0;
         }
-        __syncthreads();
-        // ---- D: certified decision (all 8 lanes of a group compute it identically)
-        int best = -1;
-        int exact = 0;
-        if (act) {
-            const double dc = val[g][8];
-            double mi = dc;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj)
-                if (vld[g][jj] && val[g][jj] > mi) { mi = val[g][jj]; best = jj; }
-            // every comparison the decision rests on must clear the margin; NaN
-            // (unhealthy) values fail every test
-            bool cert = tau > 0.0 && chol[g][27] != 0.0 && dc == dc;
-            const double top = best >= 0 ? mi : dc;
-            if (best >= 0 && !(top - dc > tau * top)) cert = false;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj)
-                if (vld[g][jj] && jj != best && !(top - val[g][jj] > tau * top)) cert = false;
-            exact = cert ? 0 : 1;
+        wave_lds_sync();
+        CUT_PROF(0);
+        // ---- B: d of neighbour j and of the centre; certified group decision
+        const double t0 = r0 + nb0, t1 = r1 + nb1;
+        int valid = act ? 1 : 0;
+        if (t0 + t1 > 1.0) valid = 0;
+        if (t0 < rlo || t0 > rhi) valid = 0;
+        if (t1 < rlo || t1 > rhi) valid = 0;
+        const double dj = cut_d(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce]);
+        const double dc = cut_d(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4]);
+        double top;
+        int best = group_first_max(dj, valid, j, dc, top);
+        // every comparison the decision rests on must clear the margin; NaN
+        // (unhealthy) values fail every test
+        int ok = 1;
+        if (best >= 0) {
+            if (valid && j != best && !(top - dj > tau * top)) ok = 0;
+            if (!(top - dc > tau * top)) ok = 0;
+        } else {
+            if (valid && !(dc - dj > tau * dc)) ok = 0;
         }
+        if (!(tau > 0.0 && chol[g][27] != 0.0 && dc == dc)) ok = 0;
+        const bool exact = act && (__ballot(!ok) & gmask) != 0;
+        CUT_PROF(1);
         if (__any(exact)) {
             // ---- X: the reference's evaluation of this step for the groups that need it
             if (exact) {
-                double tot[21];
-                double tmp[21];
+                double tot[21], tmp[21];
                 cut_assemble<false>(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], tmp);
 #pragma unroll
                 for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
-                vx[g][j] = logdet6_lower(tot);
-                if (j == 0) {
-                    // centre metric: logdet(invCov_sum) on a line's first step (:1671),
-                    // else the previous step's chosen candidate, re-evaluated (same bits)
-                    if (first) {
+                const double vj = logdet6_lower(tot);
+                // centre metric: logdet(invCov_sum) on a line's first step (:1671), else
+                // the previous step's chosen candidate, re-evaluated (same operands, same bits)
+                if (first) {
 #pragma unroll
-                        for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
-                    } else {
-                        cut_assemble<false>(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4], tmp);
+                    for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
+                } else {
+                    cut_assemble<false>(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4], tmp);
 #pragma unroll
-                        for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
-                    }
-                    vx[g][8] = logdet6_lower(tot);
+                    for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
                 }
-            }
-            __syncthreads();
-            if (exact) {
-                double mi = vx[g][8];
-                best = -1;
-#pragma unroll
-                for (int jj = 0; jj < 8; ++jj)
-                    if (vld[g][jj] && vx[g][jj] > mi) { mi = vx[g][jj]; best = jj; }
+                const double mc = logdet6_lower(tot);
+                best = group_first_max(vj, valid, j, mc, top);
             }
         }
+        CUT_PROF(2);
         int finalize = 0, stale_mid = 0;
         if (act) {
             first = 0;
@@ -503,44 +550,55 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             if (!stale_mid) {
 #pragma unroll
                 for (int i = 0; i < 7; ++i) { S7[i] = epf[g][CUT_SL * 1 + i]; E7[i] = epf[g][CUT_SL * 4 + i]; }
-            } else {
-                cut_endpoint(cam, homog, Dl, d.Jl, d.sP, d.eP, d.covS, d.covE, r0, S7);
-                cut_endpoint(cam, homog, Dl, d.Jl, d.eP, d.sP, d.covE, d.covS, r1, E7);
+            } else {   // (not reached for finite ratios: valid neighbours keep r0 + r1 <= 1)
+                cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][0], &lin[g][3], &lin[g][6], &lin[g][15], r0, S7);
+                cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][3], &lin[g][0], &lin[g][15], &lin[g][6], r1, E7);
             }
             double info[21];
             cut_assemble<false>(S7, E7, info);
+            double s21[21];
 #pragma unroll
-            for (int e = 0; e < 21; ++e)   // lane j owns entries j, j+8, j+16 (compile-time register index)
-                if ((e & 7) == j) sum[g][e] = sum[g][e] + info[e];
+            for (int e = 0; e < 21; ++e) s21[e] = sum[g][e] + info[e];
             if (j == 0) {
-                const size_t q = lb + mls[m];
-                L.cut[2 * q] = r0;
-                L.cut[2 * q + 1] = r1;
+                L.cut[2 * q_cur] = r0;
+                L.cut[2 * q_cur + 1] = r1;
             }
             ++m;
             if (m < nls) {
+                q_cur = q_nx;
+                q_nx = lb + ix_n2;
+                if (m + 2 < nls) ix_n2 = mls[m + 2];
                 first = 1;
-                need_chol = 1;
                 r0 = 0.0;
                 r1 = 0.0;
                 // line m from the prefetch buffer (same values load_line would read)
-#pragma unroll
-                for (int k = 0; k < 3; ++k) { d.sP[k] = nxt[g][k]; d.eP[k] = nxt[g][3 + k]; }
-#pragma unroll
-                for (int k = 0; k < 9; ++k) { d.covS[k] = nxt[g][6 + k]; d.covE[k] = nxt[g][15 + k]; }
-                d.Jl[0] = nxt[g][24];
-                d.Jl[1] = nxt[g][25];
+                for (int e = j; e < 26; e += 8) lin[g][e] = nxt[g][e];
                 // open line m: sumb = invCov_sum, S = invCov_sum - info(line m, r = 0)
-                for (int e = j; e < 21; e += 8) {
-                    const double s0 = sum[g][e];
-                    sumb[g][e] = s0;
-                    sum[g][e] = s0 - nxt[g][26 + e];
+#pragma unroll
+                for (int e = 0; e < 21; ++e) {
+                    const double s0 = s21[e];
+                    s21[e] = s0 - nxt[g][26 + e];
+                    if ((e & 7) == j) { sumb[g][e] = s0; sum[g][e] = s21[e]; }
                 }
+                put_chol(s21);
                 if (m + 1 < nls) pf_issue(m + 1);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 21; ++e)
+                    if ((e & 7) == j) sum[g][e] = s21[e];
             }
         }
-        __syncthreads();
+        wave_lds_sync();
+        CUT_PROF(3);
+#ifdef GFPL_CUT_PROF
+        ++cp_it;
+#endif
     }
+#ifdef GFPL_CUT_PROF
+    if (lane == 0 && (blockIdx.x % 256) == 0)
+        printf("cutprof blk %d it %llu A %llu B %llu X %llu FIN %llu\n", blockIdx.x, cp_it, cp_acc[0], cp_acc[1],
+               cp_acc[2], cp_acc[3]);
+#endif
 }
 
 // ---------------------------------------------------------------- finish --
