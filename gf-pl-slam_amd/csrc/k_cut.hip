@@ -297,6 +297,31 @@ __device__ __forceinline__ double cut_d(const double* S, const double* E) {
     return (vs > 0.0 && ve > 0.0 && d > 0.0 && d < 1e300) ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
 
+// The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
+// and the centre metric — logdet(invCov_sum) on a line's first step (:1671), else the
+// previous step's chosen candidate re-evaluated (same operands, same bits).  Out of
+// line: it is rare, and inlined its two 6x6 LLTs would set the register budget of
+// the whole search loop.
+__device__ __attribute__((noinline)) double cut_exact_step(const double* sj, const double* ej, const double* s1,
+                                                           const double* e4, const double* S, const double* Sb,
+                                                           int first, double* mc) {
+    double tot[21], tmp[21];
+    cut_assemble<false>(sj, ej, tmp);
+#pragma unroll
+    for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + S[i];
+    const double vj = logdet6_lower(tot);
+    if (first) {
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = Sb[i];
+    } else {
+        cut_assemble<false>(s1, e4, tmp);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + S[i];
+    }
+    *mc = logdet6_lower(tot);
+    return vj;
+}
+
 // Group-of-8 exchange on the DPP crossbar (no LDS): xor 1, xor 2 (quad_perm) and
 // the half-row mirror (lane i <-> 7 - i) pair every lane of a group in 3 steps.
 template <int CTRL>
@@ -391,14 +416,16 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     int m = 0;
     int first = 1;       // first step of the line: the exact centre metric is logdet(sumb)
     double r0 = 0.0, r1 = 0.0;
-    // factor of S for the certified comparisons, written by the group's lanes
-    // (lane j owns entries j, j+8, j+16, j+24: compile-time register indices)
+    // factor of S for the certified comparisons.  Group-shared LDS rows are
+    // written by all 8 lanes of the group with identical values: no per-entry
+    // lane masks, which would split the writes into branches that serialise the
+    // surrounding LDS reads.
     auto put_chol = [&](const double* s21) {
         double o[28];
         chol_s(s21, o);
 #pragma unroll
         for (int e = 0; e < 28; ++e)
-            if ((e & 7) == j) chol[g][e] = o[e];
+            chol[g][e] = o[e];
     };
     // Next-line prefetch: lane j loads elements j, j+8, ... of the 47-element vector
     // [line data | r = 0 info] of the group's next line right after a line opens;
@@ -441,7 +468,8 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         for (int e = 0; e < 21; ++e) {
             const double s0 = p.scr.cut_sum[24 * b + e];
             s21[e] = s0 - scr_l[e];
-            if ((e & 7) == j) { sumb[g][e] = s0; sum[g][e] = s21[e]; }
+            sumb[g][e] = s0;
+            sum[g][e] = s21[e];
         }
         put_chol(s21);
         if (nls > 1) pf_issue(1);
@@ -450,7 +478,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     }
     __syncthreads();
 #ifdef GFPL_CUT_PROF
-    unsigned long long cp_acc[6] = {0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0;
+    unsigned long long cp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0;
 #define CUT_PROF(k) { const unsigned long long _t = clock64(); cp_acc[k] += _t - cp_last; cp_last = _t; }
 #else
 #define CUT_PROF(k)
@@ -513,22 +541,9 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         if (__any(exact)) {
             // ---- X: the reference's evaluation of this step for the groups that need it
             if (exact) {
-                double tot[21], tmp[21];
-                cut_assemble<false>(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], tmp);
-#pragma unroll
-                for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
-                const double vj = logdet6_lower(tot);
-                // centre metric: logdet(invCov_sum) on a line's first step (:1671), else
-                // the previous step's chosen candidate, re-evaluated (same operands, same bits)
-                if (first) {
-#pragma unroll
-                    for (int i = 0; i < 21; ++i) tot[i] = sumb[g][i];
-                } else {
-                    cut_assemble<false>(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4], tmp);
-#pragma unroll
-                    for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + sum[g][i];
-                }
-                const double mc = logdet6_lower(tot);
+                double mc;
+                const double vj = cut_exact_step(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], &epf[g][CUT_SL * 1],
+                                                 &epf[g][CUT_SL * 4], sum[g], sumb[g], first, &mc);
                 best = group_first_max(vj, valid, j, mc, top);
             }
         }
@@ -554,16 +569,20 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][0], &lin[g][3], &lin[g][6], &lin[g][15], r0, S7);
                 cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][3], &lin[g][0], &lin[g][15], &lin[g][6], r1, E7);
             }
+            CUT_PROF(4);
             double info[21];
             cut_assemble<false>(S7, E7, info);
             double s21[21];
 #pragma unroll
             for (int e = 0; e < 21; ++e) s21[e] = sum[g][e] + info[e];
+#ifndef GFPL_EXP_NO_CUT_STORE
             if (j == 0) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
             }
+#endif
             ++m;
+            CUT_PROF(5);
             if (m < nls) {
                 q_cur = q_nx;
                 q_nx = lb + ix_n2;
@@ -572,20 +591,27 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 r0 = 0.0;
                 r1 = 0.0;
                 // line m from the prefetch buffer (same values load_line would read)
-                for (int e = j; e < 26; e += 8) lin[g][e] = nxt[g][e];
+                double nx[47];
+#pragma unroll
+                for (int e = 0; e < 47; ++e) nx[e] = nxt[g][e];
+#pragma unroll
+                for (int e = 0; e < 26; ++e) lin[g][e] = nx[e];
                 // open line m: sumb = invCov_sum, S = invCov_sum - info(line m, r = 0)
 #pragma unroll
                 for (int e = 0; e < 21; ++e) {
                     const double s0 = s21[e];
-                    s21[e] = s0 - nxt[g][26 + e];
-                    if ((e & 7) == j) { sumb[g][e] = s0; sum[g][e] = s21[e]; }
+                    s21[e] = s0 - nx[26 + e];
+                    sumb[g][e] = s0;
+                    sum[g][e] = s21[e];
                 }
+                CUT_PROF(6);
                 put_chol(s21);
+                CUT_PROF(7);
                 if (m + 1 < nls) pf_issue(m + 1);
+                CUT_PROF(8);
             } else {
 #pragma unroll
-                for (int e = 0; e < 21; ++e)
-                    if ((e & 7) == j) sum[g][e] = s21[e];
+                for (int e = 0; e < 21; ++e) sum[g][e] = s21[e];
             }
         }
         wave_lds_sync();
@@ -596,8 +622,9 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     }
 #ifdef GFPL_CUT_PROF
     if (lane == 0 && (blockIdx.x % 256) == 0)
-        printf("cutprof blk %d it %llu A %llu B %llu X %llu FIN %llu\n", blockIdx.x, cp_it, cp_acc[0], cp_acc[1],
-               cp_acc[2], cp_acc[3]);
+        printf("cutprof blk %d it %llu A %llu B %llu X %llu END %llu mv %llu asm %llu open %llu chol %llu pf %llu\n",
+               blockIdx.x, cp_it, cp_acc[0], cp_acc[1], cp_acc[2], cp_acc[3], cp_acc[4], cp_acc[5], cp_acc[6], cp_acc[7],
+               cp_acc[8]);
 #endif
 }
 
