@@ -96,6 +96,13 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->tr.n_inliers_pt = c.take<int32_t>(B);
     sb->tr.n_inliers_ls = c.take<int32_t>(B);
     sb->tr.num_frame_loss = c.take<int32_t>(B);
+    sb->tr.kf_T = c.take<double>(B * 16);
+    sb->tr.kf_cov = c.take<double>(B * 36);
+    sb->tr.kf_entropy0 = c.take<double>(B);
+    sb->tr.kf_ratio = c.take<double>(B);
+    sb->tr.kf_prev_iskf = c.take<int32_t>(B);
+    sb->tr.kf_nsince = c.take<int32_t>(B);
+    sb->tr.kf_flag = c.take<int32_t>(B);
     sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
     sb->scr.proj = reinterpret_cast<double*>(sb->scr.knn);
@@ -109,6 +116,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_ok = c.take<int32_t>(B);
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
     sb->scr.pose_dtini = c.take<double>(B * 16);
+    sb->scr.kf_mask = c.take<int32_t>(B);
 }
 
 DevCam devcam(const gfpl_camera& c) {
@@ -359,6 +367,48 @@ int gfpl_optimize_pose(gfpl_seqbatch* sb) {
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
     HIPCHK(launch_pose(params(sb, nullptr), sb->ctx->stream, sb->ctx->timing ? sb->ctx->ev[9] : nullptr));
     tmark(sb->ctx, 6);
+    return GFPL_OK;
+}
+
+int gfpl_need_new_kf(gfpl_seqbatch* sb, int32_t* flags) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    HIPCHK(launch_need_kf(params(sb, nullptr), sb->ctx->stream));
+    if (flags) {
+        HIPCHK(hipMemcpyAsync(flags, sb->tr.kf_flag, sizeof(int32_t) * (size_t)sb->B, hipMemcpyDeviceToHost,
+                              sb->ctx->stream));
+        HIPCHK(hipStreamSynchronize(sb->ctx->stream));
+    }
+    return GFPL_OK;
+}
+
+int gfpl_curr_frame_is_kf(gfpl_seqbatch* sb, const int32_t* mask) {
+    if (!sb) return GFPL_E_INVALID;
+    if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    const int32_t* dmask = sb->tr.kf_flag;   // NULL: the last needNewKF decisions
+    if (mask) {
+        HIPCHK(hipMemcpyAsync(sb->scr.kf_mask, mask, sizeof(int32_t) * (size_t)sb->B, hipMemcpyHostToDevice,
+                              sb->ctx->stream));
+        dmask = sb->scr.kf_mask;
+    }
+    HIPCHK(launch_curr_frame_is_kf(params(sb, nullptr), dmask, sb->ctx->stream));
+    if (mask) HIPCHK(hipStreamSynchronize(sb->ctx->stream));   // the caller's mask may be reused on return
+    return GFPL_OK;
+}
+
+int gfpl_read_kf_state(gfpl_seqbatch* sb, int seq, gfpl_kf_state* out) {
+    if (!sb || !out || seq < 0 || seq >= sb->B) return GFPL_E_INVALID;
+    hipStream_t s = sb->ctx->stream;
+    const DevTrack& T = sb->tr;
+    HIPCHK(hipMemcpyAsync(out->T_prevKF, T.kf_T + 16 * (size_t)seq, sizeof(double) * 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->cov_prevKF_currF, T.kf_cov + 36 * (size_t)seq, sizeof(double) * 36,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&out->entropy_first_prevKF, T.kf_entropy0 + seq, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&out->entropy_ratio, T.kf_ratio + seq, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&out->prev_f_iskf, T.kf_prev_iskf + seq, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&out->num_frame_since_kf, T.kf_nsince + seq, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&out->need_new_kf, T.kf_flag + seq, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return GFPL_OK;
 }
 

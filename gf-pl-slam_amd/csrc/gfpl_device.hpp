@@ -514,6 +514,95 @@ GFPL_DEV void inverse6(const double* A, double* out) {
     }
 }
 
+// adjoint_se3 (src/auxiliar.cpp:216-223): [R, skew(t) R; 0, R] (see oracle)
+GFPL_DEV void adjoint_se3(const double* T, double* Ad) {
+    double R[9], t[3] = {T[3], T[7], T[11]}, Sk[9], SR[9];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) Ad[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = T[i * 4 + j];
+    skew3(t, Sk);
+    mat3_mul(Sk, R, SR);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            Ad[i * 6 + j] = R[i * 3 + j];
+            Ad[i * 6 + 3 + j] = SR[i * 3 + j];
+            Ad[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
+        }
+}
+
+// [C +] A X A^T for 6x6, A*X first, inner products k-sequential (see oracle sandwich6)
+GFPL_DEV void sandwich6(const double* A, const double* X, const double* C, double* out) {
+    double AS[36];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double s = A[i * 6 + 0] * X[0 * 6 + j];
+#pragma unroll
+            for (int k = 1; k < 6; ++k) s = s + A[i * 6 + k] * X[k * 6 + j];
+            AS[i * 6 + j] = s;
+        }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double s = AS[i * 6 + 0] * A[j * 6 + 0];
+#pragma unroll
+            for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * A[j * 6 + k];
+            out[i * 6 + j] = C ? C[i * 6 + j] + s : s;
+        }
+}
+
+// Matrix6d::determinant: PartialPivLU, diagonal product left to right (see oracle det6)
+GFPL_DEV double det6(const double* A) {
+    double m[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) m[i] = A[i];
+    int ntr = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        double pv = fabs(m[k * 6 + k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double v = fabs(m[i * 6 + k]);
+            if (v > pv) { pv = v; p = i; }
+        }
+#pragma unroll
+        for (int c = k + 1; c < 6; ++c) {
+            if (p == c) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) swap_v(m[k * 6 + j], m[c * 6 + j]);
+                ++ntr;
+            }
+        }
+        const double piv = m[k * 6 + k];
+        if (piv != 0.0) {
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) m[i * 6 + k] = m[i * 6 + k] / piv;
+        }
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i)
+#pragma unroll
+            for (int j = k + 1; j < 6; ++j) m[i * 6 + j] = m[i * 6 + j] - m[i * 6 + k] * m[k * 6 + j];
+    }
+    double d = m[0];
+#pragma unroll
+    for (int i = 1; i < 6; ++i) d = d * m[i * 7];
+    return (ntr & 1) ? -1.0 * d : 1.0 * d;
+}
+
+// entropy of a 6-dof Gaussian as needNewKF writes it (src/stereoFrameHandler.cpp:2315,2329)
+GFPL_DEV double kf_entropy(const double* cov) {
+    const double c0 = 3.0 * (1.0 + det_log(2.0 * 3.141592653589793));   // acos(-1) = pi
+    return c0 + 0.5 * det_log(det6(cov));
+}
+
 // SelfAdjointEigenSolver eigenvalues -> cyclic Jacobi, ascending (see oracle eig_sym)
 template <int N>
 GFPL_DEV void eig_sym(const double* A, double* w) {

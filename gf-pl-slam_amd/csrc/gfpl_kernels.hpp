@@ -15,6 +15,8 @@ hipError_t launch_cross_lines(const KParams& p, hipStream_t s);
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks /* [2] or null */);
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark /* or null */);
 hipError_t launch_step_bytes(const KParams& p, hipStream_t s);
+hipError_t launch_need_kf(const KParams& p, hipStream_t s);
+hipError_t launch_curr_frame_is_kf(const KParams& p, const int32_t* mask /* device [B] */, hipStream_t s);
 
 size_t stereo_lines_lds(int cap);
 

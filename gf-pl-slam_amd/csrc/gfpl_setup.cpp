@@ -41,6 +41,8 @@ extern "C" int gfpl_config_default(gfpl_config* c) {
     c->cut_rng[0] = 0.0;
     c->cut_rng[1] = 1.0;
     c->proj_gate_px = 10.0;
+    c->min_entropy_ratio = 0.90;
+    c->max_kf_num_frames = 50;
     c->cut_certify = 1e-9;
     return GFPL_OK;
 }

@@ -62,6 +62,14 @@ struct DevTrack {
     int32_t* n_inliers_pt; // [B]
     int32_t* n_inliers_ls; // [B]
     int32_t* num_frame_loss; // [B]
+    // keyframe decision (needNewKF / currFrameIsKF, include/stereoFrameHandler.h:147-153)
+    double* kf_T;          // [B*16] T_prevKF
+    double* kf_cov;        // [B*36] cov_prevKF_currF
+    double* kf_entropy0;   // [B] entropy_first_prevKF
+    double* kf_ratio;      // [B] entropy ratio of the last decision
+    int32_t* kf_prev_iskf; // [B] prev_f_iskf
+    int32_t* kf_nsince;    // [B] numFrameSinceKeyframe
+    int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
 struct DevScratch {
@@ -78,6 +86,7 @@ struct DevScratch {
     int32_t* pose_ok;  // [B] 1: stage-2 result usable
     double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
     double* pose_dtini; // [B*16] staging of gfpl_optimize_pose_ini's DT_ini
+    int32_t* kf_mask;  // [B] staging of gfpl_curr_frame_is_kf's mask
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

@@ -401,42 +401,9 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
     if (moved) {
         mat4_mul(Tp, cDT, Tfw);
         // unccomp_se3(prev.Tfw, prev.Tfw_cov, DT_cov) (src/auxiliar.cpp:216-238)
-        double Ad[36], R[9], t[3] = {Tp[3], Tp[7], Tp[11]}, Sk[9], SR[9];
-#pragma unroll
-        for (int i = 0; i < 36; ++i) Ad[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) R[i * 3 + j] = Tp[i * 4 + j];
-        skew3(t, Sk);
-        mat3_mul(Sk, R, SR);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                Ad[i * 6 + j] = R[i * 3 + j];
-                Ad[i * 6 + 3 + j] = SR[i * 3 + j];
-                Ad[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
-            }
-        double AS[36];
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double s = Ad[i * 6 + 0] * DT_cov[0 * 6 + j];
-#pragma unroll
-                for (int k = 1; k < 6; ++k) s = s + Ad[i * 6 + k] * DT_cov[k * 6 + j];
-                AS[i * 6 + j] = s;
-            }
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double s = AS[i * 6 + 0] * Ad[j * 6 + 0];
-#pragma unroll
-                for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * Ad[j * 6 + k];
-                Tcov[i * 6 + j] = Tpc[i * 6 + j] + s;
-            }
+        double Ad[36];
+        adjoint_se3(Tp, Ad);
+        sandwich6(Ad, DT_cov, Tpc, Tcov);
         err_norm = err;
     } else {
         // rejected step or non-finite pose: identity, prev pose kept, err_norm = -1
@@ -454,6 +421,81 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) CP.DT_cov_eig[6 * b + i] = eig[i];
     CP.err_norm[b] = err_norm;
+}
+
+// needNewKF (src/stereoFrameHandler.cpp:2309-2349), one lane per sequence, on the
+// curr frame's DT / DT_cov (called after optimizePose, app/plslam_mod.cpp:436)
+__global__ void __launch_bounds__(64) k_need_kf(KParams p) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.B) return;
+    const DevPose& CP = p.curr.pose;
+    DevTrack& T = p.tr;
+    double DT[16], DTc[36];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) DT[i] = CP.DT[16 * b + i];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) DTc[i] = CP.DT_cov[36 * b + i];
+    double e0 = T.kf_entropy0[b];
+    if (T.kf_prev_iskf[b]) {
+        e0 = kf_entropy(DTc);
+        T.kf_entropy0[b] = e0;
+        T.kf_prev_iskf[b] = 0;
+    }
+    double Tk[16], adj[36], Ti[16], adjTinv[36], covDTinv[36], cov[36], acc[36];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Tk[i] = T.kf_T[16 * b + i];
+    adjoint_se3(Tk, adj);
+    inverse_se3(DT, Ti);                 // uncTinv_se3 (src/auxiliar.cpp:225-231)
+    adjoint_se3(Ti, adjTinv);
+    sandwich6(adjTinv, DTc, nullptr, covDTinv);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) cov[i] = T.kf_cov[36 * b + i];
+    sandwich6(adj, covDTinv, cov, acc);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) T.kf_cov[36 * b + i] = acc[i];
+    const double ratio = kf_entropy(acc) / e0;
+    bool zero_cov = true, ident = true;
+#pragma unroll
+    for (int i = 0; i < 36; ++i) zero_cov = zero_cov && DTc[i] == 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ident = ident && DT[i] == ((i % 5 == 0) ? 1.0 : 0.0);
+    const bool bad = !(ratio == ratio) || ratio == __builtin_inf() || ratio == -__builtin_inf();
+    T.kf_ratio[b] = ratio;
+    T.kf_flag[b] = (T.kf_nsince[b] > p.cfg.max_kf_num_frames || ratio < p.cfg.min_entropy_ratio || bad ||
+                    (zero_cov && ident)) ? 1 : 0;
+}
+
+// currFrameIsKF (src/stereoFrameHandler.cpp:2351-2379) for the masked sequences
+__global__ void __launch_bounds__(64) k_curr_frame_is_kf(KParams p, const int32_t* mask) {
+    const int b = blockIdx.x;
+    if (!mask[b]) return;
+    DevFrame& C = p.curr;
+    const size_t pb = (size_t)b * p.kp_cap, lb = (size_t)b * p.kl_cap;
+    for (int i = threadIdx.x; i < C.pt.n[b]; i += blockDim.x) C.pt.idx[pb + i] = i;
+    for (int i = threadIdx.x; i < C.ls.n[b]; i += blockDim.x) C.ls.idx[lb + i] = i;
+    if (threadIdx.x < 16) {
+        const double v = (threadIdx.x % 5 == 0) ? 1.0 : 0.0;
+        C.pose.Tfw[16 * b + threadIdx.x] = v;
+        p.tr.kf_T[16 * b + threadIdx.x] = v;   // T_prevKF = curr_frame->Tfw (= I)
+    }
+    if (threadIdx.x < 36) {
+        C.pose.Tfw_cov[36 * b + threadIdx.x] = (threadIdx.x % 7 == 0) ? 1.0 : 0.0;
+        p.tr.kf_cov[36 * b + threadIdx.x] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+        p.tr.kf_nsince[b] = 0;
+        p.tr.kf_prev_iskf[b] = 1;
+    }
+}
+
+hipError_t launch_need_kf(const KParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_need_kf, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_curr_frame_is_kf(const KParams& p, const int32_t* mask, hipStream_t s) {
+    hipLaunchKernelGGL(k_curr_frame_is_kf, dim3(p.B), dim3(64), 0, s, p, mask);
+    return hipGetLastError();
 }
 
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {

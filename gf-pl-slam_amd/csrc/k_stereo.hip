@@ -639,6 +639,14 @@ __global__ void k_init_pose(KParams p) {
     p.tr.n_matched_pt[b] = 0;
     p.tr.n_matched_ls[b] = 0;
     p.tr.n_inliers[b] = 0; p.tr.n_inliers_pt[b] = 0; p.tr.n_inliers_ls[b] = 0;
+    // SLAM variables for KF decision (src/stereoFrameHandler.cpp:54-58)
+    for (int i = 0; i < 16; ++i) p.tr.kf_T[16 * b + i] = (i % 5 == 0) ? 1.0 : 0.0;
+    for (int i = 0; i < 36; ++i) p.tr.kf_cov[36 * b + i] = 0.0;
+    p.tr.kf_prev_iskf[b] = 1;
+    p.tr.kf_nsince[b] = 0;
+    p.tr.kf_entropy0[b] = 0.0;
+    p.tr.kf_ratio[b] = 0.0;
+    p.tr.kf_flag[b] = 0;
 }
 
 // estimateStereoUncertainty on the slot passed as `prev`
@@ -683,6 +691,9 @@ __global__ void k_step_bytes(KParams p) {
     // 208 B + index 4 B), its r = 0 info from k_cut_prep (168 B), the cut ratio
     // written (16 B); per sequence invCov_sum + metric + DT_inv (272 B)
     p.scr.bytes[8 * b + 7] = (p.cfg.use_line_conf_cut && Ml > 0) ? 396 * Ml + 272 : 0;
+    // insertStereoPair's last statement, numFrameSinceKeyframe++ (src/stereoFrameHandler.cpp:150):
+    // this per-sequence kernel closes every gfpl_insert_stereo_pair
+    p.tr.kf_nsince[b] = p.tr.kf_nsince[b] + 1;
 }
 
 // ------------------------------------------------------------ launchers --

@@ -68,6 +68,7 @@ class Config(C.Structure):
                 ("orb_scale_factor", C.c_double), ("orb_n_levels", C.c_int),
                 ("lsd_scale", C.c_double), ("cut_step", C.c_double),
                 ("cut_rng", C.c_double * 2), ("proj_gate_px", C.c_double),
+                ("min_entropy_ratio", C.c_double), ("max_kf_num_frames", C.c_int),
                 ("cut_certify", C.c_double)]
 
 
@@ -126,6 +127,20 @@ class TrackHost(C.Structure):
                 "matched_ls": np.array(self.matched_ls[: self.n_matched_ls], dtype=np.int32),
                 "n_inliers": self.n_inliers, "n_inliers_pt": self.n_inliers_pt,
                 "n_inliers_ls": self.n_inliers_ls, "num_frame_loss": self.num_frame_loss}
+
+
+class KFState(C.Structure):
+    """gfpl_kf_state: keyframe-decision state (include/stereoFrameHandler.h:147-153)."""
+    _fields_ = [("T_prevKF", C.c_double * 16), ("cov_prevKF_currF", C.c_double * 36),
+                ("entropy_first_prevKF", C.c_double), ("entropy_ratio", C.c_double),
+                ("prev_f_iskf", C.c_int), ("num_frame_since_kf", C.c_int), ("need_new_kf", C.c_int)]
+
+    def as_dict(self) -> dict:
+        return {"T_prevKF": np.array(self.T_prevKF[:]).reshape(4, 4),
+                "cov_prevKF_currF": np.array(self.cov_prevKF_currF[:]).reshape(6, 6),
+                "entropy_first_prevKF": self.entropy_first_prevKF, "entropy_ratio": self.entropy_ratio,
+                "prev_f_iskf": self.prev_f_iskf, "num_frame_since_kf": self.num_frame_since_kf,
+                "need_new_kf": self.need_new_kf}
 
 
 class SynthParams(C.Structure):
@@ -201,6 +216,9 @@ def hiplib() -> C.CDLL:
             "gfpl_read_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_write_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_read_track": ([P, C.c_int, P], C.c_int),
+            "gfpl_need_new_kf": ([P, P], C.c_int),
+            "gfpl_curr_frame_is_kf": ([P, P], C.c_int),
+            "gfpl_read_kf_state": ([P, C.c_int, P], C.c_int),
             "gfpl_write_track": ([P, C.c_int, P], C.c_int),
             "gfpl_set_timing": ([P, C.c_int], C.c_int),
             "gfpl_get_stage_times": ([P, P], C.c_int),
@@ -555,6 +573,27 @@ class StereoFrameHandler:
         t = TrackHost()
         check(self.L.gfpl_read_track(self.h, seq, C.byref(t)), "read_track")
         return t.as_dict()
+
+    # keyframe decision (src/stereoFrameHandler.cpp:2309-2379)
+    def needNewKF(self) -> np.ndarray:
+        """needNewKF() of every sequence; returns the [B] decisions (bool)."""
+        flags = np.zeros(self.B, np.int32)
+        check(self.L.gfpl_need_new_kf(self.h, flags.ctypes.data), "need_new_kf")
+        return flags.astype(bool)
+
+    def currFrameIsKF(self, mask=None):
+        """currFrameIsKF() for the sequences where mask is true (None: the last
+        needNewKF decisions)."""
+        if mask is None:
+            check(self.L.gfpl_curr_frame_is_kf(self.h, None), "curr_frame_is_kf")
+            return
+        m = np.ascontiguousarray(np.broadcast_to(np.asarray(mask), (self.B,)), dtype=np.int32)
+        check(self.L.gfpl_curr_frame_is_kf(self.h, m.ctypes.data), "curr_frame_is_kf")
+
+    def read_kf_state(self, seq: int) -> dict:
+        st = KFState()
+        check(self.L.gfpl_read_kf_state(self.h, seq, C.byref(st)), "read_kf_state")
+        return st.as_dict()
 
     def write_track(self, seq: int, tr: TrackHost):
         check(self.L.gfpl_write_track(self.h, seq, C.byref(tr)), "write_track")

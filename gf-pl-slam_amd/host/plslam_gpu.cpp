@@ -4,11 +4,13 @@
 //   plslam_gpu [--camera vga|euroc|kitti|stress] [--frames N] [--seq S] [--out PREFIX] [--json]
 //
 // Per frame: initialize (frame 0) or insertStereoPair -> optimizePose(prev_frame->DT)
-// -> numFrameLoss check -> updateFrame_ECCV18(T_base), then the trajectory line of
-// PREFIX_AllFrameTrajectory.txt in the reference's format (app/plslam_mod.cpp:288-293,
-// 480-493: fixed, setprecision(7), " tx ty tz qx qy qz qw" of R^T).  Mapping / keyframes
-// are out of scope.  --json prints one line per frame with the pose bits, for the
-// parity test that compares this binary against the CPU oracle.
+// -> numFrameLoss check -> needNewKF / currFrameIsKF -> updateFrame_ECCV18(T_base),
+// then the trajectory line of PREFIX_AllFrameTrajectory.txt in the reference's format
+// (app/plslam_mod.cpp:288-293, 480-493: fixed, setprecision(7), " tx ty tz qx qy qz qw"
+// of R^T).  Mapping (local BA, loop closure) is out of scope: the keyframe chain is
+// MapHandler::addKeyFrame's composition T_kf_w = prev_kf->T_kf_w * curr_kf->T_kf_w
+// (src/mapHandler.cpp:126-127) without the later BA refinements.  --json prints one
+// line per frame with the pose bits, for the parity test against the CPU oracle.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -123,7 +125,8 @@ static int run(int argc, char** argv) {
         fAllFrameTrack << "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" << std::endl;
     }
     StereoFrameHandler* StVO = new StereoFrameHandler(&cam, 0, kp_cap, kl_cap);
-    const Matrix4d T_base = Matrix4d::Identity();
+    Matrix4d T_kf_w = Matrix4d::Identity();   // the last keyframe's world pose (first KF: frame 0)
+    int n_kf = 1;
     for (int k = 0; k < frames; ++k) {
         StereoFrame* f = make_frame(sp, &cam, seq, k, kp_cap, kl_cap);
         if (k == 0) {
@@ -133,18 +136,28 @@ static int run(int argc, char** argv) {
         StVO->insertStereoPair(f);
         const int mpt = (int)StVO->matched_pt.size(), mls = (int)StVO->matched_ls.size();
         StVO->optimizePose(StVO->prev_frame->DT);
-        if (json) {
-            const StereoFrame* c = StVO->curr_frame;
-            std::printf("{\"frame\": %d, \"n_pt\": %zu, \"n_ls\": %zu, \"matched_pt\": %d, \"matched_ls\": %d, "
-                        "\"n_inliers\": %d, \"num_frame_loss\": %d, \"err_norm\": %.17g, \"Tfw\": [",
-                        k, c->stereo_pt.size(), c->stereo_ls.size(), mpt, mls, StVO->n_inliers, StVO->numFrameLoss,
-                        c->err_norm);
-            for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->Tfw.v[i]);
-            std::printf("]}\n");
-        }
         if (StVO->numFrameLoss > 10) {   // Config::maxNumFrameLoss() (src/config.cpp)
             std::cerr << "Early termination due to track loss!" << std::endl;
             break;
+        }
+        const Matrix4d T_base = T_kf_w;   // prev_kf->T_kf_w, read before the KF decision
+        bool is_kf = false;
+        if (StVO->needNewKF()) {
+            is_kf = true;
+            T_kf_w = T_kf_w * StVO->curr_frame->Tfw;   // KeyFrame(curr_frame) + addKeyFrame
+            StVO->currFrameIsKF();
+            ++n_kf;
+        }
+        if (json) {
+            const StereoFrame* c = StVO->curr_frame;
+            std::printf("{\"frame\": %d, \"n_pt\": %zu, \"n_ls\": %zu, \"matched_pt\": %d, \"matched_ls\": %d, "
+                        "\"n_inliers\": %d, \"num_frame_loss\": %d, \"err_norm\": %.17g, \"kf\": %d, \"DT\": [",
+                        k, c->stereo_pt.size(), c->stereo_ls.size(), mpt, mls, StVO->n_inliers, StVO->numFrameLoss,
+                        c->err_norm, is_kf ? 1 : 0);
+            for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->DT.v[i]);
+            std::printf("], \"Tfw\": [");
+            for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->Tfw.v[i]);
+            std::printf("]}\n");
         }
         StVO->updateFrame_ECCV18(T_base);
         if (!out.empty() && !StVO->vec_all_frame_pose.empty()) {
@@ -157,6 +170,7 @@ static int run(int argc, char** argv) {
                            << q[0] << " " << q[1] << " " << q[2] << " " << q[3] << std::endl;
         }
     }
+    if (!json) std::cerr << "keyframes: " << n_kf << std::endl;
     delete StVO;
     return 0;
 }

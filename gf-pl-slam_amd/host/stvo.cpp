@@ -253,6 +253,33 @@ void StereoFrameHandler::pull_track() {
     numFrameLoss = t.num_frame_loss;
 }
 
+void StereoFrameHandler::pull_kf() {
+    gfpl_kf_state st;
+    check(gfpl_read_kf_state(sb_, 0, &st), "gfpl_read_kf_state");
+    numFrameSinceKeyframe = st.num_frame_since_kf;
+    prev_f_iskf = st.prev_f_iskf != 0;
+    entropy_first_prevKF = st.entropy_first_prevKF;
+    for (int i = 0; i < 16; ++i) T_prevKF.v[i] = st.T_prevKF[i];
+    for (int i = 0; i < 36; ++i) cov_prevKF_currF.v[i] = st.cov_prevKF_currF[i];
+}
+
+bool StereoFrameHandler::needNewKF() {
+    if (!curr_frame) throw std::logic_error("needNewKF without a current frame");
+    sync_config();
+    int32_t flag = 0;
+    check(gfpl_need_new_kf(sb_, &flag), "gfpl_need_new_kf");
+    pull_kf();
+    return flag != 0;
+}
+
+void StereoFrameHandler::currFrameIsKF() {
+    if (!curr_frame) throw std::logic_error("currFrameIsKF without a current frame");
+    const int32_t all = 1;
+    check(gfpl_curr_frame_is_kf(sb_, &all), "gfpl_curr_frame_is_kf");
+    pull(GFPL_CURR, curr_frame, true, true);   // idx renumbered, Tfw = Tfw_cov = I
+    pull_kf();
+}
+
 void StereoFrameHandler::initialize(StereoFrame* frame) {
     sync_config();
     gfpl_frames dev{};
@@ -265,6 +292,7 @@ void StereoFrameHandler::initialize(StereoFrame* frame) {
     matched_pt.clear();
     matched_ls.clear();
     pull(GFPL_PREV, prev_frame, true, true);
+    pull_kf();
 }
 
 void StereoFrameHandler::insertStereoPair(StereoFrame* frame) {
@@ -278,6 +306,7 @@ void StereoFrameHandler::insertStereoPair(StereoFrame* frame) {
     pull(GFPL_CURR, curr_frame, true, true);
     pull(GFPL_PREV, prev_frame, true, false);   // pl_obs, *_obs, inlier, cut endpoints, covariances
     pull_track();
+    numFrameSinceKeyframe++;   // as gfpl_insert_stereo_pair did on the device (:150)
 }
 
 void StereoFrameHandler::stereoMatching(StereoFrame* frame) {

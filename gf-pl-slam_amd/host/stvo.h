@@ -104,6 +104,8 @@ public:
     static double& orbScaleFactor() { return getInstance().c.orb_scale_factor; }
     static int& orbNLevels() { return getInstance().c.orb_n_levels; }
     static double& lsdScale() { return getInstance().c.lsd_scale; }
+    static double& minEntropyRatio() { return getInstance().c.min_entropy_ratio; }
+    static int& maxKFNumFrames() { return getInstance().c.max_kf_num_frames; }
     // the C-ABI view (bools folded in)
     static gfpl_config abi();
 
@@ -221,6 +223,9 @@ public:
     // src/stereoFrameHandler.cpp:864-922 (prev <- curr; logs T_base * old prev Tfw)
     void updateFrame_ECCV18(const Matrix4d T_base);
     void updateFrame();
+    // src/stereoFrameHandler.cpp:2309-2349 / 2351-2379 (app/plslam_mod.cpp:436-447)
+    bool needNewKF();
+    void currFrameIsKF();
 
     // stage entry points of insertStereoPair, for callers that drive them one by one
     void stereoMatching(StereoFrame* frame);                     // extractStereoFeatures_ORBSLAM minus detection
@@ -239,12 +244,20 @@ public:
     int n_inliers = 0, n_inliers_pt = 0, n_inliers_ls = 0;
     int numFrameLoss = 0;
     std::vector<Matrix4d> vec_all_frame_pose;
+    // SLAM variables for the KF decision (include/stereoFrameHandler.h:147-153),
+    // refreshed from HBM after every call that changes them
+    int numFrameSinceKeyframe = 0;
+    bool prev_f_iskf = true;
+    double entropy_first_prevKF = 0.0;
+    Matrix4d T_prevKF = Matrix4d::Identity();
+    Matrix6d cov_prevKF_currF;
 
 private:
     void sync_config();
     void upload(StereoFrame* f, gfpl_frames* dev);
     void pull(int which, StereoFrame* f, bool features, bool pose);
     void pull_track();
+    void pull_kf();
     void check(int rc, const char* what) const;
 
     gfpl_ctx* ctx_ = nullptr;

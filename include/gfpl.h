@@ -110,6 +110,8 @@ typedef struct gfpl_config {
     double cut_step;             /* stepCutRatio 0.05 (src/stereoFrameHandler.cpp:135) */
     double cut_rng[2];           /* rngCutRatio {0,1} (src/stereoFrameHandler.cpp:134)  */
     double proj_gate_px;         /* rng_included 10.0 (src/stereoFrameHandler.cpp:534)  */
+    double min_entropy_ratio;    /* :34  0.90  (needNewKF)                      */
+    int    max_kf_num_frames;    /* :35  50    (needNewKF)                      */
     double cut_certify;          /* (new) 1e-9: relative margin of the certified line-cut
                                     search; 0 = every neighbour evaluated with
                                     the reference's LLT; nonzero values below 1e-10 are rejected */
@@ -199,6 +201,17 @@ typedef struct gfpl_track_host {
     int num_frame_loss;
 } gfpl_track_host;
 
+/* Keyframe-decision state of one StereoFrameHandler (include/stereoFrameHandler.h:147-153). */
+typedef struct gfpl_kf_state {
+    double T_prevKF[16];          /* row-major                                   */
+    double cov_prevKF_currF[36];
+    double entropy_first_prevKF;
+    double entropy_ratio;         /* of the last gfpl_need_new_kf               */
+    int    prev_f_iskf;
+    int    num_frame_since_kf;    /* numFrameSinceKeyframe                       */
+    int    need_new_kf;           /* decision of the last gfpl_need_new_kf       */
+} gfpl_kf_state;
+
 typedef struct gfpl_ctx gfpl_ctx;
 typedef struct gfpl_seqbatch gfpl_seqbatch;
 
@@ -253,6 +266,18 @@ int  gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames*
  * prev <- curr, matched lists cleared.  (FAST-threshold adaptation is out of scope;
  * the T_base trajectory log lives in the host mirror, gf-pl-slam_amd/host/stvo.h.) */
 int  gfpl_update_frame(gfpl_seqbatch* sb);
+/* StereoFrameHandler::needNewKF (src/stereoFrameHandler.cpp:2309-2349) for every
+ * sequence on its curr frame (after optimize_pose, as app/plslam_mod.cpp:436):
+ * entropy of the covariance accumulated since the last keyframe vs the first one.
+ * flags: HOST [B] (synchronises) or NULL; 1 = new keyframe needed.  The decision
+ * and the ratio are kept in the sequence's gfpl_kf_state either way.          */
+int  gfpl_need_new_kf(gfpl_seqbatch* sb, int32_t* flags);
+/* StereoFrameHandler::currFrameIsKF (src/stereoFrameHandler.cpp:2351-2379) for the
+ * sequences whose mask entry is nonzero (HOST [B], synchronises; NULL = the last
+ * gfpl_need_new_kf decisions, asynchronous): numFrameSinceKeyframe = 0, curr idx
+ * renumbered, curr Tfw = Tfw_cov = I, T_prevKF = I, cov_prevKF_currF = 0.     */
+int  gfpl_curr_frame_is_kf(gfpl_seqbatch* sb, const int32_t* mask);
+int  gfpl_read_kf_state(gfpl_seqbatch* sb, int seq, gfpl_kf_state* out);
 /* insert_stereo_pair + optimize_pose + update_frame, one batched step.       */
 int  gfpl_frame_step(gfpl_seqbatch* sb, const gfpl_frames* in);
 

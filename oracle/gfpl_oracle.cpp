@@ -468,12 +468,12 @@ void eig_sym(const double* A, int n, double* w) {
     }
 }
 
-// adjoint_se3 / unccomp_se3 (src/auxiliar.cpp:216-223,233-238)
-void unccomp_se3(const double* T1, const double* cov1, const double* covInc, double* out) {
-    double Ad[36] = {0};
-    double R[9], t[3] = {T1[3], T1[7], T1[11]}, S[9], SR[9];
+// adjoint_se3 (src/auxiliar.cpp:216-223): [R, skew(t) R; 0, R]
+void adjoint_se3(const double* T, double* Ad) {
+    double R[9], t[3] = {T[3], T[7], T[11]}, S[9], SR[9];
+    for (int i = 0; i < 36; ++i) Ad[i] = 0.0;
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) R[i * 3 + j] = T1[i * 4 + j];
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = T[i * 4 + j];
     skew3(t, S);
     mat3_mul(S, R, SR);
     for (int i = 0; i < 3; ++i)
@@ -482,19 +482,67 @@ void unccomp_se3(const double* T1, const double* cov1, const double* covInc, dou
             Ad[i * 6 + 3 + j] = SR[i * 3 + j];
             Ad[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
         }
+}
+
+// [C +] A X A^T for 6x6 (Eigen: the product A*X into a temporary, then * A^T;
+// inner products k-sequential, pin N2; C + product as in `covT1 + adj*cov*adj^T`)
+void sandwich6(const double* A, const double* X, const double* C, double* out) {
     double AS[36];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) {
-            double s = Ad[i * 6 + 0] * covInc[0 * 6 + j];
-            for (int k = 1; k < 6; ++k) s = s + Ad[i * 6 + k] * covInc[k * 6 + j];
+            double s = A[i * 6 + 0] * X[0 * 6 + j];
+            for (int k = 1; k < 6; ++k) s = s + A[i * 6 + k] * X[k * 6 + j];
             AS[i * 6 + j] = s;
         }
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) {
-            double s = AS[i * 6 + 0] * Ad[j * 6 + 0];
-            for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * Ad[j * 6 + k];
-            out[i * 6 + j] = cov1[i * 6 + j] + s;
+            double s = AS[i * 6 + 0] * A[j * 6 + 0];
+            for (int k = 1; k < 6; ++k) s = s + AS[i * 6 + k] * A[j * 6 + k];
+            out[i * 6 + j] = C ? C[i * 6 + j] + s : s;
         }
+}
+
+// unccomp_se3 (src/auxiliar.cpp:233-238): covT1 + adj(T1) covTinc adj(T1)^T
+void unccomp_se3(const double* T1, const double* cov1, const double* covInc, double* out) {
+    double Ad[36];
+    adjoint_se3(T1, Ad);
+    sandwich6(Ad, covInc, cov1, out);
+}
+
+// Matrix6d::determinant (Eigen 3.3, size > 4: PartialPivLU): the factorisation of
+// inverse6, det = (-1)^transpositions * (((((d0 d1) d2) d3) d4) d5) — the
+// diagonal product pinned left to right (the reference's vectorised redux order
+// is machine-dependent)
+double det6(const double* A) {
+    double m[36];
+    std::memcpy(m, A, sizeof m);
+    int ntr = 0;
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        double pv = std::fabs(m[k * 6 + k]);
+        for (int i = k + 1; i < 6; ++i) {
+            double v = std::fabs(m[i * 6 + k]);
+            if (v > pv) { pv = v; p = i; }
+        }
+        if (p != k) {
+            for (int j = 0; j < 6; ++j) std::swap(m[k * 6 + j], m[p * 6 + j]);
+            ++ntr;
+        }
+        double piv = m[k * 6 + k];
+        if (piv != 0.0)
+            for (int i = k + 1; i < 6; ++i) m[i * 6 + k] = m[i * 6 + k] / piv;
+        for (int i = k + 1; i < 6; ++i)
+            for (int j = k + 1; j < 6; ++j) m[i * 6 + j] = m[i * 6 + j] - m[i * 6 + k] * m[k * 6 + j];
+    }
+    double d = m[0];
+    for (int i = 1; i < 6; ++i) d = d * m[i * 7];
+    return (ntr & 1) ? -1.0 * d : 1.0 * d;
+}
+
+// entropy of a 6-dof Gaussian as needNewKF writes it: 3(1 + log(2 acos(-1))) + 0.5 log det
+double kf_entropy(const double* cov) {
+    const double c0 = 3.0 * (1.0 + det_log(2.0 * 3.141592653589793));   // acos(-1) = pi
+    return c0 + 0.5 * det_log(det6(cov));
 }
 
 // is_finite (src/auxiliar.cpp:475-477)
@@ -668,6 +716,48 @@ struct gfplo_handler {
     std::vector<int> matched_pt, matched_ls;
     int n_inliers = 0, n_inliers_pt = 0, n_inliers_ls = 0;
     int numFrameLoss = 0;
+    // keyframe decision (include/stereoFrameHandler.h:147-153)
+    int numFrameSinceKeyframe = 0;
+    bool prev_f_iskf = true;
+    double entropy_first_prevKF = 0.0, entropy_ratio = 0.0;
+    double T_prevKF[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    double cov_prevKF_currF[36] = {0};
+    int need_new_kf = 0;
+
+    // needNewKF (src/stereoFrameHandler.cpp:2309-2349)
+    bool needNewKF() {
+        if (prev_f_iskf) {
+            entropy_first_prevKF = kf_entropy(curr->DT_cov);
+            prev_f_iskf = false;
+        }
+        double adj[36], Ti[16], adjTinv[36], covDTinv[36], acc[36];
+        adjoint_se3(T_prevKF, adj);
+        inverse_se3(curr->DT, Ti);            // uncTinv_se3 (src/auxiliar.cpp:225-231)
+        adjoint_se3(Ti, adjTinv);
+        sandwich6(adjTinv, curr->DT_cov, nullptr, covDTinv);
+        sandwich6(adj, covDTinv, cov_prevKF_currF, acc);
+        std::memcpy(cov_prevKF_currF, acc, sizeof acc);
+        const double entropy_curr = kf_entropy(cov_prevKF_currF);
+        entropy_ratio = entropy_curr / entropy_first_prevKF;
+        bool zero_cov = true, ident = true;
+        for (int i = 0; i < 36; ++i) zero_cov = zero_cov && curr->DT_cov[i] == 0.0;
+        for (int i = 0; i < 16; ++i) ident = ident && curr->DT[i] == ((i % 5 == 0) ? 1.0 : 0.0);
+        need_new_kf = (numFrameSinceKeyframe > cfg.max_kf_num_frames || entropy_ratio < cfg.min_entropy_ratio ||
+                       std::isnan(entropy_ratio) || std::isinf(entropy_ratio) || (zero_cov && ident)) ? 1 : 0;
+        return need_new_kf != 0;
+    }
+
+    // currFrameIsKF (src/stereoFrameHandler.cpp:2351-2379)
+    void currFrameIsKF() {
+        numFrameSinceKeyframe = 0;
+        for (size_t i = 0; i < curr->pt.size(); ++i) curr->pt[i].idx = (int)i;
+        for (size_t i = 0; i < curr->ls.size(); ++i) curr->ls[i].idx = (int)i;
+        for (int i = 0; i < 16; ++i) curr->Tfw[i] = (i % 5 == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < 36; ++i) curr->Tfw_cov[i] = (i % 7 == 0) ? 1.0 : 0.0;
+        std::memcpy(T_prevKF, curr->Tfw, sizeof T_prevKF);
+        for (int i = 0; i < 36; ++i) cov_prevKF_currF[i] = 0.0;
+        prev_f_iskf = true;
+    }
 
     // ----------------------------------------------------------- camera --
     // PinholeStereoCamera::projection / backProjection / getDisparity
@@ -1619,6 +1709,13 @@ int gfplo_initialize(gfplo_handler* h, const gfpl_frames* in, int seq) {
     for (int i = 0; i < 16; ++i) h->prev->Tfw[i] = h->prev->DT[i] = (i % 5 == 0) ? 1.0 : 0.0;
     for (int i = 0; i < 36; ++i) h->prev->Tfw_cov[i] = (i % 7 == 0) ? 1.0 : 0.0;
     h->numFrameLoss = 0;
+    // SLAM variables for KF decision (src/stereoFrameHandler.cpp:54-58); a fresh
+    // handler also starts numFrameSinceKeyframe at 0 (include/stereoFrameHandler.h:147)
+    for (int i = 0; i < 16; ++i) h->T_prevKF[i] = (i % 5 == 0) ? 1.0 : 0.0;
+    for (int i = 0; i < 36; ++i) h->cov_prevKF_currF[i] = 0.0;
+    h->prev_f_iskf = true;
+    h->numFrameSinceKeyframe = 0;
+    h->entropy_first_prevKF = 0.0; h->entropy_ratio = 0.0; h->need_new_kf = 0;
     h->matched_pt.clear(); h->matched_ls.clear();
     h->prev->in = nullptr;
     return 0;
@@ -1663,6 +1760,30 @@ int gfplo_insert_stereo_pair(gfplo_handler* h, const gfpl_frames* in, int seq) {
     h->crossLines();
     h->finishCounts();
     if (h->cfg.use_line_conf_cut) h->lineCut();
+    h->numFrameSinceKeyframe++;   // (:150)
+    return 0;
+}
+
+int gfplo_need_new_kf(gfplo_handler* h, int* flag) {
+    if (!h->prev || !h->curr) return GFPL_E_STATE;
+    const bool f = h->needNewKF();
+    if (flag) *flag = f ? 1 : 0;
+    return 0;
+}
+int gfplo_curr_frame_is_kf(gfplo_handler* h) {
+    if (!h->curr) return GFPL_E_STATE;
+    h->currFrameIsKF();
+    return 0;
+}
+int gfplo_read_kf_state(gfplo_handler* h, gfpl_kf_state* out) {
+    if (!out) return GFPL_E_INVALID;
+    std::memcpy(out->T_prevKF, h->T_prevKF, sizeof out->T_prevKF);
+    std::memcpy(out->cov_prevKF_currF, h->cov_prevKF_currF, sizeof out->cov_prevKF_currF);
+    out->entropy_first_prevKF = h->entropy_first_prevKF;
+    out->entropy_ratio = h->entropy_ratio;
+    out->prev_f_iskf = h->prev_f_iskf ? 1 : 0;
+    out->num_frame_since_kf = h->numFrameSinceKeyframe;
+    out->need_new_kf = h->need_new_kf;
     return 0;
 }
 
@@ -1743,6 +1864,7 @@ double gfplo_cos(double x) { return det_cos(x); }
 double gfplo_logdet6(const double* M) { return logdet6(M); }
 int gfplo_ldlt_solve6(const double* H, const double* g, double* x) { ldlt_solve6(H, g, x); return 0; }
 int gfplo_inverse6(const double* A, double* out) { inverse6(A, out); return 0; }
+double gfplo_det6(const double* A) { return det6(A); }
 int gfplo_inverse4(const double* A, double* out) { mat4_inv(A, out); return 0; }
 int gfplo_eig_sym(const double* A, int n, double* w) { if (n < 1 || n > 6) return GFPL_E_INVALID; eig_sym(A, n, w); return 0; }
 int gfplo_expmap_se3(const double* x, double* T) { expmap_se3(x, T); return 0; }

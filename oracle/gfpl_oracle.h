@@ -50,6 +50,10 @@ int gfplo_optimize_pose(gfplo_handler* h);
 int gfplo_optimize_pose_ini(gfplo_handler* h, const double* DT_ini);
 /* updateFrame_ECCV18 swap (src/stereoFrameHandler.cpp:864-922) */
 int gfplo_update_frame(gfplo_handler* h);
+/* needNewKF / currFrameIsKF (src/stereoFrameHandler.cpp:2309-2379) */
+int gfplo_need_new_kf(gfplo_handler* h, int* flag);
+int gfplo_curr_frame_is_kf(gfplo_handler* h);
+int gfplo_read_kf_state(gfplo_handler* h, gfpl_kf_state* out);
 
 /* stage-level entry points (same split as include/gfpl.h) */
 int gfplo_begin_frame(gfplo_handler* h, const gfpl_frames* in, int seq);   /* new curr_frame */
@@ -75,6 +79,8 @@ double gfplo_cos(double x);
 double gfplo_logdet6(const double* M36);
 int    gfplo_ldlt_solve6(const double* H36, const double* g6, double* x6);
 int    gfplo_inverse6(const double* A36, double* out36);
+/* Matrix6d::determinant (PartialPivLU, diagonal product left to right) */
+double gfplo_det6(const double* A36);
 int    gfplo_inverse4(const double* A16, double* out16);
 int    gfplo_eig_sym(const double* A, int n, double* w);
 int    gfplo_expmap_se3(const double* x6, double* T16);

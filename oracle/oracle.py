@@ -36,8 +36,10 @@ def lib() -> C.CDLL:
             getattr(L, n).argtypes = [P]; getattr(L, n).restype = C.c_int
         for n in ["gfplo_read_frame", "gfplo_write_frame"]:
             getattr(L, n).argtypes = [P, C.c_int, P]; getattr(L, n).restype = C.c_int
-        for n in ["gfplo_read_track", "gfplo_write_track"]:
+        for n in ["gfplo_read_track", "gfplo_write_track", "gfplo_need_new_kf", "gfplo_read_kf_state"]:
             getattr(L, n).argtypes = [P, P]; getattr(L, n).restype = C.c_int
+        L.gfplo_curr_frame_is_kf.argtypes = [P]; L.gfplo_curr_frame_is_kf.restype = C.c_int
+        L.gfplo_det6.argtypes = [P]; L.gfplo_det6.restype = C.c_double
         L.gfplo_optimize_pose_ini.argtypes = [P, P]; L.gfplo_optimize_pose_ini.restype = C.c_int
         L.gfplo_hamming.argtypes = [P, P, C.c_int]; L.gfplo_hamming.restype = C.c_int
         L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
@@ -124,6 +126,19 @@ class OracleHandler:
     def write_track(self, tr: gfpl.TrackHost):
         self._c(self.L.gfplo_write_track(self.h, C.byref(tr)), "write_track")
 
+    def needNewKF(self) -> bool:
+        f = C.c_int(0)
+        self._c(self.L.gfplo_need_new_kf(self.h, C.byref(f)), "need_new_kf")
+        return bool(f.value)
+
+    def currFrameIsKF(self):
+        self._c(self.L.gfplo_curr_frame_is_kf(self.h), "curr_frame_is_kf")
+
+    def read_kf_state(self) -> dict:
+        st = gfpl.KFState()
+        self._c(self.L.gfplo_read_kf_state(self.h, C.byref(st)), "read_kf_state")
+        return st.as_dict()
+
     def __del__(self):
         try:
             if self.h:
@@ -158,6 +173,10 @@ def logdet6(M: np.ndarray) -> float:
 def ldlt_solve6(H: np.ndarray, g: np.ndarray) -> np.ndarray:
     x = np.zeros(6); H = np.ascontiguousarray(H, np.float64); g = np.ascontiguousarray(g, np.float64)
     lib().gfplo_ldlt_solve6(_p(H), _p(g), _p(x)); return x
+
+
+def det6(A) -> float:
+    return lib().gfplo_det6(_p(np.ascontiguousarray(A, np.float64)))
 
 
 def inverse6(A):

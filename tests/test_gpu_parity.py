@@ -356,3 +356,51 @@ def test_line_cut_certified_matches_exact_at_scale():
         assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64))
         n_lines += len(ma)
     assert n_lines > 100 * n
+
+
+# ---- keyframe decision: needNewKF / currFrameIsKF
+def test_need_new_kf_and_curr_frame_is_kf_parity():
+    """3 sequences x 8 frames with the app's order (insert, optimizePose, needNewKF,
+    currFrameIsKF when needed, updateFrame; app/plslam_mod.cpp:387-477): decisions,
+    entropy ratios, accumulated covariances and the curr frame after a keyframe are
+    bit-identical to the oracle.  maxKFNumFrames = 3 and minEntropyRatio = 0.97 make
+    both gates fire."""
+    n, F = 3, 8
+    cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, max_kf_num_frames=3, min_entropy_ratio=0.97)
+    cam = gfpl.make_camera("vga", cfg)
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=17), n, F, 2048, 512)
+    D = gfpl.DeviceFrames(H)
+    g = gfpl.StereoFrameHandler(gfpl.Context(cam, cfg), n, 2048, 512)
+    orc = [O.OracleHandler(cam, cfg, 2048, 512) for _ in range(n)]
+    g.initialize(D.frames(0))
+    for b, o in enumerate(orc):
+        o.initialize(H.frames(0), b)
+    n_kf = 0
+    for k in range(1, F):
+        g.insertStereoPair(D.frames(k))
+        g.optimizePose()
+        flags = g.needNewKF()
+        for b, o in enumerate(orc):
+            o.insertStereoPair(H.frames(k), b)
+            o.optimizePose()
+            fo = o.needNewKF()
+            sg, so = g.read_kf_state(b), o.read_kf_state()
+            assert bool(flags[b]) == fo, (k, b, sg, so)
+            for key in ("entropy_first_prevKF", "entropy_ratio"):
+                assert np.float64(sg[key]).view(np.uint64) == np.float64(so[key]).view(np.uint64), (k, b, key)
+            assert np.array_equal(sg["cov_prevKF_currF"].view(np.uint64), so["cov_prevKF_currF"].view(np.uint64))
+            assert sg["num_frame_since_kf"] == so["num_frame_since_kf"]
+            if fo:
+                o.currFrameIsKF()
+        g.currFrameIsKF(flags)
+        n_kf += int(flags.sum())
+        for b, o in enumerate(orc):
+            report = compare_core(g.read_frame(gfpl.CURR, b), o.read_frame(gfpl.CURR), f"f{k} s{b} kf ")
+            assert not report, report[:10]
+            assert compare_pose(g.read_frame(gfpl.CURR, b), o.read_frame(gfpl.CURR))[1]
+            sg, so = g.read_kf_state(b), o.read_kf_state()
+            assert (sg["prev_f_iskf"], sg["num_frame_since_kf"]) == (so["prev_f_iskf"], so["num_frame_since_kf"])
+        g.updateFrame()
+        for o in orc:
+            o.updateFrame()
+    assert n_kf >= n

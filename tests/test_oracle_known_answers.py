@@ -279,3 +279,53 @@ def test_line_cut_zero_covariance_never_moves():
     h.estimateProjUncertainty_submodular()   # covS = covE = 0: variances 0 -> no finite metric
     p = h.read_frame(gfpl.PREV)
     assert np.all(p.get("ls_cut")[:5] == 0.0)
+
+
+# ------------------------------------------------- keyframe decision ----
+def test_det6_matches_numpy_and_permutation_sign():
+    rng = np.random.default_rng(5)
+    for _ in range(30):
+        A = rng.normal(size=(6, 6))
+        assert O.det6(A) == pytest.approx(np.linalg.det(A), rel=1e-10)
+    # a permutation matrix of odd parity has determinant exactly -1, even +1
+    P = np.eye(6)[[1, 0, 2, 3, 4, 5]]
+    assert O.det6(P) == -1.0
+    assert O.det6(np.eye(6)[[1, 2, 0, 3, 4, 5]]) == 1.0
+    assert O.det6(np.diag([2.0, 3.0, 0.5, 1.0, 4.0, 0.25])) == 3.0
+    assert O.det6(np.zeros((6, 6))) == 0.0
+
+
+def test_need_new_kf_entropy_and_frame_count(tmp_path):
+    """needNewKF on a short synthetic sequence: the first decision after a keyframe
+    compares the accumulated covariance with the first one (ratio 1 at the first
+    call), the frame-count gate fires after maxKFNumFrames, and currFrameIsKF
+    resets the state (src/stereoFrameHandler.cpp:2309-2379)."""
+    cfg = gfpl.default_config(max_iters=5, max_iters_ref=5, max_kf_num_frames=2)
+    cam = gfpl.make_camera("vga", cfg)
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=2), 1, 6, 2048, 512)
+    o = O.OracleHandler(cam, cfg, 2048, 512)
+    o.initialize(H.frames(0), 0)
+    st = o.read_kf_state()
+    assert st["prev_f_iskf"] == 1 and st["num_frame_since_kf"] == 0
+    assert np.array_equal(st["T_prevKF"], np.eye(4)) and not st["cov_prevKF_currF"].any()
+    seen = []
+    for k in range(1, 6):
+        o.insertStereoPair(H.frames(k), 0)
+        o.optimizePose()
+        f = o.needNewKF()
+        st = o.read_kf_state()
+        cov = o.read_frame(gfpl.CURR).get("DT_cov")
+        e = 3.0 * (1.0 + np.log(2.0 * np.pi)) + 0.5 * np.log(np.linalg.det(cov))
+        if k == 1:
+            assert st["entropy_first_prevKF"] == pytest.approx(e, rel=1e-9)
+            assert st["entropy_ratio"] == pytest.approx(1.0, rel=1e-9) or st["entropy_ratio"] < 1.0
+        seen.append((st["num_frame_since_kf"], f))
+        if f:
+            o.currFrameIsKF()
+            s2 = o.read_kf_state()
+            assert s2["num_frame_since_kf"] == 0 and s2["prev_f_iskf"] == 1
+            assert np.array_equal(o.read_frame(gfpl.CURR).get("Tfw"), np.eye(4))
+        o.updateFrame()
+    # the frame-count gate (numFrameSinceKeyframe > 2) fires no later than the 3rd frame after a KF
+    assert any(f for _, f in seen)
+    assert all(n <= 3 for n, _ in seen)
