@@ -136,6 +136,57 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
     d.Jl[1] = L.le_obs[3 * q + 1];
 }
 
+// ------------------------------------------------------ fast cut endpoints --
+// The certified comparisons (k_cut_search) need each endpoint's variance v and
+// pose Jacobian J only to ~1e-14, so the search evaluates them in a shorter,
+// non-reference order from per-line data:  DT is affine, so the transformed cut
+// point is (1-c) DT P0 + c DT P1, and getPoseInfoOnLine's variance
+// Jl^T Jp R cov R^T Jp^T Jl is u^T [(1-c)^2 R C0 R^T + c^2 R C1 R^T] u with
+// u = Jp^T Jl = (Jl0 f/z, Jl1 f/z, -f (Jl0 x + Jl1 y)/z^2).  Per line (CUT_FAST):
+// DT sP [3], DT eP [3], R covS R^T and R covE R^T (xx xy xz yy yz zz) [6+6], Jl [2].
+__device__ __forceinline__ void cut_fast_data(const double* Dl, const LineCutData& d, double* fd) {
+    se3_apply(Dl, d.sP, fd);
+    se3_apply(Dl, d.eP, fd + 3);
+    const double* Cs[2] = {d.covS, d.covE};
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        double T[9];   // R C
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                T[i * 3 + k] = (Dl[i * 4 + 0] * Cs[w][0 * 3 + k] + Dl[i * 4 + 1] * Cs[w][1 * 3 + k]) + Dl[i * 4 + 2] * Cs[w][2 * 3 + k];
+        const int ii[6] = {0, 0, 0, 1, 1, 2}, jj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+            fd[6 + 6 * w + e] = (T[ii[e] * 3 + 0] * Dl[jj[e] * 4 + 0] + T[ii[e] * 3 + 1] * Dl[jj[e] * 4 + 1]) +
+                                T[ii[e] * 3 + 2] * Dl[jj[e] * 4 + 2];
+    }
+    fd[18] = d.Jl[0];
+    fd[19] = d.Jl[1];
+}
+
+// one endpoint from the fast data: g0/g1 the transformed points it blends, A0/A1
+// the rotated covariances, t the cut ratio -> v, J[6]
+__device__ __forceinline__ void cut_endpoint_fast(const DevCam& cam, double homog, const double* g0, const double* g1,
+                                                  const double* A0, const double* A1, double jl0, double jl1, double t,
+                                                  double* out7) {
+    const double om = 1.0 - t;
+    double g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k] = __builtin_fma(om, g0[k], t * g1[k]);
+    const double iz = 1.0 / g[2];
+    const double fz = cam.fx * iz;
+    const double u0 = jl0 * fz, u1 = jl1 * fz, u2 = -__builtin_fma(jl0, g[0], jl1 * g[1]) * fz * iz;
+    auto quad = [&](const double* A) {
+        const double diag = __builtin_fma(A[0] * u0, u0, __builtin_fma(A[3] * u1, u1, A[5] * u2 * u2));
+        const double off = __builtin_fma(A[1] * u0, u1, __builtin_fma(A[2] * u0, u2, A[4] * u1 * u2));
+        return __builtin_fma(2.0, off, diag);
+    };
+    out7[0] = __builtin_fma(om * om, quad(A0), t * t * quad(A1));
+    poseJac(cam, homog, g, jl0, jl1, out7 + 1);
+}
+
 // ------------------------------------------------------------------ prep --
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
@@ -152,6 +203,7 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
     const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
     double* scr_l = p.scr.cut_ls + (size_t)b * p.mls_cap * 21;
+    double* fast_l = p.scr.cut_fast + (size_t)b * p.mls_cap * CUT_FAST;
     // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635), every lane
     double Dl[16];
     {
@@ -178,6 +230,10 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
 #pragma unroll
                 for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];   // k_cut_search subtracts it
+                double fd[CUT_FAST];
+                cut_fast_data(Dl, d, fd);
+#pragma unroll
+                for (int i = 0; i < CUT_FAST; ++i) fast_l[(size_t)m * CUT_FAST + i] = fd[i];
             } else {
                 const size_t q = pbase + mpt[m];
                 double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
@@ -373,12 +429,13 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
-    __shared__ double sum[CUT_G][25];    // S
-    __shared__ double sumb[CUT_G][25];   // invCov_sum when the line opened
+    __shared__ double sumA[CUT_G][25];   // approximate S of the current line
+    __shared__ double sumE[CUT_G][25];   // exact invCov_sum before line m_sync (lazy, for exact steps)
     __shared__ double chol[CUT_G][CUT_CH];
     __shared__ double epf[CUT_G][CUT_EP];
-    __shared__ double nxt[CUT_G][49];    // prefetched next line: sP eP covS covE Jl (26) | r=0 info (21)
-    __shared__ double lin[CUT_G][27];    // current line: sP eP covS covE Jl
+    __shared__ double fst[CUT_G][21];    // fast data of the current line
+    __shared__ double nxt[CUT_G][43];    // prefetched next line: fast data (20) | r = 0 info (21)
+    __shared__ double xs[CUT_G][25];     // exact step: exact S of the line / flush endpoints
     __shared__ double dtl[CUT_G][13];    // DT_inv rows 0-2
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
@@ -392,64 +449,47 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
     const double* scr_l = p.scr.cut_ls + (size_t)(live ? b : 0) * p.mls_cap * 21;
+    const double* fast_l = p.scr.cut_fast + (size_t)(live ? b : 0) * p.mls_cap * CUT_FAST;
     for (int i = j; i < 12; i += 8) dtl[g][i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
     const double* Dl = dtl[g];
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    // E role of this lane
+    // E role of this lane: lanes 0-2 start endpoint (blend sP -> eP), 3-5 end (eP -> sP)
     const int eside = j < 3 ? 0 : 1;
     const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
     double* my_slot = &epf[g][CUT_SL * (j < 6 ? j : 0)];
-    // the line as this lane's E role sees it (LDS): start endpoints blend (sP, eP,
-    // covS, covE), end endpoints (eP, sP, covE, covS) — one cut_endpoint call per
-    // lane instead of two divergent ones
-    const double* P0 = &lin[g][eside ? 3 : 0];
-    const double* P1 = &lin[g][eside ? 0 : 3];
-    const double* C0 = &lin[g][eside ? 15 : 6];
-    const double* C1 = &lin[g][eside ? 6 : 15];
-    const double* Jl = &lin[g][24];
+    const double* G0 = &fst[g][eside ? 3 : 0];
+    const double* G1 = &fst[g][eside ? 0 : 3];
+    const double* A0 = &fst[g][eside ? 12 : 6];
+    const double* A1 = &fst[g][eside ? 6 : 12];
     // C role: neighbour j
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
     const unsigned long long gmask = 0xFFull << (8 * g);
     // group state (identical in the 8 lanes of a group)
     int m = 0;
-    int first = 1;       // first step of the line: the exact centre metric is logdet(sumb)
+    int m_sync = 0;      // sumE holds the exact invCov_sum before line m_sync
+    int first = 1;       // first step of the line: the exact centre metric is logdet(invCov_sum)
     double r0 = 0.0, r1 = 0.0;
-    // factor of S for the certified comparisons.  Group-shared LDS rows are
-    // written by all 8 lanes of the group with identical values: no per-entry
-    // lane masks, which would split the writes into branches that serialise the
-    // surrounding LDS reads.
-    auto put_chol = [&](const double* s21) {
+    auto put_chol = [&](const double* s21) {   // all 8 lanes write identical values
         double o[28];
         chol_s(s21, o);
 #pragma unroll
-        for (int e = 0; e < 28; ++e)
-            chol[g][e] = o[e];
+        for (int e = 0; e < 28; ++e) chol[g][e] = o[e];
     };
-    // Next-line prefetch: lane j loads elements j, j+8, ... of the 47-element vector
-    // [line data | r = 0 info] of the group's next line right after a line opens;
-    // the values land in LDS one iteration later, so opening a line never waits on HBM.
-    double pf[6];
-    int pending = 0;
-    // mls indices run one line ahead of the data prefetch, so no HBM latency is
-    // exposed when a line opens: q_cur (line m), q_nx (line m + 1), ix_n2 (m + 2)
+    // Next-line prefetch: lane j loads elements j, j+8, ... of the 41-element vector
+    // [fast data | r = 0 info] of the group's next line right after a line opens;
+    // the values land in LDS one iteration later.  mls indices run one line ahead.
     size_t q_cur = 0, q_nx = 0;
     int ix_n2 = 0;
-    auto pf_issue = [&](int mm) {   // data of line mm = m + 1 (q_nx)
-        const size_t q = q_nx;
+    double pf[6];
+    int pending = 0;
+    auto pf_issue = [&](int mm) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int e = j + 8 * k;
-            const double* src;
-            size_t off;
-            if (e < 3) { src = L.sP; off = 3 * q + e; }
-            else if (e < 6) { src = L.eP; off = 3 * q + (e - 3); }
-            else if (e < 15) { src = L.covS; off = 9 * q + (e - 6); }
-            else if (e < 24) { src = L.covE; off = 9 * q + (e - 15); }
-            else if (e < 26) { src = L.le_obs; off = 3 * q + (e - 24); }
-            else { src = scr_l; off = (size_t)mm * 21 + (size_t)(e < 47 ? e - 26 : 0); }
-            pf[k] = src[off];
+            pf[k] = e < CUT_FAST ? fast_l[(size_t)mm * CUT_FAST + e]
+                                 : scr_l[(size_t)mm * 21 + (size_t)(e < 41 ? e - CUT_FAST : 0)];
         }
         pending = 1;
     };
@@ -457,24 +497,19 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         q_cur = lb + mls[0];
         if (nls > 1) q_nx = lb + mls[1];
         if (nls > 2) ix_n2 = mls[2];
-        {
-            const size_t q = q_cur;
-            for (int e = j; e < 26; e += 8)
-                lin[g][e] = e < 3 ? L.sP[3 * q + e] : e < 6 ? L.eP[3 * q + e - 3] : e < 15 ? L.covS[9 * q + e - 6]
-                          : e < 24 ? L.covE[9 * q + e - 15] : L.le_obs[3 * q + e - 24];
-        }
+        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = fast_l[e];
         double s21[21];
 #pragma unroll
         for (int e = 0; e < 21; ++e) {
             const double s0 = p.scr.cut_sum[24 * b + e];
             s21[e] = s0 - scr_l[e];
-            sumb[g][e] = s0;
-            sum[g][e] = s21[e];
+            sumE[g][e] = s0;
+            sumA[g][e] = s21[e];
         }
         put_chol(s21);
         if (nls > 1) pf_issue(1);
     } else {
-        for (int e = j; e < 26; e += 8) lin[g][e] = (e >= 3 && e < 6) ? 1.0 : 0.0;
+        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = (e == 2 || e == 5) ? 1.0 : 0.0;
     }
     __syncthreads();
 #ifdef GFPL_CUT_PROF
@@ -485,22 +520,22 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- A: this lane's endpoint of the step and its certified-comparison terms
+        // ---- A: this lane's endpoint (fast) and its certified-comparison terms
         if (j < 6) {
             const double t = (eside == 0 ? r0 : r1) + eoff;
             double out[7];
-            cut_endpoint(cam, homog, Dl, Jl, P0, P1, C0, C1, t, out);
+            cut_endpoint_fast(cam, homog, G0, G1, A0, A1, fst[g][18], fst[g][19], t, out);
             double w[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 double u = out[1 + i];
 #pragma unroll
-                for (int k = 0; k < i; ++k) u = u - chol[g][tri(i, k)] * w[k];
+                for (int k = 0; k < i; ++k) u = __builtin_fma(-chol[g][tri(i, k)], w[k], u);
                 w[i] = u * chol[g][21 + i];
             }
             double a = w[0] * w[0];
 #pragma unroll
-            for (int i = 1; i < 6; ++i) a = a + w[i] * w[i];
+            for (int i = 1; i < 6; ++i) a = __builtin_fma(w[i], w[i], a);
 #pragma unroll
             for (int i = 0; i < 7; ++i) my_slot[i] = out[i];
 #pragma unroll
@@ -511,7 +546,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         if (pending) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
-                if (j + 8 * k < 47) nxt[g][j + 8 * k] = pf[k];
+                if (j + 8 * k < 41) nxt[g][j + 8 * k] = pf[k];
             pending = 0;
         }
         wave_lds_sync();
@@ -539,11 +574,74 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         const bool exact = act && (__ballot(!ok) & gmask) != 0;
         CUT_PROF(1);
         if (__any(exact)) {
-            // ---- X: the reference's evaluation of this step for the groups that need it
+            // ---- X: the reference's evaluation of this step for the groups that need it.
+            // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at
+            //    their final ratios, one line per round: lanes 0 / 1 its start / end
+            //    endpoint, then every lane the reference's sum chain)
+            while (__any(exact && m_sync < m)) {
+                const bool fl = exact && m_sync < m;
+                const size_t qf = fl ? lb + mls[m_sync] : lb;
+                __threadfence_block();   // this lane's own L.cut stores are complete
+                if (fl && j == 0) {   // ratios stored by this lane at the line's finalisation
+                    xs[g][14] = L.cut[2 * qf];
+                    xs[g][15] = L.cut[2 * qf + 1];
+                }
+                wave_lds_sync();
+                if (fl && j < 2) {
+                    LineCutData d;
+                    load_line(L, qf, d);
+                    double P0[3], P1[3], C0[9], C1[9], o7[7];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) { P0[k] = j ? d.eP[k] : d.sP[k]; P1[k] = j ? d.sP[k] : d.eP[k]; }
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) { C0[k] = j ? d.covE[k] : d.covS[k]; C1[k] = j ? d.covS[k] : d.covE[k]; }
+                    cut_endpoint(cam, homog, Dl, d.Jl, P0, P1, C0, C1, xs[g][14 + j], o7);
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) xs[g][7 * j + i] = o7[i];
+                }
+                wave_lds_sync();
+                if (fl) {
+                    double info[21];
+                    cut_assemble<false>(&xs[g][0], &xs[g][7], info);
+#pragma unroll
+                    for (int e = 0; e < 21; ++e) {
+                        const double S = sumE[g][e] - scr_l[(size_t)m_sync * 21 + e];
+                        sumE[g][e] = S + info[e];
+                    }
+                    ++m_sync;
+                }
+                wave_lds_sync();
+            }
+            // 2. exact endpoints of this step's six slots, exact S of line m
+            if (exact) {
+                LineCutData d;
+                load_line(L, q_cur, d);
+                if (j < 6) {
+                    const double t = (eside == 0 ? r0 : r1) + eoff;
+                    double P0[3], P1[3], C0[9], C1[9], o7[7];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        P0[k] = eside ? d.eP[k] : d.sP[k];
+                        P1[k] = eside ? d.sP[k] : d.eP[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) {
+                        C0[k] = eside ? d.covE[k] : d.covS[k];
+                        C1[k] = eside ? d.covS[k] : d.covE[k];
+                    }
+                    cut_endpoint(cam, homog, Dl, d.Jl, P0, P1, C0, C1, t, o7);
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) my_slot[i] = o7[i];
+                }
+#pragma unroll
+                for (int e = 0; e < 21; ++e) xs[g][e] = sumE[g][e] - scr_l[(size_t)m * 21 + e];
+            }
+            wave_lds_sync();
+            // 3. the reference's metrics and decision
             if (exact) {
                 double mc;
                 const double vj = cut_exact_step(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], &epf[g][CUT_SL * 1],
-                                                 &epf[g][CUT_SL * 4], sum[g], sumb[g], first, &mc);
+                                                 &epf[g][CUT_SL * 4], xs[g], sumE[g], first, &mc);
                 best = group_first_max(vj, valid, j, mc, top);
             }
         }
@@ -560,29 +658,28 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             }
         }
         if (act && finalize) {
-            // invCov_sum += info of the chosen ratio
+            // approximate invCov_sum += info of the chosen ratio (the exact one is
+            // accumulated lazily, only when an exact step needs it)
             double S7[7], E7[7];
             if (!stale_mid) {
 #pragma unroll
                 for (int i = 0; i < 7; ++i) { S7[i] = epf[g][CUT_SL * 1 + i]; E7[i] = epf[g][CUT_SL * 4 + i]; }
             } else {   // (not reached for finite ratios: valid neighbours keep r0 + r1 <= 1)
-                cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][0], &lin[g][3], &lin[g][6], &lin[g][15], r0, S7);
-                cut_endpoint(cam, homog, Dl, &lin[g][24], &lin[g][3], &lin[g][0], &lin[g][15], &lin[g][6], r1, E7);
+                cut_endpoint_fast(cam, homog, &fst[g][0], &fst[g][3], &fst[g][6], &fst[g][12], fst[g][18], fst[g][19],
+                                  r0, S7);
+                cut_endpoint_fast(cam, homog, &fst[g][3], &fst[g][0], &fst[g][12], &fst[g][6], fst[g][18], fst[g][19],
+                                  r1, E7);
             }
-            CUT_PROF(4);
             double info[21];
             cut_assemble<false>(S7, E7, info);
             double s21[21];
 #pragma unroll
-            for (int e = 0; e < 21; ++e) s21[e] = sum[g][e] + info[e];
-#ifndef GFPL_EXP_NO_CUT_STORE
+            for (int e = 0; e < 21; ++e) s21[e] = sumA[g][e] + info[e];
             if (j == 0) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
             }
-#endif
             ++m;
-            CUT_PROF(5);
             if (m < nls) {
                 q_cur = q_nx;
                 q_nx = lb + ix_n2;
@@ -590,28 +687,19 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 first = 1;
                 r0 = 0.0;
                 r1 = 0.0;
-                // line m from the prefetch buffer (same values load_line would read)
-                double nx[47];
+                // line m from the prefetch buffer
+                double nx[41];
 #pragma unroll
-                for (int e = 0; e < 47; ++e) nx[e] = nxt[g][e];
+                for (int e = 0; e < 41; ++e) nx[e] = nxt[g][e];
 #pragma unroll
-                for (int e = 0; e < 26; ++e) lin[g][e] = nx[e];
-                // open line m: sumb = invCov_sum, S = invCov_sum - info(line m, r = 0)
+                for (int e = 0; e < CUT_FAST; ++e) fst[g][e] = nx[e];
 #pragma unroll
                 for (int e = 0; e < 21; ++e) {
-                    const double s0 = s21[e];
-                    s21[e] = s0 - nx[26 + e];
-                    sumb[g][e] = s0;
-                    sum[g][e] = s21[e];
+                    s21[e] = s21[e] - nx[CUT_FAST + e];
+                    sumA[g][e] = s21[e];
                 }
-                CUT_PROF(6);
                 put_chol(s21);
-                CUT_PROF(7);
                 if (m + 1 < nls) pf_issue(m + 1);
-                CUT_PROF(8);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 21; ++e) sum[g][e] = s21[e];
             }
         }
         wave_lds_sync();
@@ -622,9 +710,8 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     }
 #ifdef GFPL_CUT_PROF
     if (lane == 0 && (blockIdx.x % 256) == 0)
-        printf("cutprof blk %d it %llu A %llu B %llu X %llu END %llu mv %llu asm %llu open %llu chol %llu pf %llu\n",
-               blockIdx.x, cp_it, cp_acc[0], cp_acc[1], cp_acc[2], cp_acc[3], cp_acc[4], cp_acc[5], cp_acc[6], cp_acc[7],
-               cp_acc[8]);
+        printf("cutprof blk %d it %llu A %llu B %llu X %llu FIN %llu\n", blockIdx.x, cp_it, cp_acc[0], cp_acc[1],
+               cp_acc[2], cp_acc[3]);
 #endif
 }
 

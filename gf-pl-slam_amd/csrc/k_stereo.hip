@@ -703,7 +703,11 @@ hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
+#ifdef GFPL_EXP_SP1024
+    if (true)
+#else
     if (p.kp_cap > 2048)
+#endif
         hipLaunchKernelGGL(k_stereo_points<1024>, dim3(p.B), dim3(1024), lds, s, p, KP2);
     else
         hipLaunchKernelGGL(k_stereo_points<512>, dim3(p.B), dim3(512), lds, s, p, KP2);
