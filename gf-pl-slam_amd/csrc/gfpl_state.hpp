@@ -72,11 +72,11 @@ struct DevTrack {
     int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
-#define CUT_FAST 20   // doubles of per-line fast cut data (k_cut.hip)
+#define CUT_FAST 21   // doubles of per-line fast cut data (k_cut.hip)
 
 struct DevScratch {
     double* cut_ls;   // [B*mls_cap*21] lower-triangle info of matched lines
-    double* cut_fast; // [B*mls_cap*CUT_FAST] per matched line: DT sP, DT eP, R covS R^T, R covE R^T, Jl
+    double* cut_fast; // [B*mls_cap*CUT_FAST] per matched line: DT sP, DT eP, R covS R^T, R covE R^T, Jl, list index of the next line
     int32_t* knn;     // [B*6*kcap] initial-frame knn results (idx0, d0, d1, ...)
     double* proj;     // [B*kcap*2] cross-points projections (aliases knn: init never overlaps)
     int64_t* bytes;   // [B] algorithmic bytes of the last step

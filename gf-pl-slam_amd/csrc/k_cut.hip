@@ -143,7 +143,8 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
 // point is (1-c) DT P0 + c DT P1, and getPoseInfoOnLine's variance
 // Jl^T Jp R cov R^T Jp^T Jl is u^T [(1-c)^2 R C0 R^T + c^2 R C1 R^T] u with
 // u = Jp^T Jl = (Jl0 f/z, Jl1 f/z, -f (Jl0 x + Jl1 y)/z^2).  Per line (CUT_FAST):
-// DT sP [3], DT eP [3], R covS R^T and R covE R^T (xx xy xz yy yz zz) [6+6], Jl [2].
+// DT sP [3], DT eP [3], R covS R^T and R covE R^T (xx xy xz yy yz zz) [6+6], Jl [2],
+// and (k_cut_prep) the list index of the line after it [1].
 __device__ __forceinline__ void cut_fast_data(const double* Dl, const LineCutData& d, double* fd) {
     se3_apply(Dl, d.sP, fd);
     se3_apply(Dl, d.eP, fd + 3);
@@ -232,6 +233,7 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];   // k_cut_search subtracts it
                 double fd[CUT_FAST];
                 cut_fast_data(Dl, d, fd);
+                fd[CUT_FAST - 1] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
 #pragma unroll
                 for (int i = 0; i < CUT_FAST; ++i) fast_l[(size_t)m * CUT_FAST + i] = fd[i];
             } else {
@@ -434,7 +436,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     __shared__ double chol[CUT_G][CUT_CH];
     __shared__ double epf[CUT_G][CUT_EP];
     __shared__ double fst[CUT_G][21];    // fast data of the current line
-    __shared__ double nxt[CUT_G][43];    // prefetched next line: fast data (20) | r = 0 info (21)
+    __shared__ double nxt[CUT_G][43];    // prefetched next line: fast data (21) | r = 0 info (21)
     __shared__ double xs[CUT_G][25];     // exact step: exact S of the line / flush endpoints
     __shared__ double dtl[CUT_G][13];    // DT_inv rows 0-2
     const int lane = threadIdx.x;
@@ -477,11 +479,12 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #pragma unroll
         for (int e = 0; e < 28; ++e) chol[g][e] = o[e];
     };
-    // Next-line prefetch: lane j loads elements j, j+8, ... of the 41-element vector
-    // [fast data | r = 0 info] of the group's next line right after a line opens;
-    // the values land in LDS one iteration later.  mls indices run one line ahead.
+    // Next-line prefetch: lane j loads elements j, j+8, ... of the 42-element vector
+    // [fast data (its last entry: the list index of the line after it) | r = 0 info]
+    // of the group's next line right after a line opens; the values land in LDS one
+    // iteration later.  Every load is a plain f64 load whose value reaches its use
+    // through LDS, so nothing waits for it before that store.
     size_t q_cur = 0, q_nx = 0;
-    int ix_n2 = 0;
     double pf[6];
     int pending = 0;
     auto pf_issue = [&](int mm) {
@@ -489,14 +492,13 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         for (int k = 0; k < 6; ++k) {
             const int e = j + 8 * k;
             pf[k] = e < CUT_FAST ? fast_l[(size_t)mm * CUT_FAST + e]
-                                 : scr_l[(size_t)mm * 21 + (size_t)(e < 41 ? e - CUT_FAST : 0)];
+                                 : scr_l[(size_t)mm * 21 + (size_t)(e < 42 ? e - CUT_FAST : 0)];
         }
         pending = 1;
     };
     if (m < nls) {
         q_cur = lb + mls[0];
         if (nls > 1) q_nx = lb + mls[1];
-        if (nls > 2) ix_n2 = mls[2];
         for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = fast_l[e];
         double s21[21];
 #pragma unroll
@@ -513,7 +515,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     }
     __syncthreads();
 #ifdef GFPL_CUT_PROF
-    unsigned long long cp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0;
+    unsigned long long cp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0, cp_fin = 0;
 #define CUT_PROF(k) { const unsigned long long _t = clock64(); cp_acc[k] += _t - cp_last; cp_last = _t; }
 #else
 #define CUT_PROF(k)
@@ -546,7 +548,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         if (pending) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
-                if (j + 8 * k < 41) nxt[g][j + 8 * k] = pf[k];
+                if (j + 8 * k < 42) nxt[g][j + 8 * k] = pf[k];
             pending = 0;
         }
         wave_lds_sync();
@@ -671,10 +673,12 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                                   r1, E7);
             }
             double info[21];
+            CUT_PROF(4);
             cut_assemble<false>(S7, E7, info);
             double s21[21];
 #pragma unroll
             for (int e = 0; e < 21; ++e) s21[e] = sumA[g][e] + info[e];
+            CUT_PROF(5);
             if (j == 0) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
@@ -682,26 +686,30 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             ++m;
             if (m < nls) {
                 q_cur = q_nx;
-                q_nx = lb + ix_n2;
-                if (m + 2 < nls) ix_n2 = mls[m + 2];
+                q_nx = lb + (size_t)(int)nxt[g][CUT_FAST - 1];
                 first = 1;
                 r0 = 0.0;
                 r1 = 0.0;
                 // line m from the prefetch buffer
-                double nx[41];
+                double nx[42];
 #pragma unroll
-                for (int e = 0; e < 41; ++e) nx[e] = nxt[g][e];
+                for (int e = 0; e < 42; ++e) nx[e] = nxt[g][e];
+#pragma unroll
+                for (int e = 0; e < 21; ++e) s21[e] = s21[e] - nx[CUT_FAST + e];
 #pragma unroll
                 for (int e = 0; e < CUT_FAST; ++e) fst[g][e] = nx[e];
 #pragma unroll
-                for (int e = 0; e < 21; ++e) {
-                    s21[e] = s21[e] - nx[CUT_FAST + e];
-                    sumA[g][e] = s21[e];
-                }
+                for (int e = 0; e < 21; ++e) sumA[g][e] = s21[e];
+                CUT_PROF(6);
                 put_chol(s21);
+                CUT_PROF(7);
                 if (m + 1 < nls) pf_issue(m + 1);
             }
         }
+#ifdef GFPL_CUT_PROF
+        if (__any(act && finalize)) ++cp_fin;
+#endif
+        CUT_PROF(8);
         wave_lds_sync();
         CUT_PROF(3);
 #ifdef GFPL_CUT_PROF
@@ -710,8 +718,9 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     }
 #ifdef GFPL_CUT_PROF
     if (lane == 0 && (blockIdx.x % 256) == 0)
-        printf("cutprof blk %d it %llu A %llu B %llu X %llu FIN %llu\n", blockIdx.x, cp_it, cp_acc[0], cp_acc[1],
-               cp_acc[2], cp_acc[3]);
+        printf("cutprof blk %d it %llu fin %llu A %llu B %llu X %llu pre %llu asm %llu nxt %llu chol %llu post %llu sync %llu\n",
+               blockIdx.x, cp_it, cp_fin, cp_acc[0], cp_acc[1], cp_acc[2], cp_acc[4], cp_acc[5], cp_acc[6], cp_acc[7],
+               cp_acc[8], cp_acc[3]);
 #endif
 }
 

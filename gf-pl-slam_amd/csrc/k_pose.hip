@@ -32,19 +32,21 @@ struct PoseLDS {
 };
 
 #define PT_K 6    // X Y Z ox oy sigma2
-// chunk rows are 65 doubles apart: the reduction lanes read rows ia, ib of the
-// same column k, and a 64-double stride would put every row in the same LDS bank
-#define CH_STRIDE 65
+// chunk rows are 66 doubles (528 B) apart: the reduction lanes read rows ia, ib
+// of the same columns k, k + 1 as 16-B pairs, and a 64-double stride would put
+// every row in the same LDS bank
+#define CH_STRIDE 66
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
-// evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w
+// evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w;
+// in = X Y Z ox oy sigma2 (registers)
 __device__ __forceinline__ void eval_point(const DevCam& cam, double homog, const double* DT, const double* in,
-                                           size_t stride, double* o) {
-    const double Pp[3] = {in[0], in[stride], in[2 * stride]};
+                                           double* o) {
+    const double Pp[3] = {in[0], in[1], in[2]};
     double Pc[3], uv[2];
     se3_apply(DT, Pp, Pc);
     projection(cam, Pc, uv);
-    const double ex = uv[0] - in[3 * stride], ey = uv[1] - in[4 * stride];
+    const double ex = uv[0] - in[3], ey = uv[1] - in[4];
     const double n = sqrt(ex * ex + ey * ey);
     double J[6];
     poseJac(cam, homog, Pc, ex, ey, J);
@@ -52,20 +54,21 @@ __device__ __forceinline__ void eval_point(const DevCam& cam, double homog, cons
 #pragma unroll
     for (int i = 0; i < 6; ++i) o[i] = J[i] / m;
     o[6] = n;
-    o[7] = 1.0 / (1.0 + (n * n) * in[5 * stride]);
+    o[7] = 1.0 / (1.0 + (n * n) * in[5]);
 }
 
-// evaluate one line row (src/stereoFrameHandler.cpp:2175-2235)
+// evaluate one line row (src/stereoFrameHandler.cpp:2175-2235);
+// in = sX sY sZ eX eY eZ l0 l1 l2 sigma2 (registers)
 __device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const double* DT, const double* in,
-                                          size_t stride, double* o) {
-    const double sP[3] = {in[0], in[stride], in[2 * stride]};
-    const double eP[3] = {in[3 * stride], in[4 * stride], in[5 * stride]};
+                                          double* o) {
+    const double sP[3] = {in[0], in[1], in[2]};
+    const double eP[3] = {in[3], in[4], in[5]};
     double sc[3], ec[3], su[2], eu[2];
     se3_apply(DT, sP, sc);
     projection(cam, sc, su);
     se3_apply(DT, eP, ec);
     projection(cam, ec, eu);
-    const double l0 = in[6 * stride], l1 = in[7 * stride], l2 = in[8 * stride];
+    const double l0 = in[6], l1 = in[7], l2 = in[8];
     const double ds = (l0 * su[0] + l1 * su[1]) + l2;
     const double de = (l0 * eu[0] + l1 * eu[1]) + l2;
     const double n = sqrt(ds * ds + de * de);
@@ -76,7 +79,7 @@ __device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const
 #pragma unroll
     for (int i = 0; i < 6; ++i) o[i] = (Js[i] * ds + Je[i] * de) / m;
     o[6] = n;
-    o[7] = 1.0 / (1.0 + (n * n) * in[9 * stride]);
+    o[7] = 1.0 / (1.0 + (n * n) * in[9]);
 }
 
 struct PoseCtx {
@@ -110,29 +113,49 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
 #pragma unroll
         for (int i = 0; i < 16; ++i) DT[i] = S.DT[i];
         double s = 0.0;
+        // raw inputs of chunk c + 1 are loaded into registers while chunk c is
+        // reduced, so the SoA scratch latency hides behind the LDS reduction
+        double pv[PT_K], lv[LS_K];
+        auto load_chunk = [&](int c) {
+            const int f = (c << 6) + lane;
+            const int fp = min(f, max(X.npt - 1, 0)), fl = min(f, max(X.nls - 1, 0));
+#pragma unroll
+            for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
+#pragma unroll
+            for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
+        };
+        load_chunk(0);
         for (int c = 0; c < nch; ++c) {
             const int f = (c << 6) + lane;
             double o[8];
-            if (f < X.npt && actp[f]) eval_point(cam, homog, DT, X.pin + f, X.mpt_cap, o);
+            if (f < X.npt && actp[f]) eval_point(cam, homog, DT, pv, o);
             else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cp[i * CH_STRIDE + lane] = o[i];
-            if (f < X.nls && actl[f]) eval_line(cam, homog, DT, X.lin + f, X.mls_cap, o);
+            if (f < X.nls && actl[f]) eval_line(cam, homog, DT, lv, o);
             else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
+            if (c + 1 < nch) load_chunk(c + 1);
             __syncthreads();
             const double* A = buf + ia * CH_STRIDE;
             const double* Bv = buf + ib * CH_STRIDE;
             const double* W = buf + 7 * CH_STRIDE;
-#pragma unroll 16
-            for (int k = 0; k < 64; ++k) s = s + (A[k] * Bv[k]) * W[k];
+            const double2* A2 = reinterpret_cast<const double2*>(A);
+            const double2* B2 = reinterpret_cast<const double2*>(Bv);
+            const double2* W2 = reinterpret_cast<const double2*>(W);
+#pragma unroll 8
+            for (int k = 0; k < 32; ++k) {
+                const double2 a = A2[k], bb = B2[k], w = W2[k];
+                s = s + (a.x * bb.x) * w.x;
+                s = s + (a.y * bb.y) * w.y;
+            }
             __syncthreads();
         }
         S.part[lane] = s;

@@ -202,8 +202,14 @@ __global__ void __launch_bounds__(BLOCK) k_stereo_points(KParams p, int KP2) {
         }
         if (i < N) {
             const float y = KL[i].y;
+#ifdef GFPL_EXP_LVL_ORDER
+            const int row = (y >= 0.0f && y < 8190.0f) ? (int)y + 1 : 0;
+            const int lv = clamp_level(KL[i].octave, p.cam.n_levels);
+            order[i] = ((uint32_t)((lv << 13) | row) << 16) | (uint32_t)i;
+#else
             const int row = (y >= 0.0f && y < 65534.0f) ? (int)y + 1 : 0;
             order[i] = ((uint32_t)row << 16) | (uint32_t)i;
+#endif
         } else {
             order[i] = 0xFFFFFFFFu;
         }
