@@ -205,6 +205,8 @@ int gfpl_set_camera(gfpl_ctx* c, const gfpl_camera* cam) {
     int64_t need = 0;
     for (int i = 0; i < cam->n_levels; ++i) {
         if (cam->lvl_cols[i] < 1 || cam->lvl_rows[i] < 1 || cam->lvl_offset[i] < 0) return GFPL_E_INVALID;
+        // k_stereo_points packs window rows / columns into 11-bit fields
+        if (cam->lvl_cols[i] > GFPL_MAX_IMAGE_DIM || cam->lvl_rows[i] > GFPL_MAX_IMAGE_DIM) return GFPL_E_INVALID;
         need = std::max<int64_t>(need, cam->lvl_offset[i] + (int64_t)cam->lvl_cols[i] * cam->lvl_rows[i]);
     }
     if (cam->pyr_bytes < need + GFPL_PYR_TAIL) return GFPL_E_INVALID;   // window loads read past the last row

@@ -239,7 +239,10 @@ __device__ __forceinline__ int wave_sum(int v) {
 }
 
 // dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | rp[mpt_cap] rl[mls_cap]} f64 | buf[NP2] f64 | act[mpt+mls] u8
-__global__ void __launch_bounds__(64) k_pose(KParams p, int NP2) {
+#ifndef GFPL_POSE_WAVES
+#define GFPL_POSE_WAVES 2
+#endif
+__global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ PoseLDS S;
     const int b = blockIdx.x;

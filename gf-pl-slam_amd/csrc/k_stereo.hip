@@ -56,13 +56,21 @@ __device__ __forceinline__ int clamp_level(int o, int n) { return o < 0 ? 0 : (o
 // subPixelStereoRefine_ORBSLAM (src/stereoFrame.cpp:340-404); ledger Q1: both
 // patches come from the RIGHT pyramid.  SAD of integer-valued pixels is exact,
 // so int accumulation equals cv::norm(NORM_L1).  U8: out-of-image windows reject.
-__device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, const gfpl_keypoint& kpR,
-                         float& disparity, float& bestuR) {
-    disparity = -1;
-    bestuR = kpR.x;
-#ifdef GFPL_EXP_NO_SAD
-    return;
-#endif
+//
+// Four lanes (a DPP quad) refine one keypoint: lane q sums the 11 shifted SADs
+// of window rows q, q+4, q+8 and the quad adds its partial sums (integers: the
+// order is immaterial).  A workgroup pass therefore has only BLOCK/4 keypoints
+// in flight, consecutive in row order, so its window rows stay in L1/L2 across
+// neighbouring keypoints instead of being re-fetched from HBM per keypoint.
+struct SadJob {
+    const uint8_t* img;
+    int cols, o, vL, uL, uR;
+    float scaleduR0;
+};
+
+// window validity (src/stereoFrame.cpp:351-365); false = disparity -1
+__device__ __forceinline__ bool sad_setup(const KParams& p, int b, const gfpl_keypoint& kpL, const gfpl_keypoint& kpR,
+                                          SadJob& J) {
     const float uR0 = kpR.x;
     const int o = clamp_level(kpL.octave, p.cam.n_levels);
     const float sf = p.cam.inv_scale[o];
@@ -72,71 +80,96 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
     const int cols = p.cam.lvl_cols[o], rows = p.cam.lvl_rows[o];
     const float iniu = scaleduR0 + 5 - 5;
     const float endu = scaleduR0 + 5 + 5 + 1;
-    if (iniu < 0 || endu >= cols) return;
+    if (iniu < 0 || endu >= cols) return false;
     const int vL = (int)scaledvL, uL = (int)scaleduL, uR = (int)scaleduR0;
-    if (vL - 5 < 0 || vL + 5 >= rows || uL - 5 < 0 || uL + 5 >= cols || uR - 10 < 0 || uR + 10 >= cols) return;
-    const uint8_t* img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[o];
-    // Each window row is read as aligned dwords and re-aligned with v_alignbyte:
-    // 4 loads for the 11-byte IL row and 6 for the 21-byte IR row instead of 32
-    // byte loads (the camera's pyramid tail keeps the last dword in bounds).
-    const size_t aL = (size_t)(uL - 5), aR = (size_t)(uR - 10);
-    auto load_row = [&](int y, uint32_t* il4, uint32_t* ir6) {
-        const uint8_t* rowp = img + (size_t)y * cols;
-        const uintptr_t pl = (uintptr_t)(rowp + aL), pr = (uintptr_t)(rowp + aR);
-        const uint32_t* wl = reinterpret_cast<const uint32_t*>(pl & ~(uintptr_t)3);
-        const uint32_t* wr = reinterpret_cast<const uint32_t*>(pr & ~(uintptr_t)3);
-        const uint32_t shl = (uint32_t)(pl & 3u), shr = (uint32_t)(pr & 3u);
-        uint32_t a[4], c[6];
+    if (vL - 5 < 0 || vL + 5 >= rows || uL - 5 < 0 || uL + 5 >= cols || uR - 10 < 0 || uR + 10 >= cols) return false;
+    J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[o];
+    J.cols = cols; J.o = o; J.vL = vL; J.uL = uL; J.uR = uR; J.scaleduR0 = scaleduR0;
+    return true;
+}
+
+// Each window row is read as aligned dwords and re-aligned with v_alignbyte:
+// 4 loads for the 11-byte IL row and 6 for the 21-byte IR row instead of 32
+// byte loads (the camera's pyramid tail keeps the last dword in bounds).
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ void sad_load_row(const SadJob& J, int y, uint32_t* il4, uint32_t* ir6) {
+    const uint8_t* rowp = J.img + (size_t)y * J.cols;
+    const uintptr_t pl = (uintptr_t)(rowp + (J.uL - 5)), pr = (uintptr_t)(rowp + (J.uR - 10));
+    const uint32_t* wl = reinterpret_cast<const uint32_t*>(pl & ~(uintptr_t)3);
+    const uint32_t* wr = reinterpret_cast<const uint32_t*>(pr & ~(uintptr_t)3);
+    const uint32_t shl = (uint32_t)(pl & 3u), shr = (uint32_t)(pr & 3u);
+    // dword-aligned 16-B / 8-B vector loads (one load instruction per 4 / 2 dwords)
+    const u32x4a4 a = *reinterpret_cast<const u32x4a4*>(wl);
+    const u32x4a4 c0 = *reinterpret_cast<const u32x4a4*>(wr);
+    const u32x2a4 c1 = *reinterpret_cast<const u32x2a4*>(wr + 4);
+    const uint32_t c[6] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y};
+    il4[0] = __builtin_amdgcn_alignbyte(a.y, a.x, shl);
+    il4[1] = __builtin_amdgcn_alignbyte(a.z, a.y, shl);
+    il4[2] = __builtin_amdgcn_alignbyte(a.w, a.z, shl);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = wl[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) c[i] = wr[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) il4[i] = __builtin_amdgcn_alignbyte(a[i + 1], a[i], shl);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) ir6[i] = __builtin_amdgcn_alignbyte(c[i + 1], c[i], shr);
-        ir6[5] = __builtin_amdgcn_alignbyte(c[5], c[5], shr);
-    };
-    auto byte_at = [](const uint32_t* w, int k) -> int { return (int)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu); };
-    int cL, cR[11];
+    for (int i = 0; i < 5; ++i) ir6[i] = __builtin_amdgcn_alignbyte(c[i + 1], c[i], shr);
+    ir6[5] = __builtin_amdgcn_alignbyte(c[5], c[5], shr);
+}
+
+__device__ __forceinline__ int byte_at(const uint32_t* w, int k) { return (int)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu); }
+
+// partial SADs of the window rows q, q+4, q+8 (q = lane within the quad; lane 3
+// has no third row: it re-reads the centre row and drops that row's sums).  All
+// four rows are loaded before any SAD so their latencies overlap.
+__device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) {
+    uint32_t cRR[11];   // centre pixels of the 11 shifted right windows, in both 16-bit halves
+    int cL;
     {
         uint32_t il4[3], ir6[6];
-        load_row(vL, il4, ir6);
+        sad_load_row(J, J.vL, il4, ir6);
         cL = byte_at(il4, 5);
 #pragma unroll
-        for (int i = 0; i < 11; ++i) cR[i] = byte_at(ir6, 5 + i);
+        for (int i = 0; i < 11; ++i) cRR[i] = (uint32_t)byte_at(ir6, 5 + i) * 0x10001u;
     }
+#ifndef GFPL_SAD_SERIAL
+    uint32_t il4[3][3], ir6[3][6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int r = q + 4 * i;
+        sad_load_row(J, J.vL - 5 + (r < 11 ? r : 5), il4[i], ir6[i]);
+    }
+#endif
     // SAD = sum |(IL - cL) - (IR_s - cR[s])| = sum |(IL + cR[s]) - (IR_s + cL)|, both
     // sides <= 510: two columns per v_sad_u16 (16-bit lanes of one register)
-    uint32_t cRR[11];
-#pragma unroll
-    for (int i = 0; i < 11; ++i) cRR[i] = (uint32_t)cR[i] * 0x10001u;
     const uint32_t cLL = (uint32_t)cL * 0x10001u;
-    uint32_t acc[11];
 #pragma unroll
-    for (int i = 0; i < 11; ++i) acc[i] = 0;
-    for (int r = 0; r < 11; ++r) {
-        uint32_t il4[3], ir6[6];
-        load_row(vL - 5 + r, il4, ir6);
-        uint32_t ILp[5], IRe[10], IRo[10];
+    for (int i = 0; i < 3; ++i) {
+        if (q + 4 * i >= 11) break;
+#ifdef GFPL_SAD_SERIAL
+        uint32_t L[3], R[6];
+        sad_load_row(J, J.vL - 5 + q + 4 * i, L, R);
+#else
+        const uint32_t* L = il4[i];
+        const uint32_t* R = ir6[i];
+#endif
+        uint32_t ILp[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) ILp[k] = (uint32_t)byte_at(il4, 2 * k) | ((uint32_t)byte_at(il4, 2 * k + 1) << 16);
-        const int il10 = byte_at(il4, 10);
-#pragma unroll
-        for (int m = 0; m < 10; ++m) {
-            IRe[m] = ((uint32_t)byte_at(ir6, 2 * m) | ((uint32_t)byte_at(ir6, 2 * m + 1) << 16)) + cLL;
-            IRo[m] = ((uint32_t)byte_at(ir6, 2 * m + 1) | ((uint32_t)byte_at(ir6, 2 * m + 2) << 16)) + cLL;
-        }
+        for (int k = 0; k < 5; ++k) ILp[k] = (uint32_t)byte_at(L, 2 * k) | ((uint32_t)byte_at(L, 2 * k + 1) << 16);
+        const int il10 = byte_at(L, 10);
 #pragma unroll
         for (int s = 0; s < 11; ++s) {
             uint32_t a = acc[s];
 #pragma unroll
-            for (int k = 0; k < 5; ++k)
-                a = __builtin_amdgcn_sad_u16(ILp[k] + cRR[s], (s & 1) ? IRo[k + (s >> 1)] : IRe[k + (s >> 1)], a);
-            a += (uint32_t)abs((il10 + cR[s]) - (byte_at(ir6, 10 + s) + cL));
+            for (int k = 0; k < 5; ++k) {
+                const int c = s + 2 * k;   // right window column pair (c, c + 1)
+                const uint32_t ir = ((uint32_t)byte_at(R, c) | ((uint32_t)byte_at(R, c + 1) << 16)) + cLL;
+                a = __builtin_amdgcn_sad_u16(ILp[k] + cRR[s], ir, a);
+            }
+            a += (uint32_t)abs((il10 + (int)(cRR[s] & 0xFFFFu)) - (byte_at(R, 10 + s) + cL));
             acc[s] = a;
         }
     }
+}
+
+// best shift, parabola fit, disparity (src/stereoFrame.cpp:384-403)
+__device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, float xL,
+                                           const uint32_t* acc, float& disparity, float& bestuR) {
     int bestDist = 2147483647;
     int bestinc = 0;
     float vD[11];
@@ -152,11 +185,14 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
     const float dist3 = vD[5 + bestinc + 1];
     const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
     if (deltaR < -1 || deltaR > 1) return;
-    bestuR = p.cam.scale[o] * ((float)scaleduR0 + (float)bestinc + deltaR);
-    disparity = (kpL.x - bestuR);
+    bestuR = p.cam.scale[J.o] * ((float)J.scaleduR0 + (float)bestinc + deltaR);
+    disparity = (xL - bestuR);
 }
 
 // ------------------------------------------------------- stereo points --
+#ifndef GFPL_SP_WAVES
+#define GFPL_SP_WAVES 8   // waves per SIMD (4 workgroups / CU; measured faster than 6 despite a 28-B spill)
+#endif
 // dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | recx[KP2] f32 |
 //              recm[KP2] u16 | rowlo[nRows] u16 | misc[64] i32
 // Right keypoints are sorted by their row band start (the reference's
@@ -167,7 +203,7 @@ __device__ void subpixel(const KParams& p, int b, const gfpl_keypoint& kpL, cons
 // same descriptors and overlapping SAD window rows.  Results are keyed by iL: the
 // processing order has no effect on the output.
 template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_stereo_points(KParams p, int KP2) {
+__global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;
@@ -240,10 +276,12 @@ __global__ void __launch_bounds__(BLOCK) k_stereo_points(KParams p, int KP2) {
     const float minD = 0;
     const float maxD = (float)p.cam.fx;
     const float mbf = (float)(p.cam.fx * p.cam.b);
-    // per left keypoint: band search + Hamming + sub-pixel (src/stereoFrame.cpp:502-583)
+    // per left keypoint: band search + Hamming (src/stereoFrame.cpp:502-545).  A match
+    // leaves (bestDist, bestIdxR) in pairs[iL] and iL in order[t] for the sub-pixel pass;
+    // order[t] / pairs[iL] are private to the thread that owns slot t.
     for (int t = tid; t < N; t += blockDim.x) {
         const int iL = (int)(order[t] & 0xFFFFu);
-        uint32_t key = 0xFFFFFFFFu;
+        uint32_t job = 0xFFFFFFFFu;
         {
             const gfpl_keypoint kpL = KL[iL];
             const int levelL = kpL.octave;
@@ -280,17 +318,63 @@ __global__ void __launch_bounds__(BLOCK) k_stereo_points(KParams p, int KP2) {
                 }
                 if (bestDist < 80) {
                     atomicAdd(&misc[2], 1);
-                    float disparity, bestuR;
-                    subpixel(p, b, kpL, KR[bestIdxR], disparity, bestuR);
-                    if (disparity >= minD && disparity < maxD) {
-                        if (disparity <= 0) { disparity = 0.01f; bestuR = (float)((double)uL - 0.01); }
-                        depth[iL] = mbf / disparity;
-                        key = ((uint32_t)bestDist << 16) | (uint32_t)iL;
+                    SadJob J;
+                    // job: iL | uL << 16 (order[t]); bestDist | o << 7 | vL << 10 | uR << 21
+                    // (pairs[iL]); failed window checks keep only bestDist (disparity -1)
+                    if (sad_setup(p, b, kpL, KR[bestIdxR], J)) {
+                        pairs[iL] = (uint32_t)bestDist | ((uint32_t)J.o << 7) | ((uint32_t)J.vL << 10) |
+                                    ((uint32_t)J.uR << 21);
+                        job = (uint32_t)iL | ((uint32_t)J.uL << 16);
                     }
                 }
             }
         }
-        pairs[iL] = key;
+        order[t] = job;
+    }
+    __syncthreads();
+    // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
+    // per matched keypoint, BLOCK/4 consecutive (row-ordered) keypoints per pass
+    for (int base = 0; base < N; base += BLOCK / 4) {
+        const int t = base + (tid >> 2), q = tid & 3;
+        const uint32_t job = (t < N) ? order[t] : 0xFFFFFFFFu;
+        uint32_t acc[11];
+#pragma unroll
+        for (int s = 0; s < 11; ++s) acc[s] = 0;
+        SadJob J;
+        float xL = 0.0f;
+        uint32_t pr = 0;
+        if (job != 0xFFFFFFFFu) {
+            const int iL = (int)(job & 0xFFFFu);
+            xL = KL[iL].x;
+            pr = pairs[iL];
+            J.o = (int)((pr >> 7) & 7u);
+            J.vL = (int)((pr >> 10) & 0x7FFu);
+            J.uR = (int)(pr >> 21);
+            J.uL = (int)(job >> 16);
+            J.cols = p.cam.lvl_cols[J.o];
+            J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[J.o];
+            J.scaleduR0 = (float)J.uR;
+            sad_rows(J, q, acc);
+        }
+#pragma unroll
+        for (int s = 0; s < 11; ++s) {
+            uint32_t v = acc[s];
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad xor 1
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad xor 2
+            acc[s] = v;
+        }
+        if (job != 0xFFFFFFFFu && q == 0) {
+            const int iL = (int)(job & 0xFFFFu);
+            float disparity = -1, bestuR;
+            sad_finish(p, J, xL, acc, disparity, bestuR);
+            uint32_t key = 0xFFFFFFFFu;
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) { disparity = 0.01f; bestuR = (float)((double)xL - 0.01); }
+                depth[iL] = mbf / disparity;
+                key = ((pr & 0x7Fu) << 16) | (uint32_t)iL;
+            }
+            pairs[iL] = key;
+        }
     }
     __syncthreads();
     // sort(vDistIdx) (src/stereoFrame.cpp:585)

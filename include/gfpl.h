@@ -35,6 +35,7 @@ extern "C" {
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
+#define GFPL_MAX_IMAGE_DIM 2047     /* pyramid level width / height limit        */
 #define GFPL_MAX_MATCHED_PT 2048    /* capacity of matched_pt (cap from config)   */
 #define GFPL_MAX_MATCHED_LS 1024    /* capacity of matched_ls (cap from config)   */
 #define GFPL_PYR_TAIL 64            /* slack after each packed pyramid (bytes)    */
