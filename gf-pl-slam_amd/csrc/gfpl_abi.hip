@@ -496,6 +496,71 @@ int gfpl_knn2_hamming(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, i
     return GFPL_OK;
 }
 
+// MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:199-470):
+// per kind two knn-2 launches (the MFMA k_knn2m of gfpl_knn2_hamming) and one gate
+// launch (k_kf.hip); keyframe rate, so the scratch is allocated per call.
+int gfpl_kf_common_matches(gfpl_ctx* c, const gfpl_kf_view* k0, const gfpl_kf_view* k1, int32_t* pt_pairs,
+                           int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs) {
+    if (!c || !k0 || !k1 || !n_pt_pairs || !n_ls_pairs || !c->has_cam) return GFPL_E_INVALID;
+    if (k0->n_pt < 0 || k1->n_pt < 0 || k0->n_ls < 0 || k1->n_ls < 0) return GFPL_E_INVALID;
+    *n_pt_pairs = 0;
+    *n_ls_pairs = 0;
+    const bool do_pt = k0->n_pt >= 2 && k1->n_pt >= 2;   // ledger U4
+    const bool do_ls = k0->n_ls >= 2 && k1->n_ls >= 2;
+    if (do_pt && (!pt_pairs || !k0->pdesc || !k1->pdesc || !k0->P || !k0->pt_sigma2 || !k1->pl))
+        return GFPL_E_INVALID;
+    if (do_ls && (!ls_pairs || !k0->ldesc || !k1->ldesc || !k0->sP || !k0->eP || !k0->le || !k0->ls_sigma2))
+        return GFPL_E_INVALID;
+    if (!do_pt && !do_ls) return GFPL_OK;
+    const size_t npt = do_pt ? (size_t)k0->n_pt + k1->n_pt : 0, nls = do_ls ? (size_t)k0->n_ls + k1->n_ls : 0;
+    const size_t bytes = 2 * (npt + nls) * (sizeof(int32_t) + sizeof(float)) + 64;
+    char* scr = nullptr;
+    HIPCHK(hipMalloc(&scr, bytes));
+    int32_t* idx = reinterpret_cast<int32_t*>(scr);
+    float* dist = reinterpret_cast<float*>(idx + 2 * (npt + nls));
+    int* cnt = reinterpret_cast<int*>(dist + 2 * (npt + nls));
+    hipError_t e = hipSuccess;
+    gfpl::KfGate g;
+    std::memset(&g, 0, sizeof g);
+    g.cam = devcam(c->cam);
+    for (int i = 0; i < 16; ++i) { g.T0[i] = k0->T_kf_w[i]; g.T1[i] = k1->T_kf_w[i]; }
+    g.max_ratio_12_p = c->cfg.max_ratio_12_p;
+    g.desc_th_l = c->cfg.desc_th_l;
+    int counts[2] = {0, 0};
+    size_t o = 0;
+    for (int kind = 0; kind < 2 && e == hipSuccess; ++kind) {
+        if (kind == 0 ? !do_pt : !do_ls) continue;
+        const int n0 = kind == 0 ? k0->n_pt : k0->n_ls, n1 = kind == 0 ? k1->n_pt : k1->n_ls;
+        const uint8_t* d0 = kind == 0 ? k0->pdesc : k0->ldesc;
+        const uint8_t* d1 = kind == 0 ? k1->pdesc : k1->ldesc;
+        int32_t* i12 = idx + 2 * o;
+        float* f12 = dist + 2 * o;
+        int32_t* i21 = i12 + 2 * n0;
+        float* f21 = f12 + 2 * n0;
+        o += (size_t)n0 + n1;
+        e = launch_knn2(d0, n0, d1, n1, 1, i12, f12, c->stream);   // NORM_HAMMING (:213 / :343)
+        if (e == hipSuccess) e = launch_knn2(d1, n1, d0, n0, 1, i21, f21, c->stream);
+        g.lines = kind;
+        g.n0 = n0;
+        g.i12 = i12; g.d12 = f12; g.i21 = i21;
+        g.P0 = kind == 0 ? k0->P : k0->sP;
+        g.eP0 = kind == 0 ? nullptr : k0->eP;
+        g.le0 = kind == 0 ? nullptr : k0->le;
+        g.sigma2_0 = kind == 0 ? k0->pt_sigma2 : k0->ls_sigma2;
+        g.pl1 = kind == 0 ? k1->pl : nullptr;
+        g.pairs = kind == 0 ? pt_pairs : ls_pairs;
+        g.count = cnt + kind;
+        if (e == hipSuccess) e = launch_kf_gate(g, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(counts + kind, cnt + kind, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipError_t ef = hipFree(scr);
+    if (e != hipSuccess || ef != hipSuccess) return GFPL_E_HIP;
+    *n_pt_pairs = counts[0];
+    *n_ls_pairs = counts[1];
+    return GFPL_OK;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------ transfer --

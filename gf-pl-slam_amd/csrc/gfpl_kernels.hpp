@@ -20,4 +20,23 @@ hipError_t launch_curr_frame_is_kf(const KParams& p, const int32_t* mask /* devi
 
 size_t stereo_lines_lds(int cap);
 
+// lookForCommonMatches keyframe-pair gate (k_kf.hip); all pointers device
+struct KfGate {
+    DevCam cam;
+    double T0[16], T1[16];
+    double max_ratio_12_p, desc_th_l;
+    int lines, n0;
+    const int32_t* i12;     // knn-2 kf0 -> kf1 [2 n0]
+    const float* d12;
+    const int32_t* i21;     // knn-2 kf1 -> kf0 [2 n1]
+    const double* P0;       // kf0 P (points) / sP (lines) [n0][3]
+    const double* eP0;      // kf0 eP [n0][3] (lines)
+    const double* le0;      // kf0 le [n0][3] (lines)
+    const double* sigma2_0; // kf0 sigma2 [n0]
+    const double* pl1;      // kf1 pl [n1][2] (points)
+    int32_t* pairs;         // [2 n0]
+    int* count;
+};
+hipError_t launch_kf_gate(const KfGate& g, hipStream_t s);
+
 }  // namespace gfpl

@@ -143,6 +143,38 @@ class KFState(C.Structure):
                 "need_new_kf": self.need_new_kf}
 
 
+class KFViewStruct(C.Structure):
+    """gfpl_kf_view: one keyframe's stereo features (KeyFrame::stereo_frame)."""
+    _fields_ = [("n_pt", C.c_int), ("pdesc", _vp), ("P", _vp), ("pl", _vp), ("pt_sigma2", _vp),
+                ("n_ls", C.c_int), ("ldesc", _vp), ("sP", _vp), ("eP", _vp), ("le", _vp), ("ls_sigma2", _vp),
+                ("T_kf_w", C.c_double * 16)]
+
+
+KF_PT = [("pdesc", "pdesc"), ("P", "pt_P"), ("pl", "pt_pl"), ("pt_sigma2", "pt_sigma2")]
+KF_LS = [("ldesc", "ldesc"), ("sP", "ls_sP"), ("eP", "ls_eP"), ("le", "ls_le"), ("ls_sigma2", "ls_sigma2")]
+
+
+class KeyFrameView:
+    """The arrays of one KeyFrame (src/keyFrame.cpp:26-58) that the keyframe
+    consumers read: stereo_pt / stereo_ls rows of a FrameHost and T_kf_w.
+    device=None keeps host arrays (oracle); otherwise they are copied to that
+    torch device once and stay resident."""
+
+    def __init__(self, fh: "FrameHost", T_kf_w, device=None):
+        self.s = KFViewStruct()
+        self.s.n_pt, self.s.n_ls = fh.n_pt, fh.n_ls
+        self.s.T_kf_w[:] = [float(x) for x in np.asarray(T_kf_w, np.float64).reshape(16)]
+        self.keep = {}
+        for cf, fn in KF_PT + KF_LS:
+            n = fh.n_pt if cf in dict(KF_PT) else fh.n_ls
+            a = np.ascontiguousarray(fh.arr[fn][:max(n, 1)])
+            if device is not None:
+                import torch
+                a = torch.from_numpy(a.copy()).to(device)
+            self.keep[cf] = a
+            setattr(self.s, cf, _ptr(a))
+
+
 class SynthParams(C.Structure):
     _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
                 ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
@@ -213,6 +245,7 @@ def hiplib() -> C.CDLL:
             "gfpl_cross_lines": ([P], C.c_int),
             "gfpl_line_cut": ([P], C.c_int),
             "gfpl_knn2_hamming": ([P, P, C.c_int, P, C.c_int, C.c_int, P, P], C.c_int),
+            "gfpl_kf_common_matches": ([P, P, P, P, P, P, P], C.c_int),
             "gfpl_read_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_write_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_read_track": ([P, C.c_int, P], C.c_int),
@@ -494,6 +527,21 @@ class Context:
     def knn2(self, q_dev, nq: int, t_dev, nt: int, cell: int, idx_dev, dist_dev) -> int:
         return self.L.gfpl_knn2_hamming(self.h, _ptr(q_dev), nq, _ptr(t_dev), nt, cell,
                                         _ptr(idx_dev), _ptr(dist_dev))
+
+    def lookForCommonMatches(self, kf0: KeyFrameView, kf1: KeyFrameView):
+        """MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:199-470):
+        the accepted (kf0 row, kf1 row) point and line pairs, in the order the reference's
+        loops visit them; the map bookkeeping stays with the caller."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        pp = torch.zeros(2 * max(kf0.s.n_pt, 1), dtype=torch.int32, device=dev)
+        lp = torch.zeros(2 * max(kf0.s.n_ls, 1), dtype=torch.int32, device=dev)
+        npt, nls = C.c_int(0), C.c_int(0)
+        torch.cuda.synchronize()
+        check(self.L.gfpl_kf_common_matches(self.h, C.byref(kf0.s), C.byref(kf1.s), _ptr(pp), C.byref(npt),
+                                            _ptr(lp), C.byref(nls)), "kf_common_matches")
+        return (pp[: 2 * npt.value].cpu().numpy().reshape(-1, 2),
+                lp[: 2 * nls.value].cpu().numpy().reshape(-1, 2))
 
     def close(self):
         if getattr(self, "h", None):

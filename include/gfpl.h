@@ -306,6 +306,46 @@ int  gfpl_line_cut(gfpl_seqbatch* sb);
 int  gfpl_knn2_hamming(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
                        int cell, int32_t* out_idx, float* out_dist);
 
+/* ------------------------------------------------- keyframe consumers ---- */
+/* One keyframe's stereo features as KeyFrame::stereo_frame exposes them
+ * (src/keyFrame.cpp:26-58, include/stereoFrame.h public members): row i of
+ * every point array is stereo_pt[i] and row i of pdesc its left descriptor
+ * (pdesc_l); likewise stereo_ls[i] / ldesc_l.  gfpl_kf_common_matches reads
+ * the arrays from DEVICE memory (e.g. a gfpl_frame_host uploaded by the
+ * caller, or a frame slot it copied out); T_kf_w is a host 4x4 row-major pose. */
+typedef struct gfpl_kf_view {
+    int            n_pt;
+    const uint8_t* pdesc;       /* [n_pt][32]                                  */
+    const double*  P;           /* [n_pt][3]  stereo_pt[i]->P                  */
+    const double*  pl;          /* [n_pt][2]  stereo_pt[i]->pl                 */
+    const double*  pt_sigma2;   /* [n_pt]     stereo_pt[i]->sigma2             */
+    int            n_ls;
+    const uint8_t* ldesc;       /* [n_ls][32]                                  */
+    const double*  sP;          /* [n_ls][3]                                   */
+    const double*  eP;          /* [n_ls][3]                                   */
+    const double*  le;          /* [n_ls][3]                                   */
+    const double*  ls_sigma2;   /* [n_ls]                                      */
+    double         T_kf_w[16];  /* KeyFrame::T_kf_w (host)                     */
+} gfpl_kf_view;
+
+/* MapHandler::lookForCommonMatches, keyframe-pair stage (src/mapHandler.cpp:
+ * 199-470, has_refinement = false as in the reference): DT = inverse_se3(kf1
+ * T_kf_w) * kf0 T_kf_w; points: knn-2 NORM_HAMMING kf0->kf1 and kf1->kf0,
+ * mutual best, d0/d1 <= max_ratio_12_p, |proj(DT P0) - pl1| * sqrt(sigma2_0) <
+ * sqrt(7.815); lines: knn-2 NORM_HAMMING both ways, mutual, d1 - d0 >
+ * lineDescriptorMAD(matches_12).nn12 * desc_th_l, |(le0 . proj(DT sP0),
+ * le0 . proj(DT eP0))| * sqrt(sigma2_0) < sqrt(7.815).  The accepted (kf0 row,
+ * kf1 row) pairs are written in kf0 row order to pt_pairs [2 * kf0->n_pt] and
+ * ls_pairs [2 * kf0->n_ls] (device) and their counts to *n_pt_pairs /
+ * *n_ls_pairs (host; the call synchronises).  The landmark bookkeeping that
+ * follows each accepted pair (MapPoint / MapLine creation, observations,
+ * full_graph) stays with the caller, which walks the pairs in the returned
+ * order exactly as the reference's loop does.  A kind with fewer than two rows
+ * on either keyframe yields no pairs (the reference reads a missing second
+ * neighbour: ledger U4).                                                      */
+int  gfpl_kf_common_matches(gfpl_ctx* ctx, const gfpl_kf_view* kf0, const gfpl_kf_view* kf1,
+                            int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs);
+
 /* ----------------------------------------------------- state transfer ----- */
 /* Copy one sequence's frame state device -> host (synchronises).            */
 int  gfpl_read_frame(gfpl_seqbatch* sb, int which, int seq, gfpl_frame_host* out);

@@ -1878,3 +1878,81 @@ int gfplo_inverse_se3(const double* T, double* out) { inverse_se3(T, out); retur
 extern "C" void gfplo_cut_stats(int64_t* out8) {
     for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
 }
+
+// ============================================== keyframe consumers ==
+// MapHandler::lookForCommonMatches, keyframe-pair stage (src/mapHandler.cpp:199-470).
+// has_refinement is false in the reference (:199), so the loop's only effect on
+// tracking state is the list of accepted (kf0, kf1) pairs in pmatches_12 order
+// (knnMatch output is already in query order; the sort by queryIdx at :241/:364
+// is the identity).  Points :207-338, lines :340-470.
+extern "C" int gfplo_kf_common_matches(const gfpl_camera* cam, const gfpl_config* cfg, const gfpl_kf_view* kf0,
+                                       const gfpl_kf_view* kf1, int32_t* pt_pairs, int* n_pt_pairs,
+                                       int32_t* ls_pairs, int* n_ls_pairs) {
+    if (!cam || !cfg || !kf0 || !kf1 || !n_pt_pairs || !n_ls_pairs) return GFPL_E_INVALID;
+    if (kf0->n_pt < 0 || kf1->n_pt < 0 || kf0->n_ls < 0 || kf1->n_ls < 0) return GFPL_E_INVALID;
+    *n_pt_pairs = 0;
+    *n_ls_pairs = 0;
+    // DT = inverse_se3(kf1->T_kf_w) * kf0->T_kf_w (:196)
+    double Ti[16], DT[16];
+    inverse_se3(kf1->T_kf_w, Ti);
+    mat4_mul(Ti, kf0->T_kf_w, DT);
+    auto proj = [&](const double* P, double* uv) {   // PinholeStereoCamera::projection
+        uv[0] = cam->cx + (cam->fx * P[0]) / P[2];
+        uv[1] = cam->cy + (cam->fy * P[1]) / P[2];
+    };
+    auto descs = [](const uint8_t* d, int n) {
+        std::vector<Desc> v(n);
+        for (int i = 0; i < n; ++i) std::memcpy(v[i].data(), d + 32 * i, 32);
+        return v;
+    };
+    const double chi = std::sqrt(7.815);
+    // points (:207-338); U4: the second neighbour must exist on both sides
+    if (kf0->n_pt >= 2 && kf1->n_pt >= 2) {
+        if (!pt_pairs || !kf0->pdesc || !kf1->pdesc) return GFPL_E_INVALID;
+        const std::vector<Desc> d0 = descs(kf0->pdesc, kf0->n_pt), d1 = descs(kf1->pdesc, kf1->n_pt);
+        const std::vector<Knn2> m12 = knn2(d0, d1, 1), m21 = knn2(d1, d0, 1);
+        int n = 0;
+        for (size_t i = 0; i < m12.size(); ++i) {
+            const int q = m12[i][0].queryIdx, t = m12[i][0].trainIdx;
+            const int rl = m21[t][0].trainIdx;
+            const double dist_12 = (double)(m12[i][0].distance / m12[i][1].distance);   // float / float
+            if (q == rl && dist_12 <= cfg->max_ratio_12_p) {
+                double Pc[3], uv[2];
+                se3_apply(DT, kf0->P + 3 * q, Pc);
+                proj(Pc, uv);
+                const double ex = uv[0] - kf1->pl[2 * t], ey = uv[1] - kf1->pl[2 * t + 1];
+                const double err = std::sqrt(ex * ex + ey * ey) * std::sqrt(kf0->pt_sigma2[q]);
+                if (err < chi) { pt_pairs[2 * n] = q; pt_pairs[2 * n + 1] = t; ++n; }
+            }
+        }
+        *n_pt_pairs = n;
+    }
+    // lines (:340-470)
+    if (kf0->n_ls >= 2 && kf1->n_ls >= 2) {
+        if (!ls_pairs || !kf0->ldesc || !kf1->ldesc) return GFPL_E_INVALID;
+        const std::vector<Desc> d0 = descs(kf0->ldesc, kf0->n_ls), d1 = descs(kf1->ldesc, kf1->n_ls);
+        const std::vector<Knn2> m12 = knn2(d0, d1, 1), m21 = knn2(d1, d0, 1);
+        const double nn12_dist_th = lineDescriptorMAD_nn12(m12) * cfg->desc_th_l;
+        int n = 0;
+        for (size_t i = 0; i < m12.size(); ++i) {
+            const int q = m12[i][0].queryIdx, t = m12[i][0].trainIdx;
+            const int rl = m21[t][0].trainIdx;
+            const double dist_12 = (double)(m12[i][1].distance - m12[i][0].distance);
+            if (q == rl && dist_12 > nn12_dist_th) {
+                double sc[3], ec[3], su[2], eu[2];
+                se3_apply(DT, kf0->sP + 3 * q, sc);
+                proj(sc, su);
+                se3_apply(DT, kf0->eP + 3 * q, ec);
+                proj(ec, eu);
+                const double* l = kf0->le + 3 * q;
+                const double e0 = (l[0] * su[0] + l[1] * su[1]) + l[2];
+                const double e1 = (l[0] * eu[0] + l[1] * eu[1]) + l[2];
+                if (std::sqrt(e0 * e0 + e1 * e1) * std::sqrt(kf0->ls_sigma2[q]) < chi) {
+                    ls_pairs[2 * n] = q; ls_pairs[2 * n + 1] = t; ++n;
+                }
+            }
+        }
+        *n_ls_pairs = n;
+    }
+    return 0;
+}

@@ -55,6 +55,13 @@ int gfplo_need_new_kf(gfplo_handler* h, int* flag);
 int gfplo_curr_frame_is_kf(gfplo_handler* h);
 int gfplo_read_kf_state(gfplo_handler* h, gfpl_kf_state* out);
 
+/* MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:
+ * 199-470); same contract as gfpl_kf_common_matches but every pointer of the
+ * views and outputs is HOST memory. */
+int gfplo_kf_common_matches(const gfpl_camera* cam, const gfpl_config* cfg, const gfpl_kf_view* kf0,
+                            const gfpl_kf_view* kf1, int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs,
+                            int* n_ls_pairs);
+
 /* stage-level entry points (same split as include/gfpl.h) */
 int gfplo_begin_frame(gfplo_handler* h, const gfpl_frames* in, int seq);   /* new curr_frame */
 int gfplo_stereo_points(gfplo_handler* h);

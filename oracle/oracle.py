@@ -43,6 +43,8 @@ def lib() -> C.CDLL:
         L.gfplo_optimize_pose_ini.argtypes = [P, P]; L.gfplo_optimize_pose_ini.restype = C.c_int
         L.gfplo_hamming.argtypes = [P, P, C.c_int]; L.gfplo_hamming.restype = C.c_int
         L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
+        L.gfplo_kf_common_matches.argtypes = [P, P, P, P, P, P, P, P]
+        L.gfplo_kf_common_matches.restype = C.c_int
         for n in ["gfplo_log", "gfplo_sin", "gfplo_cos"]:
             getattr(L, n).argtypes = [C.c_double]; getattr(L, n).restype = C.c_double
         L.gfplo_logdet6.argtypes = [P]; L.gfplo_logdet6.restype = C.c_double
@@ -149,6 +151,18 @@ class OracleHandler:
 
 
 # ---- primitives
+def kf_common_matches(cam, cfg, kf0: "gfpl.KeyFrameView", kf1: "gfpl.KeyFrameView"):
+    """MapHandler::lookForCommonMatches keyframe-pair stage on host views (device=None)."""
+    pp = np.zeros((max(kf0.s.n_pt, 1), 2), np.int32)
+    lp = np.zeros((max(kf0.s.n_ls, 1), 2), np.int32)
+    npt, nls = C.c_int(0), C.c_int(0)
+    rc = lib().gfplo_kf_common_matches(C.byref(cam), C.byref(cfg), C.byref(kf0.s), C.byref(kf1.s),
+                                       _p(pp), C.byref(npt), _p(lp), C.byref(nls))
+    if rc != 0:
+        raise RuntimeError(f"gfplo_kf_common_matches -> {rc}")
+    return pp[: npt.value].copy(), lp[: nls.value].copy()
+
+
 def hamming(a: np.ndarray, b: np.ndarray, cell: int = 1) -> int:
     a = np.ascontiguousarray(a, np.uint8); b = np.ascontiguousarray(b, np.uint8)
     return lib().gfplo_hamming(_p(a), _p(b), cell)
