@@ -202,8 +202,11 @@ __device__ int hist_rank_c(const int* h, int r) {
 
 // dynamic LDS: tb[cap*8] u32 (train rows: curr for 12, then prev for 21) |
 //              i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
+#ifndef GFPL_CL_WAVES
+#define GFPL_CL_WAVES 1
+#endif
 template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_cross_lines(KParams p) {
+__global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;

@@ -190,6 +190,9 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 }
 
 // ------------------------------------------------------- stereo points --
+#ifndef GFPL_SL_WAVES
+#define GFPL_SL_WAVES 1
+#endif
 #ifndef GFPL_SP_WAVES
 #define GFPL_SP_WAVES 8   // waves per SIMD (4 workgroups / CU; measured faster than 6 despite a 28-B spill)
 #endif
@@ -544,7 +547,7 @@ __device__ int hist_rank(const int* h, int r) {
 // Query rows stream from HBM into registers; only the train set sits in LDS, so
 // 2000 lines per side (config 5) fit.
 template <int CELL, bool INITIAL, int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_stereo_lines(KParams p) {
+__global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
