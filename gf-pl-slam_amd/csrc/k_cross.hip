@@ -39,7 +39,10 @@ __device__ __forceinline__ int grid_axis(double v, double inv_cs, int n) {
 
 // dynamic LDS: cnt[ncell+2] start[ncell+2] i32 | sq[cap] i32 | spx[cap] spy[cap] f32 |
 //              lastT[cap] i32 | prevT[16] Tinv[16] f64 | misc[64] i32
-__global__ void __launch_bounds__(1024) k_cross_points(KParams p, CrossGrid G) {
+#ifndef GFPL_CP_WAVES
+#define GFPL_CP_WAVES 8   // 2 workgroups / CU (84-B spill; 3.2 -> 2.6 ms measured)
+#endif
+__global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p, CrossGrid G) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kp_cap;

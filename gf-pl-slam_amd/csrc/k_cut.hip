@@ -189,7 +189,10 @@ __device__ __forceinline__ void cut_endpoint_fast(const DevCam& cam, double homo
 }
 
 // ------------------------------------------------------------------ prep --
-__global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
+#ifndef GFPL_PREP_WAVES
+#define GFPL_PREP_WAVES 1
+#endif
+__global__ void __launch_bounds__(64, GFPL_PREP_WAVES) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
@@ -726,7 +729,10 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 
 // ---------------------------------------------------------------- finish --
 // invCovPose of the chosen ratio + updateEndPointByRatio (ledger Q4)
-__global__ void __launch_bounds__(64) k_cut_finish(KParams p) {
+#ifndef GFPL_FIN_WAVES
+#define GFPL_FIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
     if (nls == 0) return;
