@@ -543,6 +543,7 @@ int gfpl_kf_common_matches(gfpl_ctx* c, const gfpl_kf_view* k0, const gfpl_kf_vi
         g.lines = kind;
         g.n0 = n0;
         g.i12 = i12; g.d12 = f12; g.i21 = i21;
+        g.p_stride = 3;
         g.P0 = kind == 0 ? k0->P : k0->sP;
         g.eP0 = kind == 0 ? nullptr : k0->eP;
         g.le0 = kind == 0 ? nullptr : k0->le;
@@ -552,6 +553,93 @@ int gfpl_kf_common_matches(gfpl_ctx* c, const gfpl_kf_view* k0, const gfpl_kf_vi
         g.count = cnt + kind;
         if (e == hipSuccess) e = launch_kf_gate(g, c->stream);
         if (e == hipSuccess) e = hipMemcpyAsync(counts + kind, cnt + kind, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipError_t ef = hipFree(scr);
+    if (e != hipSuccess || ef != hipSuccess) return GFPL_E_HIP;
+    *n_pt_pairs = counts[0];
+    *n_ls_pairs = counts[1];
+    return GFPL_OK;
+}
+
+// lookForCommonMatches local-map stage (src/mapHandler.cpp:472-772): per kind one
+// filter launch (in-view local rows, compacted with their descriptors), the two
+// knn-2 launches on the compacted rows and the gate launch (k_kf.hip).
+int gfpl_kf_local_map_matches(gfpl_ctx* c, const gfpl_map_view* m, const gfpl_kf_view* k1, double max_kf_epip_p,
+                              double max_kf_epip_l, int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs,
+                              int* n_ls_pairs) {
+    if (!c || !m || !k1 || !n_pt_pairs || !n_ls_pairs || !c->has_cam) return GFPL_E_INVALID;
+    if (m->n_pt < 0 || m->n_ls < 0 || k1->n_pt < 0 || k1->n_ls < 0) return GFPL_E_INVALID;
+    *n_pt_pairs = 0;
+    *n_ls_pairs = 0;
+    const bool do_pt = m->n_pt >= 2 && k1->n_pt >= 2, do_ls = m->n_ls >= 2 && k1->n_ls >= 2;
+    if (do_pt && (!pt_pairs || !m->pdesc || !m->P || !k1->pdesc || !k1->pl)) return GFPL_E_INVALID;
+    if (do_ls && (!ls_pairs || !m->ldesc || !m->L || !k1->ldesc || !k1->le)) return GFPL_E_INVALID;
+    if (!do_pt && !do_ls) return GFPL_OK;
+    const size_t n0 = (size_t)(do_pt ? m->n_pt : 0) + (do_ls ? m->n_ls : 0);
+    const size_t n1 = (size_t)(do_pt ? k1->n_pt : 0) + (do_ls ? k1->n_ls : 0);
+    // loc [n0] | descs [n0][32] | idx [2 (n0 + n1)] | dist [2 (n0 + n1)] | counts [4]
+    const size_t bytes = n0 * 4 + n0 * 32 + 2 * (n0 + n1) * 8 + 64;
+    char* scr = nullptr;
+    HIPCHK(hipMalloc(&scr, bytes));
+    int32_t* loc = reinterpret_cast<int32_t*>(scr);
+    uint8_t* dsc = reinterpret_cast<uint8_t*>(loc + n0);
+    int32_t* idx = reinterpret_cast<int32_t*>(dsc + n0 * 32);
+    float* dist = reinterpret_cast<float*>(idx + 2 * (n0 + n1));
+    int* cnt = reinterpret_cast<int*>(dist + 2 * (n0 + n1));
+    const DevCam cam = devcam(c->cam);
+    hipError_t e = hipSuccess;
+    int nloc[2] = {0, 0};
+    size_t o0 = 0;
+    size_t lo[2] = {0, 0};
+    for (int kind = 0; kind < 2 && e == hipSuccess; ++kind) {
+        if (kind == 0 ? !do_pt : !do_ls) continue;
+        lo[kind] = o0;
+        const int n = kind == 0 ? m->n_pt : m->n_ls;
+        e = launch_kf_map_filter(cam, k1->T_kf_w, kind == 0 ? m->P : m->L, n, kind, loc + o0, dsc + 32 * o0,
+                                 kind == 0 ? m->pdesc : m->ldesc, cnt + kind, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(nloc + kind, cnt + kind, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+        o0 += n;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    gfpl::KfGate g;
+    std::memset(&g, 0, sizeof g);
+    g.cam = cam;
+    for (int i = 0; i < 16; ++i) g.T1[i] = k1->T_kf_w[i];
+    g.max_ratio_12_p = c->cfg.max_ratio_12_p;
+    g.desc_th_l = c->cfg.desc_th_l;
+    g.map = 1;
+    g.epip_p = max_kf_epip_p;
+    g.epip_l = max_kf_epip_l;
+    int counts[2] = {0, 0};
+    size_t o = 0;
+    for (int kind = 0; kind < 2 && e == hipSuccess; ++kind) {
+        if (kind == 0 ? !do_pt : !do_ls) continue;
+        const int nq = nloc[kind], nt = kind == 0 ? k1->n_pt : k1->n_ls;
+        if (nq < 2) continue;   // ledger U4 on the selected local rows
+        const uint8_t* d0 = dsc + 32 * lo[kind];
+        const uint8_t* d1 = kind == 0 ? k1->pdesc : k1->ldesc;
+        int32_t* i12 = idx + 2 * o;
+        float* f12 = dist + 2 * o;
+        int32_t* i21 = i12 + 2 * (size_t)nq;
+        float* f21 = f12 + 2 * (size_t)nq;
+        o += (size_t)nq + nt;
+        e = launch_knn2(d0, nq, d1, nt, 1, i12, f12, c->stream);
+        if (e == hipSuccess) e = launch_knn2(d1, nt, d0, nq, 1, i21, f21, c->stream);
+        g.lines = kind;
+        g.n0 = nq;
+        g.loc = loc + lo[kind];
+        g.i12 = i12; g.d12 = f12; g.i21 = i21;
+        g.P0 = kind == 0 ? m->P : m->L;
+        g.eP0 = kind == 0 ? nullptr : m->L + 3;
+        g.p_stride = kind == 0 ? 3 : 6;
+        g.pl1 = kind == 0 ? k1->pl : nullptr;
+        g.le1 = kind == 0 ? nullptr : k1->le;
+        g.pairs = kind == 0 ? pt_pairs : ls_pairs;
+        g.count = cnt + 2 + kind;
+        if (e == hipSuccess) e = launch_kf_gate(g, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(counts + kind, cnt + 2 + kind, sizeof(int), hipMemcpyDeviceToHost, c->stream);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     hipError_t ef = hipFree(scr);

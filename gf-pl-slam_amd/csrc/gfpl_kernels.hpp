@@ -26,6 +26,11 @@ struct KfGate {
     double T0[16], T1[16];
     double max_ratio_12_p, desc_th_l;
     int lines, n0;
+    int map;                // 0: keyframe pair (DT = inv(T1) T0), 1: local map (Twf = inv(T1))
+    const int32_t* loc;     // map mode: query row -> caller's map row
+    int p_stride;           // doubles between rows of P0 / eP0 (3, or 6 for line3D)
+    double epip_p, epip_l;  // map mode: maxKFEpipP / maxKFEpipL
+    const double* le1;      // map mode: kf1 le [n1][3] (lines)
     const int32_t* i12;     // knn-2 kf0 -> kf1 [2 n0]
     const float* d12;
     const int32_t* i21;     // knn-2 kf1 -> kf0 [2 n1]
@@ -38,5 +43,8 @@ struct KfGate {
     int* count;
 };
 hipError_t launch_kf_gate(const KfGate& g, hipStream_t s);
+// local-map rows in view in front of kf1 (map order): loc / n (device)
+hipError_t launch_kf_map_filter(const DevCam& cam, const double* T1, const double* P, int n, int lines,
+                                int32_t* loc, uint8_t* desc_out, const uint8_t* desc_in, int* count, hipStream_t s);
 
 }  // namespace gfpl

@@ -175,6 +175,31 @@ class KeyFrameView:
             setattr(self.s, cf, _ptr(a))
 
 
+class MapViewStruct(C.Structure):
+    """gfpl_map_view: the local map rows lookForCommonMatches' second stage reads."""
+    _fields_ = [("n_pt", C.c_int), ("pdesc", _vp), ("P", _vp), ("n_ls", C.c_int), ("ldesc", _vp), ("L", _vp)]
+
+
+class MapView:
+    """Local map points / lines (med_desc row 0, point3D, line3D) as numpy arrays,
+    copied to `device` (torch) when given."""
+
+    def __init__(self, pdesc, P, ldesc, L, device=None):
+        self.s = MapViewStruct()
+        arrs = {"pdesc": np.ascontiguousarray(pdesc, np.uint8).reshape(-1, 32),
+                "P": np.ascontiguousarray(P, np.float64).reshape(-1, 3),
+                "ldesc": np.ascontiguousarray(ldesc, np.uint8).reshape(-1, 32),
+                "L": np.ascontiguousarray(L, np.float64).reshape(-1, 6)}
+        self.s.n_pt, self.s.n_ls = len(arrs["pdesc"]), len(arrs["ldesc"])
+        self.keep = {}
+        for k, a in arrs.items():
+            if device is not None:
+                import torch
+                a = torch.from_numpy(a.copy()).to(device) if a.size else torch.zeros(1, device=device)
+            self.keep[k] = a
+            setattr(self.s, k, _ptr(a) if (device is not None or a.size) else 0)
+
+
 class SynthParams(C.Structure):
     _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
                 ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
@@ -246,6 +271,7 @@ def hiplib() -> C.CDLL:
             "gfpl_line_cut": ([P], C.c_int),
             "gfpl_knn2_hamming": ([P, P, C.c_int, P, C.c_int, C.c_int, P, P], C.c_int),
             "gfpl_kf_common_matches": ([P, P, P, P, P, P, P], C.c_int),
+            "gfpl_kf_local_map_matches": ([P, P, P, C.c_double, C.c_double, P, P, P, P], C.c_int),
             "gfpl_read_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_write_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_read_track": ([P, C.c_int, P], C.c_int),
@@ -540,6 +566,22 @@ class Context:
         torch.cuda.synchronize()
         check(self.L.gfpl_kf_common_matches(self.h, C.byref(kf0.s), C.byref(kf1.s), _ptr(pp), C.byref(npt),
                                             _ptr(lp), C.byref(nls)), "kf_common_matches")
+        return (pp[: 2 * npt.value].cpu().numpy().reshape(-1, 2),
+                lp[: 2 * nls.value].cpu().numpy().reshape(-1, 2))
+
+    def lookForLocalMapMatches(self, local_map: MapView, kf1_unmatched: KeyFrameView,
+                               max_kf_epip_p: float = 1.0, max_kf_epip_l: float = 1.0):
+        """lookForCommonMatches local-map stage (src/mapHandler.cpp:472-772): (map row,
+        kf1 unmatched row) point and line pairs in the reference's loop order."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        pp = torch.zeros(2 * max(local_map.s.n_pt, 1), dtype=torch.int32, device=dev)
+        lp = torch.zeros(2 * max(local_map.s.n_ls, 1), dtype=torch.int32, device=dev)
+        npt, nls = C.c_int(0), C.c_int(0)
+        torch.cuda.synchronize()
+        check(self.L.gfpl_kf_local_map_matches(self.h, C.byref(local_map.s), C.byref(kf1_unmatched.s),
+                                               max_kf_epip_p, max_kf_epip_l, _ptr(pp), C.byref(npt),
+                                               _ptr(lp), C.byref(nls)), "kf_local_map_matches")
         return (pp[: 2 * npt.value].cpu().numpy().reshape(-1, 2),
                 lp[: 2 * nls.value].cpu().numpy().reshape(-1, 2))
 

@@ -346,6 +346,36 @@ typedef struct gfpl_kf_view {
 int  gfpl_kf_common_matches(gfpl_ctx* ctx, const gfpl_kf_view* kf0, const gfpl_kf_view* kf1,
                             int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs);
 
+/* The local map as lookForCommonMatches' second stage reads it (src/mapHandler.cpp:
+ * 472-772): the map points / lines the caller keeps as local and not yet observed
+ * by kf1 (`local && kf_obs_list.back() != kf1_idx`), in map order, with their
+ * median descriptor (med_desc.row(0)) and 3D geometry (point3D; line3D = sP, eP).
+ * Device pointers.                                                              */
+typedef struct gfpl_map_view {
+    int            n_pt;
+    const uint8_t* pdesc;       /* [n_pt][32]                                  */
+    const double*  P;           /* [n_pt][3]  point3D (world)                  */
+    int            n_ls;
+    const uint8_t* ldesc;       /* [n_ls][32]                                  */
+    const double*  L;           /* [n_ls][6]  line3D (world sP, eP)            */
+} gfpl_map_view;
+
+/* lookForCommonMatches, local-map stage (src/mapHandler.cpp:472-772): with
+ * Twf = inverse_se3(kf1 T_kf_w), the map rows whose projection lies inside the
+ * image in front of the camera (:479-490 points, :615-632 lines, both endpoints)
+ * are matched against kf1's UNMATCHED features (the caller passes kf1 compacted
+ * to its idx == -1 rows, :495-505 / :637-647): knn-2 NORM_HAMMING both ways,
+ * mutual best; points: d0/d1 <= max_ratio_12_p, Pf.z > 0 and |proj(Pf) - pl| <
+ * max_kf_epip_p; lines: d1 - d0 > lineDescriptorMAD.nn12 * desc_th_l, both
+ * endpoints in front and the SIGNED line residuals le . proj(endpoint) both <
+ * max_kf_epip_l (the reference compares them without abs).  Pairs (map row in
+ * the caller's map_view, kf1 row) in the reference's loop order; counts on the
+ * host (synchronises).  Config::maxKFEpipP / maxKFEpipL default to 1.0
+ * (src/config.cpp:42-43).  Fewer than two rows on a side: no pairs (U4).      */
+int  gfpl_kf_local_map_matches(gfpl_ctx* ctx, const gfpl_map_view* map, const gfpl_kf_view* kf1,
+                               double max_kf_epip_p, double max_kf_epip_l,
+                               int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs);
+
 /* ----------------------------------------------------- state transfer ----- */
 /* Copy one sequence's frame state device -> host (synchronises).            */
 int  gfpl_read_frame(gfpl_seqbatch* sb, int which, int seq, gfpl_frame_host* out);

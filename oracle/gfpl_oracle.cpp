@@ -1956,3 +1956,109 @@ extern "C" int gfplo_kf_common_matches(const gfpl_camera* cam, const gfpl_config
     }
     return 0;
 }
+
+// MapHandler::lookForCommonMatches, local-map stage (src/mapHandler.cpp:472-772).
+// map_local_points / map_local_lines = the caller's rows that project inside the
+// image in front of the camera, in map order; kf1 is already compacted to its
+// unmatched rows.  Pair = (caller's map row, kf1 row).
+extern "C" int gfplo_kf_local_map_matches(const gfpl_camera* cam, const gfpl_config* cfg, const gfpl_map_view* map,
+                                          const gfpl_kf_view* kf1, double max_kf_epip_p, double max_kf_epip_l,
+                                          int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs) {
+    if (!cam || !cfg || !map || !kf1 || !n_pt_pairs || !n_ls_pairs) return GFPL_E_INVALID;
+    if (map->n_pt < 0 || map->n_ls < 0 || kf1->n_pt < 0 || kf1->n_ls < 0) return GFPL_E_INVALID;
+    *n_pt_pairs = 0;
+    *n_ls_pairs = 0;
+    double Twf[16];
+    inverse_se3(kf1->T_kf_w, Twf);   // :202
+    auto proj = [&](const double* P, double* uv) {
+        uv[0] = cam->cx + (cam->fx * P[0]) / P[2];
+        uv[1] = cam->cy + (cam->fy * P[1]) / P[2];
+    };
+    auto inside = [&](const double* Pf, const double* pf) {   // :482 / :622-625
+        return pf[0] > 0 && pf[0] < cam->width && pf[1] > 0 && pf[1] < cam->height && Pf[2] > 0.0;
+    };
+    auto descs = [](const uint8_t* d, const std::vector<int>& rows) {
+        std::vector<Desc> v(rows.size());
+        for (size_t i = 0; i < rows.size(); ++i) std::memcpy(v[i].data(), d + 32 * (size_t)rows[i], 32);
+        return v;
+    };
+    std::vector<int> all1;
+    // points (:472-562)
+    {
+        std::vector<int> loc;
+        for (int i = 0; i < map->n_pt; ++i) {
+            double Pf[3], pf[2];
+            se3_apply(Twf, map->P + 3 * i, Pf);
+            proj(Pf, pf);
+            if (inside(Pf, pf)) loc.push_back(i);
+        }
+        if (loc.size() >= 2 && kf1->n_pt >= 2) {
+            if (!pt_pairs) return GFPL_E_INVALID;
+            std::vector<int> r1(kf1->n_pt);
+            for (int i = 0; i < kf1->n_pt; ++i) r1[i] = i;
+            const std::vector<Desc> d0 = descs(map->pdesc, loc), d1 = descs(kf1->pdesc, r1);
+            const std::vector<Knn2> m12 = knn2(d0, d1, 1), m21 = knn2(d1, d0, 1);
+            int n = 0;
+            for (size_t i = 0; i < m12.size(); ++i) {
+                const int q = m12[i][0].queryIdx, t = m12[i][0].trainIdx;
+                const int rl = m21[t][0].trainIdx;
+                const double dist_12 = (double)(m12[i][0].distance / m12[i][1].distance);
+                if (q == rl && dist_12 <= cfg->max_ratio_12_p) {
+                    double Pf[3], pf[2];
+                    se3_apply(Twf, map->P + 3 * loc[q], Pf);
+                    if (Pf[2] > 0.0) {
+                        proj(Pf, pf);
+                        const double ex = pf[0] - kf1->pl[2 * t], ey = pf[1] - kf1->pl[2 * t + 1];
+                        if (std::sqrt(ex * ex + ey * ey) < max_kf_epip_p) {
+                            pt_pairs[2 * n] = loc[q]; pt_pairs[2 * n + 1] = t; ++n;
+                        }
+                    }
+                }
+            }
+            *n_pt_pairs = n;
+        }
+    }
+    // lines (:611-772)
+    {
+        std::vector<int> loc;
+        for (int i = 0; i < map->n_ls; ++i) {
+            double sPf[3], ePf[3], spf[2], epf[2];
+            se3_apply(Twf, map->L + 6 * i, sPf);
+            proj(sPf, spf);
+            se3_apply(Twf, map->L + 6 * i + 3, ePf);
+            proj(ePf, epf);
+            if (inside(sPf, spf) && inside(ePf, epf)) loc.push_back(i);
+        }
+        if (loc.size() >= 2 && kf1->n_ls >= 2) {
+            if (!ls_pairs) return GFPL_E_INVALID;
+            std::vector<int> r1(kf1->n_ls);
+            for (int i = 0; i < kf1->n_ls; ++i) r1[i] = i;
+            const std::vector<Desc> d0 = descs(map->ldesc, loc), d1 = descs(kf1->ldesc, r1);
+            const std::vector<Knn2> m12 = knn2(d0, d1, 1), m21 = knn2(d1, d0, 1);
+            const double nn12_dist_th = lineDescriptorMAD_nn12(m12) * cfg->desc_th_l;
+            int n = 0;
+            for (size_t i = 0; i < m12.size(); ++i) {
+                const int q = m12[i][0].queryIdx, t = m12[i][0].trainIdx;
+                const int rl = m21[t][0].trainIdx;
+                const double dist_12 = (double)(m12[i][1].distance - m12[i][0].distance);
+                if (q == rl && dist_12 > nn12_dist_th) {
+                    double sc[3], ec[3], su[2], eu[2];
+                    se3_apply(Twf, map->L + 6 * loc[q], sc);
+                    proj(sc, su);
+                    se3_apply(Twf, map->L + 6 * loc[q] + 3, ec);
+                    proj(ec, eu);
+                    if (sc[2] > 0.0 && ec[2] > 0.0) {
+                        const double* l = kf1->le + 3 * t;
+                        const double e0 = (l[0] * su[0] + l[1] * su[1]) + l[2];
+                        const double e1 = (l[0] * eu[0] + l[1] * eu[1]) + l[2];
+                        if (e0 < max_kf_epip_l && e1 < max_kf_epip_l) {
+                            ls_pairs[2 * n] = loc[q]; ls_pairs[2 * n + 1] = t; ++n;
+                        }
+                    }
+                }
+            }
+            *n_ls_pairs = n;
+        }
+    }
+    return 0;
+}

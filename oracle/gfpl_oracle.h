@@ -62,6 +62,12 @@ int gfplo_kf_common_matches(const gfpl_camera* cam, const gfpl_config* cfg, cons
                             const gfpl_kf_view* kf1, int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs,
                             int* n_ls_pairs);
 
+/* lookForCommonMatches local-map stage (src/mapHandler.cpp:472-772); contract of
+ * gfpl_kf_local_map_matches with HOST pointers. */
+int gfplo_kf_local_map_matches(const gfpl_camera* cam, const gfpl_config* cfg, const gfpl_map_view* map,
+                               const gfpl_kf_view* kf1, double max_kf_epip_p, double max_kf_epip_l,
+                               int32_t* pt_pairs, int* n_pt_pairs, int32_t* ls_pairs, int* n_ls_pairs);
+
 /* stage-level entry points (same split as include/gfpl.h) */
 int gfplo_begin_frame(gfplo_handler* h, const gfpl_frames* in, int seq);   /* new curr_frame */
 int gfplo_stereo_points(gfplo_handler* h);

@@ -45,6 +45,8 @@ def lib() -> C.CDLL:
         L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
         L.gfplo_kf_common_matches.argtypes = [P, P, P, P, P, P, P, P]
         L.gfplo_kf_common_matches.restype = C.c_int
+        L.gfplo_kf_local_map_matches.argtypes = [P, P, P, P, C.c_double, C.c_double, P, P, P, P]
+        L.gfplo_kf_local_map_matches.restype = C.c_int
         for n in ["gfplo_log", "gfplo_sin", "gfplo_cos"]:
             getattr(L, n).argtypes = [C.c_double]; getattr(L, n).restype = C.c_double
         L.gfplo_logdet6.argtypes = [P]; L.gfplo_logdet6.restype = C.c_double
@@ -160,6 +162,19 @@ def kf_common_matches(cam, cfg, kf0: "gfpl.KeyFrameView", kf1: "gfpl.KeyFrameVie
                                        _p(pp), C.byref(npt), _p(lp), C.byref(nls))
     if rc != 0:
         raise RuntimeError(f"gfplo_kf_common_matches -> {rc}")
+    return pp[: npt.value].copy(), lp[: nls.value].copy()
+
+
+def kf_local_map_matches(cam, cfg, local_map: "gfpl.MapView", kf1: "gfpl.KeyFrameView",
+                         max_kf_epip_p: float = 1.0, max_kf_epip_l: float = 1.0):
+    """lookForCommonMatches local-map stage on host views (device=None)."""
+    pp = np.zeros((max(local_map.s.n_pt, 1), 2), np.int32)
+    lp = np.zeros((max(local_map.s.n_ls, 1), 2), np.int32)
+    npt, nls = C.c_int(0), C.c_int(0)
+    rc = lib().gfplo_kf_local_map_matches(C.byref(cam), C.byref(cfg), C.byref(local_map.s), C.byref(kf1.s),
+                                          max_kf_epip_p, max_kf_epip_l, _p(pp), C.byref(npt), _p(lp), C.byref(nls))
+    if rc != 0:
+        raise RuntimeError(f"gfplo_kf_local_map_matches -> {rc}")
     return pp[: npt.value].copy(), lp[: nls.value].copy()
 
 

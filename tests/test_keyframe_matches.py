@@ -182,3 +182,102 @@ def test_gpu_kf_common_matches_too_few_rows():
     f0, T0, f1, T1, _, _ = known_pair(cam, n_pt=1, n_ls=0)
     gp, gl = ctx.lookForCommonMatches(gfpl.KeyFrameView(f0, T0, "cuda"), gfpl.KeyFrameView(f1, T1, "cuda"))
     assert len(gp) == 0 and len(gl) == 0
+
+
+# ----------------------------------------------------------- local-map stage --
+def known_local_map(cam, n_pt=200, n_ls=80, seed=21, flips=8):
+    """A local map seen from kf1 (T_kf_w = T1) and kf1's unmatched features, with
+    the expected (map row, kf1 row) pairs of src/mapHandler.cpp:472-772 by
+    construction: some map rows project outside the image (filtered out), some
+    kf1 observations are offset beyond maxKFEpipP / maxKFEpipL, and one line has a
+    large NEGATIVE residual, which the reference's signed test accepts."""
+    rng = np.random.default_rng(seed)
+    T1 = _pose(0.02, -0.01, 0.03, [0.4, -0.1, 0.3])
+    Twf = _inv(T1)
+    Tfw = T1   # world point = T1 @ camera point
+
+    def world(pc):
+        return Tfw[:3, :3] @ pc + Tfw[:3, 3]
+
+    def flipped(d):
+        d = d.copy()
+        for b in rng.choice(256, flips, replace=False):
+            d[b // 8] ^= np.uint8(1 << (b % 8))
+        return d
+
+    def in_view(pc):
+        u = _proj(cam, pc)
+        return 0 < u[0] < cam.width and 0 < u[1] < cam.height and pc[2] > 0
+
+    f1 = gfpl.FrameHost(max(n_pt, 2), max(n_ls, 2))
+    f1.s.n_pt, f1.s.n_ls = n_pt, n_ls
+    pdesc, P, exp_pt = [], [], []
+    perm = rng.permutation(n_pt)
+    for i in range(n_pt):
+        out = rng.random() < 0.1
+        pc = np.array([rng.uniform(-2, 2), rng.uniform(-1.5, 1.5), rng.uniform(2, 8)])
+        if out:
+            pc[0] = pc[2] * 3.0   # far right of the image
+        d = rng.integers(0, 256, 32, dtype=np.uint8)
+        pdesc.append(d)
+        P.append(world(pc))
+        j = perm[i]
+        f1.arr["pdesc"][j] = flipped(d)
+        off = 0.3 if rng.random() > 0.15 else 4.0
+        f1.arr["pt_pl"][j] = _proj(cam, pc) + np.array([off, 0.0]) if not out else np.array([10.0, 10.0])
+        if in_view(pc) and off < 1.0:
+            exp_pt.append((i, j))
+    ldesc, L, exp_ls = [], [], []
+    perm = rng.permutation(n_ls)
+    for i in range(n_ls):
+        out = rng.random() < 0.1
+        sc = np.array([rng.uniform(-1.5, 1.5), rng.uniform(-1, 1), rng.uniform(2, 8)])
+        ec = sc + np.array(rng.uniform(-0.5, 0.5, 3))
+        ec[2] = max(ec[2], 1.5)
+        if out:
+            ec[0] = ec[2] * 3.0
+        d = rng.integers(0, 256, 32, dtype=np.uint8)
+        ldesc.append(d)
+        L.append(np.concatenate([world(sc), world(ec)]))
+        su, eu = _proj(cam, sc), _proj(cam, ec)
+        le = np.cross([su[0], su[1], 1.0], [eu[0], eu[1], 1.0])
+        le = le / np.hypot(le[0], le[1])
+        kind = rng.random()
+        if kind < 0.1:
+            le[2] += 5.0     # residuals +5: rejected
+        elif kind < 0.15:
+            le[2] -= 5.0     # residuals -5: accepted by the signed test
+        j = perm[i]
+        f1.arr["ldesc"][j] = flipped(d)
+        f1.arr["ls_le"][j] = le
+        if in_view(sc) and in_view(ec) and not (kind < 0.1):
+            exp_ls.append((i, j))
+    m_args = (np.array(pdesc), np.array(P), np.array(ldesc), np.array(L))
+    return m_args, f1, T1, np.array(exp_pt, np.int32).reshape(-1, 2), np.array(exp_ls, np.int32).reshape(-1, 2)
+
+
+def test_oracle_local_map_known_answer():
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    m_args, f1, T1, ep, el = known_local_map(cam)
+    pp, lp = O.kf_local_map_matches(cam, cfg, gfpl.MapView(*m_args), gfpl.KeyFrameView(f1, T1))
+    assert len(ep) > 100 and len(el) > 40
+    np.testing.assert_array_equal(pp, ep)
+    np.testing.assert_array_equal(lp, el)
+
+
+@pytest.mark.gpu
+def test_gpu_kf_local_map_matches():
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    ctx = gfpl.Context(cam, cfg)
+    for seed, n_pt, n_ls, ep_p, ep_l in [(21, 200, 80, 1.0, 1.0), (22, 2500, 900, 1.0, 1.0), (23, 300, 120, 4.5, 0.5)]:
+        m_args, f1, T1, ep, el = known_local_map(cam, n_pt, n_ls, seed)
+        gp, gl = ctx.lookForLocalMapMatches(gfpl.MapView(*m_args, device="cuda"), gfpl.KeyFrameView(f1, T1, "cuda"),
+                                            ep_p, ep_l)
+        op, ol = O.kf_local_map_matches(cam, cfg, gfpl.MapView(*m_args), gfpl.KeyFrameView(f1, T1), ep_p, ep_l)
+        np.testing.assert_array_equal(gp, op)
+        np.testing.assert_array_equal(gl, ol)
+        if ep_p == 1.0:
+            np.testing.assert_array_equal(gp, ep)
+            np.testing.assert_array_equal(gl, el)
