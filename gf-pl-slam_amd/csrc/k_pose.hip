@@ -36,6 +36,19 @@ struct PoseLDS {
 // of the same columns k, k + 1 as 16-B pairs, and a 64-double stride would put
 // every row in the same LDS bank
 #define CH_STRIDE 66
+// register-budget knobs of the GN loop (DESIGN.md §4 k_pose): DT read from LDS and a
+// 4-deep reduction unroll bring the kernel to 149 VGPRs (3 waves / SIMD, which the
+// ~10 KB LDS workgroup now allows): 7.3 -> 6.9 ms measured; without the prefetch
+// (117 VGPRs) it was slower again
+#ifndef GFPL_POSE_DT_LDS
+#define GFPL_POSE_DT_LDS 1
+#endif
+#ifndef GFPL_POSE_PREFETCH
+#define GFPL_POSE_PREFETCH 1
+#endif
+#ifndef GFPL_POSE_RED_UNROLL
+#define GFPL_POSE_RED_UNROLL 4
+#endif
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
 // evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w;
@@ -109,9 +122,15 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     const uint8_t* actp = X.act;
     const uint8_t* actl = X.act + X.npt;
     for (int it = 0; it < max_iters; ++it) {
+#if GFPL_POSE_DT_LDS
+        // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
+        // holding 16 doubles in registers across the chunk loop
+        const double* DT = S.DT;
+#else
         double DT[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) DT[i] = S.DT[i];
+#endif
         double s = 0.0;
         // raw inputs of chunk c + 1 are loaded into registers while chunk c is
         // reduced, so the SoA scratch latency hides behind the LDS reduction
@@ -124,9 +143,14 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
 #pragma unroll
             for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
         };
+#if GFPL_POSE_PREFETCH
         load_chunk(0);
+#endif
         for (int c = 0; c < nch; ++c) {
             const int f = (c << 6) + lane;
+#if !GFPL_POSE_PREFETCH
+            load_chunk(c);
+#endif
             double o[8];
             if (f < X.npt && actp[f]) eval_point(cam, homog, DT, pv, o);
             else {
@@ -142,7 +166,9 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
+#if GFPL_POSE_PREFETCH
             if (c + 1 < nch) load_chunk(c + 1);
+#endif
             __syncthreads();
             const double* A = buf + ia * CH_STRIDE;
             const double* Bv = buf + ib * CH_STRIDE;
@@ -150,7 +176,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             const double2* A2 = reinterpret_cast<const double2*>(A);
             const double2* B2 = reinterpret_cast<const double2*>(Bv);
             const double2* W2 = reinterpret_cast<const double2*>(W);
-#pragma unroll 8
+#pragma unroll GFPL_POSE_RED_UNROLL
             for (int k = 0; k < 32; ++k) {
                 const double2 a = A2[k], bb = B2[k], w = W2[k];
                 s = s + (a.x * bb.x) * w.x;
@@ -176,11 +202,12 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             if ((fabs(ee - err_prev) < p.cfg.min_error_change) || (ee < p.cfg.min_error)) {
                 brk = 1;
             } else {
-                double inc[6], E[16], Ei[16], Dn[16];
+                double inc[6], E[16], Ei[16], Dn[16], DTc[16];
                 ldlt_solve6(H, g, inc);
                 expmap_se3(inc, E);
                 inverse_se3(E, Ei);
-                mat4_mul(DT, Ei, Dn);
+                for (int i = 0; i < 16; ++i) DTc[i] = S.DT[i];
+                mat4_mul(DTc, Ei, Dn);
                 for (int i = 0; i < 16; ++i) S.DT[i] = Dn[i];
                 const double nrm = sqrt(((((inc[0] * inc[0] + inc[1] * inc[1]) + inc[2] * inc[2]) + inc[3] * inc[3]) +
                                          inc[4] * inc[4]) + inc[5] * inc[5]);
@@ -238,7 +265,7 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | rp[mpt_cap] rl[mls_cap]} f64 | buf[NP2] f64 | act[mpt+mls] u8
+// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8
 #ifndef GFPL_POSE_WAVES
 #define GFPL_POSE_WAVES 2
 #endif
@@ -249,13 +276,11 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     const int lane = threadIdx.x;
     const int npt = p.tr.n_matched_pt[b], nls = p.tr.n_matched_ls[b];
     // the GN chunk rows and the outlier residuals are never live together
-    const int region = max(16 * CH_STRIDE, p.mpt_cap + p.mls_cap);
+    const int region = max(16 * CH_STRIDE, NP2);
     double* cp = (double*)smem;
     double* cl = cp + 8 * CH_STRIDE;
-    double* rp = cp;
-    double* rl = rp + p.mpt_cap;
-    double* buf = cp + region;
-    uint8_t* act = (uint8_t*)(buf + NP2);
+    double* buf = cp;   // MAD sort buffer: never live together with the GN chunk rows
+    uint8_t* act = (uint8_t*)(cp + region);
     const DevPose& PP = p.prev.pose;
     const DevPoints& P = p.prev.pt;
     const DevLines& L = p.prev.ls;
@@ -309,16 +334,16 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
         for (int i = 0; i < 16; ++i) { double d = DTs[i] - DTs[i]; if (!(d == d)) fin = false; }
         if (fin) {
             // removeOutliers(DT_) (:2058-2116): residuals of every list entry
-            for (int k = lane; k < npt; k += 64) {
+            auto res_p = [&](int k) {
                 const double* in = pin + k;
                 const double Pp[3] = {in[0], in[p.mpt_cap], in[2 * p.mpt_cap]};
                 double Pc[3], uv[2];
                 se3_apply(DTs, Pp, Pc);
                 projection(p.cam, Pc, uv);
                 const double ex = uv[0] - in[3 * p.mpt_cap], ey = uv[1] - in[4 * p.mpt_cap];
-                rp[k] = sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
-            }
-            for (int k = lane; k < nls; k += 64) {
+                return sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
+            };
+            auto res_l = [&](int k) {
                 const double* in = lin + k;
                 const size_t st = p.mls_cap;
                 const double sP[3] = {in[0], in[st], in[2 * st]};
@@ -331,22 +356,25 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
                 const double l0 = in[6 * st], l1 = in[7 * st], l2 = in[8 * st];
                 const double e0 = (l0 * su[0] + l1 * su[1]) + l2;
                 const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
-                rl[k] = sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
-            }
+                return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
+            };
+            // the MAD sorts run in the GN chunk region (buf aliases it); the flag pass
+            // re-evaluates each residual (same operands, same bits) instead of keeping
+            // 800 residuals in LDS, which keeps the workgroup at ~10 KB of LDS
             __syncthreads();
-            for (int k = lane; k < npt; k += 64) buf[k] = rp[k];
+            for (int k = lane; k < npt; k += 64) buf[k] = res_p(k);
             __syncthreads();
             const double th_p = p.cfg.inlier_k * stdv_mad(buf, npt, NP2);
-            for (int k = lane; k < nls; k += 64) buf[k] = rl[k];
+            for (int k = lane; k < nls; k += 64) buf[k] = res_l(k);
             __syncthreads();
             const double th_l = p.cfg.inlier_k * stdv_mad(buf, nls, NP2);
             // duplicates of one prev point share P, pl_obs and sigma2, hence the residual:
             // flagging per list position equals the reference's per-feature flag
             int op = 0, ol = 0;
             for (int k = lane; k < npt; k += 64)
-                if (rp[k] > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
+                if (res_p(k) > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
             for (int k = lane; k < nls; k += 64)
-                if (rl[k] > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+                if (res_l(k) > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
             op = wave_sum(op);
             ol = wave_sum(ol);
             // active counts for stage 2
@@ -527,8 +555,8 @@ hipError_t launch_curr_frame_is_kf(const KParams& p, const int32_t* mask, hipStr
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
-    const size_t region = (size_t)std::max(16 * CH_STRIDE, p.mpt_cap + p.mls_cap);
-    const size_t lds = (region + NP2) * 8 + (p.mpt_cap + p.mls_cap) + 16;
+    const size_t region = (size_t)std::max(16 * CH_STRIDE, NP2);
+    const size_t lds = region * 8 + (p.mpt_cap + p.mls_cap) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
