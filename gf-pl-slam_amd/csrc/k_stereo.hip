@@ -190,6 +190,9 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 }
 
 // ------------------------------------------------------- stereo points --
+#ifndef GFPL_SP_SEG
+#define GFPL_SP_SEG 1
+#endif
 #ifndef GFPL_SL_WAVES
 #define GFPL_SL_WAVES 1
 #endif
@@ -205,7 +208,14 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 // keypoints are processed in row order (order[]), so the lanes of a wave touch the
 // same descriptors and overlapping SAD window rows.  Results are keyed by iL: the
 // processing order has no effect on the output.
-template <int BLOCK>
+//
+// SEG (the 512-thread layout when it fits 40 KB of LDS): the right keypoints are keyed by
+// (octave segment, minr, iR) with one first-candidate table per octave, so a left
+// keypoint scans only the octaves levelL-1..levelL+1 from their own band start (about
+// half the entries of the single sorted list); keypoints whose octave is outside the
+// pyramid form one extra segment, searched by bisection when it is not empty.  The
+// candidates, hence the lexicographic (dist, iR) minimum, are the same either way.
+template <int BLOCK, bool SEG>
 __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
@@ -217,7 +227,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     float* recx = (float*)(pairs + KP2);
     uint16_t* recm = (uint16_t*)(recx + KP2);
     uint16_t* rowlo = recm + KP2;
-    int* misc = (int*)(rowlo + ((nRows + 1) & ~1));
+    const int nlev = p.cam.n_levels;
+    const int nrl = SEG ? nlev * nRows : nRows;
+    int* misc = (int*)(rowlo + ((nrl + 1) & ~1));   // SEG: [22 + seg] band heights, [31] out-of-range count
     float* depth = reinterpret_cast<float*>(p.scr.knn) + (size_t)b * cap;   // scratch (cross points reuses it later)
     const int tid = threadIdx.x;
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
@@ -225,7 +237,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
     const uint8_t* DL = p.in.pdesc_l + (size_t)b * cap * 32;
     const uint8_t* DR = p.in.pdesc_r + (size_t)b * cap * 32;
-    if (tid == 0) { misc[0] = 0; misc[1] = 0; misc[2] = 0; }
+    if (tid < 32) misc[tid] = 0;
     __syncthreads();
     // vRowIndices as (minr, iR) keys; left keypoints as (row, iL) keys
     for (int i = tid; i < KP2; i += blockDim.x) {
@@ -234,8 +246,18 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             const float r = 2.0f * p.cam.scale[clamp_level(kp.octave, p.cam.n_levels)];
             const int maxr = (int)ceilf(kp.y + r);
             const int minr = (int)floorf(kp.y - r);
-            rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
-            atomicMax(&misc[0], maxr - minr);
+            if (SEG) {
+                // rows are < 2048 (GFPL_MAX_IMAGE_DIM): clamping minr to [-1024, 3071]
+                // keeps every key whose band can reach a row exact
+                const int seg = (kp.octave >= 0 && kp.octave < nlev) ? kp.octave : nlev;
+                const int mc = min(max(minr, -1024), 3071);
+                rkey[i] = ((uint32_t)seg << 28) | ((uint32_t)(mc + 1024) << 16) | (uint32_t)i;
+                atomicMax(&misc[22 + seg], maxr - minr);
+                if (seg == nlev) atomicAdd(&misc[31], 1);
+            } else {
+                rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
+                atomicMax(&misc[0], maxr - minr);
+            }
         } else {
             rkey[i] = 0xFFFFFFFFu;
         }
@@ -268,12 +290,19 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         recx[j] = kp.x;
         recm[j] = (uint16_t)(((uint32_t)band << 8) | ((uint32_t)oc & 0xFFu));
     }
-    // first candidate of each row: lower bound of minr >= row - D
-    for (int row = tid; row < nRows; row += blockDim.x) {
-        const uint32_t lo_key = (uint32_t)(row - D + 32768) << 16;
+    // first candidate of each row: lower bound of minr >= row - D (SEG: per octave)
+    auto seg_key = [&](int seg, int row) {
+        const int r0 = min(max(row - misc[22 + seg], -1024), 3071);
+        return ((uint32_t)seg << 28) | ((uint32_t)(r0 + 1024) << 16);
+    };
+    auto lower = [&](uint32_t lo_key) {
         int lo = 0, hi = Nr;
         while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
-        rowlo[row] = (uint16_t)lo;
+        return lo;
+    };
+    for (int x = tid; x < nrl; x += blockDim.x) {
+        if (SEG) rowlo[x] = (uint16_t)lower(seg_key(x / nRows, x % nRows));
+        else rowlo[x] = (uint16_t)lower((uint32_t)(x - D + 32768) << 16);
     }
     __syncthreads();
     const float minD = 0;
@@ -295,13 +324,11 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                 uint32_t dl[8];
                 load_desc(DL + (size_t)iL * 32, dl);
                 int bestDist = 100, bestIdxR = 0x7FFFFFFF;
-                int j0 = rowlo[row];
-#ifdef GFPL_EXP_NO_BAND
-                j0 = Nr;
-#endif
+                auto scan = [&](int j0, int seg) {
                 for (int j = j0; j < Nr; ++j) {
                     const uint32_t k = rkey[j];
-                    const int minr = (int)(k >> 16) - 32768;
+                    if (SEG && (k >> 28) != (uint32_t)seg) break;
+                    const int minr = SEG ? (int)((k >> 16) & 0xFFFu) - 1024 : (int)(k >> 16) - 32768;
                     if (minr > row) break;
                     const uint32_t m = recm[j];
                     if (minr + (int)(m >> 8) < row) continue;   // maxr < row
@@ -319,6 +346,17 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                         if (dist < bestDist || (dist == bestDist && iR < bestIdxR)) { bestDist = dist; bestIdxR = iR; }
                     }
                 }
+                };
+#ifndef GFPL_EXP_NO_BAND
+                if (SEG) {
+                    const int olo = (int)max((long long)levelL - 1, 0LL);
+                    const int ohi = (int)min((long long)levelL + 1, (long long)nlev - 1);
+                    for (int o = olo; o <= ohi; ++o) scan(rowlo[o * nRows + row], o);
+                    if (misc[31] > 0) scan(lower(seg_key(nlev, row)), nlev);
+                } else {
+                    scan(rowlo[row], 0);
+                }
+#endif
                 if (bestDist < 80) {
                     atomicAdd(&misc[2], 1);
                     SadJob J;
@@ -795,15 +833,18 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
+    const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((p.cam.n_levels * p.cam.height + 1) & ~1) * 2 + 32 * 4;
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
 #ifdef GFPL_EXP_SP1024
     if (true)
 #else
     if (p.kp_cap > 2048)
 #endif
-        hipLaunchKernelGGL(k_stereo_points<1024>, dim3(p.B), dim3(1024), lds, s, p, KP2);
+        hipLaunchKernelGGL((k_stereo_points<1024, false>), dim3(p.B), dim3(1024), lds, s, p, KP2);
+    else if (GFPL_SP_SEG && lds_seg <= 40960)   // four workgroups per CU
+        hipLaunchKernelGGL((k_stereo_points<512, true>), dim3(p.B), dim3(512), lds_seg, s, p, KP2);
     else
-        hipLaunchKernelGGL(k_stereo_points<512>, dim3(p.B), dim3(512), lds, s, p, KP2);
+        hipLaunchKernelGGL((k_stereo_points<512, false>), dim3(p.B), dim3(512), lds, s, p, KP2);
     return hipGetLastError();
 }
 

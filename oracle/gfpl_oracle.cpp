@@ -190,6 +190,11 @@ double det_cos(double x) {
 
 // std::max as the reference uses it: (a < b) ? b : a
 inline double ref_max(double a, double b) { return (a < b) ? b : a; }
+// ledger U11: the reference indexes its per-level tables (mvScaleFactors,
+// mvInvScaleFactors, the sigma2 of PointFeature / LineFeature) with the keypoint
+// octave unchecked — UB outside the pyramid; pinned (oracle and kernels) to the
+// nearest level
+inline int clampl(int o, int n) { return o < 0 ? 0 : (o >= n ? n - 1 : o); }
 
 // ============================================================ small linalg ==
 // Row-major fixed-size helpers; inner products k-sequential (pin N2).
@@ -797,7 +802,7 @@ struct gfplo_handler {
                             p.pl[0] = kl.x; p.pl[1] = kl.y;
                             p.disp = disp_;
                             backProjection(p.pl[0], p.pl[1], disp_, p.P);
-                            p.idx = pt_idx; p.level = kl.octave; p.sigma2 = cam.sigma2_pt[kl.octave]; p.inlier = true;
+                            p.idx = pt_idx; p.level = kl.octave; p.sigma2 = cam.sigma2_pt[clampl(kl.octave, cam.nlev)]; p.inlier = true;
                             f.pt.push_back(p);
                             f.pdesc.push_back(dl[lr_qdx]);
                             ++pt_idx;
@@ -861,7 +866,7 @@ struct gfplo_handler {
         L.le[0] = le_l[0]; L.le[1] = le_l[1]; L.le[2] = le_l[2];
         L.angle = (double)a.angle;
         L.level = a.octave;
-        L.sigma2 = cam.sigma2_ln[a.octave];
+        L.sigma2 = cam.sigma2_ln[clampl(a.octave, GFPL_MAX_LEVELS)];
         L.inlier = true;
         if (!initial) {
             // endpoint covariance gate (src/stereoFrame.cpp:707-751)
@@ -901,7 +906,7 @@ struct gfplo_handler {
         disparity = -1;
         bestuR = kpR.x;
         const float uR0 = kpR.x;
-        const int o = kpL.octave;
+        const int o = clampl(kpL.octave, cam.nlev);
         const float scaleFactor = cam.inv[o];
         const float scaleduL = std::round(kpL.x * scaleFactor);
         const float scaledvL = std::round(kpL.y * scaleFactor);
@@ -959,7 +964,7 @@ struct gfplo_handler {
         for (int iR = 0; iR < Nr; ++iR) {
             const gfpl_keypoint& kp = f.kpr(iR);
             const float kpY = kp.y;
-            const float r = 2.0f * cam.scale[kp.octave];
+            const float r = 2.0f * cam.scale[clampl(kp.octave, cam.nlev)];
             const int maxr = (int)std::ceil(kpY + r);
             const int minr = (int)std::floor(kpY - r);
             for (int yi = minr; yi <= maxr; ++yi)
@@ -1017,7 +1022,7 @@ struct gfplo_handler {
             if (disparity < 0) continue;
             p.disp = (double)disparity;
             backProjection(p.pl[0], p.pl[1], p.disp, p.P);
-            p.idx = pt_idx; p.level = kpL.octave; p.sigma2 = cam.sigma2_pt[kpL.octave]; p.inlier = true;
+            p.idx = pt_idx; p.level = kpL.octave; p.sigma2 = cam.sigma2_pt[clampl(kpL.octave, cam.nlev)]; p.inlier = true;
             f.pt.push_back(p);
             Desc d; std::memcpy(d.data(), f.pdl(iL), 32);
             f.pdesc.push_back(d);

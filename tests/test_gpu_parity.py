@@ -404,3 +404,25 @@ def test_need_new_kf_and_curr_frame_is_kf_parity():
         for o in orc:
             o.updateFrame()
     assert n_kf >= n
+
+
+def _odd_octaves(H):
+    """~3% of the left and right keypoints of every tracked frame get octaves outside
+    the pyramid (negative, >= n_levels, beyond int8): the stereo band scan's
+    out-of-range segment and the int8 / HBM octave fallback."""
+    rng = np.random.default_rng(5)
+    for f in range(1, H.F):
+        for b in range(H.B):
+            for arr, n in ((H.kp_r, int(H.n_kp_r[f, b])), (H.kp_l, int(H.n_kp_l[f, b]))):
+                idx = rng.choice(n, max(1, n // 30), replace=False)
+                arr["octave"][f, b, idx] = rng.choice([-1, 4, 5, 7, 200, -128, -100000], len(idx))
+    return H
+
+
+@pytest.mark.parametrize("kp_cap", [2048, 4096])
+def test_out_of_range_octaves_parity(kp_cap):
+    # 2048: the per-octave segmented band scan; 4096: the single sorted list (1024 threads)
+    rep = _run_sequence("vga", {}, n_seq=3, n_frames=3, kp_cap=kp_cap, kl_cap=256,
+                        synth_over=dict(n_kp=900, n_kl=150, n_world_pts=1200, n_world_lines=200), seed=17,
+                        mutate=_odd_octaves)
+    _check(rep)
