@@ -781,17 +781,30 @@ __global__ void k_init_pose(KParams p) {
 }
 
 // estimateStereoUncertainty on the slot passed as `prev`
-__global__ void k_line_uncertainty(KParams p) {
+// lane per line; the two 9-double covariances go through LDS so the block writes its
+// lines' covS / covE ranges with consecutive lanes on consecutive doubles
+__global__ void __launch_bounds__(256) k_line_uncertainty(KParams p) {
+    __shared__ double cs[256 * 9], ce[256 * 9];
     const int b = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i0 = blockIdx.x * blockDim.x;
+    const int i = i0 + threadIdx.x;
     DevLines& L = p.prev.ls;
-    if (i >= L.n[b]) return;
-    const size_t q = (size_t)b * p.kl_cap + i;
-    double spl[2] = {L.spl[2 * q], L.spl[2 * q + 1]}, epl[2] = {L.epl[2 * q], L.epl[2 * q + 1]};
-    double le[3] = {L.le[3 * q], L.le[3 * q + 1], L.le[3 * q + 2]};
-    double cS[9], cE[9];
-    line_uncertainty(p, spl, epl, L.sdisp[q], L.edisp[q], le, cS, cE);
-    for (int k = 0; k < 9; ++k) { L.covS[9 * q + k] = cS[k]; L.covE[9 * q + k] = cE[k]; }
+    const int n = L.n[b];
+    if (i0 >= n) return;   // uniform per block
+    if (i < n) {
+        const size_t q = (size_t)b * p.kl_cap + i;
+        double spl[2] = {L.spl[2 * q], L.spl[2 * q + 1]}, epl[2] = {L.epl[2 * q], L.epl[2 * q + 1]};
+        double le[3] = {L.le[3 * q], L.le[3 * q + 1], L.le[3 * q + 2]};
+        double cS[9], cE[9];
+        line_uncertainty(p, spl, epl, L.sdisp[q], L.edisp[q], le, cS, cE);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { cs[9 * threadIdx.x + k] = cS[k]; ce[9 * threadIdx.x + k] = cE[k]; }
+    }
+    __syncthreads();
+    const int m = 9 * min(256, n - i0);
+    double* dS = L.covS + 9 * ((size_t)b * p.kl_cap + i0);
+    double* dE = L.covE + 9 * ((size_t)b * p.kl_cap + i0);
+    for (int k = threadIdx.x; k < m; k += 256) { dS[k] = cs[k]; dE[k] = ce[k]; }
 }
 
 // Algorithmic HBM bytes of one step of one sequence, per stage (DESIGN.md
