@@ -750,7 +750,10 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
         const double r0 = L.cut[2 * q], r1 = L.cut[2 * q + 1];
         double info[36];
         poseInfoOnLine<true>(cam, p.cfg.homog_th, Dl, d, r0, r1, info);
-        for (int i = 0; i < 36; ++i) L.invcov[36 * q + i] = info[i];
+        // 16-B stores: a line's 36 doubles are contiguous and 288-B aligned (carve: 256-B field base)
+        double2* iv = reinterpret_cast<double2*>(L.invcov + 36 * q);
+#pragma unroll
+        for (int i = 0; i < 18; ++i) iv[i] = make_double2(info[2 * i], info[2 * i + 1]);
         if (!(fabs(r0) < 0.0001 && fabs(r1) < 0.0001)) {
             double sP[3] = {d.sP[0], d.sP[1], d.sP[2]}, eP[3] = {d.eP[0], d.eP[1], d.eP[2]};
             if (fabs(r0) > 0.0001) {
