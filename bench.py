@@ -9,13 +9,29 @@ maxIters = maxItersRef = 10 and minError = minErrorChange = 0.
 
 A "step" = one StereoFrameHandler step (insertStereoPair + optimizePose +
 updateFrame, app/plslam_mod.cpp:387-477) for every one of the B independent
-sequences resident on a GPU.  Input detections for all frames are generated on
-the host (splitmix64, deterministic) and copied to HBM before the timed region.
+sequences resident on a GPU (B = 16384 by default, independent of --steps).
 
-Multi-GPU: one process per GPU (torch.distributed.run); rank r owns sequences
+Input ring: before each step the host generates the next input frame of all B
+sequences (splitmix64, deterministic; gfpl_synth) into pinned memory and
+uploads it into the seqbatch's device staging area (gfpl_upload_frames), both
+outside the timed brackets.  Each step is timed on its own, bracketed by
+barrier + device synchronize on both sides with the inputs resident in HBM;
+the reported time is the sum over the K timed steps (MAX over ranks).  The
+upload is timed separately: `host_fed` is the PCIe-inclusive rate.
+
+Parity at the operating point: `parity_sampled` replays a sample of the timed
+sequences (same ids, same frames) on the CPU oracle after every step and
+compares matched lists, stereo features, cut ratios / invCovPose and poses bit
+for bit.  The oracle is the checker here, never the thing measured.
+
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` without a
+torch.distributed environment launches `torch.distributed.run` with N workers
+(before any GPU call) and exits with its code; rank r owns sequences
 [r*B, (r+1)*B) — no data-path collective (weak scaling); the camera/config
-block is RCCL-broadcast from rank 0 over xGMI at start-up, the elapsed times
-are MAX-reduced.
+block is RCCL-broadcast from rank 0 over xGMI at start-up, B is MIN-reduced,
+times MAX-reduced and frame / mismatch counts SUM-reduced.  `--dry-run` runs
+the launcher, broadcast, sharding, input generation and reductions on CPU
+(gloo) without any tracking step (value null).
 """
 from __future__ import annotations
 
@@ -23,6 +39,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -31,10 +48,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gf-pl-slam_amd"))
-import gfpl  # noqa: E402
 
 STAGES = ["stereo_points", "stereo_lines", "cross_points", "cross_lines", "line_cut", "pose"]
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per 2 cycles
+# per SIMD (MI355X_MICROARCH.md §Wave scheduling) = 1228.8 G wave-instructions/s
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2
 
 WORKLOADS = {
     # name: (camera, synth overrides, description)
@@ -43,76 +62,76 @@ WORKLOADS = {
              "cfg3: KITTI-00 1241x376 stream (synthetic detections), 2000 ORB + 500 LBD, 10+10 GN iters"),
     # BASELINE configs[3]: the EuRoC rig following the ground-truth motion of the 8 EuRoC
     # sequences (config/asl/gt-ass/*), sequence (rank mod 8) on rank r
+    "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0),
+             "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
+             "2000 ORB + 500 LBD, 10+10 GN iters"),
     # BASELINE configs[4]: stress, 8000 ORB + 2000 LBD per 1920x1080 frame, line cut on
     "cfg5": ("stress", dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=2800, z_max=12.0),
              "cfg5: stress 1920x1080 stereo (gazebo x3), 8000 ORB + 2000 LBD per side, good-line-cut on, "
              "10+10 GN iters"),
-    "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0),
-             "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
-             "2000 ORB + 500 LBD, 10+10 GN iters"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16384, help="sequences per GPU (reduced to fit HBM if needed)")
+    ap.add_argument("--batch", type=int, default=16384, help="sequences per GPU (reduced only if HBM is short)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seqs", type=int, default=16)
-    ap.add_argument("--cpu-frames", type=int, default=128)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gen-threads", type=int, default=16, help="host threads generating the input frames")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (and the parity replay)")
+    ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only (gloo): launcher, broadcast, sharding, input generation and reductions; "
+                         "no tracking step is run and value is null")
     ap.add_argument("--diag-every-step", action="store_true",
-                    help="read the per-stage / per-kernel HIP-event times after every timed step "
-                         "(one host sync per step); default: after the last timed step only")
-    ap.add_argument("--input-mem-frac", type=float, default=0.7,
-                    help="max fraction of free HBM used by the staged input frames")
+                    help="read the per-stage / per-kernel HIP-event times after every timed step")
+    ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="PMC traffic summary written by tools/pmc_summary.py (optional)")
-    return ap.parse_args()
+                    help="PMC summary written by tools/pmc_summary.py (HBM traffic, SQ counters)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(cam, cfg, sp, n_threads, n_seqs, n_frames, kp_cap, kl_cap):
-    """The CPU oracle (C++ restatement of the reference path, oracle/) timed on this
-    host: n_seqs sequences x n_frames steps, one sequence per worker thread at a
-    time (ctypes releases the GIL), initialisation and input generation excluded."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    H = gfpl.HostFrames(cam, sp, n_seqs, n_frames + 1, kp_cap, kl_cap, seq0=100000)
-    hs = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in range(n_seqs)]
-    frames = [H.frames(f) for f in range(n_frames + 1)]
-    for b, h in enumerate(hs):
-        h.initialize(frames[0], b)
-    todo = list(range(n_seqs))
-    lock = threading.Lock()
-
-    def worker():
-        while True:
-            with lock:
-                if not todo:
-                    return
-                b = todo.pop()
-            h = hs[b]
-            for k in range(1, n_frames + 1):
-                h.insertStereoPair(frames[k], b)
-                h.optimizePose()
-                h.updateFrame()
-
-    nt = max(1, min(n_threads, n_seqs))
-    th = [threading.Thread(target=worker) for _ in range(nt)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    dt = time.perf_counter() - t0
-    return {"value": n_seqs * n_frames / dt, "unit": "stereo frames/s", "cores": nt, "kind": "port",
-            "sample": f"{n_seqs} sequences x {n_frames} frames of the same workload on {nt} host threads "
-                      f"({dt:.1f} s wall, {os.cpu_count()} CPUs visible)"}
+# ------------------------------------------------------------------ launcher --
+def launch_workers(args) -> int:
+    """--gpus N > 1 without a torch.distributed environment: run N workers through
+    torch.distributed.run as a child process (nothing here touches the GPU)."""
+    port = args.master_port or (29500 + os.getpid() % 2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
+def host_cores():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = int(q) / int(per)
+    except Exception:
+        pass
+    eff = max(1, min(n, int(quota))) if quota else n
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    return eff, {"affinity_cpus": n, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(), "model": model}
+
+
+# ------------------------------------------------------- collectives (RCCL) --
 def shard_first_seq(rank: int, batch: int) -> int:
     """Sequences are partitioned across ranks: rank r owns [r*B, (r+1)*B)."""
     return rank * batch
@@ -140,98 +159,282 @@ def reduce_job(elapsed: float, frames: int, dist, device):
     return float(el.item()), int(cnt.item())
 
 
+def reduce_min_int(v: int, dist, device) -> int:
+    import torch
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def reduce_sum_ints(vals, dist, device):
+    import torch
+    t = torch.tensor(list(vals), dtype=torch.int64, device=device)
+    dist.all_reduce(t)
+    return [int(x) for x in t.tolist()]
+
+
 def load_pmc(path, kernel_name, batch, workload):
-    """HBM bytes per launch of a kernel from the PMC summary (tools/pmc_summary.py),
-    only when it was collected on this workload and batch size."""
+    """Per-launch PMC summary of a kernel (tools/pmc_summary.py), only when it was
+    collected on this workload and batch size."""
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("batch") != batch or d.get("workload", "cfg2") != workload:
             return None
-        return float(d["kernels"][kernel_name]["hbm_bytes_per_launch"])
+        return d["kernels"].get(kernel_name)
     except Exception:
         return None
 
 
+# ------------------------------------------------------- parity at the bench --
+class ParitySampler:
+    """Replays sampled sequences of the timed batch on the CPU oracle (the checker)
+    and compares them with the GPU state after every step, bit for bit."""
+
+    def __init__(self, cam, cfg, kp_cap, kl_cap, seqs, threads):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as O
+        import parity as PT
+        self.PT = PT
+        self.seqs = list(seqs)
+        self.orc = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in self.seqs]
+        self.threads = max(1, min(threads, len(self.seqs)))
+        self.frames = self.mismatch_frames = 0
+        self.msgs = []
+
+    def _par(self, fn):
+        todo = list(range(len(self.seqs)))
+        lock = threading.Lock()
+
+        def work():
+            while True:
+                with lock:
+                    if not todo:
+                        return
+                    i = todo.pop()
+                fn(i)
+        th = [threading.Thread(target=work) for _ in range(self.threads)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    def initialize(self, host_frames, h):
+        self._par(lambda i: self.orc[i].initialize(host_frames, self.seqs[i]))
+        for i, b in enumerate(self.seqs):
+            self._record(self.PT.compare_core(h.read_frame(0, b), self.orc[i].read_frame(0), f"init s{b} "))
+
+    def step(self, host_frames, h, k):
+        # GPU side first (the ABI reads synchronise; the state is the step's result)
+        g_new = [h.read_frame(0, b) for b in self.seqs]      # PREV after update = the new frame
+        g_old = [h.read_frame(1, b) for b in self.seqs]      # CURR slot = the old prev (cut results)
+        g_tr = [h.read_last_track(b) for b in self.seqs]
+        res = [None] * len(self.seqs)
+
+        def run(i):
+            o = self.orc[i]
+            o.insertStereoPair(host_frames, self.seqs[i])
+            o.optimizePose()
+            res[i] = (o.read_frame(1), o.read_frame(0), o.read_track())
+            o.updateFrame()
+        self._par(run)
+        PT = self.PT
+        for i, b in enumerate(self.seqs):
+            o_new, o_old, o_tr = res[i]
+            tag = f"f{k} s{b} "
+            bad = PT.compare_core(g_new[i], o_new, tag) + PT.compare_track(g_tr[i], o_tr, tag)
+            pb, exact = PT.compare_pose(g_new[i], o_new, what=tag)
+            bad += pb if pb else ([] if exact else [tag + "pose not bit-identical"])
+            if not PT.compare_track(g_tr[i], o_tr):
+                bad += PT.compare_prev_matched(g_old[i], o_old, o_tr, tag)
+            self._record(bad)
+
+    def _record(self, bad):
+        self.frames += 1
+        if bad:
+            self.mismatch_frames += 1
+            self.msgs += bad[:3]
+
+
+def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, gen_threads):
+    """The CPU oracle (C++ restatement of the reference path, oracle/) timed on this
+    host: one sequence per worker thread, frames generated in chunks of 8 outside the
+    timed region, chunks timed until about target_s seconds of work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import gfpl
+    import oracle as O
+    n_seqs, chunk = n_threads, 8
+    hs = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in range(n_seqs)]
+    seq0 = 1 << 20
+    H = gfpl.HostFrames(cam, sp, n_seqs, 1, kp_cap, kl_cap, seq0=seq0, frame0=0, threads=gen_threads)
+    for b, h in enumerate(hs):
+        h.initialize(H.frames(0), b)
+    timed, frames, f0 = 0.0, 0, 1
+    while timed < target_s and f0 < 2000:
+        H = gfpl.HostFrames(cam, sp, n_seqs, chunk, kp_cap, kl_cap, seq0=seq0, frame0=f0, threads=gen_threads)
+
+        def worker(b):
+            h = hs[b]
+            for k in range(chunk):
+                h.insertStereoPair(H.frames(k), b)
+                h.optimizePose()
+                h.updateFrame()
+        th = [threading.Thread(target=worker, args=(b,)) for b in range(n_seqs)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        timed += time.perf_counter() - t0
+        frames += n_seqs * chunk
+        f0 += chunk
+    return {"value": frames / timed, "unit": "stereo frames/s", "cores": n_threads, "kind": "port",
+            "sample": f"{n_seqs} sequences x {f0 - 1} frames of the same workload, one sequence per host thread "
+                      f"({timed:.1f} s timed; oracle/ C++ -O3 restatement; input generation excluded)",
+            "host": cores_info}
+
+
+# ----------------------------------------------------------------------- main --
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if args.gpus > 1 and world == 0:
+        sys.exit(launch_workers(args))
+    world = world or 1
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+
+    import torch
+    import torch.distributed as dist
+    import gfpl
+
+    dry = args.dry_run
+    if dry:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if not torch.cuda.is_available():
+            print("error: no GPU visible (bench.py measures the HIP path; --dry-run rehearses the launcher on CPU)",
+                  file=sys.stderr)
+            sys.exit(3)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
     cam_name, synth_over, desc = WORKLOADS[args.workload]
     cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     cam = gfpl.make_camera(cam_name, cfg)
     if world > 1:
-        # RCCL broadcast of the camera + config block (SURVEY §5(h)); every rank
-        # then runs with rank 0's bytes.
+        # RCCL broadcast of the camera + config block (SURVEY §8(e)); every rank
+        # then runs with rank 0's bytes
         broadcast_setup(cam, cfg, dist, dev)
 
     B, W, K = args.batch, args.warmup, args.steps
     KP, KL = (8192, 2048) if args.workload == "cfg5" else (2048, 512)
-    F = 1 + W + K
     keep = []
     if args.workload == "cfg4":
         T, t = gfpl.euroc_traj(gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)], 64)
         keep += [T, t]   # the generator reads them through raw pointers
-        if F > len(t):
-            print(f"note: {F} frames > {len(t)} ground-truth poses; the trajectory wraps", file=sys.stderr)
         synth_over = dict(synth_over, traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data)
-        desc = desc + f" [this rank: {gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)]}]"
+        desc = desc + f" [rank 0: {gfpl.EUROC_SEQS[0]}]"
     sp = gfpl.synth_params(**synth_over)
-    # all F input frames of the B sequences are staged in HBM before timing; bound
-    # them to a fraction of device memory (SURVEY §8(d): inputs resident)
-    free, total = torch.cuda.mem_get_info(dev)
-    per_seq_frame = gfpl.input_bytes_per_frame(cam, KP, KL)
-    b_fit = int(args.input_mem_frac * free // (per_seq_frame * F)) // 64 * 64
-    if b_fit < B:
-        print(f"note: --batch {B} x {F} frames does not fit; using {b_fit} sequences", file=sys.stderr)
-        B = max(64, b_fit)
+    per_in = gfpl.input_bytes_per_frame(cam, KP, KL)
+
+    if not dry:
+        # device footprint per sequence: resident state + one staged input frame
+        ctx = gfpl.Context(cam, cfg, device=local, stream=torch.cuda.current_stream(dev).cuda_stream)
+        probe = gfpl.StereoFrameHandler(ctx, 64, KP, KL)
+        per_state = probe.nbytes() / 64
+        probe.close()
+        free, _ = torch.cuda.mem_get_info(dev)
+        b_fit = int(0.85 * free // (per_state + per_in)) // 64 * 64
+        if b_fit < B:
+            print(f"note: --batch {B} does not fit in HBM; using {b_fit} sequences", file=sys.stderr)
+            B = max(64, b_fit)
+    if world > 1:
+        B = reduce_min_int(B, dist, dev)   # one B on every rank: shards [r*B, (r+1)*B)
+    seq0 = shard_first_seq(rank, B)
+
+    cores, cores_info = host_cores()
+    gen_threads = max(1, min(args.gen_threads, cores))
+    hb = gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=not dry)
+    t_gen = 0.0
     t0 = time.perf_counter()
-    D = gfpl.DeviceFrames.generate(cam, sp, B, F, KP, KL, seq0=shard_first_seq(rank, B), device=dev, threads=16)
-    t_gen = time.perf_counter() - t0
-    in_bytes = D.nbytes()
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    ctx = gfpl.Context(cam, cfg, device=local, stream=stream)
+    hb.fill(0, gen_threads)
+    t_gen += time.perf_counter() - t0
+
+    if dry:
+        frames_total = B * K
+        if world > 1:
+            _, frames_total = reduce_job(0.0, B * K, dist, dev)
+        if rank == 0:
+            print(json.dumps({"metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)", "value": None,
+                              "unit": "stereo frames/s", "n_gpus": world, "steps": K, "warmup": W,
+                              "dry_run": True, "frames_sharded": frames_total,
+                              "config": {"workload": desc, "sequences_per_gpu": B,
+                                         "parallelism": f"sequences sharded 1/{world} per GPU"},
+                              "input_bytes_per_step": int(hb.nbytes())}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     h = gfpl.StereoFrameHandler(ctx, B, KP, KL)
-    h.initialize(D.frames(0))
-    for w in range(W):
-        h.frameStep(D.frames(1 + w))
-    torch.cuda.synchronize(dev)
-    ctx.set_timing(True)
+    sampler = None
+    if not args.no_cpu and args.parity_seqs > 0:
+        n = min(args.parity_seqs, B)
+        sampler = ParitySampler(cam, cfg, KP, KL, [int(x) for x in np.linspace(0, B - 1, n)], cores)
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    dv = h.upload_frames(hb.frames())
+    h.initialize(dv)
+    if sampler:
+        sampler.initialize(hb.frames(), h)
+    step_s, up_s = [], []
     stage_ms, stage_bytes, kern_ms, kern_bytes = [], [], [], []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(K):
-        h.frameStep(D.frames(1 + W + k))
-        if args.diag_every_step or k == K - 1:
-            # HIP events on the context stream; reading them synchronises, so by default
-            # only the last timed step is sampled (the steps are statistically identical)
-            stage_ms.append(ctx.stage_times())
-            stage_bytes.append(h.last_step_stage_bytes())
-            kern_ms.append(ctx.kernel_times())
-            kern_bytes.append(h.last_step_kernel_bytes())
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t_max, frames_total = reduce_job(elapsed, B * K, dist, dev)   # SURVEY §5(h)
-    else:
-        t_max, frames_total = elapsed, B * K
-    # tracking health: fraction of sequences still tracked
+    ctx.set_timing(True)
+    for k in range(1, 1 + W + K):
+        t0 = time.perf_counter()
+        hb.fill(k, gen_threads)                       # host input generation (untimed)
+        t_gen += time.perf_counter() - t0
+        sync_all()
+        tu0 = time.perf_counter()
+        dv = h.upload_frames(hb.frames())             # PCIe: synchronous, timed separately
+        tu1 = time.perf_counter()
+        sync_all()
+        ts0 = time.perf_counter()
+        h.frameStep(dv)                               # the step: inputs resident in HBM
+        sync_all()
+        ts1 = time.perf_counter()
+        timed = k > W
+        if timed:
+            step_s.append(ts1 - ts0)
+            up_s.append(tu1 - tu0)
+            if args.diag_every_step or k == W + K:
+                stage_ms.append(ctx.stage_times())
+                stage_bytes.append(h.last_step_stage_bytes())
+                kern_ms.append(ctx.kernel_times())
+                kern_bytes.append(h.last_step_kernel_bytes())
+        if sampler:
+            sampler.step(hb.frames(), h, k)
+    elapsed, up_total = float(np.sum(step_s)), float(np.sum(up_s))
     lost = sum(h.read_track(b)["num_frame_loss"] > 0 for b in range(0, B, max(1, B // 16)))
+    par = [sampler.frames, sampler.mismatch_frames] if sampler else [0, 0]
+    if world > 1:
+        t_max, frames_total = reduce_job(elapsed, B * K, dist, dev)
+        t_up_max, _ = reduce_job(elapsed + up_total, 0, dist, dev)
+        par = reduce_sum_ints(par, dist, dev)
+    else:
+        t_max, frames_total, t_up_max = elapsed, B * K, elapsed + up_total
 
     if rank == 0:
         sm = np.mean(np.array(stage_ms, dtype=np.float64)[:, :6], axis=0)
@@ -239,20 +442,29 @@ def main():
         km = np.mean(np.array(kern_ms, dtype=np.float64), axis=0)
         kb = np.mean(np.array(kern_bytes), axis=0).astype(np.float64)
         # candidate kernels for the roofline line: the single-kernel stages and the
-        # two kernels that dominate the line-cut and pose stages
+        # kernels that dominate the line-cut and pose stages
         cands = {"k_stereo_points": (sm[0], sb[0]), "k_stereo_lines": (sm[1], sb[1]),
                  "k_cross_points": (sm[2], sb[2]), "k_cross_lines": (sm[3], sb[3]),
                  "k_cut_search": (km[1], kb[1]), "k_pose": (km[3], kb[3])}
-        kname = max(cands, key=lambda k: cands[k][0])
+        kname = max(cands, key=lambda x: cands[x][0])
         k_ms, k_bytes = cands[kname]
         achieved = k_bytes / (k_ms * 1e-3) / 1e9
         step_bytes = float(np.mean(np.array(stage_bytes)[:, 6]))
-        ms_step = t_max / K * 1e3
         value = frames_total / t_max
-        traffic = load_pmc(args.pmc, kname, B, args.workload)
+        pmc = load_pmc(args.pmc, kname, B, args.workload) or {}
+        traffic = pmc.get("hbm_bytes_per_launch")
+        roof_valu = None
+        if pmc.get("SQ_INSTS_VALU"):
+            gips = pmc["SQ_INSTS_VALU"] / (k_ms * 1e-3) / 1e9
+            roof_valu = {"bound": "valu", "kernel": kname, "achieved": gips, "peak": VALU_PEAK_GIPS,
+                         "unit": "G wave-VALU-instructions/s", "frac": gips / VALU_PEAK_GIPS,
+                         "valu_insts_per_launch": pmc["SQ_INSTS_VALU"], "waves_per_launch": pmc.get("SQ_WAVES"),
+                         "source": os.path.relpath(args.pmc, ROOT)}
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(cam, cfg, sp, args.cpu_threads, args.cpu_seqs, args.cpu_frames, KP, KL)
+            nt = args.cpu_threads or cores
+            cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads)
+        in_bytes = hb.nbytes()
         out = {
             "metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)",
             "value": value,
@@ -260,24 +472,38 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": W,
-            "ms_per_step": ms_step,
+            "ms_per_step": t_max / K * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth)",
-            "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": int(sp.n_kp), "kl_per_side": int(sp.n_kl),
-                       "gn_iters": "10+10", "parallelism": f"sequences sharded 1/{world} per GPU"},
+            "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth), "
+                    "generated per step on the host and uploaded to HBM before each timed step",
+            "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": int(sp.n_kp),
+                       "kl_per_side": int(sp.n_kl), "gn_iters": "10+10",
+                       "parallelism": f"sequences sharded 1/{world} per GPU",
+                       "timing": "sum of K per-step brackets (barrier + device sync both sides), MAX over ranks"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": float(achieved), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": float(achieved / HBM_PEAK_GBS), "traffic": traffic,
                          "algorithmic_bytes_per_launch": float(k_bytes), "avg_launch_ms": float(k_ms)},
+            "roofline_valu": roof_valu,
             "hbm_frac_step": float(step_bytes / (t_max / K) / 1e9 / HBM_PEAK_GBS),
+            "parity_sampled": {"sequences": len(sampler.seqs) * world if sampler else 0,
+                               "frames": par[0], "mismatches": par[1],
+                               "compared": "stereo features, matched lists, inlier counts, cut ratios, invCovPose, "
+                                           "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise",
+                               "first": sampler.msgs[:3] if sampler else []},
+            "host_fed": {"value": frames_total / t_up_max, "unit": "stereo frames/s",
+                         "upload_ms_per_step": up_total / K * 1e3,
+                         "upload_GBps": in_bytes * K / up_total / 1e9,
+                         "input_bytes_per_step": int(in_bytes),
+                         "note": "each step's inputs copied from pinned host memory through gfpl_upload_frames "
+                                 "(PCIe) then the step; detection / generation excluded"},
             "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES, sm)},
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
             "stage_bytes_per_step": {n: int(v) for n, v in zip(STAGES, sb)},
             "cpu_baseline": cpu,
             "gen_s": round(t_gen, 2),
-            "input_hbm_bytes": in_bytes,
             "lost_sampled": int(lost),
         }
         print(json.dumps(out))

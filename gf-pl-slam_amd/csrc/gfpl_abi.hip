@@ -23,6 +23,7 @@ struct gfpl_ctx {
     bool timing = false;
     hipEvent_t ev[GFPL_NEV]{};
     float stage_ms[7]{};
+    std::vector<gfpl_seqbatch*> sbs;   // live seqbatches: their match-list capacities bound gfpl_set_config
 };
 
 struct gfpl_seqbatch {
@@ -38,6 +39,8 @@ struct gfpl_seqbatch {
     DevScratch scr{};
     void* stage = nullptr;   // device staging of one uploaded input batch (gfpl_upload_frames)
     size_t stage_bytes = 0;
+    int32_t* last_n_pt = nullptr;   // [B] list lengths before the last gfpl_update_frame
+    int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
 };
 
 namespace {
@@ -118,6 +121,8 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
     sb->scr.pose_dtini = c.take<double>(B * 16);
     sb->scr.kf_mask = c.take<int32_t>(B);
+    sb->last_n_pt = c.take<int32_t>(B);
+    sb->last_n_ls = c.take<int32_t>(B);
 }
 
 DevCam devcam(const gfpl_camera& c) {
@@ -146,6 +151,11 @@ KParams params(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (in) p.in = *in;
     p.B = sb->B; p.kp_cap = sb->kp_cap; p.kl_cap = sb->kl_cap;
     p.mpt_cap = sb->mpt_cap; p.mls_cap = sb->mls_cap;
+    // the kernels index matched_pt / matched_ls / cut and pose scratch with the
+    // seqbatch's capacities; gfpl_set_config refuses larger budgets while this
+    // seqbatch lives, so these clamps never change a result (defence in depth)
+    p.cfg.max_point_match_num = std::min(p.cfg.max_point_match_num, sb->mpt_cap);
+    p.cfg.max_line_match_num = std::min(p.cfg.max_line_match_num, sb->mls_cap);
     return p;
 }
 
@@ -194,6 +204,7 @@ int gfpl_create(int device, void* stream, gfpl_ctx** out) {
 
 int gfpl_destroy(gfpl_ctx* c) {
     if (!c) return GFPL_E_INVALID;
+    if (!c->sbs.empty()) return GFPL_E_STATE;   // its seqbatches use the context's stream and config
     for (int i = 0; i < GFPL_NEV; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
@@ -219,6 +230,10 @@ int gfpl_set_config(gfpl_ctx* c, const gfpl_config* cfg) {
     if (!c || !cfg) return GFPL_E_INVALID;
     int e = cfg_supported(*cfg);
     if (e) return e;
+    // match budgets size the lists of every live seqbatch (gfpl_seqbatch_create):
+    // a larger budget would index past them
+    for (const gfpl_seqbatch* sb : c->sbs)
+        if (cfg->max_point_match_num > sb->mpt_cap || cfg->max_line_match_num > sb->mls_cap) return GFPL_E_CAPACITY;
     c->cfg = *cfg;
     c->has_cfg = true;
     return GFPL_OK;
@@ -264,6 +279,7 @@ int gfpl_seqbatch_create(gfpl_ctx* c, int batch, int kp_cap, int kl_cap, gfpl_se
     if (sb->kp_cap != kp_cap || sb->kl_cap != kl_cap) {   // caps must match the input layout
         (void)hipFree(sb->base); delete sb; return GFPL_E_INVALID;
     }
+    c->sbs.push_back(sb);
     *out = sb;
     return GFPL_OK;
 }
@@ -271,6 +287,8 @@ int gfpl_seqbatch_create(gfpl_ctx* c, int batch, int kp_cap, int kl_cap, gfpl_se
 int gfpl_seqbatch_destroy(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     (void)hipStreamSynchronize(sb->ctx->stream);
+    auto& v = sb->ctx->sbs;
+    v.erase(std::remove(v.begin(), v.end(), sb), v.end());
     if (sb->base) (void)hipFree(sb->base);
     if (sb->stage) (void)hipFree(sb->stage);
     delete sb;
@@ -471,6 +489,11 @@ int gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* 
 int gfpl_update_frame(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    // the cleared lists stay readable until the next insert (gfpl_read_last_track)
+    HIPCHK(hipMemcpyAsync(sb->last_n_pt, sb->tr.n_matched_pt, sizeof(int32_t) * sb->B, hipMemcpyDeviceToDevice,
+                          sb->ctx->stream));
+    HIPCHK(hipMemcpyAsync(sb->last_n_ls, sb->tr.n_matched_ls, sizeof(int32_t) * sb->B, hipMemcpyDeviceToDevice,
+                          sb->ctx->stream));
     // matched_pt.clear(); matched_ls.clear() (src/stereoFrameHandler.cpp:889-890)
     HIPCHK(hipMemsetAsync(sb->tr.n_matched_pt, 0, sizeof(int32_t) * sb->B, sb->ctx->stream));
     HIPCHK(hipMemsetAsync(sb->tr.n_matched_ls, 0, sizeof(int32_t) * sb->B, sb->ctx->stream));
@@ -781,6 +804,24 @@ int gfpl_read_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* o) {
     std::memset(o, 0, sizeof(*o));
     XFER(d2h, &o->n_matched_pt, sb->tr.n_matched_pt + seq, 1);
     XFER(d2h, &o->n_matched_ls, sb->tr.n_matched_ls + seq, 1);
+    XFER(d2h, &o->n_inliers, sb->tr.n_inliers + seq, 1);
+    XFER(d2h, &o->n_inliers_pt, sb->tr.n_inliers_pt + seq, 1);
+    XFER(d2h, &o->n_inliers_ls, sb->tr.n_inliers_ls + seq, 1);
+    XFER(d2h, &o->num_frame_loss, sb->tr.num_frame_loss + seq, 1);
+    HIPCHK(hipStreamSynchronize(s));
+    XFER(d2h, o->matched_pt, sb->tr.matched_pt + (size_t)seq * sb->mpt_cap, (size_t)o->n_matched_pt);
+    XFER(d2h, o->matched_ls, sb->tr.matched_ls + (size_t)seq * sb->mls_cap, (size_t)o->n_matched_ls);
+    HIPCHK(hipStreamSynchronize(s));
+    return GFPL_OK;
+}
+
+int gfpl_read_last_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* o) {
+    if (!sb || !o || seq < 0 || seq >= sb->B) return GFPL_E_INVALID;
+    hipStream_t s = sb->ctx->stream;
+    HIPCHK(hipStreamSynchronize(s));
+    std::memset(o, 0, sizeof(*o));
+    XFER(d2h, &o->n_matched_pt, sb->last_n_pt + seq, 1);
+    XFER(d2h, &o->n_matched_ls, sb->last_n_ls + seq, 1);
     XFER(d2h, &o->n_inliers, sb->tr.n_inliers + seq, 1);
     XFER(d2h, &o->n_inliers_pt, sb->tr.n_inliers_pt + seq, 1);
     XFER(d2h, &o->n_inliers_ls, sb->tr.n_inliers_ls + seq, 1);

@@ -263,6 +263,7 @@ def hiplib() -> C.CDLL:
             "gfpl_optimize_pose_ini": ([P, P], C.c_int),
             "gfpl_update_frame": ([P], C.c_int),
             "gfpl_frame_step": ([P, P], C.c_int),
+            "gfpl_upload_frames": ([P, P, P], C.c_int),
             "gfpl_stereo_points": ([P, P], C.c_int),
             "gfpl_stereo_lines": ([P, P], C.c_int),
             "gfpl_line_uncertainty": ([P], C.c_int),
@@ -275,6 +276,7 @@ def hiplib() -> C.CDLL:
             "gfpl_read_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_write_frame": ([P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_read_track": ([P, C.c_int, P], C.c_int),
+            "gfpl_read_last_track": ([P, C.c_int, P], C.c_int),
             "gfpl_need_new_kf": ([P, P], C.c_int),
             "gfpl_curr_frame_is_kf": ([P, P], C.c_int),
             "gfpl_read_kf_state": ([P, C.c_int, P], C.c_int),
@@ -414,6 +416,53 @@ class HostFrames:
         """gfpl_frames with HOST pointers for frame f (what the oracle reads)."""
         a = [x[f] for x in self.arrays()]
         return make_frames(self.B, self.kp_cap, self.kl_cap, a)
+
+
+class HostBatch:
+    """One input frame of B sequences in host memory, refilled in place frame by frame
+    (the bench's input ring: generate on the host, upload with gfpl_upload_frames).
+    pinned=True page-locks the buffers (torch pinned memory) so the upload runs at the
+    PCIe DMA rate."""
+
+    def __init__(self, cam: Camera, sp: SynthParams, n_seq: int, kp_cap: int, kl_cap: int,
+                 seq0: int = 0, pinned: bool = False):
+        self.cam, self.sp, self.B, self.kp_cap, self.kl_cap, self.seq0 = cam, sp, n_seq, kp_cap, kl_cap, seq0
+        B = n_seq
+        spec = [((B,), np.int32), ((B,), np.int32), ((B, kp_cap), KEYPOINT_DT), ((B, kp_cap), KEYPOINT_DT),
+                ((B, kp_cap, DESC), np.uint8), ((B, kp_cap, DESC), np.uint8),
+                ((B,), np.int32), ((B,), np.int32), ((B, kl_cap), KEYLINE_DT), ((B, kl_cap), KEYLINE_DT),
+                ((B, kl_cap, DESC), np.uint8), ((B, kl_cap, DESC), np.uint8),
+                ((B, cam.pyr_bytes), np.uint8), ((B,), np.float64)]
+        self._keep, self._arrs = [], []
+        for shape, dt in spec:
+            dt = np.dtype(dt)
+            n = int(np.prod(shape)) * dt.itemsize
+            if pinned:
+                import torch
+                t = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+                self._keep.append(t)
+                a = t.numpy().view(dt).reshape(shape)
+            else:
+                a = np.zeros(shape, dt)
+            self._arrs.append(a)
+        self.frame_idx = -1
+
+    def arrays(self):
+        return self._arrs
+
+    def fill(self, frame_idx: int, threads: int = 0):
+        """Generate frame `frame_idx` of sequences [seq0, seq0 + B) (gfpl_synth_batch)."""
+        threads = threads or min(16, os.cpu_count() or 1)
+        check(synthlib().gfpl_synth_batch(
+            C.byref(self.sp), C.byref(self.cam), self.seq0, self.B, frame_idx, 1, self.kp_cap, self.kl_cap,
+            *[_ptr(a) for a in self._arrs], threads), "synth_batch")
+        self.frame_idx = frame_idx
+
+    def frames(self) -> Frames:
+        return make_frames(self.B, self.kp_cap, self.kl_cap, self._arrs)
+
+    def nbytes(self) -> int:
+        return sum(a.nbytes for a in self._arrs)
 
 
 def make_frames(B: int, kp_cap: int, kl_cap: int, arrs) -> Frames:
@@ -651,6 +700,14 @@ class StereoFrameHandler:
         check(self.L.gfpl_line_cut(self.h), "line_cut")
 
     # state transfer
+    def upload_frames(self, host: Frames) -> Frames:
+        """gfpl_upload_frames: copy one batch of HOST input frames into the seqbatch's
+        device staging area (synchronous, PCIe) and return its device view."""
+        dev = Frames()
+        check(self.L.gfpl_upload_frames(self.h, C.byref(host), C.byref(dev)), "upload_frames")
+        dev._keep = [host]
+        return dev
+
     def read_frame(self, which: int, seq: int) -> FrameHost:
         fh = FrameHost(self.kp_cap, self.kl_cap)
         check(self.L.gfpl_read_frame(self.h, which, seq, fh.ptr()), "read_frame")
@@ -662,6 +719,13 @@ class StereoFrameHandler:
     def read_track(self, seq: int) -> dict:
         t = TrackHost()
         check(self.L.gfpl_read_track(self.h, seq, C.byref(t)), "read_track")
+        return t.as_dict()
+
+    def read_last_track(self, seq: int) -> dict:
+        """The track of the step before the last updateFrame / frameStep: the matched lists
+        it cleared and the inlier counters (gfpl_read_last_track)."""
+        t = TrackHost()
+        check(self.L.gfpl_read_last_track(self.h, seq, C.byref(t)), "read_last_track")
         return t.as_dict()
 
     # keyframe decision (src/stereoFrameHandler.cpp:2309-2379)

@@ -122,9 +122,16 @@ StereoFrameHandler::StereoFrameHandler(PinholeStereoCamera* cam_, int device, in
     : cam(cam_), kp_cap_(kp_cap), kl_cap_(kl_cap) {
     check(gfpl_create(device, nullptr, &ctx_), "gfpl_create");
     check(gfpl_set_camera(ctx_, &cam->abi()), "gfpl_set_camera");
+    // one sequence per handler: size its matched lists for the largest budgets the
+    // ABI accepts, so a later Config::maxPointMatchNum() / maxLineMatchNum() change
+    // (e.g. the gazebo value 1000, src/config.cpp:89) stays within the seqbatch
     cfg_ = Config::abi();
-    check(gfpl_set_config(ctx_, &cfg_), "gfpl_set_config");
+    gfpl_config widest = cfg_;
+    widest.max_point_match_num = GFPL_MAX_MATCHED_PT;
+    widest.max_line_match_num = GFPL_MAX_MATCHED_LS;
+    check(gfpl_set_config(ctx_, &widest), "gfpl_set_config");
     check(gfpl_seqbatch_create(ctx_, 1, kp_cap_, kl_cap_, &sb_), "gfpl_seqbatch_create");
+    check(gfpl_set_config(ctx_, &cfg_), "gfpl_set_config");
     buf_ = new HostBuf(kp_cap_, kl_cap_);
 }
 

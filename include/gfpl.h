@@ -228,8 +228,13 @@ int  gfpl_camera_init(gfpl_camera* cam, int width, int height, double fx, double
 /* context: device + stream + camera + config (replaces the Config singleton
  * src/config.cpp:158-162 and the PinholeStereoCamera* each frame holds).   */
 int  gfpl_create(int device, void* hip_stream, gfpl_ctx** out);
+/* GFPL_E_STATE while seqbatches created on the context are still alive.       */
 int  gfpl_destroy(gfpl_ctx* ctx);
 int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
+/* max_point_match_num / max_line_match_num size the matched lists and the cut /
+ * pose scratch of a seqbatch when it is created; while any seqbatch of the
+ * context lives, a config with a larger budget than its capacity is refused with
+ * GFPL_E_CAPACITY (lower budgets are accepted).                                */
 int  gfpl_set_config(gfpl_ctx* ctx, const gfpl_config* cfg);
 int  gfpl_get_camera(const gfpl_ctx* ctx, gfpl_camera* cam);
 int  gfpl_get_config(const gfpl_ctx* ctx, gfpl_config* cfg);
@@ -385,6 +390,11 @@ int  gfpl_read_frame(gfpl_seqbatch* sb, int which, int seq, gfpl_frame_host* out
 int  gfpl_write_frame(gfpl_seqbatch* sb, int which, int seq, const gfpl_frame_host* in);
 int  gfpl_read_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* out);
 int  gfpl_write_track(gfpl_seqbatch* sb, int seq, const gfpl_track_host* in);
+/* The track of the step before the last gfpl_update_frame / gfpl_frame_step: the
+ * matched lists it cleared (matched_pt.clear(), src/stereoFrameHandler.cpp:889-890)
+ * as they stood, and the inlier counters.  Valid until the next insert; lets a
+ * caller that drives gfpl_frame_step inspect each step without splitting it.  */
+int  gfpl_read_last_track(gfpl_seqbatch* sb, int seq, gfpl_track_host* out);
 
 /* ----------------------------------------------------- instrumentation ---- */
 /* Per-stage device time of the last gfpl_frame_step (HIP events on the

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_bench_json_contract():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--batch", "128", "--steps", "2",
-                        "--warmup", "1", "--cpu-seqs", "2", "--cpu-frames", "2", "--cpu-threads", "2"],
+                        "--warmup", "1", "--cpu-seconds", "0.5", "--cpu-threads", "2", "--parity-seqs", "4"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -30,5 +30,9 @@ def test_bench_json_contract():
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert rf["achieved"] > 0 and rf["peak"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
     assert "traffic" in rf
+    ps = d["parity_sampled"]
+    assert ps["sequences"] == 4 and ps["frames"] == 4 * 4 and ps["mismatches"] == 0, ps
+    hf = d["host_fed"]
+    assert 0 < hf["value"] < d["value"] and hf["upload_GBps"] > 0
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]

@@ -426,3 +426,38 @@ def test_out_of_range_octaves_parity(kp_cap):
                         synth_over=dict(n_kp=900, n_kl=150, n_world_pts=1200, n_world_lines=200), seed=17,
                         mutate=_odd_octaves)
     _check(rep)
+
+
+def test_line_cut_ill_conditioned_s_parity():
+    """Near-singular S in the certified cut search: budgets of 2 points and 4-6 lines
+    leave S = invCov_sum - info_m(0,0) built from a handful of rank-1 / rank-2 terms,
+    so its LLT pivots collapse; such lines must fall back to the reference's exact
+    steps (GFPL_CUT_MIN_PIVOT, k_cut.hip) and the ratios / poses equal the oracle."""
+    for pts, lns in ((2, 4), (3, 6), (0 + 1, 5)):
+        rep = _run_sequence("vga", dict(cut_certify=1e-9, max_point_match_num=pts, max_line_match_num=lns,
+                                        max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
+                            n_seq=6, n_frames=3, kp_cap=1024, kl_cap=256,
+                            synth_over=dict(n_kp=700, n_kl=160, n_world_pts=900, n_world_lines=220), seed=37 + lns)
+        _check(rep)
+
+
+def test_match_budget_raise_after_seqbatch_refused():
+    """A seqbatch sizes matched_pt / matched_ls and the cut / pose scratch from the
+    config's budgets at creation: a larger budget while it lives is refused
+    (GFPL_E_CAPACITY), a smaller one is accepted, and after the seqbatch is gone the
+    larger one is accepted again; the context refuses destruction while it lives."""
+    L = gfpl.hiplib()
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    ctx = gfpl.Context(cam, cfg)
+    h = gfpl.StereoFrameHandler(ctx, 2, 512, 128)
+    raised = gfpl.default_config(max_point_match_num=1000)   # the gazebo value, src/config.cpp:89
+    assert L.gfpl_set_config(ctx.h, C.byref(raised)) == -5
+    raised = gfpl.default_config(max_line_match_num=301)
+    assert L.gfpl_set_config(ctx.h, C.byref(raised)) == -5
+    lower = gfpl.default_config(max_point_match_num=100, max_line_match_num=50)
+    assert L.gfpl_set_config(ctx.h, C.byref(lower)) == 0
+    assert L.gfpl_destroy(ctx.h) == -6
+    h.close()
+    raised = gfpl.default_config(max_point_match_num=1000)
+    assert L.gfpl_set_config(ctx.h, C.byref(raised)) == 0

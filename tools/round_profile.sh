@@ -1,25 +1,38 @@
 #!/bin/bash
-# Full measurement session on one GPU box:
+# Full measurement session on one GPU box (every GPU step under its own time limit,
+# chained so the script stops at the first failure):
 #   1. GPU parity tests
-#   2. PMC traffic passes (FETCH_SIZE, WRITE_SIZE; --kernel-trace only) on the bench
-#      workload -> profiles/pmc_latest.json (read by bench.py's roofline.traffic)
-#   3. the default bench line (with CPU baseline)
+#   2. PMC passes on the bench workload (FETCH_SIZE, WRITE_SIZE, SQ instruction /
+#      cycle counters; --kernel-trace only, one group per pass) -> $OUT/pmc_latest.json
+#      and profiles/pmc_latest.json (read by bench.py: roofline.traffic, roofline_valu)
+#   3. the default bench line (CPU baseline + sampled parity)
 #   4. rocprofv3 --kernel-trace --stats of the same bench command
-# Every GPU step has its own time limit; the script stops at the first failure.
+# Usage: bash tools/round_profile.sh [bench args...]   (env: SKIP_TESTS=1, OUT=...)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/round
+OUT=${OUT:-gpurun_out/round}
 rm -rf $OUT && mkdir -p $OUT/pmc
 BENCH_ARGS="$@"
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -20 $OUT/pytest_gpu.log; exit 1; }
-tail -1 $OUT/pytest_gpu.log
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d $OUT/pmc/$c -o $c -f csv -- \
-      python3 bench.py --no-cpu --steps 2 --warmup 1 $BENCH_ARGS > $OUT/pmc/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $OUT/pmc/$c.log; exit 1; }
-done
-python3 tools/pmc_summary.py $OUT/pmc ${PMC_BATCH:-16384} profiles/pmc_latest.json ${PMC_WORKLOAD:-cfg2} > $OUT/pmc/summary.txt && cp profiles/pmc_latest.json $OUT/pmc_latest.json || exit 1
-timeout -k 10 600 python3 bench.py $BENCH_ARGS > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 1; }
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 \
+    || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+  tail -1 $OUT/pytest_gpu.log
+fi
+pmc() {   # name counters...
+  local name=$1; shift
+  timeout -k 10 500 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/pmc/$name -o $name -f csv -- \
+      python3 bench.py --no-cpu --steps 2 --warmup 1 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
+    || { echo "pmc $name failed"; tail -5 $OUT/pmc/$name.log; return 1; }
+}
+pmc fetch FETCH_SIZE && \
+pmc write WRITE_SIZE && \
+pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY || exit 1
+B=$(python3 -c "import json,sys; print(json.loads([l for l in open('$OUT/pmc/fetch.log') if l.startswith('{')][-1])['config']['sequences_per_gpu'])") || exit 1
+python3 tools/pmc_summary.py $OUT/pmc $B $OUT/pmc_latest.json ${PMC_WORKLOAD:-cfg2} > $OUT/pmc/summary.txt && cp $OUT/pmc_latest.json profiles/pmc_latest.json || exit 1
+timeout -k 10 900 python3 bench.py $BENCH_ARGS > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 || { echo "rocprof failed"; tail -5 $OUT/bench_rocprof.log; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py --no-cpu $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 \
+  || { echo "rocprof failed"; tail -5 $OUT/bench_rocprof.log; exit 1; }
 tail -1 $OUT/bench_rocprof.log
-ls $OUT/prof
+find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/bench_kernel_stats.csv \;
+ls $OUT
