@@ -257,26 +257,27 @@ class ParitySampler:
             self.msgs += bad[:3]
 
 
-def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, gen_threads):
+def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, gen_threads, n_frames):
     """The CPU oracle (C++ restatement of the reference path, oracle/) timed on this
-    host: one sequence per worker thread, frames generated in chunks of 8 outside the
-    timed region, chunks timed until about target_s seconds of work."""
+    host on the bench's own workload: rounds of n_threads fresh sequences (one per
+    worker thread), each initialised untimed and then tracked over frames 1..n_frames
+    (the frames the GPU bench steps through), until about target_s seconds of timed
+    work.  Input generation and initialisation are excluded, as on the GPU."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import gfpl
     import oracle as O
-    n_seqs, chunk = n_threads, 8
-    hs = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in range(n_seqs)]
-    seq0 = 1 << 20
-    H = gfpl.HostFrames(cam, sp, n_seqs, 1, kp_cap, kl_cap, seq0=seq0, frame0=0, threads=gen_threads)
-    for b, h in enumerate(hs):
-        h.initialize(H.frames(0), b)
-    timed, frames, f0 = 0.0, 0, 1
-    while timed < target_s and f0 < 2000:
-        H = gfpl.HostFrames(cam, sp, n_seqs, chunk, kp_cap, kl_cap, seq0=seq0, frame0=f0, threads=gen_threads)
+    n_seqs = n_threads
+    timed, frames, rounds = 0.0, 0, 0
+    while timed < target_s and rounds < 200:
+        seq0 = (1 << 20) + rounds * n_seqs
+        H = gfpl.HostFrames(cam, sp, n_seqs, n_frames + 1, kp_cap, kl_cap, seq0=seq0, threads=gen_threads)
+        hs = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in range(n_seqs)]
+        for b, h in enumerate(hs):
+            h.initialize(H.frames(0), b)
 
         def worker(b):
             h = hs[b]
-            for k in range(chunk):
+            for k in range(1, n_frames + 1):
                 h.insertStereoPair(H.frames(k), b)
                 h.optimizePose()
                 h.updateFrame()
@@ -287,11 +288,13 @@ def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, 
         for t in th:
             t.join()
         timed += time.perf_counter() - t0
-        frames += n_seqs * chunk
-        f0 += chunk
+        frames += n_seqs * n_frames
+        rounds += 1
+        del H, hs
     return {"value": frames / timed, "unit": "stereo frames/s", "cores": n_threads, "kind": "port",
-            "sample": f"{n_seqs} sequences x {f0 - 1} frames of the same workload, one sequence per host thread "
-                      f"({timed:.1f} s timed; oracle/ C++ -O3 restatement; input generation excluded)",
+            "sample": f"{rounds} rounds x {n_seqs} sequences x frames 1..{n_frames} of the bench workload, one "
+                      f"sequence per host thread ({timed:.1f} s timed; oracle/ C++ -O3 restatement; input "
+                      f"generation and initialisation excluded)",
             "host": cores_info}
 
 
@@ -463,7 +466,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             nt = args.cpu_threads or cores
-            cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads)
+            cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads, W + K)
         in_bytes = hb.nbytes()
         out = {
             "metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)",
