@@ -82,7 +82,7 @@ def parse(argv=None):
     ap.add_argument("--gen-threads", type=int, default=16, help="host threads generating the input frames")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (and the parity replay)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (gloo): launcher, broadcast, sharding, input generation and reductions; "
@@ -389,7 +389,7 @@ def main():
 
     h = gfpl.StereoFrameHandler(ctx, B, KP, KL)
     sampler = None
-    if not args.no_cpu and args.parity_seqs > 0:
+    if args.parity_seqs > 0:
         n = min(args.parity_seqs, B)
         sampler = ParitySampler(cam, cfg, KP, KL, [int(x) for x in np.linspace(0, B - 1, n)], cores)
 

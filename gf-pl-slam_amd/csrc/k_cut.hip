@@ -354,14 +354,51 @@ __device__ __forceinline__ void chol_s(const double* a, double* out) {
     out[27] = ok ? 1.0 : 0.0;
 }
 
+// Reciprocal for the certified comparisons only (never for an output or an exact
+// step): hardware v_rcp_f64 refined by two Newton steps, within an ulp or two of 1/x;
+// 0, infinities and NaN come out NaN or infinite and fail the health tests.
+__device__ __forceinline__ double rcp_fast(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+    r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+    return r;
+}
+
 // d of the neighbour whose endpoints sit in slots S, E (NaN when not usable)
 __device__ __forceinline__ double cut_d(const double* S, const double* E) {
     double c = S[7] * E[7];
 #pragma unroll
-    for (int i = 1; i < 6; ++i) c = c + S[7 + i] * E[7 + i];
+    for (int i = 1; i < 6; ++i) c = __builtin_fma(S[7 + i], E[7 + i], c);
     const double vs = S[0], ve = E[0];
-    const double d = (1.0 + S[13]) * (1.0 + E[13]) - (c * c) / (vs * ve);
+    const double d = __builtin_fma(1.0 + S[13], 1.0 + E[13], -(c * c) * rcp_fast(vs * ve));
     return (vs > 0.0 && ve > 0.0 && d > 0.0 && d < 1e300) ? d : __longlong_as_double(0x7ff8000000000000ll);
+}
+
+// ---- polynomial form of the certified-comparison terms.
+// Along a side the cut point is g(t) = g0 + t (g1 - g0) (camera frame), so
+// J(t) = fgz2(t) P(t) with P quadratic in t and fgz2 = fx / gz^2 (lines whose
+// segment keeps gz^2 above homog_th; others are searched with exact steps), and
+// v(t) = fgz2(t)^2 v'(t) with v'(t) = p^T ((1-t)^2 A0 + t^2 A1) p,
+// p = (jl0 gz, jl1 gz, -(jl0 gx + jl1 gy)).  The factors fgz2 cancel in the
+// determinant lemma: a = |L^-1 P|^2 / v' and c^2 / (vs ve) = (Ws . We)^2 / (v's v'e)
+// with W(t) = L^-1 P(t) = W0 + t W1 + t^2 W2, whose coefficients are solved once
+// when the line opens (lane j < 6: side j / 3, power j % 3).  A step then costs no
+// triangular solve and no division but one reciprocal.
+__device__ __forceinline__ void cut_poly_coeff(const double* g0, const double* g1, double lx, double ly, int k,
+                                               double* Pk) {
+    const double dx = g1[0] - g0[0], dy = g1[1] - g0[1], dz = g1[2] - g0[2];
+    // coefficient k of the product (a0 + t a1)(b0 + t b1)
+    auto prod = [&](double a0, double a1, double b0, double b1) {
+        return k == 0 ? a0 * b0 : (k == 1 ? a0 * b1 + a1 * b0 : a1 * b1);
+    };
+    auto lin = [&](double a0, double a1) { return k == 0 ? a0 : (k == 1 ? a1 : 0.0); };
+    const double x0 = g0[0], y0 = g0[1], z0 = g0[2];
+    Pk[0] = lx * lin(z0, dz);
+    Pk[1] = ly * lin(z0, dz);
+    Pk[2] = -(lx * lin(x0, dx) + ly * lin(y0, dy));
+    Pk[3] = -((lx * prod(x0, dx, y0, dy) + ly * prod(y0, dy, y0, dy)) + ly * prod(z0, dz, z0, dz));
+    Pk[4] = (lx * prod(x0, dx, x0, dx) + lx * prod(z0, dz, z0, dz)) + ly * prod(x0, dx, y0, dy);
+    Pk[5] = ly * prod(x0, dx, z0, dz) - lx * prod(y0, dy, z0, dz);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -442,7 +479,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     // different LDS banks when their lanes read the same entry
     __shared__ double sumA[CUT_G][25];   // approximate S of the current line
     __shared__ double sumE[CUT_G][25];   // exact invCov_sum before line m_sync (lazy, for exact steps)
-    __shared__ double chol[CUT_G][CUT_CH];
+    __shared__ double wpl[CUT_G][37];    // W(t) coefficients of the current line: [side * 3 + power][6]
     __shared__ double epf[CUT_G][CUT_EP];
     __shared__ double fst[CUT_G][21];    // fast data of the current line
     __shared__ double nxt[CUT_G][43];    // prefetched next line: fast data (21) | r = 0 info (21)
@@ -482,11 +519,30 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     int m_sync = 0;      // sumE holds the exact invCov_sum before line m_sync
     int first = 1;       // first step of the line: the exact centre metric is logdet(invCov_sum)
     double r0 = 0.0, r1 = 0.0;
-    auto put_chol = [&](const double* s21) {   // all 8 lanes write identical values
+    int line_ok = 0;     // certified comparisons allowed on the current line
+    // A line opens: every lane factors S in registers (identical values), then lane
+    // j < 6 solves the W(t) coefficient of side j / 3, power j % 3 from the line's
+    // fast data fd.  Certification needs the factor healthy and gz^2 > homog_th along
+    // the segment (fgz2 = fx / gz^2 on it); otherwise the line takes exact steps.
+    auto open_line = [&](const double* s21, const double* fd) {
         double o[28];
         chol_s(s21, o);
+        const double z0 = fd[2], z1 = fd[5];
+        line_ok = (o[27] != 0.0) && ((z0 > 0.0 && z1 > 0.0) || (z0 < 0.0 && z1 < 0.0)) &&
+                  z0 * z0 > 2.0 * homog && z1 * z1 > 2.0 * homog;
+        if (j < 6) {
+            double P[6], w[6];
+            cut_poly_coeff(fd + (eside ? 3 : 0), fd + (eside ? 0 : 3), fd[18], fd[19], j % 3, P);
 #pragma unroll
-        for (int e = 0; e < 28; ++e) chol[g][e] = o[e];
+            for (int i = 0; i < 6; ++i) {
+                double u = P[i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) u = __builtin_fma(-o[tri(i, k)], w[k], u);
+                w[i] = u * o[21 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) wpl[g][6 * j + i] = w[i];
+        }
     };
     // Next-line prefetch: lane j loads elements j, j+8, ... of the 42-element vector
     // [fast data (its last entry: the list index of the line after it) | r = 0 info]
@@ -508,7 +564,10 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     if (m < nls) {
         q_cur = lb + mls[0];
         if (nls > 1) q_nx = lb + mls[1];
-        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = fast_l[e];
+        double fd0[CUT_FAST];
+#pragma unroll
+        for (int e = 0; e < CUT_FAST; ++e) fd0[e] = fast_l[e];
+        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = fd0[e];
         double s21[21];
 #pragma unroll
         for (int e = 0; e < 21; ++e) {
@@ -517,7 +576,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             sumE[g][e] = s0;
             sumA[g][e] = s21[e];
         }
-        put_chol(s21);
+        open_line(s21, fd0);
         if (nls > 1) pf_issue(1);
     } else {
         for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = (e == 2 || e == 5) ? 1.0 : 0.0;
@@ -531,27 +590,33 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- A: this lane's endpoint (fast) and its certified-comparison terms
+        // ---- A: this lane's endpoint terms for the certified comparisons (polynomial
+        //      form, see cut_poly_coeff): v' (slot 0), W (slots 7-12), a = |W|^2 / v' (13)
         if (j < 6) {
             const double t = (eside == 0 ? r0 : r1) + eoff;
-            double out[7];
-            cut_endpoint_fast(cam, homog, G0, G1, A0, A1, fst[g][18], fst[g][19], t, out);
+            const double om = 1.0 - t;
+            double gv[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) gv[k] = __builtin_fma(om, G0[k], t * G1[k]);
+            const double jl0 = fst[g][18], jl1 = fst[g][19];
+            const double p0 = jl0 * gv[2], p1 = jl1 * gv[2], p2 = -__builtin_fma(jl0, gv[0], jl1 * gv[1]);
+            auto quad = [&](const double* A) {
+                const double diag = __builtin_fma(A[0] * p0, p0, __builtin_fma(A[3] * p1, p1, A[5] * p2 * p2));
+                const double off = __builtin_fma(A[1] * p0, p1, __builtin_fma(A[2] * p0, p2, A[4] * p1 * p2));
+                return __builtin_fma(2.0, off, diag);
+            };
+            const double v = __builtin_fma(om * om, quad(A0), t * t * quad(A1));
+            const double* Wc = &wpl[g][18 * eside];
             double w[6];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                double u = out[1 + i];
-#pragma unroll
-                for (int k = 0; k < i; ++k) u = __builtin_fma(-chol[g][tri(i, k)], w[k], u);
-                w[i] = u * chol[g][21 + i];
-            }
+            for (int i = 0; i < 6; ++i) w[i] = __builtin_fma(t, __builtin_fma(t, Wc[12 + i], Wc[6 + i]), Wc[i]);
             double a = w[0] * w[0];
 #pragma unroll
             for (int i = 1; i < 6; ++i) a = __builtin_fma(w[i], w[i], a);
-#pragma unroll
-            for (int i = 0; i < 7; ++i) my_slot[i] = out[i];
+            my_slot[0] = v;
 #pragma unroll
             for (int i = 0; i < 6; ++i) my_slot[7 + i] = w[i];
-            my_slot[13] = a / out[0];
+            my_slot[13] = a * rcp_fast(v);
         }
         // the prefetched next line lands in LDS (its loads were issued >= 1 iteration ago)
         if (pending) {
@@ -581,7 +646,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         } else {
             if (valid && !(dc - dj > tau * dc)) ok = 0;
         }
-        if (!(tau > 0.0 && chol[g][27] != 0.0 && dc == dc)) ok = 0;
+        if (!(tau > 0.0 && line_ok && dc == dc)) ok = 0;
         const bool exact = act && (__ballot(!ok) & gmask) != 0;
         CUT_PROF(1);
         if (__any(exact)) {
@@ -657,13 +722,13 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             }
         }
         CUT_PROF(2);
-        int finalize = 0, stale_mid = 0;
+        int finalize = 0;
         if (act) {
             first = 0;
             if (best >= 0) {
                 r0 = r0 + nb_step(best, 0, st);
                 r1 = r1 + nb_step(best, 1, st);
-                if (!(r0 + r1 <= 1.0)) { finalize = 1; stale_mid = 1; }   // while-condition
+                if (!(r0 + r1 <= 1.0)) finalize = 1;   // while-condition
             } else {
                 finalize = 1;   // the middle endpoints of this step are (r0 + 0, r1 + 0) = (r0, r1)
             }
@@ -671,16 +736,12 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
         if (act && finalize) {
             // approximate invCov_sum += info of the chosen ratio (the exact one is
             // accumulated lazily, only when an exact step needs it)
+            // (the slots hold the polynomial-form terms, not v and J)
             double S7[7], E7[7];
-            if (!stale_mid) {
-#pragma unroll
-                for (int i = 0; i < 7; ++i) { S7[i] = epf[g][CUT_SL * 1 + i]; E7[i] = epf[g][CUT_SL * 4 + i]; }
-            } else {   // (not reached for finite ratios: valid neighbours keep r0 + r1 <= 1)
-                cut_endpoint_fast(cam, homog, &fst[g][0], &fst[g][3], &fst[g][6], &fst[g][12], fst[g][18], fst[g][19],
-                                  r0, S7);
-                cut_endpoint_fast(cam, homog, &fst[g][3], &fst[g][0], &fst[g][12], &fst[g][6], fst[g][18], fst[g][19],
-                                  r1, E7);
-            }
+            cut_endpoint_fast(cam, homog, &fst[g][0], &fst[g][3], &fst[g][6], &fst[g][12], fst[g][18], fst[g][19],
+                              r0, S7);
+            cut_endpoint_fast(cam, homog, &fst[g][3], &fst[g][0], &fst[g][12], &fst[g][6], fst[g][18], fst[g][19],
+                              r1, E7);
             double info[21];
             CUT_PROF(4);
             cut_assemble<false>(S7, E7, info);
@@ -710,7 +771,7 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
 #pragma unroll
                 for (int e = 0; e < 21; ++e) sumA[g][e] = s21[e];
                 CUT_PROF(6);
-                put_chol(s21);
+                open_line(s21, nx);
                 CUT_PROF(7);
                 if (m + 1 < nls) pf_issue(m + 1);
             }

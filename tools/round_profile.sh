@@ -21,7 +21,7 @@ fi
 pmc() {   # name counters...
   local name=$1; shift
   timeout -k 10 500 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/pmc/$name -o $name -f csv -- \
-      python3 bench.py --no-cpu --steps 2 --warmup 1 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
+      python3 bench.py --no-cpu --parity-seqs 0 --steps 2 --warmup 1 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
     || { echo "pmc $name failed"; tail -5 $OUT/pmc/$name.log; return 1; }
 }
 pmc fetch FETCH_SIZE && \
@@ -31,7 +31,7 @@ B=$(python3 -c "import json,sys; print(json.loads([l for l in open('$OUT/pmc/fet
 python3 tools/pmc_summary.py $OUT/pmc $B $OUT/pmc_latest.json ${PMC_WORKLOAD:-cfg2} > $OUT/pmc/summary.txt && cp $OUT/pmc_latest.json profiles/pmc_latest.json || exit 1
 timeout -k 10 900 python3 bench.py $BENCH_ARGS > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py --no-cpu $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 \
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py --no-cpu --parity-seqs 0 $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 \
   || { echo "rocprof failed"; tail -5 $OUT/bench_rocprof.log; exit 1; }
 tail -1 $OUT/bench_rocprof.log
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/bench_kernel_stats.csv \;
