@@ -106,8 +106,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->tr.kf_prev_iskf = c.take<int32_t>(B);
     sb->tr.kf_nsince = c.take<int32_t>(B);
     sb->tr.kf_flag = c.take<int32_t>(B);
-    sb->scr.cut_ls = c.take<double>(B * sb->mls_cap * 21);
-    sb->scr.cut_fast = c.take<double>(B * sb->mls_cap * CUT_FAST);
+    sb->scr.cut_rec = c.take<double>(B * sb->mls_cap * CUT_REC);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
     sb->scr.proj = reinterpret_cast<double*>(sb->scr.knn);
     sb->scr.bytes = c.take<int64_t>(B * 8);

@@ -72,11 +72,12 @@ struct DevTrack {
     int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
-#define CUT_FAST 21   // doubles of per-line fast cut data (k_cut.hip)
+#define CUT_FAST 48   // doubles of per-line comparison polynomials (k_cut.hip, PD_*)
+#define CUT_REC 72    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (576 B)
 
 struct DevScratch {
-    double* cut_ls;   // [B*mls_cap*21] lower-triangle info of matched lines
-    double* cut_fast; // [B*mls_cap*CUT_FAST] per matched line: DT sP, DT eP, R covS R^T, R covE R^T, Jl, list index of the next line
+    double* cut_rec;  // [B*mls_cap*CUT_REC] per matched line: P(t) coefficients of both cut endpoints, v'(t)
+                      // coefficients, geometry flag, list index of the next line | lower-triangle r = 0 info
     int32_t* knn;     // [B*6*kcap] initial-frame knn results (idx0, d0, d1, ...)
     double* proj;     // [B*kcap*2] cross-points projections (aliases knn: init never overlaps)
     int64_t* bytes;   // [B] algorithmic bytes of the last step

@@ -136,18 +136,56 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
     d.Jl[1] = L.le_obs[3 * q + 1];
 }
 
-// ------------------------------------------------------ fast cut endpoints --
-// The certified comparisons (k_cut_search) need each endpoint's variance v and
-// pose Jacobian J only to ~1e-14, so the search evaluates them in a shorter,
-// non-reference order from per-line data:  DT is affine, so the transformed cut
-// point is (1-c) DT P0 + c DT P1, and getPoseInfoOnLine's variance
-// Jl^T Jp R cov R^T Jp^T Jl is u^T [(1-c)^2 R C0 R^T + c^2 R C1 R^T] u with
-// u = Jp^T Jl = (Jl0 f/z, Jl1 f/z, -f (Jl0 x + Jl1 y)/z^2).  Per line (CUT_FAST):
-// DT sP [3], DT eP [3], R covS R^T and R covE R^T (xx xy xz yy yz zz) [6+6], Jl [2],
-// and (k_cut_prep) the list index of the line after it [1].
-__device__ __forceinline__ void cut_fast_data(const double* Dl, const LineCutData& d, double* fd) {
-    se3_apply(Dl, d.sP, fd);
-    se3_apply(Dl, d.eP, fd + 3);
+// ------------------------------------------------- comparison polynomials --
+// The greedy search compares logdet(S + info(t0, t1)) over neighbours.
+// Along a side the transformed cut point is g(t) = (1-t) g0 + t g1 (DT is affine), and
+// getPoseInfoOnLine's Jacobian and projected variance of that endpoint are
+//   J(t) = fgz2(t) P(t),  v(t) = fgz2(t)^2 v'(t),  fgz2 = fx / gz^2,
+// with P quadratic in t (its first three entries p(t) linear) and
+//   v'(t) = p(t)^T ((1-t)^2 A0 + t^2 A1) p(t),  A = R cov R^T,
+// a quartic — for lines whose segment keeps gz^2 above homog_th (PD_OK; other lines
+// are searched with the reference's exact steps).  The fgz2 factors cancel in the
+// determinant lemma, so a neighbour's comparison value needs only P and v'.
+// Per matched line, k_cut_prep stores (CUT_FAST doubles):
+#define PD_PS 0      // start side (sP -> eP, t = r0): P coefficients of t^0, t^1, t^2 [3 x 6]
+#define PD_PE 18     // end side (eP -> sP, t = r1) [3 x 6]
+#define PD_VS 36     // v'_s(t) coefficients of t^0 .. t^4 [5]
+#define PD_VE 41     // v'_e(t) [5]
+#define PD_OK 46     // 1.0: gz^2 > 2 homog_th at both ends, one sign (fgz2 = fx / gz^2 on the segment)
+#define PD_NEXT 47   // list index of the line after this one (k_cut_search's prefetch)
+static_assert(CUT_FAST == 48, "per-line comparison data layout");
+
+// x^T A y, A symmetric packed (xx xy xz yy yz zz)
+__device__ __forceinline__ double sym3(const double* A, const double* x, const double* y) {
+    const double ax = (A[0] * y[0] + A[1] * y[1]) + A[2] * y[2];
+    const double ay = (A[1] * y[0] + A[3] * y[1]) + A[4] * y[2];
+    const double az = (A[2] * y[0] + A[4] * y[1]) + A[5] * y[2];
+    return (x[0] * ax + x[1] * ay) + x[2] * az;
+}
+
+// coefficient k of P(t) for the blend g0 -> g1 (poseJac's six terms without fgz2)
+__device__ __forceinline__ void cut_poly_coeff(const double* g0, const double* g1, double lx, double ly, int k,
+                                               double* Pk) {
+    const double dx = g1[0] - g0[0], dy = g1[1] - g0[1], dz = g1[2] - g0[2];
+    // coefficient k of the product (a0 + t a1)(b0 + t b1)
+    auto prod = [&](double a0, double a1, double b0, double b1) {
+        return k == 0 ? a0 * b0 : (k == 1 ? a0 * b1 + a1 * b0 : a1 * b1);
+    };
+    auto lin = [&](double a0, double a1) { return k == 0 ? a0 : (k == 1 ? a1 : 0.0); };
+    const double x0 = g0[0], y0 = g0[1], z0 = g0[2];
+    Pk[0] = lx * lin(z0, dz);
+    Pk[1] = ly * lin(z0, dz);
+    Pk[2] = -(lx * lin(x0, dx) + ly * lin(y0, dy));
+    Pk[3] = -((lx * prod(x0, dx, y0, dy) + ly * prod(y0, dy, y0, dy)) + ly * prod(z0, dz, z0, dz));
+    Pk[4] = (lx * prod(x0, dx, x0, dx) + lx * prod(z0, dz, z0, dz)) + ly * prod(x0, dx, y0, dy);
+    Pk[5] = ly * prod(x0, dx, z0, dz) - lx * prod(y0, dy, z0, dz);
+}
+
+__device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutData& d, double homog, double* fd) {
+    double g[2][3];
+    se3_apply(Dl, d.sP, g[0]);
+    se3_apply(Dl, d.eP, g[1]);
+    double A[2][6];   // R covS R^T, R covE R^T
     const double* Cs[2] = {d.covS, d.covE};
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
@@ -160,39 +198,33 @@ __device__ __forceinline__ void cut_fast_data(const double* Dl, const LineCutDat
         const int ii[6] = {0, 0, 0, 1, 1, 2}, jj[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
         for (int e = 0; e < 6; ++e)
-            fd[6 + 6 * w + e] = (T[ii[e] * 3 + 0] * Dl[jj[e] * 4 + 0] + T[ii[e] * 3 + 1] * Dl[jj[e] * 4 + 1]) +
-                                T[ii[e] * 3 + 2] * Dl[jj[e] * 4 + 2];
+            A[w][e] = (T[ii[e] * 3 + 0] * Dl[jj[e] * 4 + 0] + T[ii[e] * 3 + 1] * Dl[jj[e] * 4 + 1]) +
+                      T[ii[e] * 3 + 2] * Dl[jj[e] * 4 + 2];
     }
-    fd[18] = d.Jl[0];
-    fd[19] = d.Jl[1];
-}
-
-// one endpoint from the fast data: g0/g1 the transformed points it blends, A0/A1
-// the rotated covariances, t the cut ratio -> v, J[6]
-__device__ __forceinline__ void cut_endpoint_fast(const DevCam& cam, double homog, const double* g0, const double* g1,
-                                                  const double* A0, const double* A1, double jl0, double jl1, double t,
-                                                  double* out7) {
-    const double om = 1.0 - t;
-    double g[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) g[k] = __builtin_fma(om, g0[k], t * g1[k]);
-    const double iz = 1.0 / g[2];
-    const double fz = cam.fx * iz;
-    const double u0 = jl0 * fz, u1 = jl1 * fz, u2 = -__builtin_fma(jl0, g[0], jl1 * g[1]) * fz * iz;
-    auto quad = [&](const double* A) {
-        const double diag = __builtin_fma(A[0] * u0, u0, __builtin_fma(A[3] * u1, u1, A[5] * u2 * u2));
-        const double off = __builtin_fma(A[1] * u0, u1, __builtin_fma(A[2] * u0, u2, A[4] * u1 * u2));
-        return __builtin_fma(2.0, off, diag);
-    };
-    out7[0] = __builtin_fma(om * om, quad(A0), t * t * quad(A1));
-    poseJac(cam, homog, g, jl0, jl1, out7 + 1);
+    for (int side = 0; side < 2; ++side) {
+        double* P = fd + (side ? PD_PE : PD_PS);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cut_poly_coeff(g[side], g[1 - side], d.Jl[0], d.Jl[1], k, P + 6 * k);
+        // v'(t) = (1-t)^2 Qa(t) + t^2 Qb(t), Q(t) = q0 + 2 t q1 + t^2 q2 for p(t) = P[0..2] = p0 + t p1
+        const double* p0 = P;
+        const double* p1 = P + 6;
+        const double a0 = sym3(A[side], p0, p0), a1 = sym3(A[side], p0, p1), a2 = sym3(A[side], p1, p1);
+        const double b0 = sym3(A[1 - side], p0, p0), b1 = sym3(A[1 - side], p0, p1), b2 = sym3(A[1 - side], p1, p1);
+        double* v = fd + (side ? PD_VE : PD_VS);
+        v[0] = a0;
+        v[1] = 2.0 * (a1 - a0);
+        v[2] = ((a2 - 4.0 * a1) + a0) + b0;
+        v[3] = 2.0 * ((a1 - a2) + b1);
+        v[4] = a2 + b2;
+    }
+    const double z0 = g[0][2], z1 = g[1][2];
+    fd[PD_OK] = (((z0 > 0.0 && z1 > 0.0) || (z0 < 0.0 && z1 < 0.0)) && z0 * z0 > 2.0 * homog && z1 * z1 > 2.0 * homog)
+                    ? 1.0 : 0.0;
 }
 
 // ------------------------------------------------------------------ prep --
-#ifndef GFPL_PREP_WAVES
-#define GFPL_PREP_WAVES 1
-#endif
-__global__ void __launch_bounds__(64, GFPL_PREP_WAVES) k_cut_prep(KParams p) {
+__global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
@@ -206,8 +238,7 @@ __global__ void __launch_bounds__(64, GFPL_PREP_WAVES) k_cut_prep(KParams p) {
     const size_t lb = (size_t)b * p.kl_cap, pbase = (size_t)b * p.kp_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
     const int32_t* mpt = p.tr.matched_pt + (size_t)b * p.mpt_cap;
-    double* scr_l = p.scr.cut_ls + (size_t)b * p.mls_cap * 21;
-    double* fast_l = p.scr.cut_fast + (size_t)b * p.mls_cap * CUT_FAST;
+    double* rec_l = p.scr.cut_rec + (size_t)b * p.mls_cap * CUT_REC;
     // DT_inv = curr.Tfw^-1 * prev.Tfw (src/stereoFrameHandler.cpp:1635), every lane
     double Dl[16];
     {
@@ -233,12 +264,12 @@ __global__ void __launch_bounds__(64, GFPL_PREP_WAVES) k_cut_prep(KParams p) {
                 load_line(L, lb + mls[m], d);
                 poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
 #pragma unroll
-                for (int i = 0; i < 21; ++i) scr_l[(size_t)m * 21 + i] = info[i];   // k_cut_search subtracts it
+                for (int i = 0; i < 21; ++i) rec_l[(size_t)m * CUT_REC + CUT_FAST + i] = info[i];   // k_cut_search subtracts it
                 double fd[CUT_FAST];
-                cut_fast_data(Dl, d, fd);
-                fd[CUT_FAST - 1] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
+                cut_poly_data(Dl, d, homog, fd);
+                fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
 #pragma unroll
-                for (int i = 0; i < CUT_FAST; ++i) fast_l[(size_t)m * CUT_FAST + i] = fd[i];
+                for (int i = 0; i < CUT_FAST; ++i) rec_l[(size_t)m * CUT_REC + i] = fd[i];
             } else {
                 const size_t q = pbase + mpt[m];
                 double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
@@ -268,40 +299,59 @@ __global__ void __launch_bounds__(64, GFPL_PREP_WAVES) k_cut_prep(KParams p) {
 // 8 sequences per wave, 8 lanes each; every wave iteration is one greedy step
 // of each of its 8 chains.
 //
-// Certified comparisons.  Within line m the search compares
+// Margined comparisons.  Within line m the search compares
 // logdet(S + info(t0, t1)) over neighbours, S = invCov_sum - info_m(0, 0) fixed
 // for the line, and info = Js Js^T / vs + Je Je^T / ve (rank 2, ledger Q10).  By
 // the matrix determinant lemma logdet(S + info) = logdet(S) + log d with
-//   d = (1 + as)(1 + ae) - c^2 / (vs ve),  as = |ws|^2 / vs, ae = |we|^2 / ve,
-//   c = ws . we,  ws = L^-1 Js, we = L^-1 Je,  S = L L^T,
-// so the step's decision (the reference's first strict maximum over the valid
-// neighbours, starting from the centre's metric) only needs the d values: ws and
-// as depend on t0 only, we and ae on t1 only, and a neighbour costs one 6-term
-// dot product instead of a 6x6 LLT and six logs.  The decision is accepted when
-// every comparison it rests on is separated by more than cfg.cut_certify
-// (relative, 1e-9) — four orders of magnitude above the measured disagreement
-// between d and the reference's own LLT arithmetic (<= 1e-13).
-// Otherwise (and whenever S or an endpoint is not healthy) the group evaluates
-// that step exactly as the reference does: neighbour j's info assembled from its
-// endpoints, + S, LLT, six fdlibm logs, against the exact centre metric.  Either
-// way the chosen ratios are the reference's; the metric values themselves are
-// never output.
+//   d = (1 + as)(1 + ae) - c^2 / (vs ve),  as = |L^-1 Js|^2 / vs, ae = |L^-1 Je|^2 / ve,
+//   c = (L^-1 Js) . (L^-1 Je),  S = L L^T,
+// and with J = fgz2 P, v = fgz2^2 v' (see PD_*) the fgz2 factors cancel:
+//   d = D / (v's v'e),  D = (v's + Ns)(v'e + Ne) - C^2,
+//   Ns(t0) = |W(t0)|^2, Ne(t1) = |W(t1)|^2, C(t0, t1) = Ws(t0) . We(t1),  W = L^-1 P.
+// W is quadratic in t, so with the Gram matrix G of the six coefficient vectors
+// L^-1 P_{side,k} (solved once when the line opens) Ns and Ne are quartics in t and
+// C is bi-quadratic in (t0, t1).  Lane j evaluates neighbour j's d from these
+// polynomial coefficients in registers: no LDS, no triangular solve, one reciprocal.
 //
-// Phases (wave barriers between them):
-//   E1  lanes 0-2 compute the start endpoint at t0 = r0 + {-s, 0, +s}, lanes 3-5
-//       the end endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint); lane 6 factors
-//       S when the line just opened;
-//   E2  lanes 0-5: w = L^-1 J and a = |w|^2 / v of their endpoint;
-//   C   lane j: d of neighbour j; every lane: d of the centre;
-//   D   certified decision, or the exact evaluation of the step (X) when any
-//       group of the wave needs it; no improvement finalises the line:
-//       invCov_sum += info of the chosen ratio (re-assembled from the middle
-//       endpoints, the same arithmetic as the chosen candidate's), the cut
-//       ratio is stored and the next line opens at (0, 0).
+// The reference's decision (first strict maximum over the valid neighbours,
+// starting from the centre's metric) is taken from the d values when
+//   (1) every comparison it rests on is separated by more than cfg.cut_certify
+//       (relative, default 1e-9), and
+//   (2) every d involved carries a computed forward rounding-error bound of at
+//       most cut_certify / 4 (cut_dval: Horner and product error bounds from the
+//       absolute values of the terms, so cancellation in Ns, C, D or v' shows up),
+//       so in exact arithmetic the lemma's gaps exceed cut_certify / 2,
+// and the line's S factored with every pivot above 1e-2 of its diagonal
+// (chol_s).  The remaining disagreement — between the lemma in exact arithmetic and
+// the reference's own rounded LLT + log evaluation — is bounded by measurement,
+// not by proof.  Otherwise (and whenever S, an endpoint variance or
+// d is not healthy) the group evaluates that step exactly as the reference does:
+// neighbour j's info assembled from its endpoints, + S, LLT, six fdlibm logs, against
+// the exact centre metric.  The metric values themselves are never output.
+//
+// Per iteration: lane j evaluates d of neighbour j, the group's first-strict-max by a
+// 3-step DPP reduction, the margin tests by ballot; the exact step (X) when any group
+// of the wave needs it; a move, or the line's finalisation: the approximate
+// invCov_sum += info of the chosen ratio (from P and v', every lane), the next line's
+// data from the prefetch registers through LDS, its S factored and the Gram matrix
+// of its W coefficients formed across the group's lanes.
 #define CUT_G 8          // sequences per wave (8 lanes each)
-#define CUT_SL 15        // endpoint slot: v, J[6], w[6], a, (pad)
-#define CUT_EP 91        // per-group endpoint block: 6 slots + 1 (odd stride)
-#define CUT_CH 29        // per-group factor of S: L (21), 1/L_kk (6), ok, (pad)
+#define CUT_SL 7         // exact endpoint slot (X): v, J[6]
+#define CUT_EP 43        // per-group exact endpoint block: 6 slots + 1 (odd stride)
+#define CUT_NX (CUT_FAST + 21)   // used part of a line record: comparison data | r = 0 info
+static_assert(CUT_REC * 8 == 576, "a record is 4.5 x 128 B: five 16-B loads per lane, the last by lanes 0-3");
+
+// One reference-order cut endpoint (cut_endpoint) of line q: side 0 the start
+// endpoint blended sP -> eP, side 1 the end endpoint eP -> sP, at ratio t.
+__device__ __forceinline__ void exact_endpoint(const DevCam& cam, double homog, const double* Dl, const DevLines& L,
+                                               size_t q, int side, double t, double* o7) {
+    const double* sP = L.sP + 3 * q;
+    const double* eP = L.eP + 3 * q;
+    const double* cS = L.covS + 9 * q;
+    const double* cE = L.covE + 9 * q;
+    const double Jl[2] = {L.le_obs[3 * q], L.le_obs[3 * q + 1]};
+    cut_endpoint(cam, homog, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS, side ? cS : cE, t, o7);
+}
 
 __device__ __forceinline__ double nb_step(int j, int side, double st) {
     // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
@@ -314,15 +364,12 @@ __device__ __forceinline__ int nb_slot(int j, int side) {   // endpoint slot: 0:
     return (j == 2 || j == 4 || j == 6) ? 2 : ((j == 3 || j == 5 || j == 7) ? 0 : 1);
 }
 
-// S = L L^T for the certified comparisons (out: L strictly lower 21, 1/L_kk 6, ok).  ok = 0
-// unless every pivot keeps at least GFPL_CUT_MIN_PIVOT (1e-2) of its diagonal; the line
-// is then searched with exact steps only.  The pivot ratios bound the condition of the
+// S = L L^T for the margined comparisons (out: L strictly lower 21, 1/L_kk 6, ok).  ok = 0
+// unless every pivot keeps at least CUT_MIN_PIVOT of its diagonal; the line is then
+// searched with exact steps only.  The pivot ratios bound the condition of the
 // diagonally scaled S, which sets both the lemma's and the reference LLT's rounding
-// error; above 1e-2 the measured disagreement stays <= 1e-13 (the
-// synthetic, KITTI and EuRoC workloads stay above 0.1), four orders below the margin.
-#ifndef GFPL_CUT_MIN_PIVOT
-#define GFPL_CUT_MIN_PIVOT 1e-2
-#endif
+// error (the synthetic, KITTI and EuRoC workloads stay above 0.1).
+constexpr double CUT_MIN_PIVOT = 1e-2;
 __device__ __forceinline__ void chol_s(const double* a, double* out) {
     double L[21];
 #pragma unroll
@@ -334,7 +381,7 @@ __device__ __forceinline__ void chol_s(const double* a, double* out) {
         double x = akk;
 #pragma unroll
         for (int j = 0; j < k; ++j) x = x - L[tri(k, j)] * L[tri(k, j)];
-        if (!(x > GFPL_CUT_MIN_PIVOT * akk && akk < 1e300)) { ok = false; x = 1.0; }
+        if (!(x > CUT_MIN_PIVOT * akk && akk < 1e300)) { ok = false; x = 1.0; }
         // 1 / L_kk (the only use of the pivot): hardware rsq + two Newton steps
         double r = __builtin_amdgcn_rsq(x);
         r = r * (1.5 - (0.5 * x) * (r * r));
@@ -354,7 +401,7 @@ __device__ __forceinline__ void chol_s(const double* a, double* out) {
     out[27] = ok ? 1.0 : 0.0;
 }
 
-// Reciprocal for the certified comparisons only (never for an output or an exact
+// Reciprocal for the margined comparisons only (never for an output or an exact
 // step): hardware v_rcp_f64 refined by two Newton steps, within an ulp or two of 1/x;
 // 0, infinities and NaN come out NaN or infinite and fail the health tests.
 __device__ __forceinline__ double rcp_fast(double x) {
@@ -364,41 +411,53 @@ __device__ __forceinline__ double rcp_fast(double x) {
     return r;
 }
 
-// d of the neighbour whose endpoints sit in slots S, E (NaN when not usable)
-__device__ __forceinline__ double cut_d(const double* S, const double* E) {
-    double c = S[7] * E[7];
-#pragma unroll
-    for (int i = 1; i < 6; ++i) c = __builtin_fma(S[7 + i], E[7 + i], c);
-    const double vs = S[0], ve = E[0];
-    const double d = __builtin_fma(1.0 + S[13], 1.0 + E[13], -(c * c) * rcp_fast(vs * ve));
-    return (vs > 0.0 && ve > 0.0 && d > 0.0 && d < 1e300) ? d : __longlong_as_double(0x7ff8000000000000ll);
+__device__ __forceinline__ double h4(const double* c, double t) {
+    return __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, c[4], c[3]), c[2]), c[1]), c[0]);
+}
+// Horner with |coefficients| (the abs is a free source modifier of v_fma_f64)
+__device__ __forceinline__ double h4abs(const double* c, double t) {
+    return __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, fabs(c[4]), fabs(c[3])), fabs(c[2])),
+                                          fabs(c[1])), fabs(c[0]));
+}
+__device__ __forceinline__ double h2(double c0, double c1, double c2, double t) {
+    return __builtin_fma(t, __builtin_fma(t, c2, c1), c0);
 }
 
-// ---- polynomial form of the certified-comparison terms.
-// Along a side the cut point is g(t) = g0 + t (g1 - g0) (camera frame), so
-// J(t) = fgz2(t) P(t) with P quadratic in t and fgz2 = fx / gz^2 (lines whose
-// segment keeps gz^2 above homog_th; others are searched with exact steps), and
-// v(t) = fgz2(t)^2 v'(t) with v'(t) = p^T ((1-t)^2 A0 + t^2 A1) p,
-// p = (jl0 gz, jl1 gz, -(jl0 gx + jl1 gy)).  The factors fgz2 cancel in the
-// determinant lemma: a = |L^-1 P|^2 / v' and c^2 / (vs ve) = (Ws . We)^2 / (v's v'e)
-// with W(t) = L^-1 P(t) = W0 + t W1 + t^2 W2, whose coefficients are solved once
-// when the line opens (lane j < 6: side j / 3, power j % 3).  A step then costs no
-// triangular solve and no division but one reciprocal.
-__device__ __forceinline__ void cut_poly_coeff(const double* g0, const double* g1, double lx, double ly, int k,
-                                               double* Pk) {
-    const double dx = g1[0] - g0[0], dy = g1[1] - g0[1], dz = g1[2] - g0[2];
-    // coefficient k of the product (a0 + t a1)(b0 + t b1)
-    auto prod = [&](double a0, double a1, double b0, double b1) {
-        return k == 0 ? a0 * b0 : (k == 1 ? a0 * b1 + a1 * b0 : a1 * b1);
-    };
-    auto lin = [&](double a0, double a1) { return k == 0 ? a0 : (k == 1 ? a1 : 0.0); };
-    const double x0 = g0[0], y0 = g0[1], z0 = g0[2];
-    Pk[0] = lx * lin(z0, dz);
-    Pk[1] = ly * lin(z0, dz);
-    Pk[2] = -(lx * lin(x0, dx) + ly * lin(y0, dy));
-    Pk[3] = -((lx * prod(x0, dx, y0, dy) + ly * prod(y0, dy, y0, dy)) + ly * prod(z0, dz, z0, dz));
-    Pk[4] = (lx * prod(x0, dx, x0, dx) + lx * prod(z0, dz, z0, dz)) + ly * prod(x0, dx, y0, dy);
-    Pk[5] = ly * prod(x0, dx, z0, dz) - lx * prod(y0, dy, z0, dz);
+// Comparison polynomials of the current line, one copy per lane (registers).
+struct CutCmp {
+    double ns[5], ne[5];     // |W_s(t)|^2, |W_e(t)|^2
+    double vs[5], ve[5];     // v'_s, v'_e
+    double cc[9];            // C(t0, t1): cc[3 i + k] multiplies t0^i t1^k
+    double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2)
+};
+
+// d at (t0, t1), NaN when not healthy; bound_ok: the forward rounding-error bound of
+// d (relative, unit roundoff u, first order) is at most tau / 4:
+//   40u [(Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2] / D + 16u (VsA / v's + VeA / v'e) + 4u,
+// where Bs^2 bounds the absolute terms of Ns and of the Gram entries behind it, Bs Be
+// those of C, VsA those of v's (Horner with absolute coefficients at |t|).
+__device__ __forceinline__ double cut_dcore(double Ns, double Vs, double Ne, double Ve, double C, double Bs, double Be,
+                                           double VsA, double VeA, double tau, int& bound_ok) {
+    const double D = __builtin_fma(Vs + Ns, Ve + Ne, -(C * C));
+    const double den = Vs * Ve;
+    const double d = D * rcp_fast(den);
+    const double Bs2 = Bs * Bs, Be2 = Be * Be;
+    const double P1 = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+    const double P2 = __builtin_fma(VsA, Ve, VeA * Vs);
+    constexpr double u = 0x1p-53;
+    const double Dd = D * den;
+    const bool healthy = Vs > 0.0 && Ve > 0.0 && D > 0.0 && d < 1e300 && Dd < 1e300;
+    bound_ok = healthy && __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= (0.25 * tau - 4.0 * u) * Dd;
+    return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
+}
+__device__ __forceinline__ double cut_dval(const CutCmp& c, double t0, double t1, double tau, int& bound_ok) {
+    const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
+    const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
+                                   h2(c.cc[0], c.cc[3], c.cc[6], t0));
+    const double a0 = fabs(t0), a1 = fabs(t1);
+    const double Bs = h2(c.bs[0], c.bs[1], c.bs[2], a0), Be = h2(c.be[0], c.be[1], c.be[2], a1);
+    const double VsA = h4abs(c.vs, a0), VeA = h4abs(c.ve, a1);
+    return cut_dcore(Ns, Vs, Ne, Ve, C, Bs, Be, VsA, VeA, tau, bound_ok);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -467,24 +526,30 @@ __device__ __forceinline__ int group_first_max(double v, int valid, int j, doubl
 // the in-flight global prefetch loads.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Per iteration (one LDS sync between the halves, one at the end):
-//   A  lanes 0-2: the start endpoint at t0 = r0 + {-s, 0, +s}, lanes 3-5: the end
-//      endpoint at t1 = r1 + {-s, 0, +s} (cut_endpoint), then w = L^-1 J and
-//      a = |w|^2 / v of that endpoint; prefetched line data lands in LDS;
-//   B  lane j: d of neighbour j and of the centre, the group decision by DPP
-//      reduction, its certification by ballot; the exact step (X) when any
-//      group of the wave needs it; a move, or the line's finalisation.
-__global__ void __launch_bounds__(64) k_cut_search(KParams p) {
+// lower-triangle index e (0..20) -> row / column, packed 3 bits per entry
+constexpr unsigned long long tri_pack(int want_row) {
+    unsigned long long v = 0;
+    int e = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int k = 0; k <= i; ++k, ++e) v |= (unsigned long long)(want_row ? i : k) << (3 * e);
+    return v;
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
-    __shared__ double sumA[CUT_G][25];   // approximate S of the current line
-    __shared__ double sumE[CUT_G][25];   // exact invCov_sum before line m_sync (lazy, for exact steps)
-    __shared__ double wpl[CUT_G][37];    // W(t) coefficients of the current line: [side * 3 + power][6]
-    __shared__ double epf[CUT_G][CUT_EP];
-    __shared__ double fst[CUT_G][21];    // fast data of the current line
-    __shared__ double nxt[CUT_G][43];    // prefetched next line: fast data (21) | r = 0 info (21)
-    __shared__ double xs[CUT_G][25];     // exact step: exact S of the line / flush endpoints
-    __shared__ double dtl[CUT_G][13];    // DT_inv rows 0-2
+    __shared__ double sumA[CUT_G][25];          // approximate S of the current line (invCov_sum - its r = 0 info)
+    __shared__ double sumE[CUT_G][25];          // exact invCov_sum before line m_sync (lazy, for exact steps)
+    __shared__ double fst[CUT_G][CUT_FAST + 1]; // comparison data of the current line
+    // next-line records, written by LDS-DMA: 16-B piece k of group g's record lands at
+    // nxl[k][16 g + ...] (the DMA writes base + 16 * lane)
+    __shared__ __attribute__((aligned(16))) double nxl[5][128];
+    // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
+    //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
+    //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
+    __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];
+    __shared__ double dtl[CUT_G][13];           // DT_inv rows 0-2
+    __shared__ CutCmp cmpl[CUT_G];              // comparison polynomials of the current line
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -496,159 +561,166 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
-    const double* scr_l = p.scr.cut_ls + (size_t)(live ? b : 0) * p.mls_cap * 21;
-    const double* fast_l = p.scr.cut_fast + (size_t)(live ? b : 0) * p.mls_cap * CUT_FAST;
+    const double* rec_l = p.scr.cut_rec + (size_t)(live ? b : 0) * p.mls_cap * CUT_REC;
     for (int i = j; i < 12; i += 8) dtl[g][i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
     const double* Dl = dtl[g];
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    // E role of this lane: lanes 0-2 start endpoint (blend sP -> eP), 3-5 end (eP -> sP)
+    // X role of this lane: lanes 0-2 start endpoint at r0 + {-s, 0, +s}, 3-5 end endpoint
     const int eside = j < 3 ? 0 : 1;
     const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
-    double* my_slot = &epf[g][CUT_SL * (j < 6 ? j : 0)];
-    const double* G0 = &fst[g][eside ? 3 : 0];
-    const double* G1 = &fst[g][eside ? 0 : 3];
-    const double* A0 = &fst[g][eside ? 12 : 6];
-    const double* A1 = &fst[g][eside ? 6 : 12];
-    // C role: neighbour j
+    double* const epf = &tmp[g][0];
+    double* const xs = &tmp[g][CUT_EP];
+    double* const wg = &tmp[g][0];
+    double* const gm = &tmp[g][36];
+    double* my_slot = &epf[CUT_SL * (j < 6 ? j : 0)];
+    // neighbour j of this lane
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
     const unsigned long long gmask = 0xFFull << (8 * g);
+    constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
     // group state (identical in the 8 lanes of a group)
     int m = 0;
     int m_sync = 0;      // sumE holds the exact invCov_sum before line m_sync
     int first = 1;       // first step of the line: the exact centre metric is logdet(invCov_sum)
     double r0 = 0.0, r1 = 0.0;
-    int line_ok = 0;     // certified comparisons allowed on the current line
-    // A line opens: every lane factors S in registers (identical values), then lane
-    // j < 6 solves the W(t) coefficient of side j / 3, power j % 3 from the line's
-    // fast data fd.  Certification needs the factor healthy and gz^2 > homog_th along
-    // the segment (fgz2 = fx / gz^2 on it); otherwise the line takes exact steps.
-    auto open_line = [&](const double* s21, const double* fd) {
+    int line_ok = 0;     // margined comparisons allowed on the current line
+    double dc = 0.0;     // d of the centre
+    int c_ok = 0;        // its error bound is within tau / 4
+    // A line opens (its data in fst, S in registers): every lane factors S (identical
+    // values), lane k < 6 solves W_k = L^-1 P_k (side k / 3, power k % 3), lane j forms
+    // Gram entries j, j + 8, j + 16, and every lane reads the 21 back into its
+    // comparison polynomials.  Margins need the factor healthy and PD_OK.
+    auto open_line = [&]() {
         double o[28];
-        chol_s(s21, o);
-        const double z0 = fd[2], z1 = fd[5];
-        line_ok = (o[27] != 0.0) && ((z0 > 0.0 && z1 > 0.0) || (z0 < 0.0 && z1 < 0.0)) &&
-                  z0 * z0 > 2.0 * homog && z1 * z1 > 2.0 * homog;
+        {
+            double S[21];
+#pragma unroll
+            for (int e = 0; e < 21; ++e) S[e] = sumA[g][e];
+            chol_s(S, o);
+        }
+        line_ok = (o[27] != 0.0) && (fst[g][PD_OK] != 0.0);
         if (j < 6) {
-            double P[6], w[6];
-            cut_poly_coeff(fd + (eside ? 3 : 0), fd + (eside ? 0 : 3), fd[18], fd[19], j % 3, P);
+            double w[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                double u = P[i];
+                double u = fst[g][6 * j + i];
 #pragma unroll
                 for (int k = 0; k < i; ++k) u = __builtin_fma(-o[tri(i, k)], w[k], u);
                 w[i] = u * o[21 + i];
             }
 #pragma unroll
-            for (int i = 0; i < 6; ++i) wpl[g][6 * j + i] = w[i];
+            for (int i = 0; i < 6; ++i) wg[6 * j + i] = w[i];
         }
-    };
-    // Next-line prefetch: lane j loads elements j, j+8, ... of the 42-element vector
-    // [fast data (its last entry: the list index of the line after it) | r = 0 info]
-    // of the group's next line right after a line opens; the values land in LDS one
-    // iteration later.  Every load is a plain f64 load whose value reaches its use
-    // through LDS, so nothing waits for it before that store.
-    size_t q_cur = 0, q_nx = 0;
-    double pf[6];
-    int pending = 0;
-    auto pf_issue = [&](int mm) {
+        wave_lds_sync();
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const int e = j + 8 * k;
-            pf[k] = e < CUT_FAST ? fast_l[(size_t)mm * CUT_FAST + e]
-                                 : scr_l[(size_t)mm * 21 + (size_t)(e < 42 ? e - CUT_FAST : 0)];
+        for (int kk = 0; kk < 3; ++kk) {
+            const int e = j + 8 * kk;
+            if (e < 21) {
+                const int ra = (int)((TRI_ROW >> (3 * e)) & 7), cb = (int)((TRI_COL >> (3 * e)) & 7);
+                double s = wg[6 * ra] * wg[6 * cb];
+#pragma unroll
+                for (int i = 1; i < 6; ++i) s = __builtin_fma(wg[6 * ra + i], wg[6 * cb + i], s);
+                gm[e] = s;
+            }
         }
-        pending = 1;
+        wave_lds_sync();
+        // the comparison polynomials, written straight into cmpl by the lanes:
+        //   lanes 0 / 1: ns / ne (side j), lanes 2 / 3: v'_s / v'e copies,
+        //   lanes 4-6: cc[3 i + k] (i = j - 4) and the bounds bs[i], be[i]
+        double* cl = reinterpret_cast<double*>(&cmpl[g]);
+        if (j < 2) {
+            const int a = 3 * j, b2 = a + 1, c2 = a + 2;
+            double* o = cl + 5 * j;   // ns | ne
+            o[0] = gm[tri(a, a)];
+            o[1] = 2.0 * gm[tri(b2, a)];
+            o[2] = __builtin_fma(2.0, gm[tri(c2, a)], gm[tri(b2, b2)]);
+            o[3] = 2.0 * gm[tri(c2, b2)];
+            o[4] = gm[tri(c2, c2)];
+        } else if (j < 4) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) cl[10 + 5 * (j - 2) + i] = fst[g][PD_VS + 5 * (j - 2) + i];
+        } else if (j < 7) {
+            const int i = j - 4;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cl[20 + 3 * i + k] = gm[tri(3 + k, i)];
+            // |W| with a 1% allowance for the approximate square root (bounds only)
+            const double gs = fmax(gm[tri(i, i)], 0.0), ge = fmax(gm[tri(3 + i, 3 + i)], 0.0);
+            cl[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
+            cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+        }
+        wave_lds_sync();
+        // the centre of the first step: d at (0, 0)
+        const double vs0 = cl[10], ve0 = cl[15];
+        dc = cut_dcore(cl[0], vs0, cl[5], ve0, cl[20], cl[29], cl[32], fabs(vs0), fabs(ve0), tau, c_ok);
+    };
+    // Next-line prefetch: right after a line opens the group's lanes copy the next line's
+    // record (576 B) from HBM straight into LDS (global_load_lds, no registers); it is
+    // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
+    size_t q_cur = 0, q_nx = 0;
+    auto pf_issue = [&](int mm) {
+        const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (k < 4 || j < 4)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
+                                                 (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
     };
     if (m < nls) {
         q_cur = lb + mls[0];
         if (nls > 1) q_nx = lb + mls[1];
-        double fd0[CUT_FAST];
+        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = rec_l[e];
 #pragma unroll
-        for (int e = 0; e < CUT_FAST; ++e) fd0[e] = fast_l[e];
-        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = fd0[e];
-        double s21[21];
-#pragma unroll
-        for (int e = 0; e < 21; ++e) {
+        for (int e = j; e < 21; e += 8) {
             const double s0 = p.scr.cut_sum[24 * b + e];
-            s21[e] = s0 - scr_l[e];
+            sumA[g][e] = s0 - rec_l[CUT_FAST + e];
             sumE[g][e] = s0;
-            sumA[g][e] = s21[e];
         }
-        open_line(s21, fd0);
+        wave_lds_sync();
+        open_line();
         if (nls > 1) pf_issue(1);
-    } else {
-        for (int e = j; e < CUT_FAST; e += 8) fst[g][e] = (e == 2 || e == 5) ? 1.0 : 0.0;
     }
     __syncthreads();
-#ifdef GFPL_CUT_PROF
-    unsigned long long cp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cp_last = clock64(), cp_it = 0, cp_fin = 0;
-#define CUT_PROF(k) { const unsigned long long _t = clock64(); cp_acc[k] += _t - cp_last; cp_last = _t; }
-#else
-#define CUT_PROF(k)
+#ifdef GFPL_CUT_STATS
+    unsigned st_it = 0, st_x = 0, st_fin = 0, st_bound = 0, st_gap = 0, st_line = 0;
 #endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls;
-        // ---- A: this lane's endpoint terms for the certified comparisons (polynomial
-        //      form, see cut_poly_coeff): v' (slot 0), W (slots 7-12), a = |W|^2 / v' (13)
-        if (j < 6) {
-            const double t = (eside == 0 ? r0 : r1) + eoff;
-            const double om = 1.0 - t;
-            double gv[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) gv[k] = __builtin_fma(om, G0[k], t * G1[k]);
-            const double jl0 = fst[g][18], jl1 = fst[g][19];
-            const double p0 = jl0 * gv[2], p1 = jl1 * gv[2], p2 = -__builtin_fma(jl0, gv[0], jl1 * gv[1]);
-            auto quad = [&](const double* A) {
-                const double diag = __builtin_fma(A[0] * p0, p0, __builtin_fma(A[3] * p1, p1, A[5] * p2 * p2));
-                const double off = __builtin_fma(A[1] * p0, p1, __builtin_fma(A[2] * p0, p2, A[4] * p1 * p2));
-                return __builtin_fma(2.0, off, diag);
-            };
-            const double v = __builtin_fma(om * om, quad(A0), t * t * quad(A1));
-            const double* Wc = &wpl[g][18 * eside];
-            double w[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) w[i] = __builtin_fma(t, __builtin_fma(t, Wc[12 + i], Wc[6 + i]), Wc[i]);
-            double a = w[0] * w[0];
-#pragma unroll
-            for (int i = 1; i < 6; ++i) a = __builtin_fma(w[i], w[i], a);
-            my_slot[0] = v;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) my_slot[7 + i] = w[i];
-            my_slot[13] = a * rcp_fast(v);
-        }
-        // the prefetched next line lands in LDS (its loads were issued >= 1 iteration ago)
-        if (pending) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k)
-                if (j + 8 * k < 42) nxt[g][j + 8 * k] = pf[k];
-            pending = 0;
-        }
-        wave_lds_sync();
-        CUT_PROF(0);
-        // ---- B: d of neighbour j and of the centre; certified group decision
+        // ---- lane j: d of neighbour j; the group decision and its margins
         const double t0 = r0 + nb0, t1 = r1 + nb1;
         int valid = act ? 1 : 0;
         if (t0 + t1 > 1.0) valid = 0;
         if (t0 < rlo || t0 > rhi) valid = 0;
         if (t1 < rlo || t1 > rhi) valid = 0;
-        const double dj = cut_d(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce]);
-        const double dc = cut_d(&epf[g][CUT_SL * 1], &epf[g][CUT_SL * 4]);
+        int bok;
+        double dj;
+        {
+            const CutCmp cmp = cmpl[g];
+            dj = cut_dval(cmp, t0, t1, tau, bok);
+        }
         double top;
         int best = group_first_max(dj, valid, j, dc, top);
-        // every comparison the decision rests on must clear the margin; NaN
-        // (unhealthy) values fail every test
+        // every comparison the decision rests on must clear the margin, every d its
+        // error bound; NaN (unhealthy) values fail every test
         int ok = 1;
+        if (valid && !bok) ok = 0;
         if (best >= 0) {
             if (valid && j != best && !(top - dj > tau * top)) ok = 0;
             if (!(top - dc > tau * top)) ok = 0;
         } else {
             if (valid && !(dc - dj > tau * dc)) ok = 0;
         }
-        if (!(tau > 0.0 && line_ok && dc == dc)) ok = 0;
+        if (!(tau > 0.0 && line_ok && c_ok && dc == dc)) ok = 0;
         const bool exact = act && (__ballot(!ok) & gmask) != 0;
-        CUT_PROF(1);
+#ifdef GFPL_CUT_STATS
+        ++st_it;
+        if (__any(exact)) ++st_x;
+        if (__any(act && valid && !bok)) ++st_bound;
+        if (__any(act && !(line_ok && c_ok))) ++st_line;
+        if (__any(exact && bok && line_ok && c_ok)) ++st_gap;
+#endif
+        double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
+        int cnext = 1;
         if (__any(exact)) {
             // ---- X: the reference's evaluation of this step for the groups that need it.
             // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at
@@ -659,30 +731,24 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
                 const size_t qf = fl ? lb + mls[m_sync] : lb;
                 __threadfence_block();   // this lane's own L.cut stores are complete
                 if (fl && j == 0) {   // ratios stored by this lane at the line's finalisation
-                    xs[g][14] = L.cut[2 * qf];
-                    xs[g][15] = L.cut[2 * qf + 1];
+                    xs[14] = L.cut[2 * qf];
+                    xs[15] = L.cut[2 * qf + 1];
                 }
                 wave_lds_sync();
                 if (fl && j < 2) {
-                    LineCutData d;
-                    load_line(L, qf, d);
-                    double P0[3], P1[3], C0[9], C1[9], o7[7];
+                    double o7[7];
+                    exact_endpoint(cam, homog, Dl, L, qf, j, xs[14 + j], o7);
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) { P0[k] = j ? d.eP[k] : d.sP[k]; P1[k] = j ? d.sP[k] : d.eP[k]; }
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) { C0[k] = j ? d.covE[k] : d.covS[k]; C1[k] = j ? d.covS[k] : d.covE[k]; }
-                    cut_endpoint(cam, homog, Dl, d.Jl, P0, P1, C0, C1, xs[g][14 + j], o7);
-#pragma unroll
-                    for (int i = 0; i < 7; ++i) xs[g][7 * j + i] = o7[i];
+                    for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
                 }
                 wave_lds_sync();
                 if (fl) {
                     double info[21];
-                    cut_assemble<false>(&xs[g][0], &xs[g][7], info);
+                    cut_assemble<false>(&xs[0], &xs[7], info);
 #pragma unroll
                     for (int e = 0; e < 21; ++e) {
-                        const double S = sumE[g][e] - scr_l[(size_t)m_sync * 21 + e];
-                        sumE[g][e] = S + info[e];
+                        const double Se = sumE[g][e] - rec_l[(size_t)m_sync * CUT_REC + CUT_FAST + e];
+                        sumE[g][e] = Se + info[e];
                     }
                     ++m_sync;
                 }
@@ -690,107 +756,124 @@ __global__ void __launch_bounds__(64) k_cut_search(KParams p) {
             }
             // 2. exact endpoints of this step's six slots, exact S of line m
             if (exact) {
-                LineCutData d;
-                load_line(L, q_cur, d);
                 if (j < 6) {
                     const double t = (eside == 0 ? r0 : r1) + eoff;
-                    double P0[3], P1[3], C0[9], C1[9], o7[7];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        P0[k] = eside ? d.eP[k] : d.sP[k];
-                        P1[k] = eside ? d.sP[k] : d.eP[k];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) {
-                        C0[k] = eside ? d.covE[k] : d.covS[k];
-                        C1[k] = eside ? d.covS[k] : d.covE[k];
-                    }
-                    cut_endpoint(cam, homog, Dl, d.Jl, P0, P1, C0, C1, t, o7);
+                    double o7[7];
+                    exact_endpoint(cam, homog, Dl, L, q_cur, eside, t, o7);
 #pragma unroll
                     for (int i = 0; i < 7; ++i) my_slot[i] = o7[i];
                 }
 #pragma unroll
-                for (int e = 0; e < 21; ++e) xs[g][e] = sumE[g][e] - scr_l[(size_t)m * 21 + e];
+                for (int e = 0; e < 21; ++e) xs[e] = sumE[g][e] - rec_l[(size_t)m * CUT_REC + CUT_FAST + e];
             }
             wave_lds_sync();
             // 3. the reference's metrics and decision
             if (exact) {
                 double mc;
-                const double vj = cut_exact_step(&epf[g][CUT_SL * cs], &epf[g][CUT_SL * ce], &epf[g][CUT_SL * 1],
-                                                 &epf[g][CUT_SL * 4], xs[g], sumE[g], first, &mc);
+                const double vj = cut_exact_step(&epf[CUT_SL * cs], &epf[CUT_SL * ce], &epf[CUT_SL * 1],
+                                                 &epf[CUT_SL * 4], xs, sumE[g], first, &mc);
                 best = group_first_max(vj, valid, j, mc, top);
             }
+            // the next centre's d and bound come from the lane that evaluated it
+            const int src = (lane & ~7) + (best >= 0 ? best : 0);
+            const double sd = __shfl(dj, src);
+            const int sb = __shfl(bok, src);
+            if (exact) { dnext = sd; cnext = sb; }
         }
-        CUT_PROF(2);
         int finalize = 0;
         if (act) {
             first = 0;
             if (best >= 0) {
                 r0 = r0 + nb_step(best, 0, st);
                 r1 = r1 + nb_step(best, 1, st);
+                dc = dnext;
+                c_ok = cnext;
                 if (!(r0 + r1 <= 1.0)) finalize = 1;   // while-condition
             } else {
-                finalize = 1;   // the middle endpoints of this step are (r0 + 0, r1 + 0) = (r0, r1)
+                finalize = 1;
             }
         }
-        if (act && finalize) {
-            // approximate invCov_sum += info of the chosen ratio (the exact one is
-            // accumulated lazily, only when an exact step needs it)
-            // (the slots hold the polynomial-form terms, not v and J)
-            double S7[7], E7[7];
-            cut_endpoint_fast(cam, homog, &fst[g][0], &fst[g][3], &fst[g][6], &fst[g][12], fst[g][18], fst[g][19],
-                              r0, S7);
-            cut_endpoint_fast(cam, homog, &fst[g][3], &fst[g][0], &fst[g][12], &fst[g][6], fst[g][18], fst[g][19],
-                              r1, E7);
-            double info[21];
-            CUT_PROF(4);
-            cut_assemble<false>(S7, E7, info);
-            double s21[21];
+#ifdef GFPL_CUT_STATS
+        if (__any(act && finalize)) ++st_fin;
+#endif
+        if (__any(act && finalize)) {
+            double info[3];
+            if (act && finalize) {
+                // approximate invCov_sum += info of the chosen ratio (the exact one is
+                // accumulated lazily, only when an exact step needs it):
+                // info = Ps Ps^T / v's + Pe Pe^T / v'e (the fgz2 factors cancel)
+                // lane i < 6: entry i of Ps and Pe at the final ratios, lane 6 / 7: v's / v'e;
+                // with PD_OK = 0 (the segment leaves the polynomial form's domain, rare)
+                // lanes 0 / 1 write the reference-order endpoints (v, J) instead, J Js^T / v
+                // being the same matrix as P P^T / v'
+                if (fst[g][PD_OK] != 0.0) {
+                    if (j < 6) {
+                        xs[1 + j] = h2(fst[g][PD_PS + j], fst[g][PD_PS + 6 + j], fst[g][PD_PS + 12 + j], r0);
+                        xs[8 + j] = h2(fst[g][PD_PE + j], fst[g][PD_PE + 6 + j], fst[g][PD_PE + 12 + j], r1);
+                    } else {
+                        const int o = j == 6 ? PD_VS : PD_VE;
+                        const double t = j == 6 ? r0 : r1;
+                        xs[7 * (j - 6)] = __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, fst[g][o + 4], fst[g][o + 3]),
+                                                       fst[g][o + 2]), fst[g][o + 1]), fst[g][o]);
+                    }
+                } else if (j < 2) {
+                    double o7[7];
+                    exact_endpoint(cam, homog, Dl, L, q_cur, j, j ? r1 : r0, o7);
 #pragma unroll
-            for (int e = 0; e < 21; ++e) s21[e] = sumA[g][e] + info[e];
-            CUT_PROF(5);
-            if (j == 0) {
-                L.cut[2 * q_cur] = r0;
-                L.cut[2 * q_cur + 1] = r1;
+                    for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
+                }
+                if (j == 0) {
+                    L.cut[2 * q_cur] = r0;
+                    L.cut[2 * q_cur + 1] = r1;
+                }
+                ++m;
             }
-            ++m;
-            if (m < nls) {
+            const bool opening = act && finalize && m < nls;
+            wave_lds_sync();   // the finished line's data is read before it is replaced
+            if (act && finalize) {
+                // lane j: entries j, j + 8, j + 16 of info = Ps Ps^T / v's + Pe Pe^T / v'e
+                const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
+#pragma unroll
+                for (int kk = 0; kk < 3; ++kk) {
+                    const int e = min(j + 8 * kk, 20);   // entries past 20 are computed and dropped
+                    const int ra = (int)((TRI_ROW >> (3 * e)) & 7), cb = (int)((TRI_COL >> (3 * e)) & 7);
+                    info[kk] = __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
+                }
+            }
+            if (opening) {
+                // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int k = 0; k < CUT_FAST / 8; ++k) {
+                    const int e = j + 8 * k;
+                    fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
+                }
+            }
+            wave_lds_sync();
+            if (opening) {
                 q_cur = q_nx;
-                q_nx = lb + (size_t)(int)nxt[g][CUT_FAST - 1];
+                q_nx = lb + (size_t)(int)fst[g][PD_NEXT];
                 first = 1;
                 r0 = 0.0;
                 r1 = 0.0;
-                // line m from the prefetch buffer
-                double nx[42];
 #pragma unroll
-                for (int e = 0; e < 42; ++e) nx[e] = nxt[g][e];
-#pragma unroll
-                for (int e = 0; e < 21; ++e) s21[e] = s21[e] - nx[CUT_FAST + e];
-#pragma unroll
-                for (int e = 0; e < CUT_FAST; ++e) fst[g][e] = nx[e];
-#pragma unroll
-                for (int e = 0; e < 21; ++e) sumA[g][e] = s21[e];
-                CUT_PROF(6);
-                open_line(s21, nx);
-                CUT_PROF(7);
+                for (int kk = 0; kk < 3; ++kk) {
+                    const int e = j + 8 * kk;
+                    const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
+                    if (e < 21) sumA[g][e] = (sumA[g][e] + info[kk]) - nxl[x >> 4][16 * g + (x & 15)];
+                }
+            }
+            wave_lds_sync();
+            if (opening) {   // group-uniform; open_line exchanges through LDS only
+                open_line();
                 if (m + 1 < nls) pf_issue(m + 1);
             }
         }
-#ifdef GFPL_CUT_PROF
-        if (__any(act && finalize)) ++cp_fin;
-#endif
-        CUT_PROF(8);
-        wave_lds_sync();
-        CUT_PROF(3);
-#ifdef GFPL_CUT_PROF
-        ++cp_it;
-#endif
     }
-#ifdef GFPL_CUT_PROF
-    if (lane == 0 && (blockIdx.x % 256) == 0)
-        printf("cutprof blk %d it %llu fin %llu A %llu B %llu X %llu pre %llu asm %llu nxt %llu chol %llu post %llu sync %llu\n",
-               blockIdx.x, cp_it, cp_fin, cp_acc[0], cp_acc[1], cp_acc[2], cp_acc[4], cp_acc[5], cp_acc[6], cp_acc[7],
-               cp_acc[8], cp_acc[3]);
+#ifdef GFPL_CUT_STATS
+    if (lane == 0 && (blockIdx.x % 128) == 0)
+        printf("cutstats blk %d it %u x %u fin %u bound %u line %u gap %u\n", blockIdx.x, st_it, st_x, st_fin, st_bound,
+               st_line, st_gap);
 #endif
 }
 
