@@ -526,6 +526,95 @@ __device__ __forceinline__ int group_first_max(double v, int valid, int j, doubl
 // the in-flight global prefetch loads.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// ---- exact step (X), out of line: rare, and its two 6x6 LLTs, reference-order endpoints
+// and the exact-sum flush would otherwise set the register budget of the search loop.
+struct CutX {
+    int best;     // the reference's decision for groups that took the exact step (else unchanged)
+    int m_sync;   // sumE now holds the exact invCov_sum before line m_sync (= m for those groups)
+};
+__device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid, int first, int m, int m_sync, double r0,
+                                                          double r1, size_t q_cur, size_t lb, int best,
+                                                          const int32_t* mls, const double* rec_l, double* sP, double* eP,
+                                                          double* covS, double* covE, double* le_obs, double* cut,
+                                                          double* sumE, double* tmp, const double* Dl, double fx, double cb,
+                                                          double homog, double st) {
+    const int j = threadIdx.x & 7;
+    DevCam cam{};
+    cam.fx = fx;
+    cam.b = cb;
+    DevLines L{};
+    L.sP = sP;
+    L.eP = eP;
+    L.covS = covS;
+    L.covE = covE;
+    L.le_obs = le_obs;
+    L.cut = cut;
+    // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at their final
+    //    ratios), eight lines per round: lane j computes the reference-order info of line
+    //    m_sync + j at its final ratios (stored by lane 0 at the line's finalisation; read
+    //    past the L1), lanes 0-6 add them into sumE in list order, seven entries per pass
+    while (__any(exact && m_sync < m)) {
+        const bool fl = exact && m_sync < m;
+        const int nl = fl ? min(8, m - m_sync) : 0;
+        __threadfence();
+        double info[21];
+        if (j < nl) {
+            const size_t qf = lb + mls[m_sync + j];
+            const double c0 = __hip_atomic_load(&L.cut[2 * qf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double c1 = __hip_atomic_load(&L.cut[2 * qf + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double s7[7], e7[7];
+            exact_endpoint(cam, homog, Dl, L, qf, 0, c0, s7);
+            exact_endpoint(cam, homog, Dl, L, qf, 1, c1, e7);
+            cut_assemble<false>(s7, e7, info);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (j < nl) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) tmp[7 * j + i] = info[7 * c + i];
+            }
+            wave_lds_sync();
+            if (fl && j < 7) {
+                const int e = 7 * c + j;
+                double Se = sumE[e];
+                for (int l = 0; l < nl; ++l)
+                    Se = (Se - rec_l[(size_t)(m_sync + l) * CUT_REC + CUT_FAST + e]) + tmp[7 * l + j];
+                sumE[e] = Se;
+            }
+            wave_lds_sync();
+        }
+        m_sync += nl;
+    }
+    // 2. exact endpoints of this step's six slots (lanes 0-2: start endpoint at
+    //    r0 + {-s, 0, +s}, lanes 3-5: end endpoint), exact S of line m
+    double* const epf = tmp;
+    double* const xs = tmp + CUT_EP;
+    if (exact) {
+        if (j < 6) {
+            const int eside = j < 3 ? 0 : 1;
+            const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
+            const double t = (eside == 0 ? r0 : r1) + eoff;
+            double o7[7];
+            exact_endpoint(cam, homog, Dl, L, q_cur, eside, t, o7);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) epf[CUT_SL * j + i] = o7[i];
+        }
+#pragma unroll
+        for (int e = 0; e < 21; ++e) xs[e] = sumE[e] - rec_l[(size_t)m * CUT_REC + CUT_FAST + e];
+    }
+    wave_lds_sync();
+    // 3. the reference's metrics and decision
+    if (exact) {
+        const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
+        double mc, top;
+        const double vj = cut_exact_step(&epf[CUT_SL * cs], &epf[CUT_SL * ce], &epf[CUT_SL * 1], &epf[CUT_SL * 4], xs,
+                                         sumE, first, &mc);
+        best = group_first_max(vj, valid, j, mc, top);
+    }
+    wave_lds_sync();
+    return CutX{best, m_sync};
+}
+
 // lower-triangle index e (0..20) -> row / column, packed 3 bits per entry
 constexpr unsigned long long tri_pack(int want_row) {
     unsigned long long v = 0;
@@ -566,17 +655,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const double* Dl = dtl[g];
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    // X role of this lane: lanes 0-2 start endpoint at r0 + {-s, 0, +s}, 3-5 end endpoint
-    const int eside = j < 3 ? 0 : 1;
-    const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
-    double* const epf = &tmp[g][0];
     double* const xs = &tmp[g][CUT_EP];
     double* const wg = &tmp[g][0];
     double* const gm = &tmp[g][36];
-    double* my_slot = &epf[CUT_SL * (j < 6 ? j : 0)];
     // neighbour j of this lane
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
-    const int cs = nb_slot(j, 0), ce = 3 + nb_slot(j, 1);
     const unsigned long long gmask = 0xFFull << (8 * g);
     constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
     // group state (identical in the 8 lanes of a group)
@@ -722,58 +805,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
         int cnext = 1;
         if (__any(exact)) {
-            // ---- X: the reference's evaluation of this step for the groups that need it.
-            // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at
-            //    their final ratios, one line per round: lanes 0 / 1 its start / end
-            //    endpoint, then every lane the reference's sum chain)
-            while (__any(exact && m_sync < m)) {
-                const bool fl = exact && m_sync < m;
-                const size_t qf = fl ? lb + mls[m_sync] : lb;
-                __threadfence_block();   // this lane's own L.cut stores are complete
-                if (fl && j == 0) {   // ratios stored by this lane at the line's finalisation
-                    xs[14] = L.cut[2 * qf];
-                    xs[15] = L.cut[2 * qf + 1];
-                }
-                wave_lds_sync();
-                if (fl && j < 2) {
-                    double o7[7];
-                    exact_endpoint(cam, homog, Dl, L, qf, j, xs[14 + j], o7);
-#pragma unroll
-                    for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
-                }
-                wave_lds_sync();
-                if (fl) {
-                    double info[21];
-                    cut_assemble<false>(&xs[0], &xs[7], info);
-#pragma unroll
-                    for (int e = 0; e < 21; ++e) {
-                        const double Se = sumE[g][e] - rec_l[(size_t)m_sync * CUT_REC + CUT_FAST + e];
-                        sumE[g][e] = Se + info[e];
-                    }
-                    ++m_sync;
-                }
-                wave_lds_sync();
-            }
-            // 2. exact endpoints of this step's six slots, exact S of line m
-            if (exact) {
-                if (j < 6) {
-                    const double t = (eside == 0 ? r0 : r1) + eoff;
-                    double o7[7];
-                    exact_endpoint(cam, homog, Dl, L, q_cur, eside, t, o7);
-#pragma unroll
-                    for (int i = 0; i < 7; ++i) my_slot[i] = o7[i];
-                }
-#pragma unroll
-                for (int e = 0; e < 21; ++e) xs[e] = sumE[g][e] - rec_l[(size_t)m * CUT_REC + CUT_FAST + e];
-            }
-            wave_lds_sync();
-            // 3. the reference's metrics and decision
-            if (exact) {
-                double mc;
-                const double vj = cut_exact_step(&epf[CUT_SL * cs], &epf[CUT_SL * ce], &epf[CUT_SL * 1],
-                                                 &epf[CUT_SL * 4], xs, sumE[g], first, &mc);
-                best = group_first_max(vj, valid, j, mc, top);
-            }
+            // ---- X: the reference's evaluation of this step for the groups that need it
+            const CutX xr = cut_exact_round(exact, valid, first, m, m_sync, r0, r1, q_cur, lb, best, mls, rec_l, L.sP, L.eP,
+                                            L.covS, L.covE, L.le_obs, L.cut, sumE[g], tmp[g], Dl, cam.fx, cam.b, homog, st);
+            best = xr.best;
+            m_sync = xr.m_sync;
             // the next centre's d and bound come from the lane that evaluated it
             const int src = (lane & ~7) + (best >= 0 ? best : 0);
             const double sd = __shfl(dj, src);
