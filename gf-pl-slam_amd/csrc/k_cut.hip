@@ -336,6 +336,15 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
 // data from the prefetch registers through LDS, its S factored and the Gram matrix
 // of its W coefficients formed across the group's lanes.
 #define CUT_G 8          // sequences per wave (8 lanes each)
+// A line transition waits until CUT_BATCH groups of the wave have finished their line
+// or one of them has waited CUT_WAIT iterations (measured at B = 16384: 8 / 16, i.e.
+// nearly lock-step lines, 6.7 ms; 3 / 3 8.5 ms; no batching 10.9 ms)
+#ifndef CUT_BATCH
+#define CUT_BATCH 8
+#endif
+#ifndef CUT_WAIT
+#define CUT_WAIT 16
+#endif
 #define CUT_SL 7         // exact endpoint slot (X): v, J[6]
 #define CUT_EP 43        // per-group exact endpoint block: 6 slots + 1 (odd stride)
 #define CUT_NX (CUT_FAST + 21)   // used part of a line record: comparison data | r = 0 info
@@ -508,7 +517,9 @@ template <int CTRL>
 __device__ __forceinline__ void argmax_step(double& v, int& k) {
     const double ov = dpp_f64<CTRL>(v);
     const int ok = dpp_i32<CTRL>(k);
-    if (ov > v || (ov == v && ok < k)) { v = ov; k = ok; }
+    const bool take = (ov > v) | ((ov == v) & (ok < k));   // selects, not branches
+    v = take ? ov : v;
+    k = take ? ok : k;
 }
 __device__ __forceinline__ int group_first_max(double v, int valid, int j, double mc, double& top) {
     double x = (valid && v == v) ? v : -__builtin_inf();
@@ -668,6 +679,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     int first = 1;       // first step of the line: the exact centre metric is logdet(invCov_sum)
     double r0 = 0.0, r1 = 0.0;
     int line_ok = 0;     // margined comparisons allowed on the current line
+    int pend = 0;        // the line finished; the next one opens at the next transition
+    int wait = 0;        // iterations spent waiting for that transition
     double dc = 0.0;     // d of the centre
     int c_ok = 0;        // its error bound is within tau / 4
     // A line opens (its data in fst, S in registers): every lane factors S (identical
@@ -768,7 +781,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     unsigned st_it = 0, st_x = 0, st_fin = 0, st_bound = 0, st_gap = 0, st_line = 0;
 #endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
-        const bool act = m < nls;
+        const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
         const double t0 = r0 + nb0, t1 = r1 + nb1;
         int valid = act ? 1 : 0;
@@ -832,9 +845,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #ifdef GFPL_CUT_STATS
         if (__any(act && finalize)) ++st_fin;
 #endif
-        if (__any(act && finalize)) {
+        if (act && finalize) {
+            if (j == 0) {
+                L.cut[2 * q_cur] = r0;
+                L.cut[2 * q_cur + 1] = r1;
+            }
+            ++m;
+            pend = m < nls;   // the next line opens at the next transition
+            wait = 0;
+        }
+        // Transitions are batched: a group whose line finished waits (no steps) until
+        // CUT_BATCH groups of the wave wait, one has waited CUT_WAIT iterations, or no
+        // group has steps left; one transition then serves all of them, so the wave
+        // pays its serial chain (factor, solves, LDS exchanges) fewer times.
+        const int npend = __popcll(__ballot(pend)) >> 3;
+        if (npend > 0 && (npend >= CUT_BATCH || __any(pend && wait >= CUT_WAIT) || __ballot(m < nls && !pend) == 0)) {
             double info[3];
-            if (act && finalize) {
+            if (pend) {
                 // approximate invCov_sum += info of the chosen ratio (the exact one is
                 // accumulated lazily, only when an exact step needs it):
                 // info = Ps Ps^T / v's + Pe Pe^T / v'e (the fgz2 factors cancel)
@@ -858,15 +885,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
                     for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
                 }
-                if (j == 0) {
-                    L.cut[2 * q_cur] = r0;
-                    L.cut[2 * q_cur + 1] = r1;
-                }
-                ++m;
             }
-            const bool opening = act && finalize && m < nls;
             wave_lds_sync();   // the finished line's data is read before it is replaced
-            if (act && finalize) {
+            if (pend) {
                 // lane j: entries j, j + 8, j + 16 of info = Ps Ps^T / v's + Pe Pe^T / v'e
                 const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
 #pragma unroll
@@ -875,8 +896,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     const int ra = (int)((TRI_ROW >> (3 * e)) & 7), cb = (int)((TRI_COL >> (3 * e)) & 7);
                     info[kk] = __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
                 }
-            }
-            if (opening) {
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -886,7 +905,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 }
             }
             wave_lds_sync();
-            if (opening) {
+            if (pend) {
                 q_cur = q_nx;
                 q_nx = lb + (size_t)(int)fst[g][PD_NEXT];
                 first = 1;
@@ -900,10 +919,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 }
             }
             wave_lds_sync();
-            if (opening) {   // group-uniform; open_line exchanges through LDS only
+            if (pend) {   // group-uniform; open_line exchanges through LDS only
                 open_line();
                 if (m + 1 < nls) pf_issue(m + 1);
+                pend = 0;
             }
+        } else if (pend) {
+            ++wait;
         }
     }
 #ifdef GFPL_CUT_STATS
