@@ -43,12 +43,24 @@ $(BINDIR)/plslam_gpu: $(PKG)/host/plslam_gpu.cpp $(LIBDIR)/libgfpl_stvo.so $(LIB
 oracle/liboracle.so: oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h include/gfpl.h
 	$(CXX) $(ORACLEFLAGS) $< -o $@
 
+# the CPU oracle (+ the synthetic generator and the host setup code it
+# uses) under ASan + UBSan, driven over every test camera; aborts on the first report
+ASANFLAGS := -O1 -g -std=c++17 -ffp-contract=off -Wall -Iinclude -fno-omit-frame-pointer \
+             -fsanitize=address,undefined -fno-sanitize-recover=all
+oracle/build/asan_driver: oracle/asan_driver.cpp oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h \
+                          $(PKG)/synth/gfpl_synth.cpp $(PKG)/csrc/gfpl_setup.cpp include/gfpl.h
+	@mkdir -p oracle/build
+	$(CXX) $(ASANFLAGS) oracle/asan_driver.cpp oracle/gfpl_oracle.cpp $(PKG)/synth/gfpl_synth.cpp \
+	    $(PKG)/csrc/gfpl_setup.cpp -o $@ -lpthread
+oracle-asan: oracle/build/asan_driver
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 ./oracle/build/asan_driver
+
 oracle: oracle/liboracle.so
 synth: $(LIBDIR)/libgfpl_synth.so
 hip: $(LIBDIR)/libgfpl_hip.so
 host: $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu
 
 clean:
-	rm -f $(LIBDIR)/*.so oracle/liboracle.so $(BINDIR)/plslam_gpu
+	rm -f $(LIBDIR)/*.so oracle/liboracle.so $(BINDIR)/plslam_gpu oracle/build/asan_driver
 
-.PHONY: all clean oracle synth hip host
+.PHONY: all clean oracle oracle-asan synth hip host

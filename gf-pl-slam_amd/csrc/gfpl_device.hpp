@@ -28,6 +28,12 @@ GFPL_DEV double from_words(uint32_t hi, uint32_t lo) {
 
 // ------------------------------------------------- fdlibm log / sin / cos
 // e_log.c, k_sin.c, k_cos.c, e_rem_pio2.c (medium range) — pin N3.
+// The log / sin / cos below restate the algorithms and coefficient tables of Sun fdlibm
+// (e_log.c, k_sin.c, k_cos.c, e_rem_pio2.c), whose notice is preserved here:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely granted,
+//   provided that this notice is preserved.
 GFPL_DEV double det_log(double x) {
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                  two54 = 1.80143985094819840000e+16,

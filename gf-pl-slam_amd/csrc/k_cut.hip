@@ -777,9 +777,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (nls > 1) pf_issue(1);
     }
     __syncthreads();
-#ifdef GFPL_CUT_STATS
-    unsigned st_it = 0, st_x = 0, st_fin = 0, st_bound = 0, st_gap = 0, st_line = 0;
-#endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -808,13 +805,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         if (!(tau > 0.0 && line_ok && c_ok && dc == dc)) ok = 0;
         const bool exact = act && (__ballot(!ok) & gmask) != 0;
-#ifdef GFPL_CUT_STATS
-        ++st_it;
-        if (__any(exact)) ++st_x;
-        if (__any(act && valid && !bok)) ++st_bound;
-        if (__any(act && !(line_ok && c_ok))) ++st_line;
-        if (__any(exact && bok && line_ok && c_ok)) ++st_gap;
-#endif
         double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
         int cnext = 1;
         if (__any(exact)) {
@@ -842,9 +832,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 finalize = 1;
             }
         }
-#ifdef GFPL_CUT_STATS
-        if (__any(act && finalize)) ++st_fin;
-#endif
         if (act && finalize) {
             if (j == 0) {
                 L.cut[2 * q_cur] = r0;
@@ -928,11 +915,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             ++wait;
         }
     }
-#ifdef GFPL_CUT_STATS
-    if (lane == 0 && (blockIdx.x % 128) == 0)
-        printf("cutstats blk %d it %u x %u fin %u bound %u line %u gap %u\n", blockIdx.x, st_it, st_x, st_fin, st_bound,
-               st_line, st_gap);
-#endif
 }
 
 // ---------------------------------------------------------------- finish --

@@ -127,27 +127,20 @@ __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) 
 #pragma unroll
         for (int i = 0; i < 11; ++i) cRR[i] = (uint32_t)byte_at(ir6, 5 + i) * 0x10001u;
     }
-#ifndef GFPL_SAD_SERIAL
     uint32_t il4[3][3], ir6[3][6];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int r = q + 4 * i;
         sad_load_row(J, J.vL - 5 + (r < 11 ? r : 5), il4[i], ir6[i]);
     }
-#endif
     // SAD = sum |(IL - cL) - (IR_s - cR[s])| = sum |(IL + cR[s]) - (IR_s + cL)|, both
     // sides <= 510: two columns per v_sad_u16 (16-bit lanes of one register)
     const uint32_t cLL = (uint32_t)cL * 0x10001u;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (q + 4 * i >= 11) break;
-#ifdef GFPL_SAD_SERIAL
-        uint32_t L[3], R[6];
-        sad_load_row(J, J.vL - 5 + q + 4 * i, L, R);
-#else
         const uint32_t* L = il4[i];
         const uint32_t* R = ir6[i];
-#endif
         uint32_t ILp[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) ILp[k] = (uint32_t)byte_at(L, 2 * k) | ((uint32_t)byte_at(L, 2 * k + 1) << 16);
@@ -263,14 +256,8 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         }
         if (i < N) {
             const float y = KL[i].y;
-#ifdef GFPL_EXP_LVL_ORDER
-            const int row = (y >= 0.0f && y < 8190.0f) ? (int)y + 1 : 0;
-            const int lv = clamp_level(KL[i].octave, p.cam.n_levels);
-            order[i] = ((uint32_t)((lv << 13) | row) << 16) | (uint32_t)i;
-#else
             const int row = (y >= 0.0f && y < 65534.0f) ? (int)y + 1 : 0;
             order[i] = ((uint32_t)row << 16) | (uint32_t)i;
-#endif
         } else {
             order[i] = 0xFFFFFFFFu;
         }
@@ -347,7 +334,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                     }
                 }
                 };
-#ifndef GFPL_EXP_NO_BAND
                 if (SEG) {
                     const int olo = (int)max((long long)levelL - 1, 0LL);
                     const int ohi = (int)min((long long)levelL + 1, (long long)nlev - 1);
@@ -356,7 +342,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                 } else {
                     scan(rowlo[row], 0);
                 }
-#endif
                 if (bestDist < 80) {
                     atomicAdd(&misc[2], 1);
                     SadJob J;
@@ -848,11 +833,7 @@ hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
     const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((p.cam.n_levels * p.cam.height + 1) & ~1) * 2 + 32 * 4;
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
-#ifdef GFPL_EXP_SP1024
-    if (true)
-#else
     if (p.kp_cap > 2048)
-#endif
         hipLaunchKernelGGL((k_stereo_points<1024, false>), dim3(p.B), dim3(1024), lds, s, p, KP2);
     else if (GFPL_SP_SEG && lds_seg <= 40960)   // four workgroups per CU
         hipLaunchKernelGGL((k_stereo_points<512, true>), dim3(p.B), dim3(512), lds_seg, s, p, KP2);

@@ -5,14 +5,21 @@
 //
 // Per frame: initialize (frame 0) or insertStereoPair -> optimizePose(prev_frame->DT)
 // -> numFrameLoss check -> needNewKF / currFrameIsKF -> updateFrame_ECCV18(T_base),
-// then the trajectory line of PREFIX_AllFrameTrajectory.txt in the reference's format
-// (app/plslam_mod.cpp:288-293, 480-493: fixed, setprecision(7), " tx ty tz qx qy qz qw"
-// of R^T).  Mapping (local BA, loop closure) is out of scope: the keyframe chain is
+// then the lines of the reference's three text outputs, in its formats:
+//  PREFIX_AllFrameTrajectory.txt (app/plslam_mod.cpp:288-293, 480-493): fixed,
+//      setprecision(7), " tx ty tz qx qy qz qw" of the logged pose, quaternion of R^T;
+//  PREFIX_Log.txt (:296-301, 494-513): the just-processed frame's TimeLog, timestamp
+//      setprecision(6), times [s] setprecision(7), counts setprecision(0);
+//  PREFIX_KeyFrameTrajectory.txt (:538-566), written at the end: "ts tx ty tz qx qy qz qw"
+//      of every keyframe's T_kf_w, timestamp setprecision(6), the rest setprecision(7),
+//      quaternion of R (not transposed).
+// Mapping (local BA, loop closure) is out of scope: the keyframe chain is
 // MapHandler::addKeyFrame's composition T_kf_w = prev_kf->T_kf_w * curr_kf->T_kf_w
 // (src/mapHandler.cpp:126-127) without the later BA refinements.  --json prints one
 // line per frame with the pose bits, for the parity test against the CPU oracle.
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
@@ -118,12 +125,17 @@ static int run(int argc, char** argv) {
     if (camname == "kitti") { sp.dt = 0.1; sp.v_fwd = 8.0; sp.z_min = 4.0; sp.z_max = 40.0; }
     const int kp_cap = 2048, kl_cap = 512;
 
-    std::ofstream fAllFrameTrack;
+    std::ofstream fAllFrameTrack, fLog;
     if (!out.empty()) {
         fAllFrameTrack.open(out + "_AllFrameTrajectory.txt");
         fAllFrameTrack << std::fixed;
         fAllFrameTrack << "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" << std::endl;
+        fLog.open(out + "_Log.txt");
+        fLog << std::fixed;
+        fLog << "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" << std::endl;   // the reference's header, as written
     }
+    struct KfRow { double time_stamp; Matrix4d T_kf_w; };
+    std::vector<KfRow> keyframes;   // MapHandler::map_keyframes (first KF: frame 0, T_kf_w = I)
     StereoFrameHandler* StVO = new StereoFrameHandler(&cam, 0, kp_cap, kl_cap);
     Matrix4d T_kf_w = Matrix4d::Identity();   // the last keyframe's world pose (first KF: frame 0)
     int n_kf = 1;
@@ -131,11 +143,17 @@ static int run(int argc, char** argv) {
         StereoFrame* f = make_frame(sp, &cam, seq, k, kp_cap, kl_cap);
         if (k == 0) {
             StVO->initialize(f);
+            keyframes.push_back({StVO->prev_frame->time_stamp, T_kf_w});
             continue;
         }
+        const auto t_track = std::chrono::steady_clock::now();
         StVO->insertStereoPair(f);
         const int mpt = (int)StVO->matched_pt.size(), mls = (int)StVO->matched_ls.size();
         StVO->optimizePose(StVO->prev_frame->DT);
+        // app/plslam_mod.cpp:388-413 (wall time here: the work runs on the GPU)
+        StVO->curr_frame->log_.frame_time_stamp = StVO->curr_frame->time_stamp;
+        StVO->curr_frame->log_.time_track =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_track).count();
         if (StVO->numFrameLoss > 10) {   // Config::maxNumFrameLoss() (src/config.cpp)
             std::cerr << "Early termination due to track loss!" << std::endl;
             break;
@@ -146,14 +164,16 @@ static int run(int argc, char** argv) {
             is_kf = true;
             T_kf_w = T_kf_w * StVO->curr_frame->Tfw;   // KeyFrame(curr_frame) + addKeyFrame
             StVO->currFrameIsKF();
+            keyframes.push_back({StVO->curr_frame->time_stamp, T_kf_w});
             ++n_kf;
         }
         if (json) {
             const StereoFrame* c = StVO->curr_frame;
             std::printf("{\"frame\": %d, \"n_pt\": %zu, \"n_ls\": %zu, \"matched_pt\": %d, \"matched_ls\": %d, "
-                        "\"n_inliers\": %d, \"num_frame_loss\": %d, \"err_norm\": %.17g, \"kf\": %d, \"DT\": [",
+                        "\"n_inliers\": %d, \"num_frame_loss\": %d, \"err_norm\": %.17g, \"kf\": %d, "
+                        "\"time_stamp\": %.17g, \"DT\": [",
                         k, c->stereo_pt.size(), c->stereo_ls.size(), mpt, mls, StVO->n_inliers, StVO->numFrameLoss,
-                        c->err_norm, is_kf ? 1 : 0);
+                        c->err_norm, is_kf ? 1 : 0, c->time_stamp);
             for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->DT.v[i]);
             std::printf("], \"Tfw\": [");
             for (int i = 0; i < 16; ++i) std::printf("%s%.17g", i ? ", " : "", c->Tfw.v[i]);
@@ -168,6 +188,29 @@ static int run(int argc, char** argv) {
             const std::vector<float> q = toQuaternion(R);
             fAllFrameTrack << std::setprecision(7) << " " << Tfw(0, 3) << " " << Tfw(1, 3) << " " << Tfw(2, 3) << " "
                            << q[0] << " " << q[1] << " " << q[2] << " " << q[3] << std::endl;
+        }
+        if (!out.empty()) {
+            const TimeLog& lg = StVO->prev_frame->log_;   // the frame just processed
+            fLog << std::setprecision(6) << lg.frame_time_stamp << " " << std::setprecision(7) << lg.time_track << " "
+                 << lg.time_pt_extract << " " << lg.time_ln_detect << " " << lg.time_ln_descri << " " << lg.time_pt_stereo
+                 << " " << lg.time_ln_stereo << " " << lg.time_pt_cross << " " << lg.time_ln_cross << " "
+                 << lg.time_ln_cut << " " << lg.time_pose_optim << " " << std::setprecision(0) << lg.num_pt_detect << " "
+                 << lg.num_ln_detect << " " << lg.num_pt_stereo << " " << lg.num_ln_stereo << " " << lg.num_pt_cross
+                 << " " << lg.num_ln_cross << std::endl;
+        }
+    }
+    if (!out.empty()) {
+        std::ofstream fKeyFrameTrack(out + "_KeyFrameTrajectory.txt");
+        fKeyFrameTrack << std::fixed;
+        fKeyFrameTrack << "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" << std::endl;
+        for (const KfRow& kf : keyframes) {
+            Matrix3d R;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) R(i, j) = kf.T_kf_w(i, j);   // T_kf_w.block(0,0,3,3)
+            const std::vector<float> q = toQuaternion(R);
+            fKeyFrameTrack << std::setprecision(6) << kf.time_stamp << std::setprecision(7) << " " << kf.T_kf_w(0, 3)
+                           << " " << kf.T_kf_w(1, 3) << " " << kf.T_kf_w(2, 3) << " " << q[0] << " " << q[1] << " "
+                           << q[2] << " " << q[3] << std::endl;
         }
     }
     if (!json) std::cerr << "keyframes: " << n_kf << std::endl;

@@ -122,6 +122,7 @@ StereoFrameHandler::StereoFrameHandler(PinholeStereoCamera* cam_, int device, in
     : cam(cam_), kp_cap_(kp_cap), kl_cap_(kl_cap) {
     check(gfpl_create(device, nullptr, &ctx_), "gfpl_create");
     check(gfpl_set_camera(ctx_, &cam->abi()), "gfpl_set_camera");
+    check(gfpl_set_timing(ctx_, 1), "gfpl_set_timing");   // stage marks for TimeLog
     // one sequence per handler: size its matched lists for the largest budgets the
     // ABI accepts, so a later Config::maxPointMatchNum() / maxLineMatchNum() change
     // (e.g. the gazebo value 1000, src/config.cpp:89) stays within the seqbatch
@@ -314,6 +315,14 @@ void StereoFrameHandler::insertStereoPair(StereoFrame* frame) {
     pull(GFPL_PREV, prev_frame, true, false);   // pl_obs, *_obs, inlier, cut endpoints, covariances
     pull_track();
     numFrameSinceKeyframe++;   // as gfpl_insert_stereo_pair did on the device (:150)
+    // counts of TimeLog (src/stereoFrame.cpp:628,765,1147,1187; src/stereoFrameHandler.cpp:601,684)
+    TimeLog& lg = curr_frame->log_;
+    lg.num_pt_detect = (double)curr_frame->points_l.size();
+    lg.num_ln_detect = (double)curr_frame->lines_l.size();
+    lg.num_pt_stereo = (double)curr_frame->stereo_pt.size();
+    lg.num_ln_stereo = (double)curr_frame->stereo_ls.size();
+    lg.num_pt_cross = (double)matched_pt.size();
+    lg.num_ln_cross = (double)matched_ls.size();
 }
 
 void StereoFrameHandler::stereoMatching(StereoFrame* frame) {
@@ -363,6 +372,18 @@ void StereoFrameHandler::optimizePose(Matrix4d DT_ini) {
     pull(GFPL_CURR, curr_frame, false, true);
     pull(GFPL_PREV, prev_frame, true, false);   // outlier flags
     pull_track();
+    // stage times of the insertStereoPair + optimizePose pair: [stereo points, stereo lines,
+    // cross points (with the prev-frame line uncertainty), cross lines, line cut, pose] in ms
+    float ms[7];
+    if (gfpl_get_stage_times(ctx_, ms) == GFPL_OK) {
+        TimeLog& lg = curr_frame->log_;
+        lg.time_pt_stereo = ms[0] * 1e-3;
+        lg.time_ln_stereo = ms[1] * 1e-3;
+        lg.time_pt_cross = ms[2] * 1e-3;
+        lg.time_ln_cross = ms[3] * 1e-3;
+        lg.time_ln_cut = ms[4] * 1e-3;
+        lg.time_pose_optim = ms[5] * 1e-3;
+    }
 }
 
 void StereoFrameHandler::updateFrame_ECCV18(const Matrix4d T_base) {

@@ -165,6 +165,32 @@ public:
     Matrix6d invCovPose;
 };
 
+// -------------------------------------------------------------- TimeLog --
+// include/stereoFrame.h:66-86: per-frame time costs [s] and counts, written out by the
+// app as PREFIX_Log.txt (app/plslam_mod.cpp:494-513).  The handler fills the stage
+// times from the device's HIP-event stage marks (gfpl_get_stage_times) and the counts;
+// the app fills frame_time_stamp and time_track.  Detection is injected,
+// so time_pt_extract / time_ln_detect / time_ln_descri stay 0.
+struct TimeLog {
+    double frame_time_stamp = 0;
+    double time_track = 0;
+    double time_pt_extract = 0;
+    double time_ln_detect = 0;
+    double time_ln_descri = 0;
+    double time_pt_stereo = 0;
+    double time_ln_stereo = 0;
+    double time_pt_cross = 0;
+    double time_ln_cross = 0;
+    double time_ln_cut = 0;
+    double time_pose_optim = 0;
+    double num_pt_detect = 0;
+    double num_ln_detect = 0;
+    double num_pt_stereo = 0;
+    double num_ln_stereo = 0;
+    double num_pt_cross = 0;
+    double num_ln_cross = 0;
+};
+
 // ----------------------------------------------------------- StereoFrame --
 // include/stereoFrame.h:89-260.  Built from injected detections; after the
 // handler matched it, stereo_pt / stereo_ls and the reordered pdesc_l / ldesc_l
@@ -190,6 +216,7 @@ public:
     Matrix6d DT_cov;
     Vector6d DT_cov_eig;
     double err_norm = 0;
+    TimeLog log_;
 
     std::vector<PointFeature*> stereo_pt;
     std::vector<LineFeature*> stereo_ls;

@@ -1,0 +1,140 @@
+// asan_driver.cpp — TEST INFRASTRUCTURE ONLY: runs the CPU oracle
+// under AddressSanitizer + UndefinedBehaviorSanitizer over short synthetic sequences of
+// every camera the tests use, the stage-by-stage entry points, the keyframe decision
+// and the numeric helpers.  Built and run by `make oracle-asan` (host code only; the
+// product library is never built with sanitizers).  Exit code 0 = clean run; a
+// sanitizer report aborts with a non-zero code (-fno-sanitize-recover=all).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../gf-pl-slam_amd/synth/gfpl_synth.h"
+#include "gfpl_oracle.h"
+
+namespace {
+
+struct CamDef { const char* name; int w, h; double fx, fy, cx, cy, b; int n_kp, n_kl, frames; };
+const CamDef kCams[] = {
+    {"vga", 640, 480, 554.25626, 554.25626, 320.0, 240.0, 0.1, 2000, 500, 4},
+    {"euroc", 752, 480, 458.654, 457.296, 367.215, 248.375, 0.110077842, 2000, 500, 3},
+    {"kitti", 1241, 376, 718.856, 718.856, 607.1928, 185.2157, 0.537165719, 2000, 500, 3},
+    {"stress", 1920, 1080, 1662.76878, 1662.76878, 960.0, 540.0, 0.1, 8000, 2000, 2},
+    {"vga-ragged", 640, 480, 554.25626, 554.25626, 320.0, 240.0, 0.1, 37, 5, 3},
+};
+
+#define CHECK(x)                                                                  \
+    do {                                                                          \
+        const int rc_ = (x);                                                      \
+        if (rc_ != 0) { std::fprintf(stderr, "%s failed: %d\n", #x, rc_); return 1; } \
+    } while (0)
+
+struct Frames {
+    int kp_cap, kl_cap;
+    int n_kp_l, n_kp_r, n_kl_l, n_kl_r;
+    std::vector<gfpl_keypoint> kp_l, kp_r;
+    std::vector<gfpl_keyline> kl_l, kl_r;
+    std::vector<uint8_t> pdesc_l, pdesc_r, ldesc_l, ldesc_r, pyr;
+    double ts;
+    gfpl_frames view;
+    Frames(int kp, int kl, size_t pyr_bytes)
+        : kp_cap(kp), kl_cap(kl), kp_l(kp), kp_r(kp), kl_l(kl), kl_r(kl), pdesc_l(32 * (size_t)kp),
+          pdesc_r(32 * (size_t)kp), ldesc_l(32 * (size_t)kl), ldesc_r(32 * (size_t)kl), pyr(pyr_bytes) {}
+    const gfpl_frames* frames() {
+        view = gfpl_frames{1, kp_cap, kl_cap, &n_kp_l, &n_kp_r, kp_l.data(), kp_r.data(), pdesc_l.data(),
+                           pdesc_r.data(), &n_kl_l, &n_kl_r, kl_l.data(), kl_r.data(), ldesc_l.data(),
+                           ldesc_r.data(), pyr.data(), &ts};
+        return &view;
+    }
+};
+
+int run_camera(const CamDef& d) {
+    gfpl_config cfg;
+    CHECK(gfpl_config_default(&cfg));
+    gfpl_camera cam;
+    CHECK(gfpl_camera_init(&cam, d.w, d.h, d.fx, d.fy, d.cx, d.cy, d.b, &cfg));
+    gfpl_synth_params sp;
+    gfpl_synth_default(&sp);
+    sp.n_kp = d.n_kp;
+    sp.n_kl = d.n_kl;
+    if (std::strcmp(d.name, "kitti") == 0) { sp.dt = 0.1; sp.v_fwd = 8.0; sp.z_min = 4.0; sp.z_max = 40.0; }
+    const int kp_cap = d.n_kp + 48, kl_cap = d.n_kl + 12;
+    Frames F(kp_cap, kl_cap, (size_t)cam.pyr_bytes);
+    gfplo_handler* h = gfplo_create(&cam, &cfg);
+    if (!h) { std::fprintf(stderr, "gfplo_create failed\n"); return 1; }
+    for (int k = 0; k < d.frames; ++k) {
+        CHECK(gfpl_synth_frame(&sp, &cam, 7, k, kp_cap, kl_cap, &F.n_kp_l, &F.n_kp_r, F.kp_l.data(), F.kp_r.data(),
+                               F.pdesc_l.data(), F.pdesc_r.data(), &F.n_kl_l, &F.n_kl_r, F.kl_l.data(),
+                               F.kl_r.data(), F.ldesc_l.data(), F.ldesc_r.data(), F.pyr.data(), &F.ts, nullptr));
+        if (k == 0) {
+            CHECK(gfplo_initialize(h, F.frames(), 0));
+            continue;
+        }
+        if (k % 2) {
+            CHECK(gfplo_insert_stereo_pair(h, F.frames(), 0));
+        } else {   // the stage-by-stage entry points
+            CHECK(gfplo_begin_frame(h, F.frames(), 0));
+            CHECK(gfplo_stereo_points(h));
+            CHECK(gfplo_stereo_lines(h));
+            CHECK(gfplo_line_uncertainty(h));
+            CHECK(gfplo_cross_points(h));
+            CHECK(gfplo_cross_lines(h));
+            CHECK(gfplo_line_cut(h));
+        }
+        gfpl_track_host tr;
+        CHECK(gfplo_read_track(h, &tr));
+        CHECK(gfplo_optimize_pose(h));
+        int flag = 0;
+        CHECK(gfplo_need_new_kf(h, &flag));
+        if (flag) CHECK(gfplo_curr_frame_is_kf(h));
+        gfpl_kf_state ks;
+        CHECK(gfplo_read_kf_state(h, &ks));
+        CHECK(gfplo_update_frame(h));
+        std::printf("%-10s frame %d: matched %d pts / %d lines, inliers %d, kf %d\n", d.name, k, tr.n_matched_pt,
+                    tr.n_matched_ls, tr.n_inliers, flag);
+    }
+    gfplo_destroy(h);
+    return 0;
+}
+
+int run_helpers() {
+    uint8_t a[32], b[32];
+    for (int i = 0; i < 32; ++i) { a[i] = (uint8_t)(37 * i + 11); b[i] = (uint8_t)(91 * i + 5); }
+    if (gfplo_hamming(a, b, 1) < 0 || gfplo_hamming(a, b, 2) < 0) return 1;
+    std::vector<uint8_t> q(32 * 9), t(32 * 13);
+    for (size_t i = 0; i < q.size(); ++i) q[i] = (uint8_t)(i * 131 + 7);
+    for (size_t i = 0; i < t.size(); ++i) t[i] = (uint8_t)(i * 29 + 3);
+    std::vector<int> idx(18);
+    std::vector<float> dist(18);
+    CHECK(gfplo_knn2(q.data(), 9, t.data(), 13, 1, idx.data(), dist.data()));
+    if (gfplo_knn2(q.data(), 9, t.data(), 1, 2, idx.data(), dist.data()) == 0) return 1;   // U4: too few train rows
+    double M[36], X[36], g[6], x[6];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) M[6 * i + j] = (i == j ? 4.0 : 0.0) + 1.0 / (1.0 + i + j);
+    for (int i = 0; i < 6; ++i) g[i] = 1.0 + i;
+    (void)gfplo_logdet6(M);
+    CHECK(gfplo_ldlt_solve6(M, g, x));
+    CHECK(gfplo_inverse6(M, X));
+    (void)gfplo_det6(M);
+    double w[6];
+    CHECK(gfplo_eig_sym(M, 6, w));
+    double T[16], Ti[16];
+    const double xi[6] = {0.1, -0.2, 0.3, 0.01, -0.02, 0.03};
+    CHECK(gfplo_expmap_se3(xi, T));
+    CHECK(gfplo_inverse_se3(T, Ti));
+    CHECK(gfplo_inverse4(T, Ti));
+    (void)gfplo_log(2.5);
+    (void)gfplo_sin(1.25);
+    (void)gfplo_cos(-7.5);
+    return 0;
+}
+
+}  // namespace
+
+int main() {
+    if (run_helpers()) return 1;
+    for (const CamDef& d : kCams)
+        if (run_camera(d)) return 1;
+    std::printf("oracle sanitizer run: clean\n");
+    return 0;
+}

@@ -19,6 +19,12 @@ namespace {
 
 // ===================================================================== N3 ==
 // fdlibm algorithms restated with + - * / only (pin N3).
+// The log / sin / cos below restate the algorithms and coefficient tables of Sun fdlibm
+// (e_log.c, k_sin.c, k_cos.c, e_rem_pio2.c), whose notice is preserved here:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely granted,
+//   provided that this notice is preserved.
 inline uint32_t hi_word(double x) { uint64_t u; std::memcpy(&u, &x, 8); return (uint32_t)(u >> 32); }
 inline uint32_t lo_word(double x) { uint64_t u; std::memcpy(&u, &x, 8); return (uint32_t)u; }
 inline double with_hi(double x, uint32_t hi) {

@@ -12,6 +12,47 @@ import gfpl
 import oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def to_quaternion(M):
+    """toQuaternion (src/auxiliar.cpp:38-50): Eigen::Quaterniond(Matrix3d) (Eigen's
+    quaternionbase_assign_impl), returned as float (x, y, z, w)."""
+    t = (M[0, 0] + M[1, 1]) + M[2, 2]
+    q = [0.0] * 4
+    if t > 0.0:
+        s = np.sqrt(t + 1.0)
+        q[3] = 0.5 * s
+        s = 0.5 / s
+        q[0] = (M[2, 1] - M[1, 2]) * s
+        q[1] = (M[0, 2] - M[2, 0]) * s
+        q[2] = (M[1, 0] - M[0, 1]) * s
+    else:
+        i = 0
+        if M[1, 1] > M[0, 0]:
+            i = 1
+        if M[2, 2] > M[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(((M[i, i] - M[j, j]) - M[k, k]) + 1.0)
+        q[i] = 0.5 * s
+        s = 0.5 / s
+        q[3] = (M[k, j] - M[j, k]) * s
+        q[j] = (M[j, i] + M[i, j]) * s
+        q[k] = (M[k, i] + M[i, k]) * s
+    return [float(np.float32(x)) for x in q]
+
+
+def fx7(v):   # std::fixed << setprecision(7)
+    return f"{v:.7f}"
+
+
+def test_to_quaternion_known_answers():
+    # identity, 90 deg about z (t > 0 branch), 180 deg about x (the else branch)
+    assert to_quaternion(np.eye(3)) == [0.0, 0.0, 0.0, 1.0]
+    Rz = np.array([[0.0, -1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 1.0]])
+    assert np.allclose(to_quaternion(Rz), [0.0, 0.0, np.sqrt(0.5), np.sqrt(0.5)], atol=1e-7)
+    Rx = np.diag([1.0, -1.0, -1.0])
+    assert to_quaternion(Rx) == [1.0, 0.0, 0.0, 0.0]
 BIN = os.path.join(ROOT, "gf-pl-slam_amd", "bin", "plslam_gpu")
 
 
@@ -41,6 +82,7 @@ def test_host_mirror_matches_oracle(camera, seq, tmp_path):
     o = O.OracleHandler(cam, cfg, 2048, 512)
     o.initialize(H.frames(0), 0)
     T_kf_w, poses = np.eye(4), []
+    kfs = [(float(H.time_stamp[0, 0]), np.eye(4))]   # MapHandler's first keyframe (frame 0)
     for k in range(1, n):
         o.insertStereoPair(H.frames(k), 0)
         tr = o.read_track()
@@ -59,14 +101,36 @@ def test_host_mirror_matches_oracle(camera, seq, tmp_path):
             T_kf_w = T_kf_w @ c.get("Tfw")
             o.currFrameIsKF()
             c = o.read_frame(gfpl.CURR)
+            kfs.append((float(H.time_stamp[k, 0]), T_kf_w))
+        assert g["time_stamp"] == float(H.time_stamp[k, 0])
         # %.17g round-trips doubles exactly: the pose is bit-identical
         assert np.array_equal(np.array(g["Tfw"]), c.get("Tfw").reshape(-1)), k
         assert np.array_equal(np.array(g["DT"]), c.get("DT").reshape(-1)), k
         assert g["err_norm"] == float(c.s.err_norm)
         poses.append(T_base @ o.read_frame(gfpl.PREV).get("Tfw"))   # updateFrame_ECCV18 (:864-922)
         o.updateFrame()
+    # the three text outputs, line for line (app/plslam_mod.cpp:288-301, 480-513, 538-566);
+    # the driver's poses are bit-identical to the oracle's, so the formatted text must be too
+    hdr = "#TimeStamp Tx Ty Tz Qx Qy Qz Qw"
     traj = (tmp_path / "run_AllFrameTrajectory.txt").read_text().splitlines()
-    assert traj[0] == "#TimeStamp Tx Ty Tz Qx Qy Qz Qw" and len(traj) == n   # header + n-1 poses
-    assert all(len(t.split()) == 7 for t in traj[1:])
+    assert traj[0] == hdr and len(traj) == n   # header + n-1 poses
     for t, T in zip(traj[1:], poses):
-        assert np.allclose([float(x) for x in t.split()[:3]], T[:3, 3], atol=2e-7)
+        q = to_quaternion(T[:3, :3].T)   # R = Tfw.block(0,0,3,3).transpose()
+        assert t == " " + " ".join(fx7(v) for v in [T[0, 3], T[1, 3], T[2, 3]] + q)
+    kft = (tmp_path / "run_KeyFrameTrajectory.txt").read_text().splitlines()
+    assert kft[0] == hdr and len(kft) == 1 + len(kfs)
+    for t, (ts, T) in zip(kft[1:], kfs):
+        q = to_quaternion(T[:3, :3])   # R = T_kf_w.block(0,0,3,3)
+        assert t == f"{ts:.6f} " + " ".join(fx7(v) for v in [T[0, 3], T[1, 3], T[2, 3]] + q)
+    log = (tmp_path / "run_Log.txt").read_text().splitlines()
+    assert log[0] == hdr and len(log) == n
+    for k, t in enumerate(log[1:], start=1):
+        f = t.split(" ")
+        assert len(f) == 17 and f[0] == f"{H.time_stamp[k, 0]:.6f}"
+        times = f[1:11]
+        assert all(len(x.split(".")[1]) == 7 and float(x) >= 0.0 for x in times)
+        assert times[1:4] == ["0.0000000"] * 3          # detection is injected (not timed)
+        assert float(times[9]) > 0.0 and float(times[0]) >= float(times[9])   # pose inside time_track
+        g = lines[k - 1]
+        assert [int(x) for x in f[11:]] == [int(H.n_kp_l[k, 0]), int(H.n_kl_l[k, 0]), g["n_pt"], g["n_ls"],
+                                             g["matched_pt"], g["matched_ls"]]
