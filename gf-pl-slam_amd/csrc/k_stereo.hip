@@ -118,14 +118,14 @@ __device__ __forceinline__ int byte_at(const uint32_t* w, int k) { return (int)(
 // has no third row: it re-reads the centre row and drops that row's sums).  All
 // four rows are loaded before any SAD so their latencies overlap.
 __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) {
-    uint32_t cRR[11];   // centre pixels of the 11 shifted right windows, in both 16-bit halves
+    // centre row: the centre pixels of the 11 shifted right windows are bytes 5..15 of
+    // its right row (kept as the 6 row dwords, expanded where used)
+    uint32_t irc[6];
     int cL;
     {
-        uint32_t il4[3], ir6[6];
-        sad_load_row(J, J.vL, il4, ir6);
+        uint32_t il4[3];
+        sad_load_row(J, J.vL, il4, irc);
         cL = byte_at(il4, 5);
-#pragma unroll
-        for (int i = 0; i < 11; ++i) cRR[i] = (uint32_t)byte_at(ir6, 5 + i) * 0x10001u;
     }
     uint32_t il4[3][3], ir6[3][6];
 #pragma unroll
@@ -147,14 +147,15 @@ __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) 
         const int il10 = byte_at(L, 10);
 #pragma unroll
         for (int s = 0; s < 11; ++s) {
+            const uint32_t cRRs = (uint32_t)byte_at(irc, 5 + s) * 0x10001u;
             uint32_t a = acc[s];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
                 const int c = s + 2 * k;   // right window column pair (c, c + 1)
                 const uint32_t ir = ((uint32_t)byte_at(R, c) | ((uint32_t)byte_at(R, c + 1) << 16)) + cLL;
-                a = __builtin_amdgcn_sad_u16(ILp[k] + cRR[s], ir, a);
+                a = __builtin_amdgcn_sad_u16(ILp[k] + cRRs, ir, a);
             }
-            a += (uint32_t)abs((il10 + (int)(cRR[s] & 0xFFFFu)) - (byte_at(R, 10 + s) + cL));
+            a += (uint32_t)abs((il10 + (int)(cRRs & 0xFFFFu)) - (byte_at(R, 10 + s) + cL));
             acc[s] = a;
         }
     }
@@ -223,7 +224,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     const int nlev = p.cam.n_levels;
     const int nrl = SEG ? nlev * nRows : nRows;
     int* misc = (int*)(rowlo + ((nrl + 1) & ~1));   // SEG: [22 + seg] band heights, [31] out-of-range count
-    float* depth = reinterpret_cast<float*>(p.scr.knn) + (size_t)b * cap;   // scratch (cross points reuses it later)
+    // mvDepth of the sub-pixel pass lives in recx: the right keypoints' x are dead once the
+    // band scan is over (LDS, no scattered 4-B global stores)
+    float* depth = recx;
     const int tid = threadIdx.x;
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
     const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
