@@ -40,17 +40,18 @@ $(BINDIR)/plslam_gpu: $(PKG)/host/plslam_gpu.cpp $(LIBDIR)/libgfpl_stvo.so $(LIB
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lgfpl_stvo -lgfpl_hip -l:libgfpl_synth.so -lpthread \
 	    -Wl,-rpath,'$$ORIGIN/../lib'
 
-oracle/liboracle.so: oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h include/gfpl.h
-	$(CXX) $(ORACLEFLAGS) $< -o $@
+ORACLE_SRC := oracle/gfpl_oracle.cpp oracle/gfpl_orb_oracle.cpp
+oracle/liboracle.so: $(ORACLE_SRC) oracle/gfpl_oracle.h include/gfpl.h $(PKG)/csrc/gfpl_orb_pattern.h
+	$(CXX) $(ORACLEFLAGS) $(ORACLE_SRC) -o $@
 
 # the CPU oracle (+ the synthetic generator and the host setup code it
 # uses) under ASan + UBSan, driven over every test camera; aborts on the first report
 ASANFLAGS := -O1 -g -std=c++17 -ffp-contract=off -Wall -Iinclude -fno-omit-frame-pointer \
              -fsanitize=address,undefined -fno-sanitize-recover=all
-oracle/build/asan_driver: oracle/asan_driver.cpp oracle/gfpl_oracle.cpp oracle/gfpl_oracle.h \
+oracle/build/asan_driver: oracle/asan_driver.cpp $(ORACLE_SRC) oracle/gfpl_oracle.h \
                           $(PKG)/synth/gfpl_synth.cpp $(PKG)/csrc/gfpl_setup.cpp include/gfpl.h
 	@mkdir -p oracle/build
-	$(CXX) $(ASANFLAGS) oracle/asan_driver.cpp oracle/gfpl_oracle.cpp $(PKG)/synth/gfpl_synth.cpp \
+	$(CXX) $(ASANFLAGS) oracle/asan_driver.cpp $(ORACLE_SRC) $(PKG)/synth/gfpl_synth.cpp \
 	    $(PKG)/csrc/gfpl_setup.cpp -o $@ -lpthread
 oracle-asan: oracle/build/asan_driver
 	ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 ./oracle/build/asan_driver

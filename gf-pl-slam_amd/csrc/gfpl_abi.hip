@@ -43,9 +43,13 @@ struct gfpl_seqbatch {
     int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
 };
 
+// for the other extern "C" objects built on a context (k_orb.hip)
+int gfpl_ctx_device(const gfpl_ctx* c) { return c->device; }
+void* gfpl_ctx_stream(const gfpl_ctx* c) { return (void*)c->stream; }
+
 namespace {
 
-#define HIPCHK(x)                                                   \
+#define HIPCHK(x)                                                  \
     do {                                                            \
         hipError_t e_ = (x);                                        \
         if (e_ != hipSuccess) {                                     \

@@ -48,3 +48,7 @@ hipError_t launch_kf_map_filter(const DevCam& cam, const double* T1, const doubl
                                 int32_t* loc, uint8_t* desc_out, const uint8_t* desc_in, int* count, hipStream_t s);
 
 }  // namespace gfpl
+
+// context accessors for the other extern "C" objects built on a context (gfpl_abi.hip)
+int gfpl_ctx_device(const gfpl_ctx* c);
+void* gfpl_ctx_stream(const gfpl_ctx* c);

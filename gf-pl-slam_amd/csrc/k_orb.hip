@@ -1,0 +1,903 @@
+// k_orb.hip — ORB extraction on the GPU: ORB_SLAM2::ORBextractor::
+// operator() (src/ORBextractor.cc:1043-1105) over a batch of grey images resident in HBM,
+// with the arithmetic of the OpenCV calls it makes pinned as in the CPU oracle (ledger
+// O1-O7, oracle/gfpl_orb_oracle.cpp).  Kernels, per launch over all images:
+//  k_orb_copy0    level 0 of the pyramid = the image
+//  k_orb_resize   level l from level l-1: cv::resize INTER_LINEAR fixed point (O1)
+//                 (ComputePyramid :1107-1132), coefficient tables built on the host
+//  k_orb_blur     GaussianBlur 7x7 sigma 2 REFLECT_101 fixed point (O2) of every level,
+//                 one 64x32 tile per workgroup through LDS (rows pass, then columns)
+//  k_orb_fast     per pixel of the cells' area: the FAST-9/16 segment test and
+//                 cornerScore at iniThFAST and at minThFAST (O3) -> two u8 score maps
+//  k_orb_cells    one workgroup per (image, level): the 30-px cells of
+//                 ComputeKeyPointsOctTree (:765-853): non-max suppression inside each
+//                 cell's ROI, the minThFAST retry for empty cells, the keys of every cell
+//                 compacted in the reference's order (cell row, cell column, row, column)
+//  k_orb_octree   one wave per (image, level): DistributeOctTree (:539-763) with the
+//                 node list in LDS (the reference's list order, O6 for ties) and every
+//                 DivideNode a wave-parallel stable 4-way partition of the node's keys
+//  k_orb_describe one thread per kept keypoint: IC_Angle (:77-104, O4), rBRIEF on the
+//                 blurred level (:108-148, O5), the level scale (:1094-1101), output in
+//                 the reference's order (level by level, node-list order)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "gfpl_kernels.hpp"
+#include "gfpl_orb_pattern.h"
+
+namespace gfpl {
+
+__constant__ int c_orb_pattern[1024];
+
+// everything the ORB kernels read, passed by value (device pointers)
+struct OrbLevel {
+    int w, h;                        // level image size (ComputePyramid :1111-1112)
+    long long off;                   // offset of the level in an image's pyramid
+    int minBX, minBY, maxBX, maxBY;  // ComputeKeyPointsOctTree borders (:773-776)
+    int nCols, nRows, wCell, hCell;  // its 30-px cells (:781-787)
+    int N;                           // mnFeaturesPerLevel (:435-446)
+    int nIni;                        // DistributeOctTree initial nodes (:543)
+    float hX;                        // their width (:545)
+    float scale;                     // mvScaleFactor
+};
+struct OrbDev {
+    int W, H, nlevels, ini_th, min_th;
+    int key_cap, sel_cap, node_cap;
+    long long pyr_stride;            // bytes between the pyramids of two images
+    OrbLevel lv[GFPL_MAX_LEVELS];
+    const int* xofs[GFPL_MAX_LEVELS];
+    const int16_t* alpha[GFPL_MAX_LEVELS];
+    const int* yofs[GFPL_MAX_LEVELS];
+    const int16_t* beta[GFPL_MAX_LEVELS];
+    int xmax[GFPL_MAX_LEVELS];
+    int blur_k[7];
+    int umax[16];
+    uint8_t* pyr;     // [n][pyr_stride] level images
+    uint8_t* blur;    // [n][pyr_stride] their Gaussian blur
+    uint8_t* s_ini;   // [n][pyr_stride] FAST scores at iniThFAST (0: no corner)
+    uint8_t* s_min;   // [n][pyr_stride] at minThFAST
+    uint32_t* keys;   // [n][nlevels][key_cap] vToDistributeKeys (packed)
+    uint32_t* tmp;    // [n][nlevels][key_cap] partition scratch
+    int* nkeys;       // [n][nlevels]
+    uint32_t* sel;    // [n][nlevels][sel_cap] kept keys in node-list order
+    int* nsel;        // [n][nlevels]
+    int* err;         // bit 0: key capacity, bit 1: node capacity, bit 2: output capacity
+};
+
+
+namespace {
+
+constexpr int kCircleX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kCircleY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
+__device__ __forceinline__ int refl101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+// packed key: x (11 bits) | y (11 bits) << 11 | score (8 bits) << 22, coordinates
+// relative to (minBorderX, minBorderY) as the reference's vToDistributeKeys
+__device__ __forceinline__ uint32_t key_pack(int x, int y, int s) {
+    return (uint32_t)x | ((uint32_t)y << 11) | ((uint32_t)s << 22);
+}
+__device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0x7FFu); }
+__device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 11) & 0x7FFu); }
+__device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 22); }
+
+}  // namespace
+
+// ------------------------------------------------------------------ pyramid --
+__global__ void k_orb_copy0(OrbDev o, const uint8_t* images, int n) {
+    const size_t npx = (size_t)o.W * o.H;
+    const int img = blockIdx.y;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x)
+        o.pyr[img * o.pyr_stride + i] = images[img * npx + i];
+}
+
+// O1: dst(x, y) = ((h(y0, x) b0 + h(y1, x) b1 + 2^21) >> 22), h = exact 11-bit horizontal blend
+__global__ void k_orb_resize(OrbDev o, int l) {
+    const OrbLevel& d = o.lv[l];
+    const OrbLevel& s = o.lv[l - 1];
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    const int img = blockIdx.z;
+    if (x >= d.w) return;
+    const uint8_t* S = o.pyr + img * o.pyr_stride + s.off;
+    const int sy = o.yofs[l][y];
+    const int r0 = min(max(sy, 0), s.h - 1), r1 = min(max(sy + 1, 0), s.h - 1);
+    const int sx = o.xofs[l][x];
+    const int a0 = o.alpha[l][2 * x], a1 = o.alpha[l][2 * x + 1];
+    const bool blend = x < o.xmax[l];
+    const uint8_t* R0 = S + (size_t)r0 * s.w;
+    const uint8_t* R1 = S + (size_t)r1 * s.w;
+    const int h0 = blend ? R0[sx] * a0 + R0[sx + 1] * a1 : R0[sx] * 2048;
+    const int h1 = blend ? R1[sx] * a0 + R1[sx + 1] * a1 : R1[sx] * 2048;
+    const int b0 = o.beta[l][2 * y], b1 = o.beta[l][2 * y + 1];
+    o.pyr[img * o.pyr_stride + d.off + (size_t)y * d.w + x] = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+}
+
+// O2: 7x7 Gaussian, 8-bit integer taps, rows exact, columns (s + 2^15) >> 16
+#define BLUR_TW 64
+#define BLUR_TH 32
+__global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
+    __shared__ uint8_t tile[BLUR_TH + 6][BLUR_TW + 8];
+    __shared__ int rows[BLUR_TH + 6][BLUR_TW + 1];
+    const int l = blockIdx.z % o.nlevels, img = blockIdx.z / o.nlevels;
+    const OrbLevel& L = o.lv[l];
+    const int x0 = blockIdx.x * BLUR_TW, y0 = blockIdx.y * BLUR_TH;
+    if (x0 >= L.w || y0 >= L.h) return;
+    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
+    for (int i = threadIdx.x; i < (BLUR_TH + 6) * (BLUR_TW + 6); i += blockDim.x) {
+        const int ty = i / (BLUR_TW + 6), tx = i % (BLUR_TW + 6);
+        tile[ty][tx] = S[(size_t)refl101(y0 + ty - 3, L.h) * L.w + refl101(x0 + tx - 3, L.w)];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (BLUR_TH + 6) * BLUR_TW; i += blockDim.x) {
+        const int ty = i / BLUR_TW, tx = i % BLUR_TW;
+        int a = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) a += o.blur_k[t] * tile[ty][tx + t];
+        rows[ty][tx] = a;
+    }
+    __syncthreads();
+    uint8_t* D = o.blur + img * o.pyr_stride + L.off;
+    for (int i = threadIdx.x; i < BLUR_TH * BLUR_TW; i += blockDim.x) {
+        const int ty = i / BLUR_TW, tx = i % BLUR_TW;
+        const int x = x0 + tx, y = y0 + ty;
+        if (x >= L.w || y >= L.h) continue;
+        // REFLECT_101 rows: the tile rows were loaded reflected, so tile row ty + 3 +- t is
+        // the reflected source row of y +- t
+        int a = o.blur_k[3] * rows[ty + 3][tx];
+#pragma unroll
+        for (int t = 1; t <= 3; ++t) a += o.blur_k[3 + t] * (rows[ty + 3 + t][tx] + rows[ty + 3 - t][tx]);
+        D[(size_t)y * L.w + x] = sat_u8((a + (1 << 15)) >> 16);
+    }
+}
+
+// ---------------------------------------------------------------------- FAST --
+// O3: FAST_t<16> segment test (>= 9 contiguous circle pixels darker than v - t or
+// brighter than v + t) and cornerScore<16>; 0 = no corner (scores are >= t - 1 > 0)
+__device__ __forceinline__ int fast_score(const int* d, int threshold) {
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        if (b >= b0) continue;
+        b = max(b, d[k + 5]);
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+__device__ __forceinline__ bool fast_test(const int* d, int t) {
+    // d[k] = v - p_k: darker means d > t, brighter means d < -t
+    uint32_t dark = 0, bright = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        dark |= (uint32_t)(d[k] > t) << k;
+        bright |= (uint32_t)(d[k] < -t) << k;
+    }
+    auto arc9 = [](uint32_t m) {
+        uint32_t w = m | (m << 16);   // wrap
+        uint32_t r = w;
+#pragma unroll
+        for (int i = 1; i < 9; ++i) r &= w >> i;
+        return (r & 0xFFFFu) != 0;
+    };
+    return arc9(dark) || arc9(bright);
+}
+
+__global__ void __launch_bounds__(256) k_orb_fast(OrbDev o) {
+    const int l = blockIdx.z % o.nlevels, img = blockIdx.z / o.nlevels;
+    const OrbLevel& L = o.lv[l];
+    const int x = L.minBX + 3 + blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = L.minBY + 3 + blockIdx.y;
+    if (x >= L.maxBX - 3 || y >= L.maxBY - 3) return;
+    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
+    const int v = S[(size_t)y * L.w + x];
+    int d[25];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - (int)S[(size_t)(y + kCircleY[k]) * L.w + (x + kCircleX[k])];
+#pragma unroll
+    for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
+    const size_t at = img * o.pyr_stride + L.off + (size_t)y * L.w + x;
+    o.s_ini[at] = fast_test(d, o.ini_th) ? (uint8_t)fast_score(d, o.ini_th) : 0;
+    o.s_min[at] = fast_test(d, o.min_th) ? (uint8_t)fast_score(d, o.min_th) : 0;
+}
+
+// -------------------------------------------------------------------- cells --
+// non-max suppression inside the ROI of one cell: neighbours outside its detectable area
+// count as 0 (FAST_t's zeroed score rows and columns)
+__device__ __forceinline__ int nms_keep(const uint8_t* M, int w, int x, int y, int dx0, int dy0, int dx1, int dy1) {
+    const int s = M[(size_t)y * w + x];
+    if (!s) return 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (!dx && !dy) continue;
+            const int xx = x + dx, yy = y + dy;
+            const int n = (xx >= dx0 && xx < dx1 && yy >= dy0 && yy < dy1) ? M[(size_t)yy * w + xx] : 0;
+            if (!(s > n)) return 0;
+        }
+    return s;
+}
+
+#define CELLS_T 256
+#define ORB_MAX_CELLS 4096
+__global__ void __launch_bounds__(CELLS_T) k_orb_cells(OrbDev o) {
+    __shared__ int cnt[ORB_MAX_CELLS];
+    const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
+    const OrbLevel& L = o.lv[l];
+    const int ncell = L.nRows * L.nCols;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t base = img * o.pyr_stride + L.off;
+    // pass 1: keys per cell (iniThFAST; minThFAST when that leaves the cell empty)
+    for (int c = wave; c < ncell; c += CELLS_T / 64) {
+        const int i = c / L.nCols, j = c % L.nCols;
+        const int iniY = L.minBY + i * L.hCell, iniX = L.minBX + j * L.wCell;
+        int total = 0, which = 0;
+        if (iniY < L.maxBY - 3 && iniX < L.maxBX - 6) {
+            const int maxY = min(iniY + L.hCell + 6, L.maxBY), maxX = min(iniX + L.wCell + 6, L.maxBX);
+            const int dx0 = iniX + 3, dy0 = iniY + 3, dx1 = maxX - 3, dy1 = maxY - 3;
+            for (int pass = 0; pass < 2 && total == 0; ++pass) {
+                const uint8_t* M = (pass ? o.s_min : o.s_ini) + base;
+                int c2 = 0;
+                for (int y = dy0; y < dy1; ++y)
+                    for (int x = dx0 + lane; x < dx1; x += 64) c2 += nms_keep(M, L.w, x, y, dx0, dy0, dx1, dy1) ? 1 : 0;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) c2 += __shfl_xor(c2, off, 64);
+                total = c2;
+                which = pass;
+            }
+        }
+        if (lane == 0) cnt[c] = total | (which << 30);
+    }
+    __syncthreads();
+    // exclusive scan of the counts in cell order
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int c = 0; c < ncell; ++c) {
+            const int v = cnt[c];
+            cnt[c] = acc | (v & (1 << 30));
+            acc += v & ~(1 << 30);
+        }
+        int tot = min(acc, o.key_cap);
+        o.nkeys[img * o.nlevels + l] = tot;
+        if (acc > o.key_cap) atomicOr(o.err, 1);
+    }
+    __syncthreads();
+    // pass 2: the keys of each cell in row-major order at the cell's offset
+    uint32_t* K = o.keys + ((size_t)img * o.nlevels + l) * o.key_cap;
+    for (int c = wave; c < ncell; c += CELLS_T / 64) {
+        const int i = c / L.nCols, j = c % L.nCols;
+        const int iniY = L.minBY + i * L.hCell, iniX = L.minBX + j * L.wCell;
+        if (!(iniY < L.maxBY - 3 && iniX < L.maxBX - 6)) continue;
+        const int maxY = min(iniY + L.hCell + 6, L.maxBY), maxX = min(iniX + L.wCell + 6, L.maxBX);
+        const int dx0 = iniX + 3, dy0 = iniY + 3, dx1 = maxX - 3, dy1 = maxY - 3;
+        const uint8_t* M = ((cnt[c] >> 30) ? o.s_min : o.s_ini) + base;
+        int pos = cnt[c] & ~(1 << 30);
+        for (int y = dy0; y < dy1; ++y)
+            for (int x0 = dx0; x0 < dx1; x0 += 64) {
+                const int x = x0 + lane;
+                const int s = x < dx1 ? nms_keep(M, L.w, x, y, dx0, dy0, dx1, dy1) : 0;
+                const unsigned long long m = __ballot(s != 0);
+                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                if (s && pos + rank < o.key_cap) K[pos + rank] = key_pack(x - L.minBX, y - L.minBY, s);
+                pos += __popcll(m);
+            }
+    }
+}
+
+// ------------------------------------------------------------------- octree --
+// DistributeOctTree (:539-763) — one wave per (image, level).  Nodes live in LDS as
+// rectangles (x0, y0, x1, y1) over a contiguous range of the level's key array; the
+// reference's std::list order is a doubly linked list (push_front, erase); DivideNode
+// (:481-537) is a stable partition of the node's range by the wave (one ballot per
+// group), through the per-level scratch array, children laid out n1 | n2 | n3 | n4.
+struct ONode {
+    int16_t x0, y0, x1, y1;
+    int32_t off, len;
+    int32_t id;            // creation order (O6)
+    int16_t prev, next;    // (bNoMore is len == 1: it is only ever set from the key count)
+};
+// vSizeAndPointerToNode entry: size << 40 | creation id << 16 | node, so the u64 order is
+// the (size, node) order of the reference's sort with O6 for ties
+typedef uint64_t OExp;
+__device__ __forceinline__ OExp oexp(int size, int id, int node) {
+    return ((uint64_t)(uint32_t)size << 40) | ((uint64_t)(uint32_t)id << 16) | (uint32_t)node;
+}
+#define ORB_MAX_INI 16
+
+__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// stable partition of K[off, off + len) into G groups (grp(key) in [0, G)), through T
+template <int G, typename F>
+__device__ __forceinline__ void wave_partition(uint32_t* K, uint32_t* T, int off, int len, F grp, int* cnt) {
+    const int lane = threadIdx.x & 63;
+    int c[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) c[q] = 0;
+    for (int b = 0; b < len; b += 64) {
+        const int i = b + lane;
+        const int g = i < len ? grp(K[off + i]) : -1;
+#pragma unroll
+        for (int q = 0; q < G; ++q) c[q] += __popcll(__ballot(g == q));
+    }
+    int run[G];
+    int acc = 0;
+#pragma unroll
+    for (int q = 0; q < G; ++q) { run[q] = acc; acc += c[q]; }
+    for (int b = 0; b < len; b += 64) {
+        const int i = b + lane;
+        const uint32_t k = i < len ? K[off + i] : 0u;
+        const int g = i < len ? grp(k) : -1;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const unsigned long long m = __ballot(g == q);
+            if (g == q) T[off + run[q] + __popcll(m & ((1ull << lane) - 1ull))] = k;
+            run[q] += __popcll(m);
+        }
+    }
+    __threadfence_block();
+    for (int i = lane; i < len; i += 64) K[off + i] = T[off + i];
+    __threadfence_block();
+#pragma unroll
+    for (int q = 0; q < G; ++q) cnt[q] = c[q];
+}
+
+__global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
+    extern __shared__ __align__(16) unsigned char osm[];
+    const int cap = o.node_cap;
+    ONode* nd = reinterpret_cast<ONode*>(osm);
+    OExp* ex = reinterpret_cast<OExp*>(nd + cap);   // vSizeAndPointerToNode
+    OExp* ex2 = ex + cap;                            // vPrevSizeAndPointerToNode
+    int16_t* freel = reinterpret_cast<int16_t*>(ex2 + cap);
+    __shared__ int st[8];   // 0 head, 1 size, 2 next id, 3 nfree, 4 nex, 5 nex2
+    const int lane = threadIdx.x;
+    const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
+    const OrbLevel& L = o.lv[l];
+    const size_t kb = ((size_t)img * o.nlevels + l) * o.key_cap;
+    uint32_t* K = o.keys + kb;
+    uint32_t* T = o.tmp + kb;
+    const int nk = o.nkeys[img * o.nlevels + l];
+    const int N = L.N;
+    uint32_t* out = o.sel + ((size_t)img * o.nlevels + l) * o.sel_cap;
+    if (nk == 0) {
+        if (lane == 0) o.nsel[img * o.nlevels + l] = 0;
+        return;
+    }
+    if (lane == 0) {
+        st[0] = -1; st[1] = 0; st[2] = 0; st[3] = 0; st[4] = 0; st[5] = 0;
+        for (int i = cap - 1; i >= 0; --i) freel[st[3]++] = (int16_t)i;
+    }
+    wave_sync_lds();
+    // list primitives: lane 0 only, callers sync the wave afterwards
+    auto push_front = [&](int i) {
+        nd[i].prev = -1;
+        nd[i].next = (int16_t)st[0];
+        if (st[0] >= 0) nd[st[0]].prev = (int16_t)i;
+        st[0] = i;
+        ++st[1];
+    };
+    auto erase = [&](int i) -> int {   // the node after i
+        const int pv = nd[i].prev, nx = nd[i].next;
+        if (pv >= 0) nd[pv].next = (int16_t)nx; else st[0] = nx;
+        if (nx >= 0) nd[nx].prev = (int16_t)pv;
+        freel[st[3]++] = (int16_t)i;
+        --st[1];
+        return nx;
+    };
+    auto new_node = [&](int x0, int y0, int x1, int y1, int off, int len) -> int {
+        if (st[3] == 0) { atomicOr(o.err, 2); return -1; }
+        const int c = freel[--st[3]];
+        nd[c].x0 = (int16_t)x0; nd[c].y0 = (int16_t)y0; nd[c].x1 = (int16_t)x1; nd[c].y1 = (int16_t)y1;
+        nd[c].off = off; nd[c].len = len;
+        nd[c].id = st[2]++;
+        return c;
+    };
+    // DivideNode (:481-537) of node i: the non-empty children go to the front of the list
+    // in n1..n4 order (:621-660); those with > 1 keys are recorded in ex (nToExpand)
+    auto divide = [&](int i) -> int {
+        const int x0 = nd[i].x0, y0 = nd[i].y0, x1 = nd[i].x1, y1 = nd[i].y1, off = nd[i].off, len = nd[i].len;
+        const int halfX = (int)ceilf((float)(x1 - x0) / 2), halfY = (int)ceilf((float)(y1 - y0) / 2);
+        const int mx = x0 + halfX, my = y0 + halfY;
+        int cnt[4];
+        wave_partition<4>(K, T, off, len, [&](uint32_t k) {
+            const float x = (float)key_x(k), y = (float)key_y(k);
+            return x < (float)mx ? (y < (float)my ? 0 : 2) : (y < (float)my ? 1 : 3);
+        }, cnt);
+        int rec = 0;
+        if (lane == 0) {
+            const int cx0[4] = {x0, mx, x0, mx}, cy0[4] = {y0, y0, my, my};
+            const int cx1[4] = {mx, x1, mx, x1}, cy1[4] = {my, my, y1, y1};
+            int o2 = off;
+            for (int q = 0; q < 4; ++q) {
+                if (cnt[q] > 0) {
+                    const int c = new_node(cx0[q], cy0[q], cx1[q], cy1[q], o2, cnt[q]);
+                    if (c >= 0) {
+                        push_front(c);
+                        if (cnt[q] > 1) { ex[st[4]++] = oexp(cnt[q], nd[c].id, c); ++rec; }
+                    }
+                }
+                o2 += cnt[q];
+            }
+        }
+        wave_sync_lds();
+        return __shfl(rec, 0);
+    };
+    // ---- initial nodes (:542-585): nIni columns of width hX over the keys' x
+    {
+        const int nIni = L.nIni;
+        const float hX = L.hX;
+        int cnt[ORB_MAX_INI];
+        wave_partition<ORB_MAX_INI>(K, T, 0, nk, [&](uint32_t k) { return (int)__fdiv_rn((float)key_x(k), hX); }, cnt);
+        if (lane == 0) {
+            // push_back in column order = the list built back to front with push_front
+            int offs[ORB_MAX_INI];
+            int acc = 0;
+            for (int q = 0; q < nIni; ++q) { offs[q] = acc; acc += cnt[q]; }
+            const int H = L.maxBY - L.minBY;
+            int ids[ORB_MAX_INI];
+            for (int q = 0; q < nIni; ++q) ids[q] = st[2]++;   // the reference creates all nIni nodes first
+            for (int q = nIni - 1; q >= 0; --q) {
+                if (cnt[q] == 0) continue;   // empty initial nodes are erased (:581-582)
+                const int c = new_node((int)(hX * (float)q), 0, (int)(hX * (float)(q + 1)), H, offs[q], cnt[q]);
+                if (c < 0) continue;
+                nd[c].id = ids[q];
+                push_front(c);
+            }
+            st[2] = nIni;
+        }
+        wave_sync_lds();
+    }
+    // ---- the subdivision loop (:594-739)
+    bool finish = false;
+    while (!finish) {
+        const int prevSize = st[1];
+        int nToExpand = 0;
+        if (lane == 0) st[4] = 0;
+        wave_sync_lds();
+        int it = st[0];
+        while (it >= 0) {
+            if (nd[it].len == 1) {
+                it = nd[it].next;
+                continue;
+            }
+            nToExpand += divide(it);
+            int nx = 0;
+            if (lane == 0) nx = erase(it);
+            wave_sync_lds();
+            it = __shfl(nx, 0);
+        }
+        const int size = st[1];
+        if (size >= N || size == prevSize) {
+            finish = true;
+        } else if (size + nToExpand * 3 > N) {
+            while (!finish) {
+                const int prev = st[1];
+                // vPrevSizeAndPointerToNode = vSizeAndPointerToNode, sorted by (size, node) (O6)
+                const int ne = st[4];
+                for (int i = lane; i < ne; i += 64) ex2[i] = ex[i];
+                wave_sync_lds();
+                if (lane == 0) {
+                    st[4] = 0;
+                    for (int a = 1; a < ne; ++a) {   // insertion sort (stable; keys distinct)
+                        const OExp v = ex2[a];
+                        int b = a - 1;
+                        while (b >= 0 && ex2[b] > v) {
+                            ex2[b + 1] = ex2[b];
+                            --b;
+                        }
+                        ex2[b + 1] = v;
+                    }
+                }
+                wave_sync_lds();
+                for (int j = ne - 1; j >= 0; --j) {
+                    const int node = (int)(ex2[j] & 0xFFFFu);
+                    divide(node);
+                    if (lane == 0) erase(node);
+                    wave_sync_lds();
+                    if (st[1] >= N) break;
+                }
+                if (st[1] >= N || st[1] == prev) finish = true;
+            }
+        }
+    }
+    // ---- the best key of every node, in list order (:741-760): first strict maximum
+    int n_out = 0;
+    for (int it = st[0]; it >= 0; it = nd[it].next) {
+        const int off = nd[it].off, len = nd[it].len;
+        int best = -1;
+        uint32_t bk = 0;
+        for (int b = 0; b < len; b += 64) {
+            const int i = b + lane;
+            const uint32_t k = i < len ? K[off + i] : 0u;
+            int s = i < len ? key_s(k) : -1;
+            int mi = i < len ? i : 0x7FFFFFFF;
+            // wave argmax: larger score, then smaller index
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                const int os = __shfl_xor(s, sh, 64), oi = __shfl_xor(mi, sh, 64);
+                if (os > s || (os == s && oi < mi)) { s = os; mi = oi; }
+            }
+            if (best < 0 || s > key_s(bk)) { best = mi; bk = K[off + mi]; }
+        }
+        if (lane == 0 && n_out < o.sel_cap) out[n_out] = bk;
+        ++n_out;
+    }
+    if (lane == 0) {
+        if (n_out > o.sel_cap) atomicOr(o.err, 4);
+        o.nsel[img * o.nlevels + l] = min(n_out, o.sel_cap);
+    }
+}
+
+// ----------------------------------------------------------------- describe --
+// O4: cv::fastAtan2 (degrees)
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI), p3 = -0.3258083974640975f * (float)(180 / M_PI),
+                p5 = 0.1555786518463281f * (float)(180 / M_PI), p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, ax + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = __fdiv_rn(ax, ay + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keypoint* kps, uint8_t* desc, int* n_kp,
+                                                      float* angle_out, float* resp_out, int kp_cap) {
+    const int img = blockIdx.y;
+    int nl[GFPL_MAX_LEVELS], tot = 0;
+    for (int l = 0; l < o.nlevels; ++l) { nl[l] = o.nsel[img * o.nlevels + l]; tot += nl[l]; }
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        n_kp[img] = min(tot, kp_cap);
+        if (tot > kp_cap) atomicOr(o.err, 4);
+    }
+    if (t >= tot || t >= kp_cap) return;
+    int l = 0, r = t;
+    while (r >= nl[l]) { r -= nl[l]; ++l; }
+    const OrbLevel& L = o.lv[l];
+    const uint32_t k = o.sel[((size_t)img * o.nlevels + l) * o.sel_cap + r];
+    const int x = key_x(k) + L.minBX, y = key_y(k) + L.minBY;   // level coordinates (:843-844)
+    // IC_Angle (:77-104) on the level image
+    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
+    int m_01 = 0, m_10 = 0;
+    const uint8_t* center = S + (size_t)y * L.w + x;
+    for (int u = -15; u <= 15; ++u) m_10 += u * center[u];
+    for (int v = 1; v <= 15; ++v) {
+        int v_sum = 0;
+        const int d = o.umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int vp = center[u + v * L.w], vm = center[u - v * L.w];
+            v_sum += vp - vm;
+            m_10 += u * (vp + vm);
+        }
+        m_01 += v * v_sum;
+    }
+    const float ang = fast_atan2((float)m_01, (float)m_10);
+    // computeOrbDescriptor (:108-148) on the blurred level, O5
+    const float factorPI = (float)(M_PI / 180.f);
+    const float a_ = ang * factorPI;
+    const float ca = (float)det_cos((double)a_), sa = (float)det_sin((double)a_);
+    const uint8_t* B = o.blur + img * o.pyr_stride + L.off + (size_t)y * L.w + x;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+    for (int i = 0; i < 32; ++i) {
+        uint32_t val = 0;
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const int idx0 = 16 * i + 2 * bit, idx1 = idx0 + 1;
+            const int px0 = c_orb_pattern[2 * idx0], py0 = c_orb_pattern[2 * idx0 + 1];
+            const int px1 = c_orb_pattern[2 * idx1], py1 = c_orb_pattern[2 * idx1 + 1];
+            const int t0 = B[__float2int_rn(px0 * sa + py0 * ca) * L.w + __float2int_rn(px0 * ca - py0 * sa)];
+            const int t1 = B[__float2int_rn(px1 * sa + py1 * ca) * L.w + __float2int_rn(px1 * ca - py1 * sa)];
+            val |= (uint32_t)(t0 < t1) << bit;
+        }
+        w[i >> 2] |= val << (8 * (i & 3));
+    }
+    const size_t q = (size_t)img * kp_cap + t;
+    uint4* dd = reinterpret_cast<uint4*>(desc + 32 * q);
+    dd[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dd[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    // keypoint coordinates scaled to level 0 (:1094-1101)
+    float fx = (float)x, fy = (float)y;
+    if (l != 0) { fx = fx * L.scale; fy = fy * L.scale; }
+    kps[q] = gfpl_keypoint{fx, fy, l};
+    if (angle_out) angle_out[q] = ang;
+    if (resp_out) resp_out[q] = (float)key_s(k);
+}
+
+// copy the level images into a caller's pyramid array (gfpl_frames.pyr_r layout)
+__global__ void k_orb_pyr_out(OrbDev o, uint8_t* dst, long long dst_stride, long long bytes) {
+    const int img = blockIdx.y;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < bytes; i += (long long)gridDim.x * blockDim.x)
+        dst[img * dst_stride + i] = o.pyr[img * o.pyr_stride + i];
+}
+
+}  // namespace gfpl
+
+// ======================================================================= ABI ==
+using namespace gfpl;
+
+struct gfpl_orb {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    gfpl_orb_params prm{};
+    int max_images = 0, kp_cap = 0;
+    OrbDev d{};
+    void* base = nullptr;         // one allocation for everything
+    long long pyr_bytes = 0;      // used bytes of one pyramid
+};
+
+namespace {
+
+#define ORB_HIPCHK(x)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            std::fprintf(stderr, "gfpl_orb: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return GFPL_E_HIP;                                                         \
+        }                                                                              \
+    } while (0)
+
+size_t orb_octree_lds(int node_cap) { return (size_t)node_cap * (sizeof(ONode) + 2 * sizeof(OExp) + 2) + 16; }
+
+inline int cv_round_f(float v) { return (int)std::nearbyintf(v); }
+inline int cv_round_d(double v) { return (int)std::nearbyint(v); }
+inline int16_t sat_short(float v) { return (int16_t)std::min(std::max(cv_round_f(v), -32768), 32767); }
+
+}  // namespace
+
+extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_orb_params* prm, int max_images,
+                               int kp_cap, gfpl_orb** out) {
+    if (!ctx || !prm || !out || max_images < 1 || kp_cap < 1) return GFPL_E_INVALID;
+    if (prm->nlevels < 1 || prm->nlevels > GFPL_MAX_LEVELS || !(prm->scale_factor > 1.0f) || prm->nfeatures < 1)
+        return GFPL_E_INVALID;
+    if (width < 64 || height < 64 || width > 2047 || height > 2047) return GFPL_E_INVALID;
+    const int dev = gfpl_ctx_device(ctx);
+    ORB_HIPCHK(hipSetDevice(dev));
+    gfpl_orb* o = new gfpl_orb();
+    o->device = dev;
+    o->stream = (hipStream_t)gfpl_ctx_stream(ctx);
+    o->prm = *prm;
+    o->max_images = max_images;
+    o->kp_cap = kp_cap;
+    OrbDev& d = o->d;
+    d.W = width;
+    d.H = height;
+    d.nlevels = prm->nlevels;
+    d.ini_th = std::min(std::max(prm->ini_th_fast, 0), 255);
+    d.min_th = std::min(std::max(prm->min_th_fast, 0), 255);
+    // ORBextractor::ORBextractor (:410-470)
+    float sc[GFPL_MAX_LEVELS], isc[GFPL_MAX_LEVELS];
+    sc[0] = 1.0f;
+    for (int i = 1; i < d.nlevels; ++i) sc[i] = sc[i - 1] * prm->scale_factor;
+    for (int i = 0; i < d.nlevels; ++i) isc[i] = 1.0f / sc[i];
+    int nPer[GFPL_MAX_LEVELS];
+    {
+        const float factor = 1.0f / prm->scale_factor;
+        float nDesired = prm->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)d.nlevels));
+        int sum = 0;
+        for (int l = 0; l < d.nlevels - 1; ++l) {
+            nPer[l] = cv_round_f(nDesired);
+            sum += nPer[l];
+            nDesired *= factor;
+        }
+        nPer[d.nlevels - 1] = std::max(prm->nfeatures - sum, 0);
+    }
+    {
+        int umax[16];
+        const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1), vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+        for (int v = 0; v <= vmax; ++v) umax[v] = cv_round_d(std::sqrt(225.0 - v * v));
+        for (int v = 15, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+        for (int v = 0; v < 16; ++v) d.umax[v] = umax[v];
+    }
+    {   // O2 taps
+        float cf[7];
+        double sum = 0;
+        for (int i = 0; i < 7; ++i) {
+            const double x = i - 3.0;
+            cf[i] = (float)std::exp(-0.125 * x * x);
+            sum += cf[i];
+        }
+        sum = 1. / sum;
+        for (int i = 0; i < 7; ++i) d.blur_k[i] = cv_round_f((float)(cf[i] * sum) * 256.0f);
+    }
+    long long off = 0;
+    int max_cells = 0, max_n = 0;
+    for (int l = 0; l < d.nlevels; ++l) {
+        OrbLevel& L = d.lv[l];
+        L.w = cv_round_f((float)width * isc[l]);
+        L.h = cv_round_f((float)height * isc[l]);
+        L.off = off;
+        off += (long long)L.w * L.h;
+        L.minBX = 19 - 3;
+        L.minBY = L.minBX;
+        L.maxBX = L.w - 19 + 3;
+        L.maxBY = L.h - 19 + 3;
+        const float wf = (float)(L.maxBX - L.minBX), hf = (float)(L.maxBY - L.minBY);
+        L.nCols = (int)(wf / 30.f);
+        L.nRows = (int)(hf / 30.f);
+        if (L.nCols < 1 || L.nRows < 1) { delete o; return GFPL_E_INVALID; }
+        L.wCell = (int)std::ceil(wf / L.nCols);
+        L.hCell = (int)std::ceil(hf / L.nRows);
+        L.N = nPer[l];
+        L.nIni = (int)std::round(wf / (float)(L.maxBY - L.minBY));
+        if (L.nIni < 1 || L.nIni > ORB_MAX_INI) { delete o; return GFPL_E_UNSUPPORTED; }
+        L.hX = wf / L.nIni;
+        L.scale = sc[l];
+        max_cells = std::max(max_cells, L.nRows * L.nCols);
+        max_n = std::max(max_n, L.N);
+    }
+    if (max_cells > ORB_MAX_CELLS) { delete o; return GFPL_E_UNSUPPORTED; }
+    d.node_cap = max_n + 4 * ORB_MAX_INI + 16;   // list size <= max(N, 4 nIni) + 3, + 4 children in flight
+    if (orb_octree_lds(d.node_cap) > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
+    if (hipFuncSetAttribute((const void*)k_orb_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)orb_octree_lds(d.node_cap)) != hipSuccess) { delete o; return GFPL_E_HIP; }
+    o->pyr_bytes = off;
+    d.pyr_stride = (off + 255) & ~255LL;
+    // FAST keys per level: the reference keeps them all; strict 3x3 maxima are never
+    // 8-adjacent, so a level holds at most ~1/4 of its cells' pixels
+    d.key_cap = (int)std::min<long long>((long long)width * height / 4 + 4LL * (width + height) + 1024, 1 << 22);
+    d.sel_cap = max_n + 4 * ORB_MAX_INI + 8;   // DistributeOctTree keeps <= max(N, 4 nIni) + 3 nodes
+    // resize tables (O1), one set per level
+    std::vector<int> xofs_h, yofs_h;
+    std::vector<int16_t> alpha_h, beta_h;
+    long long xoff[GFPL_MAX_LEVELS] = {}, yoff[GFPL_MAX_LEVELS] = {};
+    for (int l = 1; l < d.nlevels; ++l) {
+        const OrbLevel& s = d.lv[l - 1];
+        const OrbLevel& t = d.lv[l];
+        const double scale_x = 1. / ((double)t.w / s.w), scale_y = 1. / ((double)t.h / s.h);
+        xoff[l] = (long long)xofs_h.size();
+        int xmax = t.w;
+        for (int dx = 0; dx < t.w; ++dx) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)std::floor(fx);
+            fx -= sx;
+            if (sx < 0) { fx = 0; sx = 0; }
+            if (sx + 1 >= s.w) {
+                xmax = std::min(xmax, dx);
+                if (sx >= s.w - 1) { fx = 0; sx = s.w - 1; }
+            }
+            xofs_h.push_back(sx);
+            alpha_h.push_back(sat_short((1.f - fx) * 2048));
+            alpha_h.push_back(sat_short(fx * 2048));
+        }
+        d.xmax[l] = xmax;
+        yoff[l] = (long long)yofs_h.size();
+        for (int dy = 0; dy < t.h; ++dy) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            const int sy = (int)std::floor(fy);
+            fy -= sy;
+            yofs_h.push_back(sy);
+            beta_h.push_back(sat_short((1.f - fy) * 2048));
+            beta_h.push_back(sat_short(fy * 2048));
+        }
+    }
+    // one allocation: tables | pyr | blur | s_ini | s_min | keys | tmp | nkeys | sel | nsel | err
+    const long long M = max_images;
+    auto al = [](long long v) { return (v + 255) & ~255LL; };
+    const long long b_x = al(4 * (long long)xofs_h.size() + 4), b_a = al(2 * (long long)alpha_h.size() + 4);
+    const long long b_y = al(4 * (long long)yofs_h.size() + 4), b_b = al(2 * (long long)beta_h.size() + 4);
+    const long long b_img = al(M * d.pyr_stride);
+    const long long b_keys = al(4 * M * d.nlevels * (long long)d.key_cap);
+    const long long b_n = al(4 * M * d.nlevels);
+    const long long b_sel = al(4 * M * d.nlevels * (long long)d.sel_cap);
+    const long long total = b_x + b_a + b_y + b_b + 4 * b_img + 2 * b_keys + 2 * b_n + b_sel + 256;
+    if (hipMalloc(&o->base, (size_t)total) != hipSuccess) { delete o; return GFPL_E_HIP; }
+    char* p = (char*)o->base;
+    int* xo = (int*)p; p += b_x;
+    int16_t* ap = (int16_t*)p; p += b_a;
+    int* yo = (int*)p; p += b_y;
+    int16_t* bp = (int16_t*)p; p += b_b;
+    d.pyr = (uint8_t*)p; p += b_img;
+    d.blur = (uint8_t*)p; p += b_img;
+    d.s_ini = (uint8_t*)p; p += b_img;
+    d.s_min = (uint8_t*)p; p += b_img;
+    d.keys = (uint32_t*)p; p += b_keys;
+    d.tmp = (uint32_t*)p; p += b_keys;
+    d.nkeys = (int*)p; p += b_n;
+    d.nsel = (int*)p; p += b_n;
+    d.sel = (uint32_t*)p; p += b_sel;
+    d.err = (int*)p;
+    for (int l = 1; l < d.nlevels; ++l) {
+        d.xofs[l] = xo + xoff[l];
+        d.alpha[l] = ap + 2 * xoff[l];
+        d.yofs[l] = yo + yoff[l];
+        d.beta[l] = bp + 2 * yoff[l];
+    }
+    bool ok = true;
+    if (!xofs_h.empty()) {
+        ok = ok && hipMemcpy(xo, xofs_h.data(), 4 * xofs_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(ap, alpha_h.data(), 2 * alpha_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(yo, yofs_h.data(), 4 * yofs_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(bp, beta_h.data(), 2 * beta_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_orb_pattern), kOrbPattern, sizeof(kOrbPattern)) == hipSuccess;
+    ok = ok && hipMemset(d.s_ini, 0, 2 * b_img) == hipSuccess;   // s_ini | s_min outside the cells' area
+    if (!ok) { (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
+    *out = o;
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_orb_destroy(gfpl_orb* o) {
+    if (!o) return GFPL_E_INVALID;
+    if (o->base) (void)hipFree(o->base);
+    delete o;
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_orb_pyramid_bytes(const gfpl_orb* o, int64_t* bytes) {
+    if (!o || !bytes) return GFPL_E_INVALID;
+    *bytes = o->pyr_bytes;
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_keypoint* kps, uint8_t* desc,
+                                int* n_kp, float* angle, float* response, uint8_t* pyramid, int64_t pyr_stride) {
+    if (!o || !images || n < 1 || n > o->max_images || !kps || !desc || !n_kp) return GFPL_E_INVALID;
+    if (pyramid && pyr_stride < o->pyr_bytes) return GFPL_E_INVALID;
+    ORB_HIPCHK(hipSetDevice(o->device));
+    OrbDev& d = o->d;
+    hipStream_t s = o->stream;
+    ORB_HIPCHK(hipMemsetAsync(d.err, 0, 4, s));
+    hipLaunchKernelGGL(k_orb_copy0, dim3(64, n), dim3(256), 0, s, d, images, n);
+    for (int l = 1; l < d.nlevels; ++l)
+        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].w + 255) / 256, d.lv[l].h, n), dim3(256), 0, s, d, l);
+    const OrbLevel& L0 = d.lv[0];
+    hipLaunchKernelGGL(k_orb_blur, dim3((L0.w + BLUR_TW - 1) / BLUR_TW, (L0.h + BLUR_TH - 1) / BLUR_TH, n * d.nlevels),
+                       dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_orb_fast, dim3((L0.maxBX - L0.minBX + 255) / 256, L0.maxBY - L0.minBY, n * d.nlevels), dim3(256),
+                       0, s, d);
+    hipLaunchKernelGGL(k_orb_cells, dim3(n * d.nlevels), dim3(CELLS_T), 0, s, d);
+    const size_t lds = orb_octree_lds(d.node_cap);
+    hipLaunchKernelGGL(k_orb_octree, dim3(n * d.nlevels), dim3(64), lds, s, d);
+    const int max_tot = d.sel_cap * d.nlevels;
+    hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 255) / 256, n), dim3(256), 0, s, d, n, kps,
+                       desc, n_kp, angle, response, o->kp_cap);
+    if (pyramid) hipLaunchKernelGGL(k_orb_pyr_out, dim3(64, n), dim3(256), 0, s, d, pyramid, (long long)pyr_stride, o->pyr_bytes);
+    ORB_HIPCHK(hipGetLastError());
+    int err = 0;
+    ORB_HIPCHK(hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s));
+    ORB_HIPCHK(hipStreamSynchronize(s));
+    return err ? GFPL_E_CAPACITY : GFPL_OK;
+}

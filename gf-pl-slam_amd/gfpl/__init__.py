@@ -73,6 +73,9 @@ class Config(C.Structure):
 
 
 KEYPOINT_DT = np.dtype([("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])
+# cv::KeyPoint fields ORBextractor::operator() fills (src/ORBextractor.cc:1085-1101)
+CV_KEYPOINT_DT = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4")])
 KEYLINE_DT = np.dtype([("sx", "<f4"), ("sy", "<f4"), ("ex", "<f4"), ("ey", "<f4"),
                        ("angle", "<f4"), ("octave", "<i4")])
 
@@ -200,6 +203,12 @@ class MapView:
             setattr(self.s, k, _ptr(a) if (device is not None or a.size) else 0)
 
 
+class OrbParams(C.Structure):
+    """gfpl_orb_params: ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)."""
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
 class SynthParams(C.Structure):
     _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
                 ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
@@ -288,6 +297,10 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_bytes": ([P, P], C.c_int),
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_strerror": ([C.c_int], C.c_char_p),
+            "gfpl_orb_create": ([P, C.c_int, C.c_int, P, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_orb_destroy": ([P], C.c_int),
+            "gfpl_orb_pyramid_bytes": ([P, P], C.c_int),
+            "gfpl_orb_extract": ([P, P, C.c_int, P, P, P, P, P, P, C.c_int64], C.c_int),
         }
         for n, (a, r) in sigs.items():
             try:
@@ -309,6 +322,8 @@ def synthlib() -> C.CDLL:
         L.gfpl_synth_batch.argtypes = ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
                                        + [P] * 14 + [C.c_int])
         L.gfpl_synth_batch.restype = C.c_int
+        L.gfpl_synth_image.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P]
+        L.gfpl_synth_image.restype = C.c_int
         L._gfpl_typed = True
     return L
 
@@ -361,6 +376,14 @@ def make_camera(name: str = "vga", cfg: Optional[Config] = None, **over) -> Came
     check(hiplib().gfpl_camera_init(C.byref(cam), p["width"], p["height"], p["fx"], p["fy"],
                                     p["cx"], p["cy"], p["b"], C.byref(cfg)), "camera_init")
     return cam
+
+
+def synth_image(seq: int, frame: int, width: int, height: int, seed: int = 0x6A09E667) -> np.ndarray:
+    """A synthetic grey image [height][width] u8 (gfpl_synth_image: shapes on a gradient +
+    noise), deterministic in (seed, seq, frame)."""
+    out = np.zeros((height, width), np.uint8)
+    check(synthlib().gfpl_synth_image(seed, seq, frame, width, height, out.ctypes.data), "synth_image")
+    return out
 
 
 def synth_params(**over) -> SynthParams:
@@ -793,3 +816,114 @@ def track_from_dict(d: dict) -> TrackHost:
     t.n_inliers, t.n_inliers_pt, t.n_inliers_ls = d["n_inliers"], d["n_inliers_pt"], d["n_inliers_ls"]
     t.num_frame_loss = d["num_frame_loss"]
     return t
+
+
+class ORBextractor:
+    """ORB_SLAM2::ORBextractor on the GPU (include/ORBextractor.h:49-106; constructor
+    src/ORBextractor.cc:410-470, operator() :1043-1105), as StereoFrame builds it
+    (src/stereoFrame.cpp:33-36).  One extractor serves images of one size; __call__
+    takes one host image like the reference's operator(), extract() a batch of images
+    already on the device (the product path's form).
+
+    ctx: a Context (its device and stream), or None for a bare context on `device`."""
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
+                 width: int, height: int, max_images: int = 1, kp_cap: Optional[int] = None,
+                 ctx: Optional[Context] = None, device: int = 0):
+        self.L = hiplib()
+        self.prm = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.width, self.height, self.max_images = width, height, max_images
+        self.kp_cap = kp_cap or nfeatures + 64 * nlevels + 64
+        self._own = None
+        if ctx is None:
+            h = C.c_void_p()
+            check(self.L.gfpl_create(device, None, C.byref(h)), "gfpl_create")
+            self._own = h
+            ch = h
+        else:
+            ch = ctx.h
+        self._ctx = ctx
+        o = C.c_void_p()
+        check(self.L.gfpl_orb_create(ch, width, height, C.byref(self.prm), max_images, self.kp_cap, C.byref(o)),
+              "orb_create")
+        self.h = o
+        b = C.c_int64()
+        check(self.L.gfpl_orb_pyramid_bytes(o, C.byref(b)), "orb_pyramid_bytes")
+        self.pyramid_bytes = b.value
+        # ORBextractor tables (:414-431)
+        sc = [1.0]
+        for _ in range(1, nlevels):
+            sc.append(float(np.float32(sc[-1]) * np.float32(scaleFactor)))
+        self.mvScaleFactor = np.array(sc, np.float32)
+        self.mvLevelSigma2 = self.mvScaleFactor * self.mvScaleFactor
+        self.mvInvScaleFactor = np.float32(1.0) / self.mvScaleFactor
+        self.mvInvLevelSigma2 = np.float32(1.0) / self.mvLevelSigma2
+        self.mvImagePyramid = []
+
+    # the reference's accessors (include/ORBextractor.h:65-88)
+    def GetLevels(self) -> int: return self.prm.nlevels
+    def GetScaleFactor(self) -> float: return float(np.float32(self.prm.scale_factor))
+    def GetScaleFactors(self): return self.mvScaleFactor.copy()
+    def GetInverseScaleFactors(self): return self.mvInvScaleFactor.copy()
+    def GetScaleSigmaSquares(self): return self.mvLevelSigma2.copy()
+    def GetInverseScaleSigmaSquares(self): return self.mvInvLevelSigma2.copy()
+
+    def level_sizes(self):
+        """(cols, rows) of every level: cvRound(W / scale), cvRound(H / scale) (:1111-1112)."""
+        return [(int(np.rint(np.float32(self.width) * self.mvInvScaleFactor[l])),
+                 int(np.rint(np.float32(self.height) * self.mvInvScaleFactor[l]))) for l in range(self.prm.nlevels)]
+
+    def extract(self, images_dev, n: int, kps_dev, desc_dev, n_kp_dev, angle_dev=None, response_dev=None,
+                pyramid_dev=None, pyr_stride: int = 0) -> None:
+        """gfpl_orb_extract on device buffers: images [n][H][W] u8; per image i the rows
+        [i*kp_cap, i*kp_cap + n_kp[i]) of kps (KEYPOINT_DT) / desc (32 B) / angle / response."""
+        check(self.L.gfpl_orb_extract(self.h, _ptr(images_dev), n, _ptr(kps_dev), _ptr(desc_dev), _ptr(n_kp_dev),
+                                      _ptr(angle_dev), _ptr(response_dev), _ptr(pyramid_dev), pyr_stride),
+              "orb_extract")
+
+    def __call__(self, image: np.ndarray):
+        """operator()(image, noArray(), keypoints, descriptors) on one HOST grey image:
+        returns (keypoints [CV_KEYPOINT_DT], descriptors [n][32] u8); mvImagePyramid holds
+        the level images afterwards."""
+        import torch
+        image = np.ascontiguousarray(image, np.uint8)
+        if image.shape != (self.height, self.width):
+            raise ValueError(f"image {image.shape} != ({self.height}, {self.width})")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        img = torch.from_numpy(image).to(dev)
+        kc = self.kp_cap
+        kps = torch.zeros(kc * KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+        desc = torch.zeros(kc * DESC, dtype=torch.uint8, device=dev)
+        nkp = torch.zeros(1, dtype=torch.int32, device=dev)
+        ang = torch.zeros(kc, dtype=torch.float32, device=dev)
+        rsp = torch.zeros(kc, dtype=torch.float32, device=dev)
+        pyr = torch.zeros(self.pyramid_bytes, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        self.extract(img, 1, kps, desc, nkp, ang, rsp, pyr, self.pyramid_bytes)
+        n = int(nkp.item())
+        k = kps.cpu().numpy().view(KEYPOINT_DT)[:n]
+        out = np.zeros(n, CV_KEYPOINT_DT)
+        out["x"], out["y"], out["octave"] = k["x"], k["y"], k["octave"]
+        out["size"] = np.float32(31) * self.mvScaleFactor[k["octave"]]   # scaledPatchSize (:1090)
+        out["angle"] = ang[:n].cpu().numpy()
+        out["response"] = rsp[:n].cpu().numpy()
+        p = pyr.cpu().numpy()
+        self.mvImagePyramid, off = [], 0
+        for (w, h) in self.level_sizes():
+            self.mvImagePyramid.append(p[off:off + w * h].reshape(h, w).copy())
+            off += w * h
+        return out, desc.cpu().numpy().reshape(kc, DESC)[:n].copy()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_orb_destroy(self.h)
+            self.h = None
+        if getattr(self, "_own", None):
+            self.L.gfpl_destroy(self._own)
+            self._own = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -395,3 +395,38 @@ extern "C" int gfpl_synth_batch(const gfpl_synth_params* p, const gfpl_camera* c
     for (int e : rc) if (e) return e;
     return 0;
 }
+
+// Synthetic grey image for the ORB extraction row: a deterministic
+// piecewise-constant scene of overlapping axis-aligned and rotated rectangles and discs
+// of random intensity on a smooth gradient, plus mild pixel noise — corners and blobs at
+// every scale of a 4-level 1.2 pyramid.  Pure function of (seed, seq_id, frame_idx).
+extern "C" int gfpl_synth_image(uint64_t seed, int seq_id, int frame_idx, int width, int height, uint8_t* out) {
+    if (!out || width <= 0 || height <= 0) return -1;
+    Rng r(mix(seed ^ 0x5A17ull, ((uint64_t)(uint32_t)seq_id << 32) | (uint32_t)frame_idx));
+    std::vector<float> img((size_t)width * height);
+    const double gx = r.uni(-0.15, 0.15), gy = r.uni(-0.15, 0.15), g0 = r.uni(60, 190);
+    for (int y = 0; y < height; ++y)
+        for (int x = 0; x < width; ++x) img[(size_t)y * width + x] = (float)(g0 + gx * x + gy * y);
+    const int n_shapes = 60 + (int)(r.next() % 40);
+    for (int k = 0; k < n_shapes; ++k) {
+        const double cx = r.uni(0, width), cy = r.uni(0, height);
+        const double sx = r.uni(6, 70), sy = r.uni(6, 70), th = r.uni(0, 3.141592653589793);
+        const float val = (float)r.uni(0, 255);
+        const bool disc = (r.next() & 3) == 0;
+        const double c = std::cos(th), s = std::sin(th);
+        const int x0 = std::max(0, (int)(cx - sx - sy - 2)), x1 = std::min(width - 1, (int)(cx + sx + sy + 2));
+        const int y0 = std::max(0, (int)(cy - sx - sy - 2)), y1 = std::min(height - 1, (int)(cy + sx + sy + 2));
+        for (int y = y0; y <= y1; ++y)
+            for (int x = x0; x <= x1; ++x) {
+                const double dx = x - cx, dy = y - cy;
+                const double u = c * dx + s * dy, v = -s * dx + c * dy;
+                const bool in = disc ? (u * u) / (sx * sx) + (v * v) / (sy * sy) <= 1.0 : (std::fabs(u) <= sx && std::fabs(v) <= sy);
+                if (in) img[(size_t)y * width + x] = val;
+            }
+    }
+    for (size_t i = 0; i < img.size(); ++i) {
+        const double v = img[i] + 2.0 * r.gauss();
+        out[i] = (uint8_t)std::min(255.0, std::max(0.0, std::floor(v + 0.5)));
+    }
+    return 0;
+}

@@ -58,6 +58,9 @@ int gfpl_synth_batch(const gfpl_synth_params* p, const gfpl_camera* cam,
                      uint8_t* ldesc_l, uint8_t* ldesc_r,
                      uint8_t* pyr_r, double* time_stamp, int n_threads);
 
+/* Synthetic grey image (width x height, row-major) for the ORB extraction row. */
+int gfpl_synth_image(uint64_t seed, int seq_id, int frame_idx, int width, int height, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

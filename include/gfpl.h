@@ -120,6 +120,15 @@ typedef struct gfpl_config {
 
 /* cv::KeyPoint subset used by the path */
 typedef struct gfpl_keypoint { float x, y; int octave; } gfpl_keypoint;
+/* ORB_SLAM2::ORBextractor parameters (src/ORBextractor.cc:410-470), as the path builds it
+ * (src/stereoFrame.cpp:33-36): Config::orbNFeatures, orbScaleFactor, orbNLevels, 20, 7 */
+typedef struct gfpl_orb_params {
+    int   nfeatures;      /* Config::orbNFeatures (src/config.cpp:134; 2000 in BASELINE cfg 2) */
+    float scale_factor;   /* Config::orbScaleFactor 1.2 */
+    int   nlevels;        /* Config::orbNLevels 4 */
+    int   ini_th_fast;    /* iniThFAST 20 */
+    int   min_th_fast;    /* minThFAST 7 */
+} gfpl_orb_params;
 /* line_descriptor::KeyLine subset (3rdparty/line_descriptor/include/line_descriptor/descriptor_custom.hpp:105-170) */
 typedef struct gfpl_keyline { float sx, sy, ex, ey, angle; int octave; } gfpl_keyline;
 
@@ -310,6 +319,30 @@ int  gfpl_line_cut(gfpl_seqbatch* sb);
  * Returns GFPL_E_TOO_FEW_TRAIN when nt < 2 (reference UB).        */
 int  gfpl_knn2_hamming(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
                        int cell, int32_t* out_idx, float* out_dist);
+
+/* --------------------------------------------- ORB extraction (§8(f)1) ---- */
+/* ORB_SLAM2::ORBextractor (src/ORBextractor.cc:410-470 constructor, :1043-1105
+ * operator()) as StereoFrame builds it (src/stereoFrame.cpp:33-36), over a batch of
+ * grey images on the device.  The extractor owns its workspace for images of
+ * width x height (64..2047 px) and up to max_images per call; kp_cap bounds the
+ * keypoints returned per image.  Arithmetic of the OpenCV calls pinned as the CPU
+ * oracle's ledger O1-O7.                                          */
+typedef struct gfpl_orb gfpl_orb;
+int  gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_orb_params* prm,
+                     int max_images, int kp_cap, gfpl_orb** out);
+int  gfpl_orb_destroy(gfpl_orb* orb);
+/* bytes of one image's packed level images (the gfpl_frames.pyr_r layout) */
+int  gfpl_orb_pyramid_bytes(const gfpl_orb* orb, int64_t* bytes);
+/* operator()(image, noArray(), keypoints, descriptors) for n images, all pointers
+ * DEVICE: images [n][height][width] u8; per image i, rows [i*kp_cap, +n_kp[i]) of
+ * kps / desc (32 B) / angle (degrees) / response (FAST score) hold the keypoints
+ * in the reference's order (level by level, DistributeOctTree node order),
+ * coordinates scaled to level 0.  angle, response, pyramid may be NULL; pyramid
+ * receives each image's level images at pyr_stride bytes apart.  Synchronises;
+ * GFPL_E_CAPACITY when an internal or kp_cap capacity was exceeded.            */
+int  gfpl_orb_extract(gfpl_orb* orb, const uint8_t* images, int n, gfpl_keypoint* kps,
+                      uint8_t* desc, int* n_kp, float* angle, float* response,
+                      uint8_t* pyramid, int64_t pyr_stride);
 
 /* ------------------------------------------------- keyframe consumers ---- */
 /* One keyframe's stereo features as KeyFrame::stereo_frame exposes them

@@ -55,6 +55,19 @@ int gfplo_need_new_kf(gfplo_handler* h, int* flag);
 int gfplo_curr_frame_is_kf(gfplo_handler* h);
 int gfplo_read_kf_state(gfplo_handler* h, gfpl_kf_state* out);
 
+/* ORB_SLAM2::ORBextractor::operator() (src/ORBextractor.cc:1043-1105) on one grey image
+ * (gfpl_orb_oracle.cpp; ledger O1-O7): keypoints (x, y, octave) in the reference's output
+ * order, their angle / FAST response, 32-byte descriptors; pyramid (nullable) receives the
+ * level images packed consecutively (the right pyramid of gfpl_frames). */
+int gfplo_orb_extract(const gfpl_orb_params* prm, const uint8_t* image, int width, int height, int kp_cap,
+                      gfpl_keypoint* kps, float* angle, float* response, uint8_t* desc, int* n_kp,
+                      uint8_t* pyramid);
+int gfplo_orb_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh);   /* O1 */
+int gfplo_orb_blur(const uint8_t* src, int w, int h, uint8_t* dst);                       /* O2 */
+/* O3: FAST(img, kps, threshold, nonmax) on a whole image; xy_score[3*i] = x, y, response */
+int gfplo_orb_fast(const uint8_t* img, int w, int h, int threshold, int cap, float* xy_score);
+float gfplo_fast_atan2(float y, float x);                                                 /* O4 */
+
 /* MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:
  * 199-470); same contract as gfpl_kf_common_matches but every pointer of the
  * views and outputs is HOST memory. */

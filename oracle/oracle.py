@@ -54,6 +54,12 @@ def lib() -> C.CDLL:
         for n in ["gfplo_inverse6", "gfplo_inverse4", "gfplo_expmap_se3", "gfplo_inverse_se3"]:
             getattr(L, n).argtypes = [P, P]; getattr(L, n).restype = C.c_int
         L.gfplo_eig_sym.argtypes = [P, C.c_int, P]; L.gfplo_eig_sym.restype = C.c_int
+        L.gfplo_orb_extract.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P]
+        L.gfplo_orb_extract.restype = C.c_int
+        L.gfplo_orb_resize.argtypes = [P, C.c_int, C.c_int, P, C.c_int, C.c_int]; L.gfplo_orb_resize.restype = C.c_int
+        L.gfplo_orb_blur.argtypes = [P, C.c_int, C.c_int, P]; L.gfplo_orb_blur.restype = C.c_int
+        L.gfplo_orb_fast.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, P]; L.gfplo_orb_fast.restype = C.c_int
+        L.gfplo_fast_atan2.argtypes = [C.c_float, C.c_float]; L.gfplo_fast_atan2.restype = C.c_float
         _L = L
     return _L
 
@@ -227,3 +233,47 @@ def expmap_se3(x):
 
 def inverse_se3(T):
     T = np.ascontiguousarray(T, np.float64); o = np.zeros((4, 4)); lib().gfplo_inverse_se3(_p(T), _p(o)); return o
+
+
+# ---- ORB extraction (gfpl_orb_oracle.cpp, ledger O1-O7)
+def orb_extract(image: np.ndarray, nfeatures: int = 2000, scale_factor: float = 1.2, nlevels: int = 4,
+                ini_th: int = 20, min_th: int = 7, kp_cap: int = 0):
+    """ORBextractor::operator() on one grey image: dict of keypoints (KEYPOINT_DT), angle,
+    response, desc [n][32] and the packed level images."""
+    image = np.ascontiguousarray(image, np.uint8)
+    h, w = image.shape
+    prm = gfpl.OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th)
+    kp_cap = kp_cap or nfeatures + 64 * nlevels + 64
+    kps = np.zeros(kp_cap, gfpl.KEYPOINT_DT)
+    ang = np.zeros(kp_cap, np.float32); rsp = np.zeros(kp_cap, np.float32)
+    desc = np.zeros((kp_cap, 32), np.uint8)
+    pyr = np.zeros(w * h * 4, np.uint8)   # sum of 1/scale^2 < 1 / (1 - 1/1.2^2) < 4
+    n = C.c_int(0)
+    rc = lib().gfplo_orb_extract(C.byref(prm), _p(image), w, h, kp_cap, _p(kps), _p(ang), _p(rsp), _p(desc),
+                                 C.byref(n), _p(pyr))
+    if rc != 0:
+        raise RuntimeError(f"gfplo_orb_extract -> {rc}")
+    k = n.value
+    return {"kps": kps[:k].copy(), "angle": ang[:k].copy(), "response": rsp[:k].copy(), "desc": desc[:k].copy(),
+            "pyramid": pyr}
+
+
+def orb_resize(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8); d = np.zeros((dh, dw), np.uint8)
+    lib().gfplo_orb_resize(_p(src), src.shape[1], src.shape[0], _p(d), dw, dh); return d
+
+
+def orb_blur(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8); d = np.zeros_like(src)
+    lib().gfplo_orb_blur(_p(src), src.shape[1], src.shape[0], _p(d)); return d
+
+
+def orb_fast(img: np.ndarray, threshold: int, cap: int = 1 << 16) -> np.ndarray:
+    """cv::FAST(img, kps, threshold, true): [n][3] (x, y, response) in row-major order."""
+    img = np.ascontiguousarray(img, np.uint8); o = np.zeros((cap, 3), np.float32)
+    n = lib().gfplo_orb_fast(_p(img), img.shape[1], img.shape[0], threshold, cap, _p(o))
+    return o[:min(n, cap)].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().gfplo_fast_atan2(y, x)

@@ -1,0 +1,118 @@
+"""GPU ORB extraction (gfpl_orb_extract, k_orb.hip) vs the CPU oracle
+(gfplo_orb_extract), SURVEY.md §8(f)1.  Bar: bit-exact — keypoint coordinates,
+octaves, angles, responses, descriptors and the pyramid bytes, in the reference's
+output order, for every image of a batch."""
+import numpy as np
+import pytest
+
+import gfpl
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _images(n, w, h, seq0, noise=0):
+    imgs = np.stack([gfpl.synth_image(seq0 + i, i, w, h) for i in range(n)])
+    if noise:
+        rng = np.random.default_rng(seq0)
+        imgs = np.clip(imgs.astype(int) + rng.integers(-noise, noise + 1, imgs.shape), 0, 255).astype(np.uint8)
+    return imgs
+
+
+def _run_gpu(orb, imgs):
+    import torch
+    n, h, w = imgs.shape
+    kc = orb.kp_cap
+    dev = torch.device("cuda", 0)
+    d_img = torch.from_numpy(imgs).to(dev)
+    kps = torch.zeros(n * kc * gfpl.KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(n * kc * 32, dtype=torch.uint8, device=dev)
+    nkp = torch.zeros(n, dtype=torch.int32, device=dev)
+    ang = torch.zeros(n * kc, dtype=torch.float32, device=dev)
+    rsp = torch.zeros(n * kc, dtype=torch.float32, device=dev)
+    stride = (orb.pyramid_bytes + 255) // 256 * 256
+    pyr = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    orb.extract(d_img, n, kps, desc, nkp, ang, rsp, pyr, stride)
+    return (kps.cpu().numpy().view(gfpl.KEYPOINT_DT).reshape(n, kc), desc.cpu().numpy().reshape(n, kc, 32),
+            nkp.cpu().numpy(), ang.cpu().numpy().reshape(n, kc), rsp.cpu().numpy().reshape(n, kc),
+            pyr.cpu().numpy().reshape(n, stride))
+
+
+def _compare(orb, imgs, nfeatures, nlevels, scale=1.2):
+    k, d, nk, a, r, p = _run_gpu(orb, imgs)
+    total = 0
+    for i, img in enumerate(imgs):
+        o = O.orb_extract(img, nfeatures=nfeatures, scale_factor=scale, nlevels=nlevels, kp_cap=orb.kp_cap)
+        n = len(o["kps"])
+        assert nk[i] == n, (i, nk[i], n)
+        assert (k[i, :n] == o["kps"]).all(), i
+        assert (a[i, :n].view(np.uint32) == o["angle"].view(np.uint32)).all(), i
+        assert (r[i, :n] == o["response"]).all(), i
+        assert (d[i, :n] == o["desc"]).all(), i
+        pb = orb.pyramid_bytes
+        assert (p[i, :pb] == o["pyramid"][:pb]).all(), i
+        total += n
+    return total
+
+
+@pytest.mark.parametrize("cam", ["vga", "euroc", "kitti"])
+def test_orb_parity_batch(cam):
+    c = gfpl.CAMERAS[cam]
+    orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, c["width"], c["height"], max_images=3)
+    n = _compare(orb, _images(3, c["width"], c["height"], 40), 2000, 4)
+    assert n > 900
+
+
+def test_orb_parity_textured_many_corners():
+    """Heavy texture: far more FAST corners than the quotas, so DistributeOctTree runs its
+    second (sorted-expansion) phase on every level."""
+    orb = gfpl.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_images=2)
+    n = _compare(orb, _images(2, 640, 480, 7, noise=40), 1000, 8)
+    assert n >= 990
+
+
+@pytest.mark.parametrize("nf,nl,sf", [(500, 3, 1.3), (150, 5, 1.2), (8000, 4, 1.2)])
+def test_orb_parity_params(nf, nl, sf):
+    orb = gfpl.ORBextractor(nf, sf, nl, 20, 7, 752, 480, max_images=2)
+    _compare(orb, _images(2, 752, 480, 91, noise=10), nf, nl, sf)
+
+
+def test_orb_edge_images():
+    """Flat (no corners), small (one or two 30-px cells per level) and a single bright
+    square; and the sizes the reference cannot handle (a level without a cell) refused."""
+    orb = gfpl.ORBextractor(2000, 1.2, 3, 20, 7, 128, 112, max_images=3)
+    sq = np.full((112, 128), 40, np.uint8)
+    sq[40:70, 45:90] = 220
+    imgs = np.stack([np.full((112, 128), 90, np.uint8), _images(1, 128, 112, 5, noise=30)[0], sq])
+    _compare(orb, imgs, 2000, 3)
+    _, _, nk, _, _, _ = _run_gpu(orb, imgs[:1])
+    assert nk[0] == 0
+    with pytest.raises(gfpl.GfplError):
+        gfpl.ORBextractor(2000, 1.2, 5, 20, 7, 128, 112)      # level 4 has no 30-px cell row
+    with pytest.raises(RuntimeError):
+        O.orb_extract(imgs[0], nlevels=5)
+
+
+def test_orb_host_call_matches_oracle():
+    """operator()(image) on a host image: keypoints as cv::KeyPoint fields, mvImagePyramid."""
+    c = gfpl.CAMERAS["vga"]
+    orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, c["width"], c["height"])
+    img = _images(1, c["width"], c["height"], 77)[0]
+    kps, desc = orb(img)
+    o = O.orb_extract(img)
+    assert (kps["x"] == o["kps"]["x"]).all() and (kps["octave"] == o["kps"]["octave"]).all()
+    assert (kps["size"] == np.float32(31) * orb.GetScaleFactors()[kps["octave"]]).all()
+    assert (desc == o["desc"]).all()
+    assert orb.mvImagePyramid[0].shape == (480, 640) and (orb.mvImagePyramid[0] == img).all()
+    assert [p.shape for p in orb.mvImagePyramid] == [(h, w) for (w, h) in orb.level_sizes()]
+
+
+def test_orb_rejects_bad_arguments():
+    with pytest.raises(gfpl.GfplError):
+        gfpl.ORBextractor(2000, 1.2, 9, 20, 7, 640, 480)       # > GFPL_MAX_LEVELS
+    with pytest.raises(gfpl.GfplError):
+        gfpl.ORBextractor(2000, 1.0, 4, 20, 7, 640, 480)       # scale factor must be > 1
+    orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, 640, 480, max_images=1)
+    with pytest.raises(gfpl.GfplError):
+        orb.extract(None, 2, None, None, None)                # n > max_images
