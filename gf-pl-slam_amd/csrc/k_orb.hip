@@ -7,12 +7,12 @@
 //                 (ComputePyramid :1107-1132), coefficient tables built on the host
 //  k_orb_blur     GaussianBlur 7x7 sigma 2 REFLECT_101 fixed point (O2) of every level,
 //                 one 64x32 tile per workgroup through LDS (rows pass, then columns)
-//  k_orb_fast     per pixel of the cells' area: the FAST-9/16 segment test and
-//                 cornerScore at iniThFAST and at minThFAST (O3) -> two u8 score maps
-//  k_orb_cells    one workgroup per (image, level): the 30-px cells of
-//                 ComputeKeyPointsOctTree (:765-853): non-max suppression inside each
-//                 cell's ROI, the minThFAST retry for empty cells, the keys of every cell
-//                 compacted in the reference's order (cell row, cell column, row, column)
+//  k_orb_cellfast one wave per 30-px cell of ComputeKeyPointsOctTree (:765-853), all
+//                 levels and images in one launch: FAST_t + cornerScore (O3) on the cell's
+//                 ROI in LDS, non-max suppression, the minThFAST retry for empty cells,
+//                 the keys in cv::FAST's row-major order into the cell's slot
+//  k_orb_gather   one workgroup per (image, level): the cells' keys concatenated in cell
+//                 order = vToDistributeKeys
 //  k_orb_octree   one wave per (image, level): DistributeOctTree (:539-763) with the
 //                 node list in LDS (the reference's list order, O6 for ties) and every
 //                 DivideNode a wave-parallel stable 4-way partition of the node's keys
@@ -58,8 +58,12 @@ struct OrbDev {
     int umax[16];
     uint8_t* pyr;     // [n][pyr_stride] level images
     uint8_t* blur;    // [n][pyr_stride] their Gaussian blur
-    uint8_t* s_ini;   // [n][pyr_stride] FAST scores at iniThFAST (0: no corner)
-    uint8_t* s_min;   // [n][pyr_stride] at minThFAST
+    int ncell;        // 30-px cells of all levels of one image
+    int cbase[GFPL_MAX_LEVELS + 1];   // first cell of each level
+    int ccap;         // key slots per cell (strict 3x3 maxima: <= ceil(w/2) ceil(h/2))
+    int patch_cap;    // LDS bytes of one cell's ROI, and of its score map
+    uint32_t* ckeys;  // [n][ncell][ccap] the keys of each cell in FAST's row-major order
+    int* ccnt;        // [n][ncell]
     uint32_t* keys;   // [n][nlevels][key_cap] vToDistributeKeys (packed)
     uint32_t* tmp;    // [n][nlevels][key_cap] partition scratch
     int* nkeys;       // [n][nlevels]
@@ -74,12 +78,12 @@ namespace {
 constexpr int kCircleX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 constexpr int kCircleY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
+// LDS written by some lanes of a wave, then read by others (the wave's DS operations
+// complete in order; the clobber keeps the compiler from moving accesses across)
+__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#define ORB_MAX_CELLS 4096
+
 __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
-__device__ __forceinline__ int refl101(int i, int n) {
-    if (n == 1) return 0;
-    while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
-    return i;
-}
 
 // packed key: x (11 bits) | y (11 bits) << 11 | score (8 bits) << 22, coordinates
 // relative to (minBorderX, minBorderY) as the reference's vToDistributeKeys
@@ -121,9 +125,13 @@ __global__ void k_orb_resize(OrbDev o, int l) {
     o.pyr[img * o.pyr_stride + d.off + (size_t)y * d.w + x] = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
 }
 
-// O2: 7x7 Gaussian, 8-bit integer taps, rows exact, columns (s + 2^15) >> 16
+// O2: 7x7 Gaussian, 8-bit integer taps, rows exact, columns (s + 2^15) >> 16.  One 64x32
+// tile per workgroup: the (32+6)x(64+6) source bytes (REFLECT_101 at the level's edges:
+// levels are >= 38 px, so one reflection suffices), the row pass into LDS, then every
+// thread slides the column pass down 8 rows of one column.
 #define BLUR_TW 64
 #define BLUR_TH 32
+__device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 __global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
     __shared__ uint8_t tile[BLUR_TH + 6][BLUR_TW + 8];
     __shared__ int rows[BLUR_TH + 6][BLUR_TW + 1];
@@ -132,30 +140,32 @@ __global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
     const int x0 = blockIdx.x * BLUR_TW, y0 = blockIdx.y * BLUR_TH;
     if (x0 >= L.w || y0 >= L.h) return;
     const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
-    for (int i = threadIdx.x; i < (BLUR_TH + 6) * (BLUR_TW + 6); i += blockDim.x) {
-        const int ty = i / (BLUR_TW + 6), tx = i % (BLUR_TW + 6);
-        tile[ty][tx] = S[(size_t)refl101(y0 + ty - 3, L.h) * L.w + refl101(x0 + tx - 3, L.w)];
+    const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
+    for (int c = tx; c < BLUR_TW + 6; c += 64) {
+        const int sx = refl1(min(x0 + c - 3, L.w + 2), L.w);
+        for (int r = ty0; r < BLUR_TH + 6; r += 4) tile[r][c] = S[(size_t)refl1(min(y0 + r - 3, L.h + 2), L.h) * L.w + sx];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < (BLUR_TH + 6) * BLUR_TW; i += blockDim.x) {
-        const int ty = i / BLUR_TW, tx = i % BLUR_TW;
-        int a = 0;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) a += o.blur_k[t] * tile[ty][tx + t];
-        rows[ty][tx] = a;
+    const int k0 = o.blur_k[0], k1 = o.blur_k[1], k2 = o.blur_k[2], k3 = o.blur_k[3];
+    for (int r = ty0; r < BLUR_TH + 6; r += 4) {
+        const uint8_t* T = &tile[r][tx];
+        rows[r][tx] = k0 * (T[0] + T[6]) + k1 * (T[1] + T[5]) + k2 * (T[2] + T[4]) + k3 * T[3];
     }
     __syncthreads();
     uint8_t* D = o.blur + img * o.pyr_stride + L.off;
-    for (int i = threadIdx.x; i < BLUR_TH * BLUR_TW; i += blockDim.x) {
-        const int ty = i / BLUR_TW, tx = i % BLUR_TW;
-        const int x = x0 + tx, y = y0 + ty;
-        if (x >= L.w || y >= L.h) continue;
-        // REFLECT_101 rows: the tile rows were loaded reflected, so tile row ty + 3 +- t is
-        // the reflected source row of y +- t
-        int a = o.blur_k[3] * rows[ty + 3][tx];
+    const int x = x0 + tx;
+    if (x >= L.w) return;
+    const int r0 = ty0 * 8;
+    int w[14];
 #pragma unroll
-        for (int t = 1; t <= 3; ++t) a += o.blur_k[3 + t] * (rows[ty + 3 + t][tx] + rows[ty + 3 - t][tx]);
-        D[(size_t)y * L.w + x] = sat_u8((a + (1 << 15)) >> 16);
+    for (int t = 0; t < 14; ++t) w[t] = rows[r0 + t][tx];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int y = y0 + r0 + q;
+        if (y < L.h) {
+            const int a = k3 * w[q + 3] + k2 * (w[q + 2] + w[q + 4]) + k1 * (w[q + 1] + w[q + 5]) + k0 * (w[q] + w[q + 6]);
+            D[(size_t)y * L.w + x] = sat_u8((a + (1 << 15)) >> 16);
+        }
     }
 }
 
@@ -211,105 +221,150 @@ __device__ __forceinline__ bool fast_test(const int* d, int t) {
     return arc9(dark) || arc9(bright);
 }
 
-__global__ void __launch_bounds__(256) k_orb_fast(OrbDev o) {
-    const int l = blockIdx.z % o.nlevels, img = blockIdx.z / o.nlevels;
-    const OrbLevel& L = o.lv[l];
-    const int x = L.minBX + 3 + blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = L.minBY + 3 + blockIdx.y;
-    if (x >= L.maxBX - 3 || y >= L.maxBY - 3) return;
-    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
-    const int v = S[(size_t)y * L.w + x];
-    int d[25];
+// ---------------------------------------------------------------- cells --
+// One wave per 30-px cell of ComputeKeyPointsOctTree (:765-853), all cells of all levels
+// of all images in one launch: the cell's ROI [iniX, maxX) x [iniY, maxY) into LDS, the
+// FAST_t segment test + cornerScore on its detectable area [3, w - 3) x [3, h - 3) (O3),
+// strict 3x3 non-max suppression with 0 outside that area, the surviving keys compacted
+// in row-major order (cv::FAST's output order) into the cell's slot; the minThFAST pass
+// only for cells the iniThFAST pass left empty (:803-808).
+__device__ __forceinline__ void cell_fast(const uint8_t* P, int pw, uint8_t* Sc, int dw, int dh, int th, int lane) {
+    for (int i = lane; i < dw * dh; i += 64) {
+        const int y = i / dw, x = i - y * dw;
+        const uint8_t* c = P + (y + 3) * pw + (x + 3);
+        const int v = c[0];
+        int d[25];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - (int)S[(size_t)(y + kCircleY[k]) * L.w + (x + kCircleX[k])];
+        for (int k = 0; k < 16; ++k) d[k] = v - (int)c[kCircleY[k] * pw + kCircleX[k]];
 #pragma unroll
-    for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
-    const size_t at = img * o.pyr_stride + L.off + (size_t)y * L.w + x;
-    o.s_ini[at] = fast_test(d, o.ini_th) ? (uint8_t)fast_score(d, o.ini_th) : 0;
-    o.s_min[at] = fast_test(d, o.min_th) ? (uint8_t)fast_score(d, o.min_th) : 0;
+        for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
+        const int s = fast_test(d, th) ? fast_score(d, th) : 0;
+        Sc[i] = (uint8_t)s;
+    }
 }
 
-// -------------------------------------------------------------------- cells --
-// non-max suppression inside the ROI of one cell: neighbours outside its detectable area
-// count as 0 (FAST_t's zeroed score rows and columns)
-__device__ __forceinline__ int nms_keep(const uint8_t* M, int w, int x, int y, int dx0, int dy0, int dx1, int dy1) {
-    const int s = M[(size_t)y * w + x];
-    if (!s) return 0;
+// strict 3x3 maxima of the score map (0 outside it), compacted in row-major order;
+// returns their count (keys beyond cap are counted, not written)
+__device__ __forceinline__ int cell_nms(const uint8_t* Sc, int dw, int dh, uint32_t* K, int cap, int kx0, int ky0,
+                                        int lane) {
+    int pos = 0;
+    for (int b = 0; b < dw * dh; b += 64) {
+        const int idx = b + lane;
+        int keep = 0, x = 0, y = 0;
+        if (idx < dw * dh) {
+            y = idx / dw;
+            x = idx - y * dw;
+            keep = Sc[idx];
+            if (keep) {
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
+                for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (!dx && !dy) continue;
-            const int xx = x + dx, yy = y + dy;
-            const int n = (xx >= dx0 && xx < dx1 && yy >= dy0 && yy < dy1) ? M[(size_t)yy * w + xx] : 0;
-            if (!(s > n)) return 0;
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        if (!dx && !dy) continue;
+                        const int xx = x + dx, yy = y + dy;
+                        const int nb = (xx >= 0 && xx < dw && yy >= 0 && yy < dh) ? Sc[yy * dw + xx] : 0;
+                        if (!(keep > nb)) keep = 0;
+                    }
+            }
         }
-    return s;
+        const unsigned long long m = __ballot(keep != 0);
+        if (keep) {
+            const int rank = pos + __popcll(m & ((1ull << lane) - 1ull));
+            if (rank < cap) K[rank] = key_pack(kx0 + x, ky0 + y, keep);
+        }
+        pos += __popcll(m);
+    }
+    return pos;
 }
 
-#define CELLS_T 256
-#define ORB_MAX_CELLS 4096
-__global__ void __launch_bounds__(CELLS_T) k_orb_cells(OrbDev o) {
-    __shared__ int cnt[ORB_MAX_CELLS];
-    const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
-    const OrbLevel& L = o.lv[l];
-    const int ncell = L.nRows * L.nCols;
+__global__ void __launch_bounds__(256) k_orb_cellfast(OrbDev o) {
+    extern __shared__ __align__(16) unsigned char csm[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t base = img * o.pyr_stride + L.off;
-    // pass 1: keys per cell (iniThFAST; minThFAST when that leaves the cell empty)
-    for (int c = wave; c < ncell; c += CELLS_T / 64) {
-        const int i = c / L.nCols, j = c % L.nCols;
-        const int iniY = L.minBY + i * L.hCell, iniX = L.minBX + j * L.wCell;
-        int total = 0, which = 0;
-        if (iniY < L.maxBY - 3 && iniX < L.maxBX - 6) {
-            const int maxY = min(iniY + L.hCell + 6, L.maxBY), maxX = min(iniX + L.wCell + 6, L.maxBX);
-            const int dx0 = iniX + 3, dy0 = iniY + 3, dx1 = maxX - 3, dy1 = maxY - 3;
-            for (int pass = 0; pass < 2 && total == 0; ++pass) {
-                const uint8_t* M = (pass ? o.s_min : o.s_ini) + base;
-                int c2 = 0;
-                for (int y = dy0; y < dy1; ++y)
-                    for (int x = dx0 + lane; x < dx1; x += 64) c2 += nms_keep(M, L.w, x, y, dx0, dy0, dx1, dy1) ? 1 : 0;
+    const int c = blockIdx.x * 4 + wave, img = blockIdx.y;
+    if (c >= o.ncell) return;
+    uint8_t* P = csm + wave * 2 * o.patch_cap;
+    uint8_t* Sc = P + o.patch_cap;
+    int l = 0;
+    while (c >= o.cbase[l + 1]) ++l;
+    const OrbLevel& L = o.lv[l];
+    const int ci = c - o.cbase[l];
+    const int i = ci / L.nCols, j = ci - (ci / L.nCols) * L.nCols;
+    int* cnt_out = o.ccnt + (size_t)img * o.ncell + c;
+    const int iniY = L.minBY + i * L.hCell, iniX = L.minBX + j * L.wCell;
+    if (!(iniY < L.maxBY - 3 && iniX < L.maxBX - 6)) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    const int maxY = min(iniY + L.hCell + 6, L.maxBY), maxX = min(iniX + L.wCell + 6, L.maxBX);
+    const int pw = maxX - iniX, ph = maxY - iniY, dw = pw - 6, dh = ph - 6;
+    if (dw <= 0 || dh <= 0) {
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off + (size_t)iniY * L.w + iniX;
+    for (int r = 0; r < ph; ++r)
+        for (int x = lane; x < pw; x += 64) P[r * pw + x] = S[(size_t)r * L.w + x];
+    wave_sync_lds();
+    uint32_t* K = o.ckeys + ((size_t)img * o.ncell + c) * o.ccap;
+    cell_fast(P, pw, Sc, dw, dh, o.ini_th, lane);
+    wave_sync_lds();
+    int pos = cell_nms(Sc, dw, dh, K, o.ccap, iniX + 3 - L.minBX, iniY + 3 - L.minBY, lane);
+    if (pos == 0) {   // vKeysCell.empty(): FAST again at minThFAST (:803-808)
+        cell_fast(P, pw, Sc, dw, dh, o.min_th, lane);
+        wave_sync_lds();
+        pos = cell_nms(Sc, dw, dh, K, o.ccap, iniX + 3 - L.minBX, iniY + 3 - L.minBY, lane);
+    }
+    if (lane == 0) {
+        if (pos > o.ccap) atomicOr(o.err, 1);
+        *cnt_out = min(pos, o.ccap);
+    }
+}
+
+// one workgroup per (image, level): the cells' keys concatenated in cell order (cell row,
+// cell column) = vToDistributeKeys (:810-816)
+#define GATHER_T 256
+__global__ void __launch_bounds__(GATHER_T) k_orb_gather(OrbDev o) {
+    __shared__ int off[ORB_MAX_CELLS + 1];
+    __shared__ int wsum[GATHER_T / 64];
+    const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
+    const int c0 = o.cbase[l], nc = o.cbase[l + 1] - c0;
+    const int* cnt = o.ccnt + (size_t)img * o.ncell + c0;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // exclusive scan: GATHER_T contiguous chunks
+    const int per = (nc + GATHER_T - 1) / GATHER_T;
+    int acc = 0;
+    for (int q = 0; q < per; ++q) {
+        const int c = t * per + q;
+        if (c < nc) acc += cnt[c];
+    }
+    int incl = acc;
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) c2 += __shfl_xor(c2, off, 64);
-                total = c2;
-                which = pass;
-            }
-        }
-        if (lane == 0) cnt[c] = total | (which << 30);
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const int v = __shfl_up(incl, sh, 64);
+        if (lane >= sh) incl += v;
     }
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    // exclusive scan of the counts in cell order
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int c = 0; c < ncell; ++c) {
-            const int v = cnt[c];
-            cnt[c] = acc | (v & (1 << 30));
-            acc += v & ~(1 << 30);
-        }
-        int tot = min(acc, o.key_cap);
-        o.nkeys[img * o.nlevels + l] = tot;
-        if (acc > o.key_cap) atomicOr(o.err, 1);
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    int run = base + incl - acc;
+    for (int q = 0; q < per; ++q) {
+        const int c = t * per + q;
+        if (c < nc) { off[c] = run; run += cnt[c]; }
     }
+    if (t == GATHER_T - 1) off[nc] = run;
     __syncthreads();
-    // pass 2: the keys of each cell in row-major order at the cell's offset
+    const int total = off[nc];
     uint32_t* K = o.keys + ((size_t)img * o.nlevels + l) * o.key_cap;
-    for (int c = wave; c < ncell; c += CELLS_T / 64) {
-        const int i = c / L.nCols, j = c % L.nCols;
-        const int iniY = L.minBY + i * L.hCell, iniX = L.minBX + j * L.wCell;
-        if (!(iniY < L.maxBY - 3 && iniX < L.maxBX - 6)) continue;
-        const int maxY = min(iniY + L.hCell + 6, L.maxBY), maxX = min(iniX + L.wCell + 6, L.maxBX);
-        const int dx0 = iniX + 3, dy0 = iniY + 3, dx1 = maxX - 3, dy1 = maxY - 3;
-        const uint8_t* M = ((cnt[c] >> 30) ? o.s_min : o.s_ini) + base;
-        int pos = cnt[c] & ~(1 << 30);
-        for (int y = dy0; y < dy1; ++y)
-            for (int x0 = dx0; x0 < dx1; x0 += 64) {
-                const int x = x0 + lane;
-                const int s = x < dx1 ? nms_keep(M, L.w, x, y, dx0, dy0, dx1, dy1) : 0;
-                const unsigned long long m = __ballot(s != 0);
-                const int rank = __popcll(m & ((1ull << lane) - 1ull));
-                if (s && pos + rank < o.key_cap) K[pos + rank] = key_pack(x - L.minBX, y - L.minBY, s);
-                pos += __popcll(m);
-            }
+    const uint32_t* CK = o.ckeys + ((size_t)img * o.ncell + c0) * o.ccap;
+    for (int c = wave; c < nc; c += GATHER_T / 64) {
+        const int n = cnt[c], b = off[c];
+        for (int k = lane; k < n; k += 64)
+            if (b + k < o.key_cap) K[b + k] = CK[(size_t)c * o.ccap + k];
+    }
+    if (t == 0) {
+        o.nkeys[img * o.nlevels + l] = min(total, o.key_cap);
+        if (total > o.key_cap) atomicOr(o.err, 1);
     }
 }
 
@@ -333,7 +388,6 @@ __device__ __forceinline__ OExp oexp(int size, int id, int node) {
 }
 #define ORB_MAX_INI 16
 
-__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // stable partition of K[off, off + len) into G groups (grp(key) in [0, G)), through T
 template <int G, typename F>
@@ -577,69 +631,75 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
     return a;
 }
 
+// one wave per kept keypoint (4 per workgroup): IC_Angle's integer moments over the
+// 31-px disc split across the lanes and reduced (exact in any order), then bit b of the
+// descriptor (pattern points 2b, 2b + 1) on lane b % 64 and one ballot per 64 bits
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, 64);
+    return v;
+}
+
 __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keypoint* kps, uint8_t* desc, int* n_kp,
                                                       float* angle_out, float* resp_out, int kp_cap) {
-    const int img = blockIdx.y;
-    int nl[GFPL_MAX_LEVELS], tot = 0;
-    for (int l = 0; l < o.nlevels; ++l) { nl[l] = o.nsel[img * o.nlevels + l]; tot += nl[l]; }
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t == 0) {
+    const int img = blockIdx.y, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    int tot = 0;
+    for (int l = 0; l < o.nlevels; ++l) tot += o.nsel[img * o.nlevels + l];
+    if (t == 0 && lane == 0) {
         n_kp[img] = min(tot, kp_cap);
         if (tot > kp_cap) atomicOr(o.err, 4);
     }
     if (t >= tot || t >= kp_cap) return;
     int l = 0, r = t;
-    while (r >= nl[l]) { r -= nl[l]; ++l; }
+    while (r >= o.nsel[img * o.nlevels + l]) { r -= o.nsel[img * o.nlevels + l]; ++l; }
     const OrbLevel& L = o.lv[l];
     const uint32_t k = o.sel[((size_t)img * o.nlevels + l) * o.sel_cap + r];
     const int x = key_x(k) + L.minBX, y = key_y(k) + L.minBY;   // level coordinates (:843-844)
-    // IC_Angle (:77-104) on the level image
-    const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
+    // IC_Angle (:77-104): lane handles u = lane % 32 - 15 (u = 16 unused) on rows
+    // v = lane / 32 + 2q; row 0 feeds m_10 only
+    const uint8_t* center = o.pyr + img * o.pyr_stride + L.off + (size_t)y * L.w + x;
+    const int u = (lane & 31) - 15;
     int m_01 = 0, m_10 = 0;
-    const uint8_t* center = S + (size_t)y * L.w + x;
-    for (int u = -15; u <= 15; ++u) m_10 += u * center[u];
-    for (int v = 1; v <= 15; ++v) {
-        int v_sum = 0;
-        const int d = o.umax[v];
-        for (int u = -d; u <= d; ++u) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int v = (lane >> 5) + 2 * q;
+        if (v == 0) {
+            if (u <= 15) m_10 += u * center[u];
+        } else if (u >= -o.umax[v] && u <= o.umax[v]) {
             const int vp = center[u + v * L.w], vm = center[u - v * L.w];
-            v_sum += vp - vm;
+            m_01 += v * (vp - vm);
             m_10 += u * (vp + vm);
         }
-        m_01 += v * v_sum;
     }
+    m_01 = wave_sum(m_01);
+    m_10 = wave_sum(m_10);
     const float ang = fast_atan2((float)m_01, (float)m_10);
     // computeOrbDescriptor (:108-148) on the blurred level, O5
     const float factorPI = (float)(M_PI / 180.f);
     const float a_ = ang * factorPI;
     const float ca = (float)det_cos((double)a_), sa = (float)det_sin((double)a_);
     const uint8_t* B = o.blur + img * o.pyr_stride + L.off + (size_t)y * L.w + x;
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = 0;
-    for (int i = 0; i < 32; ++i) {
-        uint32_t val = 0;
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const int idx0 = 16 * i + 2 * bit, idx1 = idx0 + 1;
-            const int px0 = c_orb_pattern[2 * idx0], py0 = c_orb_pattern[2 * idx0 + 1];
-            const int px1 = c_orb_pattern[2 * idx1], py1 = c_orb_pattern[2 * idx1 + 1];
-            const int t0 = B[__float2int_rn(px0 * sa + py0 * ca) * L.w + __float2int_rn(px0 * ca - py0 * sa)];
-            const int t1 = B[__float2int_rn(px1 * sa + py1 * ca) * L.w + __float2int_rn(px1 * ca - py1 * sa)];
-            val |= (uint32_t)(t0 < t1) << bit;
-        }
-        w[i >> 2] |= val << (8 * (i & 3));
-    }
     const size_t q = (size_t)img * kp_cap + t;
-    uint4* dd = reinterpret_cast<uint4*>(desc + 32 * q);
-    dd[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    dd[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    // keypoint coordinates scaled to level 0 (:1094-1101)
-    float fx = (float)x, fy = (float)y;
-    if (l != 0) { fx = fx * L.scale; fy = fy * L.scale; }
-    kps[q] = gfpl_keypoint{fx, fy, l};
-    if (angle_out) angle_out[q] = ang;
-    if (resp_out) resp_out[q] = (float)key_s(k);
+    unsigned long long* dd = reinterpret_cast<unsigned long long*>(desc + 32 * q);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int bit = 64 * w + lane;
+        const int px0 = c_orb_pattern[4 * bit], py0 = c_orb_pattern[4 * bit + 1];
+        const int px1 = c_orb_pattern[4 * bit + 2], py1 = c_orb_pattern[4 * bit + 3];
+        const int t0 = B[__float2int_rn(px0 * sa + py0 * ca) * L.w + __float2int_rn(px0 * ca - py0 * sa)];
+        const int t1 = B[__float2int_rn(px1 * sa + py1 * ca) * L.w + __float2int_rn(px1 * ca - py1 * sa)];
+        const unsigned long long m = __ballot(t0 < t1);
+        if (lane == w) dd[w] = m;
+    }
+    if (lane == 0) {
+        // keypoint coordinates scaled to level 0 (:1094-1101)
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) { fx = fx * L.scale; fy = fy * L.scale; }
+        kps[q] = gfpl_keypoint{fx, fy, l};
+        if (angle_out) angle_out[q] = ang;
+        if (resp_out) resp_out[q] = (float)key_s(k);
+    }
 }
 
 // copy the level images into a caller's pyramid array (gfpl_frames.pyr_r layout)
@@ -769,6 +829,20 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
         max_n = std::max(max_n, L.N);
     }
     if (max_cells > ORB_MAX_CELLS) { delete o; return GFPL_E_UNSUPPORTED; }
+    {
+        int ncell = 0, maxw = 0, maxh = 0;
+        for (int l = 0; l < d.nlevels; ++l) {
+            d.cbase[l] = ncell;
+            ncell += d.lv[l].nRows * d.lv[l].nCols;
+            maxw = std::max(maxw, d.lv[l].wCell);
+            maxh = std::max(maxh, d.lv[l].hCell);
+        }
+        d.cbase[d.nlevels] = ncell;
+        d.ncell = ncell;
+        d.ccap = ((maxw + 1) / 2) * ((maxh + 1) / 2);
+        d.patch_cap = ((maxw + 6) * (maxh + 6) + 15) & ~15;
+        if (8 * d.patch_cap > 64 * 1024) { delete o; return GFPL_E_UNSUPPORTED; }
+    }
     d.node_cap = max_n + 4 * ORB_MAX_INI + 16;   // list size <= max(N, 4 nIni) + 3, + 4 children in flight
     if (orb_octree_lds(d.node_cap) > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
     if (hipFuncSetAttribute((const void*)k_orb_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -822,7 +896,8 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
     const long long b_keys = al(4 * M * d.nlevels * (long long)d.key_cap);
     const long long b_n = al(4 * M * d.nlevels);
     const long long b_sel = al(4 * M * d.nlevels * (long long)d.sel_cap);
-    const long long total = b_x + b_a + b_y + b_b + 4 * b_img + 2 * b_keys + 2 * b_n + b_sel + 256;
+    const long long b_ck = al(4 * M * d.ncell * (long long)d.ccap), b_cc = al(4 * M * d.ncell);
+    const long long total = b_x + b_a + b_y + b_b + 2 * b_img + 2 * b_keys + 2 * b_n + b_sel + b_ck + b_cc + 256;
     if (hipMalloc(&o->base, (size_t)total) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
     int* xo = (int*)p; p += b_x;
@@ -831,8 +906,8 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
     int16_t* bp = (int16_t*)p; p += b_b;
     d.pyr = (uint8_t*)p; p += b_img;
     d.blur = (uint8_t*)p; p += b_img;
-    d.s_ini = (uint8_t*)p; p += b_img;
-    d.s_min = (uint8_t*)p; p += b_img;
+    d.ckeys = (uint32_t*)p; p += b_ck;
+    d.ccnt = (int*)p; p += b_cc;
     d.keys = (uint32_t*)p; p += b_keys;
     d.tmp = (uint32_t*)p; p += b_keys;
     d.nkeys = (int*)p; p += b_n;
@@ -853,7 +928,6 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
         ok = ok && hipMemcpy(bp, beta_h.data(), 2 * beta_h.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_orb_pattern), kOrbPattern, sizeof(kOrbPattern)) == hipSuccess;
-    ok = ok && hipMemset(d.s_ini, 0, 2 * b_img) == hipSuccess;   // s_ini | s_min outside the cells' area
     if (!ok) { (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
     *out = o;
     return GFPL_OK;
@@ -886,13 +960,12 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     const OrbLevel& L0 = d.lv[0];
     hipLaunchKernelGGL(k_orb_blur, dim3((L0.w + BLUR_TW - 1) / BLUR_TW, (L0.h + BLUR_TH - 1) / BLUR_TH, n * d.nlevels),
                        dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_orb_fast, dim3((L0.maxBX - L0.minBX + 255) / 256, L0.maxBY - L0.minBY, n * d.nlevels), dim3(256),
-                       0, s, d);
-    hipLaunchKernelGGL(k_orb_cells, dim3(n * d.nlevels), dim3(CELLS_T), 0, s, d);
+    hipLaunchKernelGGL(k_orb_cellfast, dim3((d.ncell + 3) / 4, n), dim3(256), 8 * d.patch_cap, s, d);
+    hipLaunchKernelGGL(k_orb_gather, dim3(n * d.nlevels), dim3(GATHER_T), 0, s, d);
     const size_t lds = orb_octree_lds(d.node_cap);
     hipLaunchKernelGGL(k_orb_octree, dim3(n * d.nlevels), dim3(64), lds, s, d);
     const int max_tot = d.sel_cap * d.nlevels;
-    hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 255) / 256, n), dim3(256), 0, s, d, n, kps,
+    hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 3) / 4, n), dim3(256), 0, s, d, n, kps,
                        desc, n_kp, angle, response, o->kp_cap);
     if (pyramid) hipLaunchKernelGGL(k_orb_pyr_out, dim3(64, n), dim3(256), 0, s, d, pyramid, (long long)pyr_stride, o->pyr_bytes);
     ORB_HIPCHK(hipGetLastError());
