@@ -47,7 +47,9 @@ struct OrbLevel {
 struct OrbDev {
     int W, H, nlevels, ini_th, min_th;
     int key_cap, sel_cap, node_cap;
+    int key_lds;      // levels with up to key_lds keys keep them in the octree's LDS
     long long pyr_stride;            // bytes between the pyramids of two images
+    long long blur_stride;           // ... between their blurred copies
     OrbLevel lv[GFPL_MAX_LEVELS];
     const int* xofs[GFPL_MAX_LEVELS];
     const int16_t* alpha[GFPL_MAX_LEVELS];
@@ -56,8 +58,8 @@ struct OrbDev {
     int xmax[GFPL_MAX_LEVELS];
     int blur_k[7];
     int umax[16];
-    uint8_t* pyr;     // [n][pyr_stride] level images
-    uint8_t* blur;    // [n][pyr_stride] their Gaussian blur
+    uint8_t* pyr;     // [n][pyr_stride] level images (the caller's pyramid array when it asks for one)
+    uint8_t* blur;    // [n][blur_stride] their Gaussian blur
     int ncell;        // 30-px cells of all levels of one image
     int cbase[GFPL_MAX_LEVELS + 1];   // first cell of each level
     int ccap;         // key slots per cell (strict 3x3 maxima: <= ceil(w/2) ceil(h/2))
@@ -100,8 +102,16 @@ __device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 22); }
 __global__ void k_orb_copy0(OrbDev o, const uint8_t* images, int n) {
     const size_t npx = (size_t)o.W * o.H;
     const int img = blockIdx.y;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x)
-        o.pyr[img * o.pyr_stride + i] = images[img * npx + i];
+    const uint8_t* src = images + img * npx;
+    uint8_t* dst = o.pyr + img * o.pyr_stride;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {   // 16-B rows of the image, then the tail
+        const size_t nv = npx / 16;
+        for (size_t i = t0; i < nv; i += nt) reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+        for (size_t i = nv * 16 + t0; i < npx; i += nt) dst[i] = src[i];
+    } else {
+        for (size_t i = t0; i < npx; i += nt) dst[i] = src[i];
+    }
 }
 
 // O1: dst(x, y) = ((h(y0, x) b0 + h(y1, x) b1 + 2^21) >> 22), h = exact 11-bit horizontal blend
@@ -133,7 +143,7 @@ __global__ void k_orb_resize(OrbDev o, int l) {
 #define BLUR_TH 32
 __device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 __global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
-    __shared__ uint8_t tile[BLUR_TH + 6][BLUR_TW + 8];
+    __shared__ int tile[BLUR_TH + 6][BLUR_TW + 8];   // (dword cells: byte LDS traffic measured slower)
     __shared__ int rows[BLUR_TH + 6][BLUR_TW + 1];
     const int l = blockIdx.z % o.nlevels, img = blockIdx.z / o.nlevels;
     const OrbLevel& L = o.lv[l];
@@ -141,18 +151,34 @@ __global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
     if (x0 >= L.w || y0 >= L.h) return;
     const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
     const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
-    for (int c = tx; c < BLUR_TW + 6; c += 64) {
-        const int sx = refl1(min(x0 + c - 3, L.w + 2), L.w);
-        for (int r = ty0; r < BLUR_TH + 6; r += 4) tile[r][c] = S[(size_t)refl1(min(y0 + r - 3, L.h + 2), L.h) * L.w + sx];
+    {   // 10 rows x (1 or 2) columns per thread, loads in flight before the LDS stores
+        const int sx0 = refl1(min(x0 + tx - 3, L.w + 2), L.w);
+        const int sx1 = refl1(min(x0 + tx + 61, L.w + 2), L.w);
+        uint8_t a[10], b[10];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int r = ty0 + 4 * q;
+            const size_t row = (size_t)refl1(min(y0 + min(r, BLUR_TH + 5) - 3, L.h + 2), L.h) * L.w;
+            a[q] = S[row + sx0];
+            b[q] = tx < 6 ? S[row + sx1] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int r = ty0 + 4 * q;
+            if (r < BLUR_TH + 6) {
+                tile[r][tx] = a[q];
+                if (tx < 6) tile[r][tx + 64] = b[q];
+            }
+        }
     }
     __syncthreads();
     const int k0 = o.blur_k[0], k1 = o.blur_k[1], k2 = o.blur_k[2], k3 = o.blur_k[3];
     for (int r = ty0; r < BLUR_TH + 6; r += 4) {
-        const uint8_t* T = &tile[r][tx];
+        const int* T = &tile[r][tx];
         rows[r][tx] = k0 * (T[0] + T[6]) + k1 * (T[1] + T[5]) + k2 * (T[2] + T[4]) + k3 * T[3];
     }
     __syncthreads();
-    uint8_t* D = o.blur + img * o.pyr_stride + L.off;
+    uint8_t* D = o.blur + img * o.blur_stride + L.off;
     const int x = x0 + tx;
     if (x >= L.w) return;
     const int r0 = ty0 * 8;
@@ -228,18 +254,50 @@ __device__ __forceinline__ bool fast_test(const int* d, int t) {
 // strict 3x3 non-max suppression with 0 outside that area, the surviving keys compacted
 // in row-major order (cv::FAST's output order) into the cell's slot; the minThFAST pass
 // only for cells the iniThFAST pass left empty (:803-808).
-__device__ __forceinline__ void cell_fast(const uint8_t* P, int pw, uint8_t* Sc, int dw, int dh, int th, int lane) {
-    for (int i = lane; i < dw * dh; i += 64) {
-        const int y = i / dw, x = i - y * dw;
-        const uint8_t* c = P + (y + 3) * pw + (x + 3);
-        const int v = c[0];
-        int d[25];
+// Pass A: OpenCV's FAST_t prefilter on the four opposite pairs (0,8) (2,10) (4,12) (6,14)
+// (every 9-arc holds one pixel of each pair: a necessary condition), zero scores, the
+// candidates' indices compacted into LDS; pass B: the segment test + cornerScore on the
+// candidates only, 64 at a time.
+__device__ __forceinline__ void cell_fast(const uint8_t* P, int pw, uint8_t* Sc, uint16_t* cand, int dw, int dh,
+                                          int th, int lane) {
+    const float rdw = 1.0f / (float)dw;
+    int nc = 0;
+    for (int b = 0; b < dw * dh; b += 64) {
+        const int i = b + lane;
+        bool pass = false;
+        if (i < dw * dh) {
+            const int y = (int)(((float)i + 0.5f) * rdw), x = i - y * dw;
+            const uint8_t* c = P + (y + 3) * pw + (x + 3);
+            const int v = c[0];
+            int dk = 1, br = 1;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = v - (int)c[kCircleY[k] * pw + kCircleX[k]];
+            for (int k = 0; k < 8; k += 2) {
+                const int d0 = v - (int)c[kCircleY[k] * pw + kCircleX[k]];
+                const int d1 = v - (int)c[kCircleY[k + 8] * pw + kCircleX[k + 8]];
+                dk &= (d0 > th) | (d1 > th);
+                br &= (d0 < -th) | (d1 < -th);
+            }
+            pass = (dk | br) != 0;
+            Sc[i] = 0;
+        }
+        const unsigned long long m = __ballot(pass);
+        if (pass) cand[nc + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)i;
+        nc += __popcll(m);
+    }
+    wave_sync_lds();
+    for (int b = 0; b < nc; b += 64) {
+        if (b + lane < nc) {
+            const int i = cand[b + lane];
+            const int y = (int)(((float)i + 0.5f) * rdw), x = i - y * dw;
+            const uint8_t* c = P + (y + 3) * pw + (x + 3);
+            const int v = c[0];
+            int d[25];
 #pragma unroll
-        for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
-        const int s = fast_test(d, th) ? fast_score(d, th) : 0;
-        Sc[i] = (uint8_t)s;
+            for (int k = 0; k < 16; ++k) d[k] = v - (int)c[kCircleY[k] * pw + kCircleX[k]];
+#pragma unroll
+            for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
+            if (fast_test(d, th)) Sc[i] = (uint8_t)fast_score(d, th);
+        }
     }
 }
 
@@ -277,13 +335,15 @@ __device__ __forceinline__ int cell_nms(const uint8_t* Sc, int dw, int dh, uint3
     return pos;
 }
 
+#define CELL_LD 24
 __global__ void __launch_bounds__(256) k_orb_cellfast(OrbDev o) {
     extern __shared__ __align__(16) unsigned char csm[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + wave, img = blockIdx.y;
     if (c >= o.ncell) return;
-    uint8_t* P = csm + wave * 2 * o.patch_cap;
+    uint8_t* P = csm + wave * 4 * o.patch_cap;
     uint8_t* Sc = P + o.patch_cap;
+    uint16_t* cand = reinterpret_cast<uint16_t*>(Sc + o.patch_cap);
     int l = 0;
     while (c >= o.cbase[l + 1]) ++l;
     const OrbLevel& L = o.lv[l];
@@ -302,15 +362,30 @@ __global__ void __launch_bounds__(256) k_orb_cellfast(OrbDev o) {
         return;
     }
     const uint8_t* S = o.pyr + img * o.pyr_stride + L.off + (size_t)iniY * L.w + iniX;
-    for (int r = 0; r < ph; ++r)
-        for (int x = lane; x < pw; x += 64) P[r * pw + x] = S[(size_t)r * L.w + x];
+    // the ROI in batches of CELL_LD bytes per lane, all loads in flight before the stores
+    // (row = floor((idx + 0.5) / pw) is exact in float for ROIs below 2^12 bytes)
+    const float rpw = 1.0f / (float)pw;
+    for (int b = 0; b < pw * ph; b += 64 * CELL_LD) {
+        uint8_t v[CELL_LD];
+#pragma unroll
+        for (int q = 0; q < CELL_LD; ++q) {
+            const int idx = b + q * 64 + lane;
+            const int r = (int)(((float)idx + 0.5f) * rpw), x = idx - r * pw;
+            v[q] = idx < pw * ph ? S[(size_t)r * L.w + x] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < CELL_LD; ++q) {
+            const int idx = b + q * 64 + lane;
+            if (idx < pw * ph) P[idx] = v[q];
+        }
+    }
     wave_sync_lds();
     uint32_t* K = o.ckeys + ((size_t)img * o.ncell + c) * o.ccap;
-    cell_fast(P, pw, Sc, dw, dh, o.ini_th, lane);
+    cell_fast(P, pw, Sc, cand, dw, dh, o.ini_th, lane);
     wave_sync_lds();
     int pos = cell_nms(Sc, dw, dh, K, o.ccap, iniX + 3 - L.minBX, iniY + 3 - L.minBY, lane);
     if (pos == 0) {   // vKeysCell.empty(): FAST again at minThFAST (:803-808)
-        cell_fast(P, pw, Sc, dw, dh, o.min_th, lane);
+        cell_fast(P, pw, Sc, cand, dw, dh, o.min_th, lane);
         wave_sync_lds();
         pos = cell_nms(Sc, dw, dh, K, o.ccap, iniX + 3 - L.minBX, iniY + 3 - L.minBY, lane);
     }
@@ -387,6 +462,9 @@ __device__ __forceinline__ OExp oexp(int size, int id, int node) {
     return ((uint64_t)(uint32_t)size << 40) | ((uint64_t)(uint32_t)id << 16) | (uint32_t)node;
 }
 #define ORB_MAX_INI 16
+#define DIV_REG 8   // nodes of up to 64 * DIV_REG keys are divided from registers
+
+__device__ __forceinline__ void wave_fence_global() { __threadfence_block(); }
 
 
 // stable partition of K[off, off + len) into G groups (grp(key) in [0, G)), through T
@@ -424,19 +502,29 @@ __device__ __forceinline__ void wave_partition(uint32_t* K, uint32_t* T, int off
     for (int q = 0; q < G; ++q) cnt[q] = c[q];
 }
 
+__host__ __device__ __forceinline__ size_t orb_octree_node_lds(int node_cap) {
+    return (size_t)node_cap * (sizeof(ONode) + 2 * sizeof(OExp) + 2);
+}
+
+// The list bookkeeping runs on wave-uniform registers (head, size, ids, allocation) with
+// lane 0 storing the node records, so a DivideNode costs a few LDS round trips.  The
+// nodes a main-loop pass divides are, in list order, the previous pass's children with
+// more than one key in reverse creation order (every child is pushed to the front), i.e.
+// vSizeAndPointerToNode of that pass read backwards; the first pass divides the initial
+// nodes in column order.
 __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
     extern __shared__ __align__(16) unsigned char osm[];
     const int cap = o.node_cap;
     ONode* nd = reinterpret_cast<ONode*>(osm);
-    OExp* ex = reinterpret_cast<OExp*>(nd + cap);   // vSizeAndPointerToNode
-    OExp* ex2 = ex + cap;                            // vPrevSizeAndPointerToNode
-    int16_t* freel = reinterpret_cast<int16_t*>(ex2 + cap);
-    __shared__ int st[8];   // 0 head, 1 size, 2 next id, 3 nfree, 4 nex, 5 nex2
+    OExp* exA = reinterpret_cast<OExp*>(nd + cap);
+    OExp* exB = exA + cap;
+    int16_t* freel = reinterpret_cast<int16_t*>(exB + cap);
+    __shared__ int ini[ORB_MAX_INI];
     const int lane = threadIdx.x;
     const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
     const OrbLevel& L = o.lv[l];
     const size_t kb = ((size_t)img * o.nlevels + l) * o.key_cap;
-    uint32_t* K = o.keys + kb;
+    uint32_t* K = o.keys + kb;   // generic pointer: global, or the LDS copy below
     uint32_t* T = o.tmp + kb;
     const int nk = o.nkeys[img * o.nlevels + l];
     const int N = L.N;
@@ -445,168 +533,267 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         if (lane == 0) o.nsel[img * o.nlevels + l] = 0;
         return;
     }
-    if (lane == 0) {
-        st[0] = -1; st[1] = 0; st[2] = 0; st[3] = 0; st[4] = 0; st[5] = 0;
-        for (int i = cap - 1; i >= 0; --i) freel[st[3]++] = (int16_t)i;
+    if (nk <= o.key_lds) {   // every divide then reads and writes LDS instead of HBM
+        uint32_t* KL = reinterpret_cast<uint32_t*>(osm + ((orb_octree_node_lds(cap) + 15) & ~(size_t)15));
+        for (int i = lane; i < nk; i += 64) KL[i] = K[i];
+        K = KL;
     }
-    wave_sync_lds();
-    // list primitives: lane 0 only, callers sync the wave afterwards
-    auto push_front = [&](int i) {
-        nd[i].prev = -1;
-        nd[i].next = (int16_t)st[0];
-        if (st[0] >= 0) nd[st[0]].prev = (int16_t)i;
-        st[0] = i;
-        ++st[1];
+    // wave-uniform list state
+    int head = -1, lsize = 0, next_id = 0, nfree = 0, nalloc = 0;
+    OExp* cur = exA;   // vSizeAndPointerToNode of the running pass / round
+    OExp* prv = exB;   // ... of the previous one
+    int ncur = 0;
+    bool overflow = false;
+    auto alloc = [&]() -> int {
+        if (nfree > 0) return freel[--nfree];
+        if (nalloc < cap) return nalloc++;
+        overflow = true;
+        return -1;
     };
-    auto erase = [&](int i) -> int {   // the node after i
-        const int pv = nd[i].prev, nx = nd[i].next;
-        if (pv >= 0) nd[pv].next = (int16_t)nx; else st[0] = nx;
-        if (nx >= 0) nd[nx].prev = (int16_t)pv;
-        freel[st[3]++] = (int16_t)i;
-        --st[1];
-        return nx;
+    auto push_front = [&](int c) {
+        if (lane == 0) {
+            nd[c].prev = -1;
+            nd[c].next = (int16_t)head;
+            if (head >= 0) nd[head].prev = (int16_t)c;
+        }
+        head = c;
+        ++lsize;
     };
-    auto new_node = [&](int x0, int y0, int x1, int y1, int off, int len) -> int {
-        if (st[3] == 0) { atomicOr(o.err, 2); return -1; }
-        const int c = freel[--st[3]];
-        nd[c].x0 = (int16_t)x0; nd[c].y0 = (int16_t)y0; nd[c].x1 = (int16_t)x1; nd[c].y1 = (int16_t)y1;
-        nd[c].off = off; nd[c].len = len;
-        nd[c].id = st[2]++;
-        return c;
-    };
-    // DivideNode (:481-537) of node i: the non-empty children go to the front of the list
-    // in n1..n4 order (:621-660); those with > 1 keys are recorded in ex (nToExpand)
+    // DivideNode (:481-537) of node i and the list surgery of :621-660 / :700-730: the
+    // non-empty children pushed to the front in n1..n4 order, those with > 1 keys recorded,
+    // the parent erased.  Returns the number recorded.
     auto divide = [&](int i) -> int {
-        const int x0 = nd[i].x0, y0 = nd[i].y0, x1 = nd[i].x1, y1 = nd[i].y1, off = nd[i].off, len = nd[i].len;
+        wave_sync_lds();
+        const ONode nv = nd[i];
+        const int x0 = nv.x0, y0 = nv.y0, x1 = nv.x1, y1 = nv.y1, off = nv.off, len = nv.len;
+        int pv = nv.prev;
+        const int nx = nv.next;
         const int halfX = (int)ceilf((float)(x1 - x0) / 2), halfY = (int)ceilf((float)(y1 - y0) / 2);
         const int mx = x0 + halfX, my = y0 + halfY;
         int cnt[4];
-        wave_partition<4>(K, T, off, len, [&](uint32_t k) {
+        auto quad = [&](uint32_t k) {
             const float x = (float)key_x(k), y = (float)key_y(k);
             return x < (float)mx ? (y < (float)my ? 0 : 2) : (y < (float)my ? 1 : 3);
-        }, cnt);
-        int rec = 0;
-        if (lane == 0) {
-            const int cx0[4] = {x0, mx, x0, mx}, cy0[4] = {y0, y0, my, my};
-            const int cx1[4] = {mx, x1, mx, x1}, cy1[4] = {my, my, y1, y1};
-            int o2 = off;
-            for (int q = 0; q < 4; ++q) {
-                if (cnt[q] > 0) {
-                    const int c = new_node(cx0[q], cy0[q], cx1[q], cy1[q], o2, cnt[q]);
-                    if (c >= 0) {
-                        push_front(c);
-                        if (cnt[q] > 1) { ex[st[4]++] = oexp(cnt[q], nd[c].id, c); ++rec; }
+        };
+        if (len <= 64 * DIV_REG) {
+            // the node's keys in registers: one read, one scatter in place (stores reach
+            // memory before the pass ends: wave_fence_global at the end of every pass)
+            uint32_t kr[DIV_REG];
+            int g[DIV_REG];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cnt[q] = 0;
+#pragma unroll
+            for (int r = 0; r < DIV_REG; ++r) {
+                if (r * 64 < len) {
+                    const int idx = r * 64 + lane;
+                    kr[r] = idx < len ? K[off + idx] : 0u;
+                    g[r] = idx < len ? quad(kr[r]) : -1;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) cnt[q] += __popcll(__ballot(g[r] == q));
+                }
+            }
+            int run[4] = {off, off + cnt[0], off + cnt[0] + cnt[1], off + cnt[0] + cnt[1] + cnt[2]};
+#pragma unroll
+            for (int r = 0; r < DIV_REG; ++r) {
+                if (r * 64 < len) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const unsigned long long m = __ballot(g[r] == q);
+                        if (g[r] == q) K[run[q] + __popcll(m & ((1ull << lane) - 1ull))] = kr[r];
+                        run[q] += __popcll(m);
                     }
                 }
-                o2 += cnt[q];
             }
+        } else {
+            wave_partition<4>(K, T, off, len, quad, cnt);
         }
-        wave_sync_lds();
-        return __shfl(rec, 0);
+        const int cx0[4] = {x0, mx, x0, mx}, cy0[4] = {y0, y0, my, my};
+        const int cx1[4] = {mx, x1, mx, x1}, cy1[4] = {my, my, y1, y1};
+        int o2 = off, rec = 0, first = -1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (cnt[q] > 0) {
+                const int c = alloc();
+                if (c >= 0) {
+                    const int id = next_id++;
+                    if (lane == 0) {
+                        nd[c].x0 = (int16_t)cx0[q]; nd[c].y0 = (int16_t)cy0[q];
+                        nd[c].x1 = (int16_t)cx1[q]; nd[c].y1 = (int16_t)cy1[q];
+                        nd[c].off = o2; nd[c].len = cnt[q]; nd[c].id = id;
+                    }
+                    push_front(c);
+                    if (first < 0) first = c;
+                    if (cnt[q] > 1) {
+                        if (lane == 0) cur[ncur] = oexp(cnt[q], id, c);
+                        ++ncur;
+                        ++rec;
+                    }
+                }
+            }
+            o2 += cnt[q];
+        }
+        // erase the parent: a parent at the head has the first child pushed as prev now
+        if (pv < 0 && first >= 0) pv = first;
+        if (lane == 0) {
+            if (pv >= 0) nd[pv].next = (int16_t)nx;
+            if (nx >= 0) nd[nx].prev = (int16_t)pv;
+            freel[nfree] = (int16_t)i;
+        }
+        if (pv < 0) head = nx;
+        ++nfree;
+        --lsize;
+        return rec;
     };
     // ---- initial nodes (:542-585): nIni columns of width hX over the keys' x
+    const int nIni = L.nIni;
     {
-        const int nIni = L.nIni;
         const float hX = L.hX;
         int cnt[ORB_MAX_INI];
         wave_partition<ORB_MAX_INI>(K, T, 0, nk, [&](uint32_t k) { return (int)__fdiv_rn((float)key_x(k), hX); }, cnt);
-        if (lane == 0) {
-            // push_back in column order = the list built back to front with push_front
-            int offs[ORB_MAX_INI];
-            int acc = 0;
-            for (int q = 0; q < nIni; ++q) { offs[q] = acc; acc += cnt[q]; }
-            const int H = L.maxBY - L.minBY;
-            int ids[ORB_MAX_INI];
-            for (int q = 0; q < nIni; ++q) ids[q] = st[2]++;   // the reference creates all nIni nodes first
-            for (int q = nIni - 1; q >= 0; --q) {
-                if (cnt[q] == 0) continue;   // empty initial nodes are erased (:581-582)
-                const int c = new_node((int)(hX * (float)q), 0, (int)(hX * (float)(q + 1)), H, offs[q], cnt[q]);
-                if (c < 0) continue;
-                nd[c].id = ids[q];
-                push_front(c);
-            }
-            st[2] = nIni;
-        }
-        wave_sync_lds();
-    }
-    // ---- the subdivision loop (:594-739)
-    bool finish = false;
-    while (!finish) {
-        const int prevSize = st[1];
-        int nToExpand = 0;
-        if (lane == 0) st[4] = 0;
-        wave_sync_lds();
-        int it = st[0];
-        while (it >= 0) {
-            if (nd[it].len == 1) {
-                it = nd[it].next;
-                continue;
-            }
-            nToExpand += divide(it);
-            int nx = 0;
-            if (lane == 0) nx = erase(it);
-            wave_sync_lds();
-            it = __shfl(nx, 0);
-        }
-        const int size = st[1];
-        if (size >= N || size == prevSize) {
-            finish = true;
-        } else if (size + nToExpand * 3 > N) {
-            while (!finish) {
-                const int prev = st[1];
-                // vPrevSizeAndPointerToNode = vSizeAndPointerToNode, sorted by (size, node) (O6)
-                const int ne = st[4];
-                for (int i = lane; i < ne; i += 64) ex2[i] = ex[i];
-                wave_sync_lds();
-                if (lane == 0) {
-                    st[4] = 0;
-                    for (int a = 1; a < ne; ++a) {   // insertion sort (stable; keys distinct)
-                        const OExp v = ex2[a];
-                        int b = a - 1;
-                        while (b >= 0 && ex2[b] > v) {
-                            ex2[b + 1] = ex2[b];
-                            --b;
-                        }
-                        ex2[b + 1] = v;
-                    }
-                }
-                wave_sync_lds();
-                for (int j = ne - 1; j >= 0; --j) {
-                    const int node = (int)(ex2[j] & 0xFFFFu);
-                    divide(node);
-                    if (lane == 0) erase(node);
-                    wave_sync_lds();
-                    if (st[1] >= N) break;
-                }
-                if (st[1] >= N || st[1] == prev) finish = true;
-            }
-        }
-    }
-    // ---- the best key of every node, in list order (:741-760): first strict maximum
-    int n_out = 0;
-    for (int it = st[0]; it >= 0; it = nd[it].next) {
-        const int off = nd[it].off, len = nd[it].len;
-        int best = -1;
-        uint32_t bk = 0;
-        for (int b = 0; b < len; b += 64) {
-            const int i = b + lane;
-            const uint32_t k = i < len ? K[off + i] : 0u;
-            int s = i < len ? key_s(k) : -1;
-            int mi = i < len ? i : 0x7FFFFFFF;
-            // wave argmax: larger score, then smaller index
+        int offs[ORB_MAX_INI];
+        int acc = 0;
 #pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) {
-                const int os = __shfl_xor(s, sh, 64), oi = __shfl_xor(mi, sh, 64);
-                if (os > s || (os == s && oi < mi)) { s = os; mi = oi; }
+        for (int q = 0; q < ORB_MAX_INI; ++q) { offs[q] = acc; acc += cnt[q]; }
+        const int H = L.maxBY - L.minBY;
+        next_id = nIni;   // the reference creates all nIni nodes, then erases the empty ones
+        // push_back in column order = push_front from the last column
+#pragma unroll
+        for (int q = ORB_MAX_INI - 1; q >= 0; --q) {
+            int c = -1;
+            if (q < nIni && cnt[q] > 0) {
+                c = alloc();
+                if (c >= 0) {
+                    if (lane == 0) {
+                        nd[c].x0 = (int16_t)(int)(hX * (float)q); nd[c].y0 = 0;
+                        nd[c].x1 = (int16_t)(int)(hX * (float)(q + 1)); nd[c].y1 = (int16_t)H;
+                        nd[c].off = offs[q]; nd[c].len = cnt[q]; nd[c].id = q;
+                    }
+                    push_front(c);
+                }
             }
-            if (best < 0 || s > key_s(bk)) { best = mi; bk = K[off + mi]; }
+            if (lane == 0 && q < nIni) ini[q] = (c >= 0 && cnt[q] > 1) ? c : -1;
         }
-        if (lane == 0 && n_out < o.sel_cap) out[n_out] = bk;
-        ++n_out;
     }
+    wave_sync_lds();
+#ifdef ORB_PROF
+    const long long t_start = clock64();
+    int prof_div = 0, prof_pass = 0, prof_round = 0;
+#endif
+    // ---- the subdivision loop (:594-739)
+    bool finish = false, first_pass = true;
+    while (!finish) {
+        const int prevSize = lsize;
+        // this pass divides the previous pass's recorded children, newest first
+        OExp* t = prv; prv = cur; cur = t;
+        const int nprev = ncur;
+        ncur = 0;
+        int nToExpand = 0;
+        if (first_pass) {
+            for (int q = 0; q < nIni; ++q) {
+                const int c = ini[q];
+                if (c >= 0) nToExpand += divide(c);
+#ifdef ORB_PROF
+                ++prof_div;
+#endif
+            }
+            first_pass = false;
+        } else {
+            for (int j = nprev - 1; j >= 0; --j) {
+                nToExpand += divide((int)(prv[j] & 0xFFFFu));
+#ifdef ORB_PROF
+                ++prof_div;
+#endif
+            }
+        }
+        wave_fence_global();
+#ifdef ORB_PROF
+        ++prof_pass;
+#endif
+        if (overflow) break;
+        if (lsize >= N || lsize == prevSize) {
+            finish = true;
+        } else if (lsize + nToExpand * 3 > N) {
+            while (!finish) {
+                const int prev = lsize;
+                // vPrevSizeAndPointerToNode = vSizeAndPointerToNode sorted by (size, node) (O6):
+                // rank sort (the entries are distinct) from cur into prv, then prv is read
+                // from the back while cur collects this round's children
+                const int ne = ncur;
+                wave_sync_lds();
+                for (int e = lane; e < ne; e += 64) {
+                    const OExp v = cur[e];
+                    int rank = 0;
+                    for (int j = 0; j < ne; ++j) rank += cur[j] < v;
+                    prv[rank] = v;
+                }
+                wave_sync_lds();
+                ncur = 0;
+                for (int j = ne - 1; j >= 0; --j) {
+                    divide((int)(prv[j] & 0xFFFFu));
+#ifdef ORB_PROF
+                    ++prof_round;
+#endif
+                    if (lsize >= N) break;
+                }
+                wave_fence_global();
+                if (overflow) break;
+                if (lsize >= N || lsize == prev) finish = true;
+            }
+            if (overflow) break;
+        }
+    }
+    wave_sync_lds();
+    // ---- the best key of every node, in list order (:741-760): first strict maximum.
+    // The list order into LDS (prv is free now), then a lane per node for nodes of up to
+    // 16 keys and the whole wave for the larger ones
+    int16_t* ordl = reinterpret_cast<int16_t*>(prv);
     if (lane == 0) {
+        int k = 0;
+        for (int it = head; it >= 0; it = nd[it].next) ordl[k++] = (int16_t)it;
+    }
+    wave_sync_lds();
+    const int n_out = lsize;
+    for (int base = 0; base < n_out; base += 64) {
+        const int idx = base + lane;
+        const int node = idx < n_out ? ordl[idx] : -1;
+        const int off = node >= 0 ? nd[node].off : 0, len = node >= 0 ? nd[node].len : 0;
+        uint32_t bk = len > 0 ? K[off] : 0u;
+        if (len <= 16) {
+            for (int q = 1; q < len; ++q) {
+                const uint32_t k = K[off + q];
+                if (key_s(k) > key_s(bk)) bk = k;
+            }
+        }
+        unsigned long long big = __ballot(len > 16);
+        while (big) {
+            const int src = __ffsll((long long)big) - 1;
+            big &= big - 1;
+            const int boff = __shfl(off, src), blen = __shfl(len, src);
+            int bs = -1, bi = 0x7FFFFFFF;
+            for (int b = 0; b < blen; b += 64) {
+                const int i = b + lane;
+                int sc = i < blen ? key_s(K[boff + i]) : -1;
+                int mi = i < blen ? i : 0x7FFFFFFF;
+#pragma unroll
+                for (int sh = 32; sh > 0; sh >>= 1) {
+                    const int os = __shfl_xor(sc, sh, 64), oi = __shfl_xor(mi, sh, 64);
+                    if (os > sc || (os == sc && oi < mi)) { sc = os; mi = oi; }
+                }
+                if (sc > bs) { bs = sc; bi = mi; }   // strictly larger: the earlier block keeps ties
+            }
+            if (lane == src) bk = K[boff + bi];
+        }
+        if (idx < n_out && idx < o.sel_cap) out[idx] = bk;
+    }
+#ifdef ORB_PROF
+    if (lane == 0)
+        printf("orbprof img %d l %d nk %d nout %d div %d pass %d div2 %d tree %lld total %lld\n", img, l, nk, n_out,
+               prof_div, prof_pass, prof_round, (long long)(clock64() - t_start), (long long)clock64());
+#endif
+    if (lane == 0) {
+        if (overflow) atomicOr(o.err, 2);
         if (n_out > o.sel_cap) atomicOr(o.err, 4);
-        o.nsel[img * o.nlevels + l] = min(n_out, o.sel_cap);
+        o.nsel[img * o.nlevels + l] = overflow ? 0 : min(n_out, o.sel_cap);
     }
 }
 
@@ -679,7 +866,7 @@ __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keyp
     const float factorPI = (float)(M_PI / 180.f);
     const float a_ = ang * factorPI;
     const float ca = (float)det_cos((double)a_), sa = (float)det_sin((double)a_);
-    const uint8_t* B = o.blur + img * o.pyr_stride + L.off + (size_t)y * L.w + x;
+    const uint8_t* B = o.blur + img * o.blur_stride + L.off + (size_t)y * L.w + x;
     const size_t q = (size_t)img * kp_cap + t;
     unsigned long long* dd = reinterpret_cast<unsigned long long*>(desc + 32 * q);
 #pragma unroll
@@ -702,12 +889,6 @@ __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keyp
     }
 }
 
-// copy the level images into a caller's pyramid array (gfpl_frames.pyr_r layout)
-__global__ void k_orb_pyr_out(OrbDev o, uint8_t* dst, long long dst_stride, long long bytes) {
-    const int img = blockIdx.y;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < bytes; i += (long long)gridDim.x * blockDim.x)
-        dst[img * dst_stride + i] = o.pyr[img * o.pyr_stride + i];
-}
 
 }  // namespace gfpl
 
@@ -735,7 +916,9 @@ namespace {
         }                                                                              \
     } while (0)
 
-size_t orb_octree_lds(int node_cap) { return (size_t)node_cap * (sizeof(ONode) + 2 * sizeof(OExp) + 2) + 16; }
+size_t orb_octree_lds(int node_cap, int key_lds) {
+    return ((orb_octree_node_lds(node_cap) + 15) & ~(size_t)15) + 4 * (size_t)key_lds;
+}
 
 inline int cv_round_f(float v) { return (int)std::nearbyintf(v); }
 inline int cv_round_d(double v) { return (int)std::nearbyint(v); }
@@ -841,14 +1024,17 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
         d.ncell = ncell;
         d.ccap = ((maxw + 1) / 2) * ((maxh + 1) / 2);
         d.patch_cap = ((maxw + 6) * (maxh + 6) + 15) & ~15;
-        if (8 * d.patch_cap > 64 * 1024) { delete o; return GFPL_E_UNSUPPORTED; }
+        if (16 * d.patch_cap > 64 * 1024 || (maxw + 6) * (maxh + 6) >= 4096) { delete o; return GFPL_E_UNSUPPORTED; }
     }
     d.node_cap = max_n + 4 * ORB_MAX_INI + 16;   // list size <= max(N, 4 nIni) + 3, + 4 children in flight
-    if (orb_octree_lds(d.node_cap) > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
+    // keys in LDS up to a 40 KB workgroup (four single-wave octree workgroups per CU)
+    d.key_lds = std::max(0, (int)((40 * 1024 - (long long)orb_octree_lds(d.node_cap, 0)) / 4) & ~63);
+    if (orb_octree_lds(d.node_cap, d.key_lds) > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
     if (hipFuncSetAttribute((const void*)k_orb_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)orb_octree_lds(d.node_cap)) != hipSuccess) { delete o; return GFPL_E_HIP; }
+                            (int)orb_octree_lds(d.node_cap, d.key_lds)) != hipSuccess) { delete o; return GFPL_E_HIP; }
     o->pyr_bytes = off;
     d.pyr_stride = (off + 255) & ~255LL;
+    d.blur_stride = d.pyr_stride;
     // FAST keys per level: the reference keeps them all; strict 3x3 maxima are never
     // 8-adjacent, so a level holds at most ~1/4 of its cells' pixels
     d.key_cap = (int)std::min<long long>((long long)width * height / 4 + 4LL * (width + height) + 1024, 1 << 22);
@@ -951,23 +1137,26 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     if (!o || !images || n < 1 || n > o->max_images || !kps || !desc || !n_kp) return GFPL_E_INVALID;
     if (pyramid && pyr_stride < o->pyr_bytes) return GFPL_E_INVALID;
     ORB_HIPCHK(hipSetDevice(o->device));
-    OrbDev& d = o->d;
+    OrbDev d = o->d;   // this call's view: the caller's pyramid array is the working pyramid
+    if (pyramid) {
+        d.pyr = pyramid;
+        d.pyr_stride = pyr_stride;
+    }
     hipStream_t s = o->stream;
     ORB_HIPCHK(hipMemsetAsync(d.err, 0, 4, s));
-    hipLaunchKernelGGL(k_orb_copy0, dim3(64, n), dim3(256), 0, s, d, images, n);
+    hipLaunchKernelGGL(k_orb_copy0, dim3(128, n), dim3(256), 0, s, d, images, n);
     for (int l = 1; l < d.nlevels; ++l)
         hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].w + 255) / 256, d.lv[l].h, n), dim3(256), 0, s, d, l);
     const OrbLevel& L0 = d.lv[0];
     hipLaunchKernelGGL(k_orb_blur, dim3((L0.w + BLUR_TW - 1) / BLUR_TW, (L0.h + BLUR_TH - 1) / BLUR_TH, n * d.nlevels),
                        dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_orb_cellfast, dim3((d.ncell + 3) / 4, n), dim3(256), 8 * d.patch_cap, s, d);
+    hipLaunchKernelGGL(k_orb_cellfast, dim3((d.ncell + 3) / 4, n), dim3(256), 16 * d.patch_cap, s, d);
     hipLaunchKernelGGL(k_orb_gather, dim3(n * d.nlevels), dim3(GATHER_T), 0, s, d);
-    const size_t lds = orb_octree_lds(d.node_cap);
+    const size_t lds = orb_octree_lds(d.node_cap, d.key_lds);
     hipLaunchKernelGGL(k_orb_octree, dim3(n * d.nlevels), dim3(64), lds, s, d);
     const int max_tot = d.sel_cap * d.nlevels;
     hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 3) / 4, n), dim3(256), 0, s, d, n, kps,
                        desc, n_kp, angle, response, o->kp_cap);
-    if (pyramid) hipLaunchKernelGGL(k_orb_pyr_out, dim3(64, n), dim3(256), 0, s, d, pyramid, (long long)pyr_stride, o->pyr_bytes);
     ORB_HIPCHK(hipGetLastError());
     int err = 0;
     ORB_HIPCHK(hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s));
