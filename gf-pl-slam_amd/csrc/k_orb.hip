@@ -464,7 +464,7 @@ __device__ __forceinline__ OExp oexp(int size, int id, int node) {
     return ((uint64_t)(uint32_t)size << 40) | ((uint64_t)(uint32_t)id << 16) | (uint32_t)node;
 }
 #define ORB_MAX_INI 16
-#define DIV_REG 8   // nodes of up to 64 * DIV_REG keys are divided from registers
+#define DIV_REG 4   // nodes of up to 64 * DIV_REG keys are divided from registers
 
 __device__ __forceinline__ void wave_fence_global() { __threadfence_block(); }
 
@@ -521,7 +521,6 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
     OExp* exA = reinterpret_cast<OExp*>(nd + cap);
     OExp* exB = exA + cap;
     int16_t* freel = reinterpret_cast<int16_t*>(exB + cap);
-    __shared__ int ini[ORB_MAX_INI];
     const int lane = threadIdx.x;
     const int l = blockIdx.x % o.nlevels, img = blockIdx.x / o.nlevels;
     const OrbLevel& L = o.lv[l];
@@ -650,12 +649,32 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
     const int nIni = L.nIni;
     {
         const float hX = L.hX;
-        int cnt[ORB_MAX_INI];
-        wave_partition<ORB_MAX_INI>(K, T, 0, nk, [&](uint32_t k) { return (int)__fdiv_rn((float)key_x(k), hX); }, cnt);
-        int offs[ORB_MAX_INI];
-        int acc = 0;
+        // stable partition by column, one pass over the keys per column (nIni is 1-4 for
+        // camera aspect ratios; a loop keeps the code small), through T
+        int cnt[ORB_MAX_INI], offs[ORB_MAX_INI];
+        int run = 0;
+#pragma unroll 1
+        for (int q = 0; q < nIni; ++q) {
+            const int r0 = run;
+            for (int b = 0; b < nk; b += 64) {
+                const int i = b + lane;
+                const uint32_t k = i < nk ? K[i] : 0u;
+                const bool in = i < nk && (int)__fdiv_rn((float)key_x(k), hX) == q;
+                const unsigned long long m = __ballot(in);
+                if (in) T[run + __popcll(m & ((1ull << lane) - 1ull))] = k;
+                run += __popcll(m);
+            }
+            // (registers indexed by the loop counter: written through a select chain)
 #pragma unroll
-        for (int q = 0; q < ORB_MAX_INI; ++q) { offs[q] = acc; acc += cnt[q]; }
+            for (int u = 0; u < ORB_MAX_INI; ++u)
+                if (u == q) { offs[u] = r0; cnt[u] = run - r0; }
+        }
+#pragma unroll
+        for (int u = 0; u < ORB_MAX_INI; ++u)
+            if (u >= nIni) { offs[u] = run; cnt[u] = 0; }
+        wave_fence_global();
+        for (int i = lane; i < nk; i += 64) K[i] = T[i];
+        wave_fence_global();
         const int H = L.maxBY - L.minBY;
         next_id = nIni;   // the reference creates all nIni nodes, then erases the empty ones
         // push_back in column order = push_front from the last column
@@ -673,78 +692,69 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
                     push_front(c);
                 }
             }
-            if (lane == 0 && q < nIni) ini[q] = (c >= 0 && cnt[q] > 1) ? c : -1;
+            // the first pass's work list: the initial nodes with > 1 keys, read from the back
+            if (q < nIni && c >= 0 && cnt[q] > 1) {
+                if (lane == 0) cur[ncur] = (OExp)c;
+                ++ncur;
+            }
         }
     }
     wave_sync_lds();
 #ifdef ORB_PROF
-    const long long t_start = clock64();
+    const long long t_start = clock64(), w_start = wall_clock64();
     int prof_div = 0, prof_pass = 0, prof_round = 0;
+    long long t_sort = 0;
 #endif
-    // ---- the subdivision loop (:594-739)
-    bool finish = false, first_pass = true;
+    // ---- the subdivision loop (:594-739), one call site of divide (code size): phase 0 =
+    // the first pass, 1 = a later pass of the main loop, 2 = a round of the sorted expansion
+    // (:699-737).  Each pass / round reads its work list `prv` from the back and records
+    // this pass's children in `cur`.
+    bool finish = false;
+    int phase = 0;
     while (!finish) {
         const int prevSize = lsize;
-        // this pass divides the previous pass's recorded children, newest first
-        OExp* t = prv; prv = cur; cur = t;
-        const int nprev = ncur;
+        const int ntodo = ncur;
+        if (phase < 2) {
+            OExp* t = prv; prv = cur; cur = t;
+        } else {
+            // vPrevSizeAndPointerToNode = vSizeAndPointerToNode sorted by (size, node) (O6):
+            // rank sort (the entries are distinct) from cur into prv
+#ifdef ORB_PROF
+            const long long ts0 = clock64();
+#endif
+            wave_sync_lds();
+            for (int e = lane; e < ntodo; e += 64) {
+                const OExp v = cur[e];
+                int rank = 0;
+                for (int j = 0; j < ntodo; ++j) rank += cur[j] < v;
+                prv[rank] = v;
+            }
+#ifdef ORB_PROF
+            t_sort += clock64() - ts0;
+#endif
+        }
+        wave_sync_lds();
         ncur = 0;
         int nToExpand = 0;
-        if (first_pass) {
-            for (int q = 0; q < nIni; ++q) {
-                const int c = ini[q];
-                if (c >= 0) nToExpand += divide(c);
+        for (int j = ntodo - 1; j >= 0; --j) {
+            nToExpand += divide((int)(prv[j] & 0xFFFFu));
 #ifdef ORB_PROF
-                ++prof_div;
+            ++(phase < 2 ? prof_div : prof_round);
 #endif
-            }
-            first_pass = false;
-        } else {
-            for (int j = nprev - 1; j >= 0; --j) {
-                nToExpand += divide((int)(prv[j] & 0xFFFFu));
-#ifdef ORB_PROF
-                ++prof_div;
-#endif
-            }
+            if (phase == 2 && lsize >= N) break;
         }
         wave_fence_global();
 #ifdef ORB_PROF
         ++prof_pass;
 #endif
         if (overflow) break;
-        if (lsize >= N || lsize == prevSize) {
-            finish = true;
-        } else if (lsize + nToExpand * 3 > N) {
-            while (!finish) {
-                const int prev = lsize;
-                // vPrevSizeAndPointerToNode = vSizeAndPointerToNode sorted by (size, node) (O6):
-                // rank sort (the entries are distinct) from cur into prv, then prv is read
-                // from the back while cur collects this round's children
-                const int ne = ncur;
-                wave_sync_lds();
-                for (int e = lane; e < ne; e += 64) {
-                    const OExp v = cur[e];
-                    int rank = 0;
-                    for (int j = 0; j < ne; ++j) rank += cur[j] < v;
-                    prv[rank] = v;
-                }
-                wave_sync_lds();
-                ncur = 0;
-                for (int j = ne - 1; j >= 0; --j) {
-                    divide((int)(prv[j] & 0xFFFFu));
-#ifdef ORB_PROF
-                    ++prof_round;
-#endif
-                    if (lsize >= N) break;
-                }
-                wave_fence_global();
-                if (overflow) break;
-                if (lsize >= N || lsize == prev) finish = true;
-            }
-            if (overflow) break;
-        }
+        if (lsize >= N || lsize == prevSize) finish = true;
+        else if (phase < 2) phase = (lsize + nToExpand * 3 > N) ? 2 : 1;
     }
     wave_sync_lds();
+#ifdef ORB_PROF
+    const long long t_tree = clock64();
+#endif
     // ---- the best key of every node, in list order (:741-760): first strict maximum.
     // The list order into LDS (prv is free now), then a lane per node for nodes of up to
     // 16 keys and the whole wave for the larger ones
@@ -754,6 +764,9 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         for (int it = head; it >= 0; it = nd[it].next) ordl[k++] = (int16_t)it;
     }
     wave_sync_lds();
+#ifdef ORB_PROF
+    const long long t_walk = clock64();
+#endif
     const int n_out = lsize;
     for (int base = 0; base < n_out; base += 64) {
         const int idx = base + lane;
@@ -789,8 +802,9 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
     }
 #ifdef ORB_PROF
     if (lane == 0)
-        printf("orbprof img %d l %d nk %d nout %d div %d pass %d div2 %d tree %lld total %lld\n", img, l, nk, n_out,
-               prof_div, prof_pass, prof_round, (long long)(clock64() - t_start), (long long)clock64());
+        printf("orbprof img %d l %d nk %d nout %d div %d pass %d divb %d tree %lld sort %lld walk %lld best %lld wall %lld\n",
+               img, l, nk, n_out, prof_div, prof_pass, prof_round, (long long)(t_tree - t_start), t_sort,
+               (long long)(t_walk - t_tree), (long long)(clock64() - t_walk), (long long)(wall_clock64() - w_start));
 #endif
     if (lane == 0) {
         if (overflow) atomicOr(o.err, 2);
