@@ -834,49 +834,51 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
     return a;
 }
 
-// one wave per kept keypoint (4 per workgroup): IC_Angle's integer moments over the
-// 31-px disc split across the lanes and reduced (exact in any order), then bit b of the
-// descriptor (pattern points 2b, 2b + 1) on lane b % 64 and one ballot per 64 bits
-__device__ __forceinline__ int wave_sum(int v) {
+// two kept keypoints per wave (one per 32-lane half, 8 per workgroup): IC_Angle's integer
+// moments over the 31-px disc split across the half's lanes (u = lane - 15, rows v = 0..15)
+// and reduced (exact in any order); bit 32w + lane of the descriptor (pattern points 2b,
+// 2b + 1) on lane `lane` of the half, one ballot per 32 bits of each keypoint
+__device__ __forceinline__ int half_sum(int v) {
 #pragma unroll
-    for (int sh = 32; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, 64);
+    for (int sh = 16; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, 64);
     return v;
 }
 
 __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keypoint* kps, uint8_t* desc, int* n_kp,
                                                       float* angle_out, float* resp_out, int kp_cap) {
-    const int img = blockIdx.y, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int img = blockIdx.y, lane = threadIdx.x & 63, hl = lane & 31, half = lane >> 5;
+    const int t = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;
     int tot = 0;
     for (int l = 0; l < o.nlevels; ++l) tot += o.nsel[img * o.nlevels + l];
-    if (t == 0 && lane == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         n_kp[img] = min(tot, kp_cap);
         if (tot > kp_cap) atomicOr(o.err, 4);
     }
-    if (t >= tot || t >= kp_cap) return;
-    int l = 0, r = t;
+    const int nt = min(tot, kp_cap);
+    if ((t & ~1) >= nt) return;   // both halves idle (the wave is uniform here)
+    const bool valid = t < nt;
+    int l = 0, r = valid ? t : 0;
     while (r >= o.nsel[img * o.nlevels + l]) { r -= o.nsel[img * o.nlevels + l]; ++l; }
     const OrbLevel& L = o.lv[l];
     const uint32_t k = o.sel[((size_t)img * o.nlevels + l) * o.sel_cap + r];
     const int x = key_x(k) + L.minBX, y = key_y(k) + L.minBY;   // level coordinates (:843-844)
-    // IC_Angle (:77-104): lane handles u = lane % 32 - 15 (u = 16 unused) on rows
-    // v = lane / 32 + 2q; row 0 feeds m_10 only
+    // IC_Angle (:77-104)
     const uint8_t* center = o.pyr + img * o.pyr_stride + L.off + (size_t)y * L.w + x;
-    const int u = (lane & 31) - 15;
+    const int u = hl - 15;
     int m_01 = 0, m_10 = 0;
+    if (u <= 15) {
+        m_10 = u * center[u];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int v = (lane >> 5) + 2 * q;
-        if (v == 0) {
-            if (u <= 15) m_10 += u * center[u];
-        } else if (u >= -o.umax[v] && u <= o.umax[v]) {
-            const int vp = center[u + v * L.w], vm = center[u - v * L.w];
-            m_01 += v * (vp - vm);
-            m_10 += u * (vp + vm);
+        for (int v = 1; v <= 15; ++v) {
+            if (u >= -o.umax[v] && u <= o.umax[v]) {
+                const int vp = center[u + v * L.w], vm = center[u - v * L.w];
+                m_01 += v * (vp - vm);
+                m_10 += u * (vp + vm);
+            }
         }
     }
-    m_01 = wave_sum(m_01);
-    m_10 = wave_sum(m_10);
+    m_01 = half_sum(m_01);
+    m_10 = half_sum(m_10);
     const float ang = fast_atan2((float)m_01, (float)m_10);
     // computeOrbDescriptor (:108-148) on the blurred level, O5
     const float factorPI = (float)(M_PI / 180.f);
@@ -884,18 +886,18 @@ __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keyp
     const float ca = (float)det_cos((double)a_), sa = (float)det_sin((double)a_);
     const uint8_t* B = o.blur + img * o.blur_stride + L.off + (size_t)y * L.w + x;
     const size_t q = (size_t)img * kp_cap + t;
-    unsigned long long* dd = reinterpret_cast<unsigned long long*>(desc + 32 * q);
+    uint32_t* dd = reinterpret_cast<uint32_t*>(desc + 32 * q);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int bit = 64 * w + lane;
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w + hl;
         const int px0 = c_orb_pattern[4 * bit], py0 = c_orb_pattern[4 * bit + 1];
         const int px1 = c_orb_pattern[4 * bit + 2], py1 = c_orb_pattern[4 * bit + 3];
         const int t0 = B[__float2int_rn(px0 * sa + py0 * ca) * L.w + __float2int_rn(px0 * ca - py0 * sa)];
         const int t1 = B[__float2int_rn(px1 * sa + py1 * ca) * L.w + __float2int_rn(px1 * ca - py1 * sa)];
         const unsigned long long m = __ballot(t0 < t1);
-        if (lane == w) dd[w] = m;
+        if (valid && hl == w) dd[w] = (uint32_t)(m >> (32 * half));
     }
-    if (lane == 0) {
+    if (valid && hl == 0) {
         // keypoint coordinates scaled to level 0 (:1094-1101)
         float fx = (float)x, fy = (float)y;
         if (l != 0) { fx = fx * L.scale; fy = fy * L.scale; }
@@ -904,7 +906,6 @@ __global__ void __launch_bounds__(256) k_orb_describe(OrbDev o, int n, gfpl_keyp
         if (resp_out) resp_out[q] = (float)key_s(k);
     }
 }
-
 
 }  // namespace gfpl
 
@@ -1177,7 +1178,7 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     const size_t lds = orb_octree_lds(d.node_cap, d.key_lds);
     hipLaunchKernelGGL(k_orb_octree, dim3(n * d.nlevels), dim3(64), lds, s, d);
     const int max_tot = d.sel_cap * d.nlevels;
-    hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 3) / 4, n), dim3(256), 0, s, d, n, kps,
+    hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 7) / 8, n), dim3(256), 0, s, d, n, kps,
                        desc, n_kp, angle, response, o->kp_cap);
     ORB_HIPCHK(hipGetLastError());
     int err = 0;
