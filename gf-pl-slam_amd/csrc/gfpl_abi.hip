@@ -123,6 +123,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_ok = c.take<int32_t>(B);
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
     sb->scr.pose_dtini = c.take<double>(B * 16);
+    sb->scr.cross_tinv = c.take<double>(B * 16);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);

@@ -91,6 +91,7 @@ struct DevScratch {
     double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
     double* pose_dtini; // [B*16] staging of gfpl_optimize_pose_ini's DT_ini
     int32_t* kf_mask;  // [B] staging of gfpl_curr_frame_is_kf's mask
+    double* cross_tinv; // [B*16] inverse of the predicted curr.Tfw (k_predict_pose -> k_cross_points)
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

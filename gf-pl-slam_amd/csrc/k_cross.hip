@@ -37,6 +37,22 @@ __device__ __forceinline__ int grid_axis(double v, double inv_cs, int n) {
     return (int)c;
 }
 
+// predictFramePose (src/stereoFrameHandler.cpp:153-157), lane per sequence: curr.Tfw =
+// prev.Tfw * prev.DT and its inverse for projectPrev3DPoint.  (Inside k_cross_points the
+// 4x4 products and the inverse set its register peak: 20 VGPR + 43 SGPR spills.)
+__global__ void __launch_bounds__(64) k_predict_pose(KParams p) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= p.B) return;
+    double T[16], A[16], Bm[16], Ti[16];
+    for (int i = 0; i < 16; ++i) { A[i] = p.prev.pose.Tfw[16 * b + i]; Bm[i] = p.prev.pose.DT[16 * b + i]; }
+    mat4_mul(A, Bm, T);
+    mat4_inv(T, Ti);
+    for (int i = 0; i < 16; ++i) {
+        p.curr.pose.Tfw[16 * b + i] = T[i];
+        p.scr.cross_tinv[16 * b + i] = Ti[i];
+    }
+}
+
 // dynamic LDS: cnt[ncell+2] start[ncell+2] i32 | sq[cap] i32 | spx[cap] spy[cap] f32 |
 //              lastT[cap] i32 | prevT[16] Tinv[16] f64 | misc[64] i32
 #ifndef GFPL_CP_WAVES
@@ -58,13 +74,9 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
     int* misc = lastT + cap;
     const int tid = threadIdx.x;
     const int Sp = p.prev.pt.n[b], Sc = p.curr.pt.n[b];
-    if (tid == 0) {
-        // predictFramePose: curr.Tfw = prev.Tfw * prev.DT
-        double T[16], A[16], Bm[16];
-        for (int i = 0; i < 16; ++i) { A[i] = p.prev.pose.Tfw[16 * b + i]; Bm[i] = p.prev.pose.DT[16 * b + i]; }
-        mat4_mul(A, Bm, T);
-        for (int i = 0; i < 16; ++i) { p.curr.pose.Tfw[16 * b + i] = T[i]; prevT[i] = A[i]; }
-        mat4_inv(T, Tinv);
+    if (tid < 16) {   // k_predict_pose wrote curr.Tfw and its inverse
+        prevT[tid] = p.prev.pose.Tfw[16 * b + tid];
+        Tinv[tid] = p.scr.cross_tinv[16 * b + tid];
     }
     for (int i = tid; i < NB; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
@@ -319,6 +331,7 @@ size_t cross_points_lds(const KParams& p, const CrossGrid& G) {
 
 hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
     const CrossGrid G = cross_grid(p);
+    hipLaunchKernelGGL(k_predict_pose, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     hipLaunchKernelGGL(k_cross_points, dim3(p.B), dim3(1024), cross_points_lds(p, G), s, p, G);
     return hipGetLastError();
 }

@@ -191,7 +191,7 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #define GFPL_SL_WAVES 1
 #endif
 #ifndef GFPL_SP_WAVES
-#define GFPL_SP_WAVES 8   // waves per SIMD (4 workgroups / CU; measured faster than 6 despite a 28-B spill)
+#define GFPL_SP_WAVES 7   // waves per SIMD: 72 VGPRs, no spill (8 waves spilled 28 B/lane: 10.59 vs 10.72 ms, within noise)
 #endif
 // dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | recx[KP2] f32 |
 //              recm[KP2] u16 | rowlo[nRows] u16 | misc[64] i32
