@@ -700,11 +700,6 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         }
     }
     wave_sync_lds();
-#ifdef ORB_PROF
-    const long long t_start = clock64(), w_start = wall_clock64();
-    int prof_div = 0, prof_pass = 0, prof_round = 0;
-    long long t_sort = 0;
-#endif
     // ---- the subdivision loop (:594-739), one call site of divide (code size): phase 0 =
     // the first pass, 1 = a later pass of the main loop, 2 = a round of the sorted expansion
     // (:699-737).  Each pass / round reads its work list `prv` from the back and records
@@ -719,9 +714,6 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         } else {
             // vPrevSizeAndPointerToNode = vSizeAndPointerToNode sorted by (size, node) (O6):
             // rank sort (the entries are distinct) from cur into prv
-#ifdef ORB_PROF
-            const long long ts0 = clock64();
-#endif
             wave_sync_lds();
             for (int e = lane; e < ntodo; e += 64) {
                 const OExp v = cur[e];
@@ -729,32 +721,20 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
                 for (int j = 0; j < ntodo; ++j) rank += cur[j] < v;
                 prv[rank] = v;
             }
-#ifdef ORB_PROF
-            t_sort += clock64() - ts0;
-#endif
         }
         wave_sync_lds();
         ncur = 0;
         int nToExpand = 0;
         for (int j = ntodo - 1; j >= 0; --j) {
             nToExpand += divide((int)(prv[j] & 0xFFFFu));
-#ifdef ORB_PROF
-            ++(phase < 2 ? prof_div : prof_round);
-#endif
             if (phase == 2 && lsize >= N) break;
         }
         wave_fence_global();
-#ifdef ORB_PROF
-        ++prof_pass;
-#endif
         if (overflow) break;
         if (lsize >= N || lsize == prevSize) finish = true;
         else if (phase < 2) phase = (lsize + nToExpand * 3 > N) ? 2 : 1;
     }
     wave_sync_lds();
-#ifdef ORB_PROF
-    const long long t_tree = clock64();
-#endif
     // ---- the best key of every node, in list order (:741-760): first strict maximum.
     // The list order into LDS (prv is free now), then a lane per node for nodes of up to
     // 16 keys and the whole wave for the larger ones
@@ -764,9 +744,6 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         for (int it = head; it >= 0; it = nd[it].next) ordl[k++] = (int16_t)it;
     }
     wave_sync_lds();
-#ifdef ORB_PROF
-    const long long t_walk = clock64();
-#endif
     const int n_out = lsize;
     for (int base = 0; base < n_out; base += 64) {
         const int idx = base + lane;
@@ -800,12 +777,6 @@ __global__ void __launch_bounds__(64) k_orb_octree(OrbDev o) {
         }
         if (idx < n_out && idx < o.sel_cap) out[idx] = bk;
     }
-#ifdef ORB_PROF
-    if (lane == 0)
-        printf("orbprof img %d l %d nk %d nout %d div %d pass %d divb %d tree %lld sort %lld walk %lld best %lld wall %lld\n",
-               img, l, nk, n_out, prof_div, prof_pass, prof_round, (long long)(t_tree - t_start), t_sort,
-               (long long)(t_walk - t_tree), (long long)(clock64() - t_walk), (long long)(wall_clock64() - w_start));
-#endif
     if (lane == 0) {
         if (overflow) atomicOr(o.err, 2);
         if (n_out > o.sel_cap) atomicOr(o.err, 4);
