@@ -301,6 +301,9 @@ def hiplib() -> C.CDLL:
             "gfpl_orb_destroy": ([P], C.c_int),
             "gfpl_orb_pyramid_bytes": ([P, P], C.c_int),
             "gfpl_orb_extract": ([P, P, C.c_int, P, P, P, P, P, P, C.c_int64], C.c_int),
+            "gfpl_lbd_create": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_lbd_destroy": ([P], C.c_int),
+            "gfpl_lbd_compute": ([P, P, C.c_int, P, P, P], C.c_int),
         }
         for n, (a, r) in sigs.items():
             try:
@@ -917,6 +920,70 @@ class ORBextractor:
     def close(self):
         if getattr(self, "h", None):
             self.L.gfpl_orb_destroy(self.h)
+            self.h = None
+        if getattr(self, "_own", None):
+            self.L.gfpl_destroy(self._own)
+            self._own = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BinaryDescriptor:
+    """line_descriptor::BinaryDescriptor on the GPU, the compute() path StereoFrame uses
+    (3rdparty/line_descriptor/src/binary_descriptor_custom.cpp:539-687; computeLBD
+    :1026-1372): 32-byte LBD descriptors of octave-0 keylines (Config::lsdOctaveNum = 1)
+    for images of one size.  compute() takes one host image like the reference;
+    compute_batch() device buffers (the product path's form)."""
+
+    def __init__(self, width: int, height: int, max_images: int = 1, kl_cap: int = 512,
+                 ctx: Optional[Context] = None, device: int = 0):
+        self.L = hiplib()
+        self.width, self.height, self.max_images, self.kl_cap = width, height, max_images, kl_cap
+        self._own = None
+        if ctx is None:
+            h = C.c_void_p()
+            check(self.L.gfpl_create(device, None, C.byref(h)), "gfpl_create")
+            self._own = h
+            ch = h
+        else:
+            ch = ctx.h
+        self._ctx = ctx
+        o = C.c_void_p()
+        check(self.L.gfpl_lbd_create(ch, width, height, max_images, kl_cap, C.byref(o)), "lbd_create")
+        self.h = o
+
+    def compute_batch(self, images_dev, n: int, keylines_dev, n_kl_dev, desc_dev) -> None:
+        check(self.L.gfpl_lbd_compute(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
+                                      _ptr(desc_dev)), "lbd_compute")
+
+    def compute(self, image: np.ndarray, keylines: np.ndarray) -> np.ndarray:
+        """compute(image, keylines, descriptors) on one HOST image; keylines: KEYLINE_DT rows.
+        Returns [n][32] u8."""
+        import torch
+        image = np.ascontiguousarray(image, np.uint8)
+        if image.shape != (self.height, self.width):
+            raise ValueError(f"image {image.shape} != ({self.height}, {self.width})")
+        n = len(keylines)
+        if n > self.kl_cap:
+            raise ValueError(f"{n} keylines > kl_cap {self.kl_cap}")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        kl = np.zeros(self.kl_cap, KEYLINE_DT)
+        kl[:n] = keylines
+        d_img = torch.from_numpy(image).to(dev)
+        d_kl = torch.from_numpy(kl.view(np.uint8)).to(dev)
+        d_n = torch.tensor([n], dtype=torch.int32, device=dev)
+        d_desc = torch.zeros(self.kl_cap * DESC, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        self.compute_batch(d_img, 1, d_kl, d_n, d_desc)
+        return d_desc.cpu().numpy().reshape(self.kl_cap, DESC)[:n].copy()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_lbd_destroy(self.h)
             self.h = None
         if getattr(self, "_own", None):
             self.L.gfpl_destroy(self._own)

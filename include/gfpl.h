@@ -344,6 +344,22 @@ int  gfpl_orb_extract(gfpl_orb* orb, const uint8_t* images, int n, gfpl_keypoint
                       uint8_t* desc, int* n_kp, float* angle, float* response,
                       uint8_t* pyramid, int64_t pyr_stride);
 
+/* ---------------------------------------- LBD descriptors (§8(f)2 part) ---- */
+/* line_descriptor::BinaryDescriptor::compute(image, keylines, descriptors)
+ * (3rdparty/line_descriptor/src/binary_descriptor_custom.cpp:539-687, computeLBD :1026-1372)
+ * as StereoFrame::detectLineFeatures calls it (src/stereoFrame.cpp:1194,1220): keylines of
+ * octave 0 (Config::lsdOctaveNum = 1; another octave returns GFPL_E_UNSUPPORTED), images of
+ * width x height (8..8192 px), up to max_images per call, kl_cap keylines per image.
+ * Arithmetic pinned as the CPU oracle's ledger L1-L5.                        */
+typedef struct gfpl_lbd gfpl_lbd;
+int  gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_images, int kl_cap, gfpl_lbd** out);
+int  gfpl_lbd_destroy(gfpl_lbd* lbd);
+/* all pointers DEVICE: images [n][height][width] u8, keylines [n][kl_cap] (sx sy ex ey angle
+ * octave, LSDDetectorC's fields), n_kl [n]; desc [n][kl_cap][32] receives row i of image j's
+ * 32-byte LBD for keyline i < n_kl[j].  Synchronises.                                      */
+int  gfpl_lbd_compute(gfpl_lbd* lbd, const uint8_t* images, int n, const gfpl_keyline* keylines,
+                      const int* n_kl, uint8_t* desc);
+
 /* ------------------------------------------------- keyframe consumers ---- */
 /* One keyframe's stereo features as KeyFrame::stereo_frame exposes them
  * (src/keyFrame.cpp:26-58, include/stereoFrame.h public members): row i of

@@ -68,6 +68,19 @@ int gfplo_orb_blur(const uint8_t* src, int w, int h, uint8_t* dst);             
 int gfplo_orb_fast(const uint8_t* img, int w, int h, int threshold, int cap, float* xy_score);
 float gfplo_fast_atan2(float y, float x);                                                 /* O4 */
 
+/* line_descriptor::BinaryDescriptor::compute(image, keylines, descriptors)
+ * (3rdparty/line_descriptor/src/binary_descriptor_custom.cpp:539-687, computeLBD :1026-1372) for
+ * octave-0 keylines (gfpl_lbd_oracle.cpp; ledger L1-L5): desc [n][32] (nullable), desc_f [n][72]
+ * the float LBD vector before binarisation (nullable). */
+int gfplo_lbd_compute(const uint8_t* image, int width, int height, const gfpl_keyline* kl, int n,
+                      uint8_t* desc, float* desc_f);
+/* the Gaussian-blurred image (L1) and its 16-bit Sobel derivatives (L2); outputs nullable */
+int gfplo_lbd_gradients(const uint8_t* image, int width, int height, uint8_t* blur, int16_t* dx, int16_t* dy);
+/* gaussCoefL_[21], gaussCoefG_[63] as the float values computeLBD uses (L4) */
+int gfplo_lbd_coefs(float* coef_l, float* coef_g);
+/* LSDDetectorC's numOfPixels of a keyline (cv::LineIterator count, 8-connectivity) */
+int gfplo_lbd_num_pixels(const gfpl_keyline* kl, int width, int height);
+
 /* MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:
  * 199-470); same contract as gfpl_kf_common_matches but every pointer of the
  * views and outputs is HOST memory. */

@@ -60,6 +60,10 @@ def lib() -> C.CDLL:
         L.gfplo_orb_blur.argtypes = [P, C.c_int, C.c_int, P]; L.gfplo_orb_blur.restype = C.c_int
         L.gfplo_orb_fast.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, P]; L.gfplo_orb_fast.restype = C.c_int
         L.gfplo_fast_atan2.argtypes = [C.c_float, C.c_float]; L.gfplo_fast_atan2.restype = C.c_float
+        L.gfplo_lbd_compute.argtypes = [P, C.c_int, C.c_int, P, C.c_int, P, P]; L.gfplo_lbd_compute.restype = C.c_int
+        L.gfplo_lbd_gradients.argtypes = [P, C.c_int, C.c_int, P, P, P]; L.gfplo_lbd_gradients.restype = C.c_int
+        L.gfplo_lbd_coefs.argtypes = [P, P]; L.gfplo_lbd_coefs.restype = C.c_int
+        L.gfplo_lbd_num_pixels.argtypes = [P, C.c_int, C.c_int]; L.gfplo_lbd_num_pixels.restype = C.c_int
         _L = L
     return _L
 
@@ -277,3 +281,36 @@ def orb_fast(img: np.ndarray, threshold: int, cap: int = 1 << 16) -> np.ndarray:
 
 def fast_atan2(y: float, x: float) -> float:
     return lib().gfplo_fast_atan2(y, x)
+
+
+# ---- LBD descriptors (gfpl_lbd_oracle.cpp, ledger L1-L5)
+def lbd_compute(image: np.ndarray, keylines: np.ndarray):
+    """BinaryDescriptor::compute on one grey image: (desc [n][32] u8, the float LBD [n][72])."""
+    image = np.ascontiguousarray(image, np.uint8)
+    kl = np.ascontiguousarray(keylines, gfpl.KEYLINE_DT)
+    n = len(kl)
+    d = np.zeros((max(n, 1), 32), np.uint8)
+    f = np.zeros((max(n, 1), 72), np.float32)
+    rc = lib().gfplo_lbd_compute(_p(image), image.shape[1], image.shape[0], _p(kl) if n else None, n, _p(d), _p(f))
+    if rc != 0:
+        raise RuntimeError(f"gfplo_lbd_compute -> {rc}")
+    return d[:n].copy(), f[:n].copy()
+
+
+def lbd_gradients(image: np.ndarray):
+    image = np.ascontiguousarray(image, np.uint8)
+    h, w = image.shape
+    b = np.zeros_like(image); dx = np.zeros((h, w), np.int16); dy = np.zeros((h, w), np.int16)
+    lib().gfplo_lbd_gradients(_p(image), w, h, _p(b), _p(dx), _p(dy))
+    return b, dx, dy
+
+
+def lbd_coefs():
+    cl = np.zeros(21, np.float32); cg = np.zeros(63, np.float32)
+    lib().gfplo_lbd_coefs(_p(cl), _p(cg))
+    return cl, cg
+
+
+def lbd_num_pixels(kl) -> int:
+    k = np.ascontiguousarray(np.asarray(kl, gfpl.KEYLINE_DT).reshape(1))
+    return lib().gfplo_lbd_num_pixels(_p(k), 0, 0)
