@@ -37,8 +37,7 @@ struct LbdDev {
     float coefG[LBD_ROWS];        // gaussCoefG_
     int pairs[32];                // band pair c: i | j << 4
     uint8_t* blur;                // [n][W*H]
-    int16_t* dx;                  // [n][W*H]
-    int16_t* dy;
+    uint32_t* grad;               // [n][W*H] dx (low 16 bits) | dy (high 16 bits)
     int* err;                     // bit 0: a keyline of another octave
 };
 
@@ -117,8 +116,7 @@ __global__ void __launch_bounds__(256) k_lbd_sobel(LbdDev o) {
     const uint8_t* Rp = B + (size_t)yp * o.W;
     const int gx = ((int)Rm[xp] - Rm[xm]) + 2 * ((int)R0[xp] - R0[xm]) + ((int)Rp[xp] - Rp[xm]);
     const int gy = ((int)Rp[xm] - Rm[xm]) + 2 * ((int)Rp[x] - Rm[x]) + ((int)Rp[xp] - Rm[xp]);
-    o.dx[img * npx + (size_t)y * o.W + x] = (int16_t)gx;
-    o.dy[img * npx + (size_t)y * o.W + x] = (int16_t)gy;
+    o.grad[img * npx + (size_t)y * o.W + x] = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
 }
 
 // one wave per keyline; LDS per wave: the 63 rows' eight values, the 72 band statistics
@@ -136,8 +134,7 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
         return;
     }
     const size_t npx = (size_t)o.W * o.H;
-    const int16_t* DX = o.dx + img * npx;
-    const int16_t* DY = o.dy + img * npx;
+    const uint32_t* G = o.grad + img * npx;
     // numOfPixels: cv::LineIterator count of the rounded endpoints (8-connectivity)
     const int ax = __float2int_rn(kl.sx), ay = __float2int_rn(kl.sy);
     const int bx = __float2int_rn(kl.ex), by = __float2int_rn(kl.ey);
@@ -161,12 +158,14 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
     float pl = 0.0f, nl = 0.0f, po = 0.0f, no = 0.0f;
     if (lane < LBD_ROWS) {
         const int iw = o.W - 1, ih = o.H - 1;
+#pragma unroll 4
         for (int w = 0; w < L; ++w) {
             int t = (int)(short)(int)roundf(sX);
             const int xc = t < 0 ? 0 : (t > iw ? iw : t);
             t = (int)(short)(int)roundf(sY);
             const int yc = t < 0 ? 0 : (t > ih ? ih : t);
-            const float dx = (float)DX[(size_t)yc * o.W + xc], dy = (float)DY[(size_t)yc * o.W + xc];
+            const uint32_t g = G[(size_t)yc * o.W + xc];
+            const float dx = (float)(int16_t)(g & 0xFFFFu), dy = (float)(int16_t)(g >> 16);
             const float gDL = dx * dL0 + dy * dL1;
             const float gDO = dx * dO0 + dy * dO1;
             if (gDL > 0) pl += gDL; else nl -= gDL;
@@ -321,12 +320,11 @@ extern "C" int gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_ima
     }
     const size_t npx = (size_t)width * height, M = (size_t)max_images;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_blur = al(M * npx), b_g = al(2 * M * npx);
-    if (hipMalloc(&o->base, b_blur + 2 * b_g + 256) != hipSuccess) { delete o; return GFPL_E_HIP; }
+    const size_t b_blur = al(M * npx), b_g = al(4 * M * npx);
+    if (hipMalloc(&o->base, b_blur + b_g + 256) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
     d.blur = (uint8_t*)p; p += b_blur;
-    d.dx = (int16_t*)p; p += b_g;
-    d.dy = (int16_t*)p; p += b_g;
+    d.grad = (uint32_t*)p; p += b_g;
     d.err = (int*)p;
     *out = o;
     return GFPL_OK;
