@@ -17,7 +17,8 @@ from parity import compare_core, compare_pose, compare_prev_matched, compare_tra
 pytestmark = pytest.mark.gpu
 
 
-def _run_sequence(cam_name, cfg_over, n_seq, n_frames, kp_cap, kl_cap, synth_over=None, seed=1, mutate=None):
+def _run_sequence(cam_name, cfg_over, n_seq, n_frames, kp_cap, kl_cap, synth_over=None, seed=1, mutate=None,
+                  dev_hook=None):
     cfg = gfpl.default_config(**cfg_over)
     cam = gfpl.make_camera(cam_name, cfg)
     sp = gfpl.synth_params(seed=seed, **(synth_over or {}))
@@ -25,6 +26,8 @@ def _run_sequence(cam_name, cfg_over, n_seq, n_frames, kp_cap, kl_cap, synth_ove
     if mutate:
         H = mutate(H)
     D = gfpl.DeviceFrames(H)
+    if dev_hook:
+        dev_hook(cam, H, D)
     ctx = gfpl.Context(cam, cfg)
     g = gfpl.StereoFrameHandler(ctx, n_seq, kp_cap, kl_cap)
     orc = [O.OracleHandler(cam, cfg, kp_cap, kl_cap) for _ in range(n_seq)]

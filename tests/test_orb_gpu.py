@@ -116,3 +116,48 @@ def test_orb_rejects_bad_arguments():
     orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, 640, 480, max_images=1)
     with pytest.raises(gfpl.GfplError):
         orb.extract(None, 2, None, None, None)                # n > max_images
+
+
+def test_orb_pyramid_is_the_trackers_right_pyramid():
+    """The right pyramid the tracker's sub-pixel SAD reads (gfpl_frames.pyr_r) written by
+    gfpl_orb_extract straight into the device frame buffers (no PCIe): the GPU pyramid of
+    each right image equals the oracle's, and tracking on it stays bit-exact with the oracle
+    tracking on the oracle's pyramid."""
+    import torch
+    from test_gpu_parity import _check, _run_sequence
+    seen = {}
+
+    def host_pyr(H):
+        cam = H.cam
+        for f in range(H.F):
+            for b in range(H.B):
+                img = gfpl.synth_image(500 + b, f, cam.width, cam.height)
+                o = O.orb_extract(img, nfeatures=2000, scale_factor=1.2, nlevels=cam.n_levels)
+                pb = int(sum(cam.lvl_cols[l] * cam.lvl_rows[l] for l in range(cam.n_levels)))
+                H.pyr_r[f, b, :pb] = o["pyramid"][:pb]
+        return H
+
+    def dev_hook(cam, H, D):
+        orb = gfpl.ORBextractor(2000, 1.2, cam.n_levels, 20, 7, cam.width, cam.height, max_images=H.B)
+        assert [int(cam.lvl_offset[l]) for l in range(cam.n_levels)] == list(
+            np.cumsum([0] + [cam.lvl_cols[l] * cam.lvl_rows[l] for l in range(cam.n_levels - 1)]))
+        kc = orb.kp_cap
+        dev = torch.device("cuda", 0)
+        kps = torch.zeros(H.B * kc * gfpl.KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+        desc = torch.zeros(H.B * kc * 32, dtype=torch.uint8, device=dev)
+        nkp = torch.zeros(H.B, dtype=torch.int32, device=dev)
+        pb = orb.pyramid_bytes
+        for f in range(H.F):
+            imgs = np.stack([gfpl.synth_image(500 + b, f, cam.width, cam.height) for b in range(H.B)])
+            pyr = D.bufs[12][f]                       # [B * cam.pyr_bytes] device bytes
+            view = pyr.view(H.B, int(cam.pyr_bytes))
+            view[:, :pb] = 0                          # the ORB launch must write every level byte
+            torch.cuda.synchronize()
+            orb.extract(torch.from_numpy(imgs).to(dev), H.B, kps, desc, nkp, None, None, pyr, int(cam.pyr_bytes))
+            got = view[:, :pb].cpu().numpy()
+            assert (got == H.pyr_r[f, :, :pb]).all(), f
+        seen["ok"] = True
+
+    rep = _run_sequence("vga", {}, n_seq=2, n_frames=3, kp_cap=2048, kl_cap=512, mutate=host_pyr, dev_hook=dev_hook)
+    assert seen.get("ok")
+    _check(rep)
