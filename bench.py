@@ -79,6 +79,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=16384, help="sequences per GPU (reduced only if HBM is short)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-detect", action="store_true", help="skip the ORB / LBD detection rates")
     ap.add_argument("--gen-threads", type=int, default=16, help="host threads generating the input frames")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
@@ -299,6 +300,68 @@ def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, 
 
 
 # ----------------------------------------------------------------------- main --
+def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
+    """SURVEY §8(f)1-2 on the bench camera, measured after the timed tracking steps (not part of
+    `value`): ORB extraction (gfpl_orb_extract, nfeatures 2000 / 1.2 / 4 levels / FAST 20-7) and
+    LBD descriptors (gfpl_lbd_compute, 300 octave-0 keylines) over n_img synthetic images resident
+    in HBM, each call synchronised; one image of each checked bit-exact against the oracle."""
+    import torch
+    import gfpl
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    W, H = int(cam.width), int(cam.height)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    imgs = np.stack([gfpl.synth_image(i, i % 7, W, H) for i in range(n_img)])
+    d_img = torch.from_numpy(imgs).to(dev)
+    out = {"images_per_call": n_img, "image": f"{W}x{H}", "data": "synthetic (gfpl_synth_image)"}
+    # ORB
+    orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, W, H, max_images=n_img)
+    kc = orb.kp_cap
+    kps = torch.zeros(n_img * kc * gfpl.KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(n_img * kc * 32, dtype=torch.uint8, device=dev)
+    nkp = torch.zeros(n_img, dtype=torch.int32, device=dev)
+    stride = (orb.pyramid_bytes + 255) // 256 * 256
+    pyr = torch.zeros(n_img * stride, dtype=torch.uint8, device=dev)
+    orb.extract(d_img, n_img, kps, desc, nkp, None, None, pyr, stride)
+    t = []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        orb.extract(d_img, n_img, kps, desc, nkp, None, None, pyr, stride)
+        t.append(time.perf_counter() - t0)
+    o = O.orb_extract(imgs[0], kp_cap=kc)
+    n0 = len(o["kps"])
+    k0 = kps.cpu().numpy().view(gfpl.KEYPOINT_DT)[:n0]
+    d0 = desc.cpu().numpy().reshape(n_img, kc, 32)[0, :n0]
+    out["orb"] = {"images_per_s": n_img / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
+                  "kp_per_image": float(nkp.float().mean().item()),
+                  "parity_image0": bool(int(nkp[0].item()) == n0 and (k0 == o["kps"]).all() and (d0 == o["desc"]).all())}
+    orb.close()
+    # LBD
+    kls = np.stack([gfpl.synth_keylines(n_lines, W, H, 1000 + i, max_len=150.0) for i in range(n_img)])
+    lbd = gfpl.BinaryDescriptor(W, H, max_images=n_img, kl_cap=n_lines)
+    d_kl = torch.from_numpy(np.ascontiguousarray(kls).view(np.uint8).reshape(-1)).to(dev)
+    d_n = torch.full((n_img,), n_lines, dtype=torch.int32, device=dev)
+    d_desc = torch.zeros(n_img * n_lines * 32, dtype=torch.uint8, device=dev)
+    lbd.compute_batch(d_img, n_img, d_kl, d_n, d_desc)
+    t = []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lbd.compute_batch(d_img, n_img, d_kl, d_n, d_desc)
+        t.append(time.perf_counter() - t0)
+    ref, _ = O.lbd_compute(imgs[0], kls[0])
+    out["lbd"] = {"images_per_s": n_img / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
+                  "keylines_per_image": n_lines,
+                  "parity_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
+    lbd.close()
+    # with detection on the GPU a host-fed pipeline uploads the two grey images of a stereo
+    # frame instead of the pyramid + features: the PCIe ceiling derived from the measured rate
+    out["host_fed_images_ceiling"] = {"value": upload_Bps / (2.0 * W * H), "unit": "stereo frames/s",
+                                      "note": "derived: measured upload GB/s / (2 x W x H bytes); LSD stays on the host"}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -468,6 +531,9 @@ def main():
             nt = args.cpu_threads or cores
             cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads, W + K)
         in_bytes = hb.nbytes()
+        det = None
+        if world == 1 and not args.no_detect:
+            det = detection_rates(cam, in_bytes * K / up_total)
         out = {
             "metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)",
             "value": value,
@@ -506,6 +572,7 @@ def main():
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
             "stage_bytes_per_step": {n: int(v) for n, v in zip(STAGES, sb)},
             "cpu_baseline": cpu,
+            "detection": det,
             "gen_s": round(t_gen, 2),
             "lost_sampled": int(lost),
         }

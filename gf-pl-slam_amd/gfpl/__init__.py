@@ -389,6 +389,29 @@ def synth_image(seq: int, frame: int, width: int, height: int, seed: int = 0x6A0
     return out
 
 
+def synth_keylines(n: int, w: int, h: int, seed: int, min_len: float = 2.0, max_len: float = 200.0,
+                   border: bool = False) -> np.ndarray:
+    """n synthetic octave-0 keylines (KEYLINE_DT) inside a w x h image: fractional endpoints,
+    the LSD wrapper's angle = atan2(ey - sy, ex - sx) in float (src/LSDDetector_custom.cpp:285);
+    border=True clamps the far endpoint onto the image edge."""
+    rng = np.random.default_rng(seed)
+    kl = np.zeros(n, KEYLINE_DT)
+    for i in range(n):
+        while True:
+            sx, sy = rng.uniform(0, w - 1), rng.uniform(0, h - 1)
+            a = rng.uniform(-np.pi, np.pi)
+            ln = rng.uniform(min_len, max_len)
+            ex, ey = sx + ln * np.cos(a), sy + ln * np.sin(a)
+            if border:
+                ex, ey = min(max(ex, 0.0), w - 1.0), min(max(ey, 0.0), h - 1.0)
+            if 0 <= ex <= w - 1 and 0 <= ey <= h - 1:
+                break
+        fs, fe = np.float32(sx), np.float32(sy)
+        gx, gy = np.float32(ex), np.float32(ey)
+        kl[i] = (fs, fe, gx, gy, np.arctan2(gy - fe, gx - fs).astype(np.float32), 0)
+    return kl
+
+
 def synth_params(**over) -> SynthParams:
     sp = SynthParams()
     synthlib().gfpl_synth_default(C.byref(sp))
