@@ -103,20 +103,36 @@ __global__ void __launch_bounds__(256) k_lbd_blur(LbdDev o, const uint8_t* image
     }
 }
 
-// L2: dx = [-1 0 1] x [1 2 1]^T, dy its transpose, REFLECT_101
+// L2: dx = [-1 0 1] x [1 2 1]^T, dy its transpose, REFLECT_101; four pixels per thread
+// (six bytes of each of the three rows), one 16-B store when the row allows it
 __global__ void __launch_bounds__(256) k_lbd_sobel(LbdDev o) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, img = blockIdx.z;
-    if (x >= o.W) return;
+    const int x0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x), y = blockIdx.y, img = blockIdx.z;
+    if (x0 >= o.W) return;
     const size_t npx = (size_t)o.W * o.H;
     const uint8_t* B = o.blur + img * npx;
-    const int xm = refl1(x - 1, o.W), xp = refl1(x + 1, o.W);
     const int ym = refl1(y - 1, o.H), yp = refl1(y + 1, o.H);
-    const uint8_t* Rm = B + (size_t)ym * o.W;
-    const uint8_t* R0 = B + (size_t)y * o.W;
-    const uint8_t* Rp = B + (size_t)yp * o.W;
-    const int gx = ((int)Rm[xp] - Rm[xm]) + 2 * ((int)R0[xp] - R0[xm]) + ((int)Rp[xp] - Rp[xm]);
-    const int gy = ((int)Rp[xm] - Rm[xm]) + 2 * ((int)Rp[x] - Rm[x]) + ((int)Rp[xp] - Rm[xp]);
-    o.grad[img * npx + (size_t)y * o.W + x] = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
+    const uint8_t* R[3] = {B + (size_t)ym * o.W, B + (size_t)y * o.W, B + (size_t)yp * o.W};
+    int v[3][6];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[r][i] = R[r][refl1(min(x0 - 1 + i, o.W), o.W)];
+    uint32_t g[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // pixel x0 + i: columns i (x - 1), i + 1 (x), i + 2 (x + 1)
+        const int gx = (v[0][i + 2] - v[0][i]) + 2 * (v[1][i + 2] - v[1][i]) + (v[2][i + 2] - v[2][i]);
+        const int gy = (v[2][i] - v[0][i]) + 2 * (v[2][i + 1] - v[0][i + 1]) + (v[2][i + 2] - v[0][i + 2]);
+        g[i] = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
+    }
+    uint32_t* D = o.grad + img * npx + (size_t)y * o.W + x0;
+    if ((o.W & 3) == 0) {
+        *reinterpret_cast<uint4*>(D) = make_uint4(g[0], g[1], g[2], g[3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (x0 + i < o.W) D[i] = g[i];
+    }
 }
 
 // one wave per keyline; LDS per wave: the 63 rows' eight values, the 72 band statistics
@@ -346,7 +362,7 @@ extern "C" int gfpl_lbd_compute(gfpl_lbd* o, const uint8_t* images, int n, const
     if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
     hipLaunchKernelGGL(k_lbd_blur, dim3((d.W + LBD_TW - 1) / LBD_TW, (d.H + LBD_TH - 1) / LBD_TH, n), dim3(256), 0, s, d,
                        images);
-    hipLaunchKernelGGL(k_lbd_sobel, dim3((d.W + 255) / 256, d.H, n), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_lbd_sobel, dim3((d.W + 1023) / 1024, d.H, n), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_lbd_describe, dim3((d.kl_cap + 3) / 4, n), dim3(256), 0, s, d, keylines, n_kl, desc);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
     int err = 0;
