@@ -2,7 +2,8 @@
 // operator() (src/ORBextractor.cc:1043-1105) over a batch of grey images resident in HBM,
 // with the arithmetic of the OpenCV calls it makes pinned as in the CPU oracle (ledger
 // O1-O7, oracle/gfpl_orb_oracle.cpp).  Kernels, per launch over all images:
-//  k_orb_copy0    level 0 of the pyramid = the image
+//  k_orb_copy0    level 0 of the pyramid = the image (the pyramid is the caller's array
+//                 when it asks for one, so the levels never need a second copy)
 //  k_orb_resize   level l from level l-1: cv::resize INTER_LINEAR fixed point (O1)
 //                 (ComputePyramid :1107-1132), coefficient tables built on the host
 //  k_orb_blur     GaussianBlur 7x7 sigma 2 REFLECT_101 fixed point (O2) of every level,
@@ -14,9 +15,10 @@
 //  k_orb_gather   one workgroup per (image, level): the cells' keys concatenated in cell
 //                 order = vToDistributeKeys
 //  k_orb_octree   one wave per (image, level): DistributeOctTree (:539-763) with the
-//                 node list in LDS (the reference's list order, O6 for ties) and every
-//                 DivideNode a wave-parallel stable 4-way partition of the node's keys
-//  k_orb_describe one thread per kept keypoint: IC_Angle (:77-104, O4), rBRIEF on the
+//                 node list in LDS (the reference's list order, O6 for ties), the list
+//                 bookkeeping in wave-uniform registers and every DivideNode a
+//                 wave-parallel stable 4-way partition of the node's keys
+//  k_orb_describe two kept keypoints per wave: IC_Angle (:77-104, O4), rBRIEF on the
 //                 blurred level (:108-148, O5), the level scale (:1094-1101), output in
 //                 the reference's order (level by level, node-list order)
 #include <hip/hip_runtime.h>
@@ -1066,7 +1068,7 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
             beta_h.push_back(sat_short(fy * 2048));
         }
     }
-    // one allocation: tables | pyr | blur | s_ini | s_min | keys | tmp | nkeys | sel | nsel | err
+    // one allocation: tables | pyr | blur | keys | tmp | nkeys | nsel | sel | ckeys | ccnt | err
     const long long M = max_images;
     auto al = [](long long v) { return (v + 255) & ~255LL; };
     const long long b_x = al(4 * (long long)xofs_h.size() + 4), b_a = al(2 * (long long)alpha_h.size() + 4);
