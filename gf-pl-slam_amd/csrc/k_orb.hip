@@ -1068,7 +1068,7 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
             beta_h.push_back(sat_short(fy * 2048));
         }
     }
-    // one allocation: tables | pyr | blur | keys | tmp | nkeys | nsel | sel | ckeys | ccnt | err
+    // one allocation: tables | pyr | blur | ckeys | ccnt | keys | tmp | nkeys | nsel | sel | err
     const long long M = max_images;
     auto al = [](long long v) { return (v + 255) & ~255LL; };
     const long long b_x = al(4 * (long long)xofs_h.size() + 4), b_a = al(2 * (long long)alpha_h.size() + 4);
