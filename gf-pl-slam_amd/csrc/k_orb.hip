@@ -118,24 +118,56 @@ __global__ void k_orb_copy0(OrbDev o, const uint8_t* images, int n) {
 }
 
 // O1: dst(x, y) = ((h(y0, x) b0 + h(y1, x) b1 + 2^21) >> 22), h = exact 11-bit horizontal blend
-__global__ void k_orb_resize(OrbDev o, int l) {
-    const OrbLevel& d = o.lv[l];
-    const OrbLevel& s = o.lv[l - 1];
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    const int img = blockIdx.z;
-    if (x >= d.w) return;
-    const uint8_t* S = o.pyr + img * o.pyr_stride + s.off;
-    const int sy = o.yofs[l][y];
-    const int r0 = min(max(sy, 0), s.h - 1), r1 = min(max(sy + 1, 0), s.h - 1);
-    const int sx = o.xofs[l][x];
-    const int a0 = o.alpha[l][2 * x], a1 = o.alpha[l][2 * x + 1];
-    const bool blend = x < o.xmax[l];
-    const uint8_t* R0 = S + (size_t)r0 * s.w;
-    const uint8_t* R1 = S + (size_t)r1 * s.w;
+__device__ __forceinline__ uint32_t resize_px(const uint8_t* R0, const uint8_t* R1, int sx, uint32_t al, bool blend,
+                                              int b0, int b1) {
+    const int a0 = (int16_t)(al & 0xFFFFu), a1 = (int16_t)(al >> 16);
     const int h0 = blend ? R0[sx] * a0 + R0[sx + 1] * a1 : R0[sx] * 2048;
     const int h1 = blend ? R1[sx] * a0 + R1[sx + 1] * a1 : R1[sx] * 2048;
-    const int b0 = o.beta[l][2 * y], b1 = o.beta[l][2 * y + 1];
-    o.pyr[img * o.pyr_stride + d.off + (size_t)y * d.w + x] = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+    return sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+}
+// RESIZE_ROWS output rows per workgroup (one pixel per thread and one row per workgroup was
+// bound by the workgroup launch rate: 1.2 M workgroups a level at 1024 VGA images).  A row
+// is split into units: its unaligned head bytes (k = -1), 4-px dwords at 4-B aligned
+// addresses (one store each), its tail bytes; the threads stride over (row, unit) pairs.
+#define RESIZE_ROWS 16
+__global__ void __launch_bounds__(256) k_orb_resize(OrbDev o, int l) {
+    const OrbLevel& d = o.lv[l];
+    const OrbLevel& s = o.lv[l - 1];
+    const int img = blockIdx.y;
+    const uint8_t* S = o.pyr + img * o.pyr_stride + s.off;
+    uint8_t* Dl = o.pyr + img * o.pyr_stride + d.off;
+    const int* xofs = o.xofs[l];
+    const uint32_t* al = reinterpret_cast<const uint32_t*>(o.alpha[l]);   // (alpha0, alpha1) int16 pairs
+    const int xmax = o.xmax[l];
+    const int y0 = blockIdx.x * RESIZE_ROWS;
+    const int nr = min(RESIZE_ROWS, d.h - y0);
+    const int U = (d.w >> 2) + 2;   // units of a row: k = -1 .. w / 4
+    for (int i = threadIdx.x; i < nr * U; i += blockDim.x) {
+        const int r = i / U, k = i - r * U - 1;
+        const int y = y0 + r;
+        uint8_t* D = Dl + (size_t)y * d.w;
+        const int lead = (int)((4u - ((uint32_t)(uintptr_t)D & 3u)) & 3u);
+        const int nd = (d.w - lead) >> 2;
+        if (k > nd) continue;
+        const int sy = o.yofs[l][y];
+        const uint8_t* R0 = S + (size_t)min(max(sy, 0), s.h - 1) * s.w;
+        const uint8_t* R1 = S + (size_t)min(max(sy + 1, 0), s.h - 1) * s.w;
+        const int b0 = o.beta[l][2 * y], b1 = o.beta[l][2 * y + 1];
+        if (k < 0 || k == nd) {   // the row's bytes before its first / after its last aligned dword
+            const int xa = k < 0 ? 0 : lead + 4 * nd, xb = k < 0 ? lead : d.w;
+            for (int x = xa; x < xb; ++x) D[x] = (uint8_t)resize_px(R0, R1, xofs[x], al[x], x < xmax, b0, b1);
+        } else {
+            const int x = lead + 4 * k;
+            uint32_t q[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = resize_px(R0, R1, xofs[x + i], al[x + i], x + i < xmax, b0, b1);
+            // packed with v_perm: the shift-or form was selected as v_ashr_pk_u8_i32, whose
+            // result's upper half then leaked into bytes 2-3 (measured wrong on gfx950)
+            const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0C0C0400u);
+            const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x0C0C0400u);
+            *reinterpret_cast<uint32_t*>(D + x) = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+        }
+    }
 }
 
 // O2: 7x7 Gaussian, 8-bit integer taps, rows exact, columns (s + 2^15) >> 16.  One 64x32
@@ -1141,7 +1173,7 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     ORB_HIPCHK(hipMemsetAsync(d.err, 0, 4, s));
     hipLaunchKernelGGL(k_orb_copy0, dim3(128, n), dim3(256), 0, s, d, images, n);
     for (int l = 1; l < d.nlevels; ++l)
-        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].w + 255) / 256, d.lv[l].h, n), dim3(256), 0, s, d, l);
+        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].h + RESIZE_ROWS - 1) / RESIZE_ROWS, n), dim3(256), 0, s, d, l);
     const OrbLevel& L0 = d.lv[0];
     hipLaunchKernelGGL(k_orb_blur, dim3((L0.w + BLUR_TW - 1) / BLUR_TW, (L0.h + BLUR_TH - 1) / BLUR_TH, n * d.nlevels),
                        dim3(256), 0, s, d);

@@ -1,0 +1,145 @@
+"""Images -> detection -> tracking on one device (SURVEY.md §8(f)1-2 feeding rows a-e).
+
+StereoFrame's detectFeatures (src/stereoFrame.cpp:1145-1200) runs ORB_SLAM2::ORBextractor on
+both images and BinaryDescriptor::compute on the LSD keylines of both; here both run on the
+GPU (gfpl_orb_extract, gfpl_lbd_compute) straight into the device buffers a gfpl_frames view
+points at — keypoints, descriptors, the right pyramid for the sub-pixel SAD — so the tracker
+(StereoFrameHandler) reads them without a copy.  LSD line detection stays on the host: the
+keylines are an input.
+
+The synthetic scene helper renders what a calibrated rig would see while translating along
+x over a fronto-parallel textured plane: every pixel has the same disparity, the right image is
+the left one shifted by it, and each frame shifts the view by a fixed number of pixels.
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+
+from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, ORBextractor, make_frames, synth_image,
+               synth_keylines)
+
+
+@functools.lru_cache(maxsize=4096)
+def _plane(seq: int, base_w: int, height: int, n_segs: int):
+    base = synth_image(0xB45E + seq, 0, base_w, height)
+    base.setflags(write=False)
+    segs = synth_keylines(n_segs, base_w, height, 0x5E65 + seq, min_len=8.0, max_len=120.0)
+    segs.setflags(write=False)
+    return base, segs
+
+
+def synth_stereo_scene(seq: int, frame: int, width: int, height: int, disparity: int = 12, step_px: int = 2,
+                       n_lines: int = 300, frames: int = 64):
+    """Left / right grey images of a textured plane seen from a camera translating along x
+    (every frame `step_px` pixels), and the plane's line segments as keylines in both images
+    (those leaving the view dropped).  Returns (left, right, kl_left, kl_right)."""
+    base_w = width + disparity + step_px * frames + 8
+    base, segs = _plane(seq, base_w, height, n_lines * 3)
+    off = step_px * frame
+    left = np.ascontiguousarray(base[:, off:off + width])
+    right = np.ascontiguousarray(base[:, off + disparity:off + disparity + width])
+    def view(shift):
+        k = segs.copy()
+        k["sx"] -= shift
+        k["ex"] -= shift
+        inside = (k["sx"] >= 0) & (k["ex"] >= 0) & (k["sx"] <= width - 1) & (k["ex"] <= width - 1)
+        return k[inside]
+
+    kl_l, kl_r = view(off), view(off + disparity)
+    # the same plane segments on both sides, LSD's cap (Config::lsdNFeatures) on the left count
+    return left, right, kl_l[:n_lines], kl_r[:n_lines]
+
+
+def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparities=(2, 12, 20, 8), band: int = 96,
+                       n_lines: int = 300, frames: int = 64):
+    """A staircase of fronto-parallel textured bands (world columns [band i, band (i+1)) at
+    disparity disparities[i % len]) seen from a camera translating along x by half a baseline
+    per frame: band b moves d_b / 2 px per frame in the left image and sits d_b px further
+    left in the right one; nearer bands occlude farther ones, and columns no band covers show
+    the farthest band's texture.  Unlike the single plane, the depth spread keeps the pose
+    information of the lines well conditioned (the single plane couples rotation and
+    translation, and the line cut then takes the reference's exact step at every step).
+    Keylines are the plane segments lying inside one band, shifted per view and kept when both
+    endpoints stay in the image.  Returns (left, right, kl_left, kl_right)."""
+    ds = [int(d) for d in disparities]
+    assert all(d % 2 == 0 and d > 0 for d in ds)
+    dmax = max(ds)
+    base_w = width + dmax * (frames // 2 + 1) + band
+    base, segs = _plane(seq, base_w, height, n_lines * 6)
+    n_band = (base_w + band - 1) // band
+    disp = [ds[i % len(ds)] for i in range(n_band)]
+    far = min(ds)
+    views = []
+    for side in range(2):
+        shift = lambda d: (frame * d) // 2 + (d if side else 0)
+        img = np.ascontiguousarray(base[:, shift(far):shift(far) + width])   # the far layer
+        for i in sorted(range(n_band), key=lambda i: disp[i]):   # far to near: near bands occlude
+            u0, u1 = i * band, min((i + 1) * band, base_w)
+            x0, x1 = u0 - shift(disp[i]), u1 - shift(disp[i])
+            c0, c1 = max(x0, 0), min(x1, width)
+            if c0 < c1:
+                img[:, c0:c1] = base[:, u0 + (c0 - x0):u0 + (c1 - x0)]
+        views.append(img)
+    bi = np.floor(segs["sx"] / band).astype(np.int64)
+    same = (bi == np.floor(segs["ex"] / band).astype(np.int64))
+    inner = (np.minimum(segs["sx"], segs["ex"]) >= bi * band + 2) & (np.maximum(segs["sx"], segs["ex"]) <= (bi + 1) * band - 3)
+    pool = segs[same & inner]
+    d_of = np.array(disp, np.int64)[np.floor(pool["sx"] / band).astype(np.int64)]
+    kls = []
+    for side in range(2):
+        k = pool.copy()
+        sh = ((frame * d_of) // 2 + (d_of if side else 0)).astype(np.float32)
+        k["sx"] -= sh
+        k["ex"] -= sh
+        kls.append(k)
+    inside = np.ones(len(pool), bool)
+    for k in kls:
+        inside &= (k["sx"] >= 0) & (k["ex"] >= 0) & (k["sx"] <= width - 1) & (k["ex"] <= width - 1)
+    return views[0], views[1], kls[0][inside][:n_lines], kls[1][inside][:n_lines]
+
+
+class ImagePipeline:
+    """Detection for B sequences on the device, as gfpl_frames for StereoFrameHandler:
+    ORB (nfeatures, scale 1.2, the camera's levels, FAST 20 / 7) and LBD of given keylines."""
+
+    def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000):
+        import torch
+        self.cam, self.B, self.kl_cap = cam, batch, kl_cap
+        W, H = int(cam.width), int(cam.height)
+        self.orb = ORBextractor(nfeatures, 1.2, int(cam.n_levels), 20, 7, W, H, max_images=batch, ctx=ctx)
+        self.lbd = BinaryDescriptor(W, H, max_images=batch, kl_cap=kl_cap, ctx=ctx)
+        self.kp_cap = self.orb.kp_cap
+        dev = torch.device("cuda", torch.cuda.current_device())
+        B, kc = batch, self.kp_cap
+        z = lambda n, dt=torch.uint8: torch.zeros(n, dtype=dt, device=dev)
+        self.n_kp = [z(B, torch.int32), z(B, torch.int32)]
+        self.kps = [z(B * kc * KEYPOINT_DT.itemsize), z(B * kc * KEYPOINT_DT.itemsize)]
+        self.pdesc = [z(B * kc * DESC), z(B * kc * DESC)]
+        self.n_kl = [z(B, torch.int32), z(B, torch.int32)]
+        self.kl = [z(B * kl_cap * KEYLINE_DT.itemsize), z(B * kl_cap * KEYLINE_DT.itemsize)]
+        self.ldesc = [z(B * kl_cap * DESC), z(B * kl_cap * DESC)]
+        self.pyr_l = z(B * int(cam.pyr_bytes))   # the left pyramid (not read by the tracker)
+        self.pyr_r = z(B * int(cam.pyr_bytes))
+        self.ts = torch.zeros(B, dtype=torch.float64, device=dev)
+
+    def detect(self, left, right, kl_left, n_kl_left, kl_right, n_kl_right, time_stamp):
+        """left / right: device u8 [B][H][W]; kl_*: device KEYLINE_DT rows [B][kl_cap];
+        n_kl_*: device int32 [B]; time_stamp: device f64 [B].  Returns the gfpl_frames."""
+        B, pb = self.B, int(self.cam.pyr_bytes)
+        for side, img in ((0, left), (1, right)):
+            pyr = self.pyr_l if side == 0 else self.pyr_r
+            self.orb.extract(img, B, self.kps[side], self.pdesc[side], self.n_kp[side], None, None, pyr, pb)
+        for side, (kl, n) in enumerate(((kl_left, n_kl_left), (kl_right, n_kl_right))):
+            self.kl[side].copy_(kl.view(-1))
+            self.n_kl[side].copy_(n)
+            self.lbd.compute_batch(left if side == 0 else right, B, self.kl[side], self.n_kl[side], self.ldesc[side])
+        self.ts.copy_(time_stamp)
+        arrs = [self.n_kp[0], self.n_kp[1], self.kps[0], self.kps[1], self.pdesc[0], self.pdesc[1],
+                self.n_kl[0], self.n_kl[1], self.kl[0], self.kl[1], self.ldesc[0], self.ldesc[1], self.pyr_r, self.ts]
+        return make_frames(B, self.kp_cap, self.kl_cap, arrs)
+
+    def close(self):
+        self.orb.close()
+        self.lbd.close()
