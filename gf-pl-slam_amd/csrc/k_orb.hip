@@ -118,54 +118,113 @@ __global__ void k_orb_copy0(OrbDev o, const uint8_t* images, int n) {
 }
 
 // O1: dst(x, y) = ((h(y0, x) b0 + h(y1, x) b1 + 2^21) >> 22), h = exact 11-bit horizontal blend
-__device__ __forceinline__ uint32_t resize_px(const uint8_t* R0, const uint8_t* R1, int sx, uint32_t al, bool blend,
-                                              int b0, int b1) {
+// RESIZE_ROWS output rows per workgroup, in three phases through LDS:
+//  1. the source rows they read (yofs of the first row .. of the last + 1) with aligned dword
+//     loads (a row's bytes start at its address & 3 in its LDS row);
+//  2. per 4-px column unit, the x tables loaded once, every output row's 4 px from the LDS
+//     source bytes into an LDS output row as one dword;
+//  3. each output row stored as dwords at 4-B aligned addresses (two LDS dwords funnel-shifted
+//     by the row's misalignment), its unaligned head / tail bytes one by one.
+// (One pixel per thread from global bytes ran 171 us per level at 256 VGA images.)
+#define RESIZE_ROWS 16
+#define RESIZE_T 128
+__device__ __forceinline__ uint32_t resize_lds_px(const uint8_t* L0, const uint8_t* L1, int sx, uint32_t al, bool blend,
+                                                  int b0, int b1) {
     const int a0 = (int16_t)(al & 0xFFFFu), a1 = (int16_t)(al >> 16);
-    const int h0 = blend ? R0[sx] * a0 + R0[sx + 1] * a1 : R0[sx] * 2048;
-    const int h1 = blend ? R1[sx] * a0 + R1[sx + 1] * a1 : R1[sx] * 2048;
+    const int h0 = blend ? L0[sx] * a0 + L0[sx + 1] * a1 : L0[sx] * 2048;
+    const int h1 = blend ? L1[sx] * a0 + L1[sx + 1] * a1 : L1[sx] * 2048;
     return sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
 }
-// RESIZE_ROWS output rows per workgroup (one pixel per thread and one row per workgroup was
-// bound by the workgroup launch rate: 1.2 M workgroups a level at 1024 VGA images).  A row
-// is split into units: its unaligned head bytes (k = -1), 4-px dwords at 4-B aligned
-// addresses (one store each), its tail bytes; the threads stride over (row, unit) pairs.
-#define RESIZE_ROWS 16
-__global__ void __launch_bounds__(256) k_orb_resize(OrbDev o, int l) {
+__global__ void __launch_bounds__(RESIZE_T) k_orb_resize(OrbDev o, int l) {
+    extern __shared__ uint32_t rz_lds[];
     const OrbLevel& d = o.lv[l];
     const OrbLevel& s = o.lv[l - 1];
     const int img = blockIdx.y;
     const uint8_t* S = o.pyr + img * o.pyr_stride + s.off;
     uint8_t* Dl = o.pyr + img * o.pyr_stride + d.off;
+    const int* yofs = o.yofs[l];
+    const int16_t* beta = o.beta[l];
+    const int y0 = blockIdx.x * RESIZE_ROWS;
+    const int nr = min(RESIZE_ROWS, d.h - y0);
+    const int r_lo = min(max(yofs[y0], 0), s.h - 1);
+    const int r_hi = min(max(yofs[y0 + nr - 1] + 1, 0), s.h - 1);
+    const int sdw = (s.w + 6) >> 2;   // dwords per source row (any alignment)
+    const int odw = (d.w >> 2) + 2;   // dwords per output row (+1 for the funnel shift)
+    uint32_t* src = rz_lds;
+    uint32_t* out = rz_lds + (r_hi - r_lo + 1) * sdw;
+    // 1. source rows
+    const int nsrc = (r_hi - r_lo + 1) * sdw;
+    for (int i0 = 0; i0 < nsrc; i0 += 8 * RESIZE_T) {   // eight loads per thread in flight
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * RESIZE_T + threadIdx.x;
+            if (i < nsrc) {
+                const int j = i / sdw, m = i - j * sdw;
+                const uintptr_t row = (uintptr_t)(S + (size_t)(r_lo + j) * s.w);
+                v[u] = reinterpret_cast<const uint32_t*>(row & ~(uintptr_t)3)[m];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * RESIZE_T + threadIdx.x;
+            if (i < nsrc) src[i] = v[u];
+        }
+    }
+    __syncthreads();
+    // 2. 4-px units
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(src);
+    const uint32_t sh0 = (uint32_t)((uintptr_t)(S + (size_t)r_lo * s.w) & 3u);
+    const uint32_t wmod = (uint32_t)s.w & 3u;
     const int* xofs = o.xofs[l];
     const uint32_t* al = reinterpret_cast<const uint32_t*>(o.alpha[l]);   // (alpha0, alpha1) int16 pairs
     const int xmax = o.xmax[l];
-    const int y0 = blockIdx.x * RESIZE_ROWS;
-    const int nr = min(RESIZE_ROWS, d.h - y0);
-    const int U = (d.w >> 2) + 2;   // units of a row: k = -1 .. w / 4
-    for (int i = threadIdx.x; i < nr * U; i += blockDim.x) {
-        const int r = i / U, k = i - r * U - 1;
-        const int y = y0 + r;
-        uint8_t* D = Dl + (size_t)y * d.w;
-        const int lead = (int)((4u - ((uint32_t)(uintptr_t)D & 3u)) & 3u);
-        const int nd = (d.w - lead) >> 2;
-        if (k > nd) continue;
-        const int sy = o.yofs[l][y];
-        const uint8_t* R0 = S + (size_t)min(max(sy, 0), s.h - 1) * s.w;
-        const uint8_t* R1 = S + (size_t)min(max(sy + 1, 0), s.h - 1) * s.w;
-        const int b0 = o.beta[l][2 * y], b1 = o.beta[l][2 * y + 1];
-        if (k < 0 || k == nd) {   // the row's bytes before its first / after its last aligned dword
-            const int xa = k < 0 ? 0 : lead + 4 * nd, xb = k < 0 ? lead : d.w;
-            for (int x = xa; x < xb; ++x) D[x] = (uint8_t)resize_px(R0, R1, xofs[x], al[x], x < xmax, b0, b1);
-        } else {
-            const int x = lead + 4 * k;
+    const int nu = (d.w + 3) >> 2;
+    for (int k = threadIdx.x; k < nu; k += RESIZE_T) {
+        int sx[4];
+        uint32_t a4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int x = min(4 * k + i, d.w - 1);   // a short last unit repeats its last pixel
+            sx[i] = xofs[x];
+            a4[i] = al[x];
+        }
+#pragma unroll 2
+        for (int r = 0; r < nr; ++r) {
+            const int sy = yofs[y0 + r];
+            const int j0 = min(max(sy, 0), s.h - 1) - r_lo, j1 = min(max(sy + 1, 0), s.h - 1) - r_lo;
+            // byte offset of source row j in LDS: its row * 4 sdw + the row address & 3
+            const uint8_t* L0 = sb + j0 * 4 * sdw + ((sh0 + (uint32_t)j0 * wmod) & 3u);
+            const uint8_t* L1 = sb + j1 * 4 * sdw + ((sh0 + (uint32_t)j1 * wmod) & 3u);
+            const int b0 = beta[2 * (y0 + r)], b1 = beta[2 * (y0 + r) + 1];
             uint32_t q[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = resize_px(R0, R1, xofs[x + i], al[x + i], x + i < xmax, b0, b1);
+            for (int i = 0; i < 4; ++i) q[i] = resize_lds_px(L0, L1, sx[i], a4[i], 4 * k + i < xmax, b0, b1);
             // packed with v_perm: the shift-or form was selected as v_ashr_pk_u8_i32, whose
             // result's upper half then leaked into bytes 2-3 (measured wrong on gfx950)
             const uint32_t lo = __builtin_amdgcn_perm(q[1], q[0], 0x0C0C0400u);
             const uint32_t hi = __builtin_amdgcn_perm(q[3], q[2], 0x0C0C0400u);
-            *reinterpret_cast<uint32_t*>(D + x) = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            out[r * odw + k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+        }
+    }
+    __syncthreads();
+    // 3. aligned stores
+    const uint8_t* ob = reinterpret_cast<const uint8_t*>(out);
+    const int U = (d.w >> 2) + 2;   // units of a row: head bytes (k = -1), dwords, tail bytes
+    for (int i = threadIdx.x; i < nr * U; i += RESIZE_T) {
+        const int r = i / U, k = i - r * U - 1;
+        uint8_t* D = Dl + (size_t)(y0 + r) * d.w;
+        const int lead = (int)((4u - ((uint32_t)(uintptr_t)D & 3u)) & 3u);
+        const int nd = (d.w - lead) >> 2;
+        if (k > nd) continue;
+        if (k < 0 || k == nd) {
+            const int xa = k < 0 ? 0 : lead + 4 * nd, xb = k < 0 ? lead : d.w;
+            for (int x = xa; x < xb; ++x) D[x] = ob[4 * r * odw + x];
+        } else {
+            const uint32_t* orow = out + r * odw;
+            const int x = lead + 4 * k;   // bytes x .. x + 3 of the output row
+            *reinterpret_cast<uint32_t*>(D + x) =
+                __builtin_amdgcn_alignbyte(orow[(x >> 2) + 1], orow[x >> 2], (uint32_t)(x & 3));
         }
     }
 }
@@ -925,6 +984,7 @@ struct gfpl_orb {
     OrbDev d{};
     void* base = nullptr;         // one allocation for everything
     long long pyr_bytes = 0;      // used bytes of one pyramid
+    int resize_lds[GFPL_MAX_LEVELS] = {};   // k_orb_resize's LDS bytes per level
 };
 
 namespace {
@@ -1099,7 +1159,21 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
             beta_h.push_back(sat_short((1.f - fy) * 2048));
             beta_h.push_back(sat_short(fy * 2048));
         }
+        // k_orb_resize's LDS: the most source rows a RESIZE_ROWS band reads + its output rows
+        int rows = 1;
+        for (int y0 = 0; y0 < t.h; y0 += RESIZE_ROWS) {
+            const int y1 = std::min(y0 + RESIZE_ROWS, t.h) - 1;
+            const int lo = std::min(std::max(yofs_h[yoff[l] + y0], 0), s.h - 1);
+            const int hi = std::min(std::max(yofs_h[yoff[l] + y1] + 1, 0), s.h - 1);
+            rows = std::max(rows, hi - lo + 1);
+        }
+        o->resize_lds[l] = 4 * (rows * ((s.w + 6) >> 2) + RESIZE_ROWS * ((t.w >> 2) + 2));
     }
+    int rz_max = 0;
+    for (int l = 1; l < d.nlevels; ++l) rz_max = std::max(rz_max, o->resize_lds[l]);
+    if (rz_max > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
+    if (rz_max > 0 && hipFuncSetAttribute((const void*)k_orb_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          rz_max) != hipSuccess) { delete o; return GFPL_E_HIP; }
     // one allocation: tables | pyr | blur | ckeys | ccnt | keys | tmp | nkeys | nsel | sel | err
     const long long M = max_images;
     auto al = [](long long v) { return (v + 255) & ~255LL; };
@@ -1173,7 +1247,8 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     ORB_HIPCHK(hipMemsetAsync(d.err, 0, 4, s));
     hipLaunchKernelGGL(k_orb_copy0, dim3(128, n), dim3(256), 0, s, d, images, n);
     for (int l = 1; l < d.nlevels; ++l)
-        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].h + RESIZE_ROWS - 1) / RESIZE_ROWS, n), dim3(256), 0, s, d, l);
+        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].h + RESIZE_ROWS - 1) / RESIZE_ROWS, n), dim3(RESIZE_T),
+                           o->resize_lds[l], s, d, l);
     const OrbLevel& L0 = d.lv[0];
     hipLaunchKernelGGL(k_orb_blur, dim3((L0.w + BLUR_TW - 1) / BLUR_TW, (L0.h + BLUR_TH - 1) / BLUR_TH, n * d.nlevels),
                        dim3(256), 0, s, d);
