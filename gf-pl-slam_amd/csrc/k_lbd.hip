@@ -5,9 +5,9 @@
 // of one octave (Config::lsdOctaveNum = 1), over a batch of images resident in HBM; the
 // arithmetic of the OpenCV / libm calls pinned as the CPU oracle's ledger L1-L5
 // (oracle/gfpl_lbd_oracle.cpp).  Kernels, per launch over all images:
-//  k_lbd_blur     GaussianBlur 5x5 sigma 1 (computeGaussianPyramid :350-371, L1), one
-//                 64x32 tile per workgroup, rows pass into dword LDS cells, columns pass
-//  k_lbd_sobel    cv::Sobel 3x3 dx and dy, 8U -> 16S (computeSobel :373-399, L2), exact
+//  k_lbd_grad     GaussianBlur 5x5 sigma 1 (computeGaussianPyramid :350-371, L1) and
+//                 cv::Sobel 3x3 dx and dy, 8U -> 16S (computeSobel :373-399, L2), exact,
+//                 fused per 64x32 tile through LDS (the blurred image stays on chip)
 //  k_lbd_describe one wave per keyline (computeLBD :1026-1372): lane h < 63 walks row h
 //                 of the 9-band x 7-row line support region (its start point after h
 //                 sequential float steps, as the reference steps it), the row sums to
@@ -36,7 +36,6 @@ struct LbdDev {
     float coefL[3 * LBD_BANDW];   // gaussCoefL_ (L4)
     float coefG[LBD_ROWS];        // gaussCoefG_
     int pairs[32];                // band pair c: i | j << 4
-    uint8_t* blur;                // [n][W*H]
     uint32_t* grad;               // [n][W*H] dx (low 16 bits) | dy (high 16 bits)
     int* err;                     // bit 0: a keyline of another octave
 };
@@ -48,90 +47,78 @@ __device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i : (i >= n
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 }  // namespace
 
-// L1: 5 taps, rows exact, columns (s + 2^15) >> 16; images >= 8 px, so one reflection suffices
+// L1 + L2 fused: GaussianBlur 5x5 (rows exact, columns (s + 2^15) >> 16, REFLECT_101) and
+// cv::Sobel 3x3 of the blurred image (REFLECT_101) for one 64x32 output tile: the (32+6) x
+// (64+6) source bytes (sources reflected, clamped past the image's reflection span: those
+// tile columns feed no output), the rows pass, the columns pass into a (32+2) x (64+2)
+// blurred tile, then dx / dy from LDS.  The blurred image never leaves the chip: a blurred
+// value just outside the image, computed from reflected sources, equals the reflected
+// blurred value Sobel's border wants (the taps are symmetric).  Images >= 8 px.
 #define LBD_TW 64
 #define LBD_TH 32
-__global__ void __launch_bounds__(256) k_lbd_blur(LbdDev o, const uint8_t* images) {
-    __shared__ int tile[LBD_TH + 4][LBD_TW + 4];
-    __shared__ int rows[LBD_TH + 4][LBD_TW + 1];
+__global__ void __launch_bounds__(256) k_lbd_grad(LbdDev o, const uint8_t* images) {
+    __shared__ int tile[LBD_TH + 6][LBD_TW + 8];    // source bytes, later the blurred tile
+    __shared__ int rows[LBD_TH + 6][LBD_TW + 3];    // rows pass
     const int img = blockIdx.z;
     const int x0 = blockIdx.x * LBD_TW, y0 = blockIdx.y * LBD_TH;
     const size_t npx = (size_t)o.W * o.H;
     const uint8_t* S = images + img * npx;
     const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
-    {
-        const int sx0 = refl1(min(x0 + tx - 2, o.W + 1), o.W);
-        const int sx1 = refl1(min(x0 + tx + 62, o.W + 1), o.W);
-        uint8_t a[9], b[9];
+    {   // tile column j = source column x0 - 3 + j (j < 70), tile row i = source row y0 - 3 + i
+        const int sx0 = refl1(min(x0 + tx - 3, o.W + 2), o.W);
+        const int sx1 = refl1(min(x0 + tx + 61, o.W + 2), o.W);
+        uint8_t a[10], b[10];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) {
-            const int r = min(ty0 + 4 * q, LBD_TH + 3);
-            const size_t row = (size_t)refl1(min(y0 + r - 2, o.H + 1), o.H) * o.W;
+        for (int q = 0; q < 10; ++q) {
+            const int r = min(ty0 + 4 * q, LBD_TH + 5);
+            const size_t row = (size_t)refl1(min(y0 + r - 3, o.H + 2), o.H) * o.W;
             a[q] = S[row + sx0];
-            b[q] = tx < 4 ? S[row + sx1] : 0;
+            b[q] = tx < 6 ? S[row + sx1] : 0;
         }
 #pragma unroll
-        for (int q = 0; q < 9; ++q) {
+        for (int q = 0; q < 10; ++q) {
             const int r = ty0 + 4 * q;
-            if (r < LBD_TH + 4) {
+            if (r < LBD_TH + 6) {
                 tile[r][tx] = a[q];
-                if (tx < 4) tile[r][tx + 64] = b[q];
+                if (tx < 6) tile[r][tx + 64] = b[q];
             }
         }
     }
     __syncthreads();
     const int k0 = o.blur_k[0], k1 = o.blur_k[1], k2 = o.blur_k[2];
-    for (int r = ty0; r < LBD_TH + 4; r += 4) {
-        const int* T = &tile[r][tx];
-        rows[r][tx] = k0 * (T[0] + T[4]) + k1 * (T[1] + T[3]) + k2 * T[2];
+    // rows pass: blurred-tile column c (image column x0 - 1 + c) from tile columns c .. c + 4
+    for (int i = threadIdx.x; i < (LBD_TH + 6) * (LBD_TW + 2); i += 256) {
+        const int r = i / (LBD_TW + 2), c = i - r * (LBD_TW + 2);
+        const int* T = &tile[r][c];
+        rows[r][c] = k0 * (T[0] + T[4]) + k1 * (T[1] + T[3]) + k2 * T[2];
     }
     __syncthreads();
+    // columns pass: blurred-tile row r (image row y0 - 1 + r) from rows pass rows r .. r + 4
+    for (int i = threadIdx.x; i < (LBD_TH + 2) * (LBD_TW + 2); i += 256) {
+        const int r = i / (LBD_TW + 2), c = i - r * (LBD_TW + 2);
+        const int a = k2 * rows[r + 2][c] + k1 * (rows[r + 1][c] + rows[r + 3][c]) + k0 * (rows[r][c] + rows[r + 4][c]);
+        tile[r][c] = min(max((a + (1 << 15)) >> 16, 0), 255);
+    }
+    __syncthreads();
+    // Sobel: thread (tx, ty0) outputs column x0 + tx, rows y0 + 8 ty0 .. + 7
     const int x = x0 + tx;
     if (x >= o.W) return;
-    uint8_t* D = o.blur + img * npx;
-    const int r0 = ty0 * 8;
-    int w[12];
+    const int r0 = 8 * ty0;
+    int v[10][3];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) w[t] = rows[r0 + t][tx];
+    for (int t = 0; t < 10; ++t)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[t][c] = tile[r0 + t][tx + c];
+    uint32_t* D = o.grad + img * npx + x;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int y = y0 + r0 + q;
         if (y < o.H) {
-            const int a = k2 * w[q + 2] + k1 * (w[q + 1] + w[q + 3]) + k0 * (w[q] + w[q + 4]);
-            D[(size_t)y * o.W + x] = (uint8_t)min(max((a + (1 << 15)) >> 16, 0), 255);
+            // rows q (y - 1), q + 1 (y), q + 2 (y + 1); columns 0 (x - 1), 1 (x), 2 (x + 1)
+            const int gx = (v[q][2] - v[q][0]) + 2 * (v[q + 1][2] - v[q + 1][0]) + (v[q + 2][2] - v[q + 2][0]);
+            const int gy = (v[q + 2][0] - v[q][0]) + 2 * (v[q + 2][1] - v[q][1]) + (v[q + 2][2] - v[q][2]);
+            D[(size_t)y * o.W] = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
         }
-    }
-}
-
-// L2: dx = [-1 0 1] x [1 2 1]^T, dy its transpose, REFLECT_101; four pixels per thread
-// (six bytes of each of the three rows), one 16-B store when the row allows it
-__global__ void __launch_bounds__(256) k_lbd_sobel(LbdDev o) {
-    const int x0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x), y = blockIdx.y, img = blockIdx.z;
-    if (x0 >= o.W) return;
-    const size_t npx = (size_t)o.W * o.H;
-    const uint8_t* B = o.blur + img * npx;
-    const int ym = refl1(y - 1, o.H), yp = refl1(y + 1, o.H);
-    const uint8_t* R[3] = {B + (size_t)ym * o.W, B + (size_t)y * o.W, B + (size_t)yp * o.W};
-    int v[3][6];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int i = 0; i < 6; ++i) v[r][i] = R[r][refl1(min(x0 - 1 + i, o.W), o.W)];
-    uint32_t g[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        // pixel x0 + i: columns i (x - 1), i + 1 (x), i + 2 (x + 1)
-        const int gx = (v[0][i + 2] - v[0][i]) + 2 * (v[1][i + 2] - v[1][i]) + (v[2][i + 2] - v[2][i]);
-        const int gy = (v[2][i] - v[0][i]) + 2 * (v[2][i + 1] - v[0][i + 1]) + (v[2][i + 2] - v[0][i + 2]);
-        g[i] = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
-    }
-    uint32_t* D = o.grad + img * npx + (size_t)y * o.W + x0;
-    if ((o.W & 3) == 0) {
-        *reinterpret_cast<uint4*>(D) = make_uint4(g[0], g[1], g[2], g[3]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (x0 + i < o.W) D[i] = g[i];
     }
 }
 
@@ -336,10 +323,9 @@ extern "C" int gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_ima
     }
     const size_t npx = (size_t)width * height, M = (size_t)max_images;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_blur = al(M * npx), b_g = al(4 * M * npx);
-    if (hipMalloc(&o->base, b_blur + b_g + 256) != hipSuccess) { delete o; return GFPL_E_HIP; }
+    const size_t b_g = al(4 * M * npx);
+    if (hipMalloc(&o->base, b_g + 256) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
-    d.blur = (uint8_t*)p; p += b_blur;
     d.grad = (uint32_t*)p; p += b_g;
     d.err = (int*)p;
     *out = o;
@@ -360,9 +346,8 @@ extern "C" int gfpl_lbd_compute(gfpl_lbd* o, const uint8_t* images, int n, const
     const LbdDev& d = o->d;
     hipStream_t s = o->stream;
     if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
-    hipLaunchKernelGGL(k_lbd_blur, dim3((d.W + LBD_TW - 1) / LBD_TW, (d.H + LBD_TH - 1) / LBD_TH, n), dim3(256), 0, s, d,
+    hipLaunchKernelGGL(k_lbd_grad, dim3((d.W + LBD_TW - 1) / LBD_TW, (d.H + LBD_TH - 1) / LBD_TH, n), dim3(256), 0, s, d,
                        images);
-    hipLaunchKernelGGL(k_lbd_sobel, dim3((d.W + 1023) / 1024, d.H, n), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_lbd_describe, dim3((d.kl_cap + 3) / 4, n), dim3(256), 0, s, d, keylines, n_kl, desc);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
     int err = 0;
