@@ -125,8 +125,9 @@ __global__ void k_orb_copy0(OrbDev o, const uint8_t* images, int n) {
 //     source bytes into an LDS output row as one dword;
 //  3. each output row stored as dwords at 4-B aligned addresses (two LDS dwords funnel-shifted
 //     by the row's misalignment), its unaligned head / tail bytes one by one.
-// (One pixel per thread from global bytes ran 171 us per level at 256 VGA images.)
-#define RESIZE_ROWS 16
+// (One pixel per thread from global bytes: 171 us per level at 256 VGA images; this layout with
+// 16 / 8 / 4 / 2 rows per workgroup: 95, 63, 62, 74 us — 16 rows left too few waves resident.)
+#define RESIZE_ROWS 8
 #define RESIZE_T 128
 __device__ __forceinline__ uint32_t resize_lds_px(const uint8_t* L0, const uint8_t* L1, int sx, uint32_t al, bool blend,
                                                   int b0, int b1) {
