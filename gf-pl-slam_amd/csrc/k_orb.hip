@@ -246,7 +246,34 @@ __global__ void __launch_bounds__(256) k_orb_blur(OrbDev o) {
     if (x0 >= L.w || y0 >= L.h) return;
     const uint8_t* S = o.pyr + img * o.pyr_stride + L.off;
     const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
-    {   // 10 rows x (1 or 2) columns per thread, loads in flight before the LDS stores
+    if (x0 >= 3 && x0 + BLUR_TW + 2 < L.w && y0 >= 3 && y0 + BLUR_TH + 2 < L.h) {
+        // interior tile: each source row's 70 bytes as 19 aligned dwords (byte loads bound
+        // the border path's memory pipeline), three loads per thread in flight
+        constexpr int NDW = 19, NLD = (BLUR_TH + 6) * NDW;
+        uint32_t v[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < NLD) {
+                const int r = i / NDW, m = i - r * NDW;
+                const uintptr_t a = (uintptr_t)(S + (size_t)(y0 - 3 + r) * L.w + (x0 - 3));
+                v[u] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[m];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < NLD) {
+                const int r = i / NDW, m = i - r * NDW;
+                const int sh = (int)((uintptr_t)(S + (size_t)(y0 - 3 + r) * L.w + (x0 - 3)) & 3u);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int c = 4 * m + k - sh;
+                    if (c >= 0 && c < BLUR_TW + 6) tile[r][c] = (int)((v[u] >> (8 * k)) & 0xFFu);
+                }
+            }
+        }
+    } else {   // 10 rows x (1 or 2) columns per thread, loads in flight before the LDS stores
         const int sx0 = refl1(min(x0 + tx - 3, L.w + 2), L.w);
         const int sx1 = refl1(min(x0 + tx + 61, L.w + 2), L.w);
         uint8_t a[10], b[10];
