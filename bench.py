@@ -362,6 +362,54 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     return out
 
 
+def pipeline_rate(cam, cfg, B=1024, steps=3):
+    """Images in HBM to poses on one device (gfpl.pipeline), measured after the
+    timed tracking steps (not part of `value`): per step ORB on both images of B stereo frames,
+    LBD of the given keylines, one StereoFrameHandler step; staircase scene
+    (gfpl.pipeline.synth_stereo_steps), one untimed warm-up step.  Parity is the -m gpu test's
+    (tests/test_pipeline_gpu.py)."""
+    import torch
+    import gfpl
+    from gfpl.pipeline import ImagePipeline, synth_stereo_steps
+    W, H, KL = int(cam.width), int(cam.height), 320
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ctx = gfpl.Context(cam, cfg)
+    pipe = ImagePipeline(ctx, cam, B, KL)
+    g = gfpl.StereoFrameHandler(ctx, B, pipe.kp_cap, KL)
+    frames = []
+    for k in range(steps + 2):
+        sc = [synth_stereo_steps(b, k, W, H) for b in range(B)]
+        kl = [np.zeros((B, KL), gfpl.KEYLINE_DT) for _ in range(2)]
+        n = [np.zeros(B, np.int32) for _ in range(2)]
+        for b, x in enumerate(sc):
+            for side in range(2):
+                n[side][b] = len(x[2 + side])
+                kl[side][b, :n[side][b]] = x[2 + side]
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        frames.append((to(np.stack([x[0] for x in sc])), to(np.stack([x[1] for x in sc])),
+                       to(kl[0].view(np.uint8).reshape(-1)), to(n[0]), to(kl[1].view(np.uint8).reshape(-1)), to(n[1]),
+                       torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev)))
+    g.initialize(pipe.detect(*frames[0]))
+    g.frameStep(pipe.detect(*frames[1]))
+    t_det = t_trk = 0.0
+    for k in range(2, steps + 2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fr = pipe.detect(*frames[k])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        g.frameStep(fr)
+        torch.cuda.synchronize()
+        t_det += t1 - t0
+        t_trk += time.perf_counter() - t1
+    tr = g.read_last_track(0)
+    pipe.close()
+    return {"value": B * steps / (t_det + t_trk), "unit": "stereo frames/s", "sequences": B, "steps": steps,
+            "detect_ms_per_step": 1e3 * t_det / steps, "track_ms_per_step": 1e3 * t_trk / steps,
+            "matched_pt_seq0": len(tr["matched_pt"]), "matched_ls_seq0": len(tr["matched_ls"]),
+            "scene": "staircase bands at disparity 2/12/20/8 px, 2000 ORB, 300 keylines per side (LSD on the host)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -534,6 +582,10 @@ def main():
         det = None
         if world == 1 and not args.no_detect:
             det = detection_rates(cam, in_bytes * K / up_total)
+            try:
+                det["images_to_poses"] = pipeline_rate(cam, cfg)
+            except Exception as e:   # reported, never fatal to the contract line
+                det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}
         out = {
             "metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)",
             "value": value,
