@@ -40,7 +40,7 @@ $(BINDIR)/plslam_gpu: $(PKG)/host/plslam_gpu.cpp $(LIBDIR)/libgfpl_stvo.so $(LIB
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lgfpl_stvo -lgfpl_hip -l:libgfpl_synth.so -lpthread \
 	    -Wl,-rpath,'$$ORIGIN/../lib'
 
-ORACLE_SRC := oracle/gfpl_oracle.cpp oracle/gfpl_orb_oracle.cpp oracle/gfpl_lbd_oracle.cpp
+ORACLE_SRC := oracle/gfpl_oracle.cpp oracle/gfpl_orb_oracle.cpp oracle/gfpl_lbd_oracle.cpp oracle/gfpl_lsd_oracle.cpp
 oracle/liboracle.so: $(ORACLE_SRC) oracle/gfpl_oracle.h include/gfpl.h $(PKG)/csrc/gfpl_orb_pattern.h
 	$(CXX) $(ORACLEFLAGS) $(ORACLE_SRC) -o $@
 

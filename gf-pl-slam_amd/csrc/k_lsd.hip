@@ -1,0 +1,1065 @@
+// k_lsd.hip — LSD line detection on the GPU (detector part):
+// line_descriptor::LSDDetectorC::detect(image, keylines, scale, numOctaves, opts)
+// (3rdparty/line_descriptor/src/LSDDetector_custom.cpp:218-316) as
+// StereoFrame::detectLineFeatures calls it (src/stereoFrame.cpp:1160-1186), over a batch of
+// images resident in HBM, the arithmetic pinned as the CPU oracle's ledger S1-S7
+// (oracle/gfpl_lsd_oracle.cpp).  Kernels, one launch each for the whole batch:
+//  k_lsd_grad      per pixel (lsd.cpp ll_angle, S1): the 2x2 gradient, NOTDEF test, fastAtan2
+//                  angle (degrees, float), cos / sin of float(angle) (S3), the image's max norm
+//  k_lsd_keys      per pixel: the 64-bit sort element (norm bin << 32 | y << 16 | x), row-major
+//  k_lsd_sort      one wave per image: libstdc++ std::sort's permutation (S2).  Introsort's
+//                  Hoare partition is restated in parallel: the k-th left stopper swaps with
+//                  the k-th right stopper while it lies left of it, so one ballot pass ranks
+//                  the stoppers, a 64-ary search finds the crossing, and the swaps run in
+//                  parallel; ranges <= 2048 elements finish in LDS; heapsort (depth limit) on
+//                  one lane; the final insertion sort is per-leaf (ranges <= 16 never exchange
+//                  elements with their neighbours), one leaf per lane
+//  k_lsd_grow      one wave per image: the seed loop over the sorted pixels (64 candidates per
+//                  ballot), region_grow (lanes 0-8 load a region point's 3x3 neighbours, the
+//                  order-dependent angle update runs lane-uniform over them), region2rect /
+//                  get_theta (list-ordered sums from lane values), refine and
+//                  reduce_region_radius (its swap-with-last removal as a parallel hole/filler
+//                  pairing); the used map is an LDS bitmap when it fits
+//  k_lsd_keylines  one wave per image: checkLineExtremes, the min-length filter (order-
+//                  preserving), KeyLine angle / response, and the response std::sort + resize
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+
+#include "gfpl_kernels.hpp"
+
+namespace gfpl {
+
+#define LSD_SORT_LDS 2048          // ranges up to this many elements are sorted in LDS
+#define LSD_RING 1024              // region list entries mirrored in LDS
+#define LSD_USED_LDS_MAX (64 * 1024)   // bytes of LDS bitmap (W*H <= 524288 px)
+
+struct LsdDev {
+    int W, H, NP;                  // NP = (W-1)(H-1) sorted pixels
+    int n_bins, min_reg_size, seg_cap, kl_cap, n_features;
+    double prec, rho, density_th, min_length;
+    float* ang;                    // [n][W*H] fastAtan2 degrees, -1 = NOTDEF
+    float2* csn;                   // [n][W*H] (cos, sin) of float(angle)
+    uint32_t* gxy;                 // [n][W*H] gx (low 16) | gy (high 16), int16 each
+    unsigned long long* maxg;      // [n] bits of the max norm of defined pixels
+    uint64_t* keys;                // [n][NP]
+    int* lpos;                     // [n][NP] partition scratch
+    int* rpos;                     // [n][NP]
+    uint32_t* reg;                 // [n][W*H] region list
+    uint32_t* tmp;                 // [n][W*H] region scratch
+    uint8_t* used_g;               // [n][W*H] used map when the bitmap does not fit LDS
+    float4* segs;                  // [n][seg_cap]
+    int* nseg;                     // [n]
+    float* kl_tmp;                 // [n][seg_cap][6]  filtered keylines (sx sy ex ey angle response)
+    uint64_t* rkeys;               // [n][seg_cap] response sort elements
+    int* rl;                       // [n][seg_cap]
+    int* rr;                       // [n][seg_cap]
+    int* err;                      // bit 0 segment overflow, bit 1 keyline overflow
+};
+
+namespace {
+
+constexpr double kPi = 3.1415926535897932384626433832795;
+constexpr double k32Pi = (3 * kPi) / 2;
+constexpr double k2Pi = 2 * kPi;
+constexpr double kDeg2Rad = kPi / 180;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void mem_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+__device__ __forceinline__ int below(unsigned long long m) { return __popcll(m & ((1ull << lane_id()) - 1ull)); }
+__device__ __forceinline__ double rl_d(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float rl_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int rl_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double wmax(double v) {
+    for (int o = 32; o; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+    for (int o = 32; o; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+
+// O4: cv::fastAtan2 (degrees)
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI), p3 = -0.3258083974640975f * (float)(180 / M_PI),
+                p5 = 0.1555786518463281f * (float)(180 / M_PI), p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, ax + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = __fdiv_rn(ax, ay + (float)2.2204460492503131e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// S4: fdlibm s_atan.c / e_atan2.c (finite arguments), + - * / only
+__device__ double fd_atan(double x) {
+    const double atanhi[] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                             1.57079632679489655800e+00};
+    const double atanlo[] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                             6.12323399573676603587e-17};
+    const double aT[] = {3.33333333333329318027e-01,  -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                         -1.11111104054623557880e-01, 9.09088713343650656196e-02,  -7.69187620504482999495e-02,
+                         6.66107313738753120669e-02,  -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                         -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+    const int hx = __double2hiint(x);
+    const int ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    if (ix < 0x3fdc0000) {
+        if (ix < 0x3e200000) return x;
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else {
+            if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+            else { id = 3; x = -1.0 / x; }
+        }
+    }
+    const double z = x * x, w = z * z;
+    const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+__device__ double fd_atan2(double y, double x) {
+    const double pi_o_2 = 1.5707963267948965580e+00, pi = 3.1415926535897931160e+00,
+                 pi_lo = 1.2246467991473531772e-16, tiny = 1.0e-300;
+    const int hx = __double2hiint(x), hy = __double2hiint(y);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const unsigned lx = (unsigned)__double2loint(x), ly = (unsigned)__double2loint(y);
+    if (((unsigned)(hx - 0x3ff00000) | lx) == 0) return fd_atan(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (((unsigned)iy | ly) == 0) {
+        if (m <= 1) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (((unsigned)ix | lx) == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = pi_o_2 + 0.5 * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = fd_atan(fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+__device__ __forceinline__ double angle_diff_signed(double a, double b) {
+    double diff = a - b;
+    while (diff <= -kPi) diff += k2Pi;
+    while (diff > kPi) diff -= k2Pi;
+    return diff;
+}
+
+// ------------------------------------------------------------- std::sort (S2) --
+// comp(a, b) = key(a) > key(b): the descending order of the high 32 bits
+__device__ __forceinline__ uint32_t skey(uint64_t e) { return (uint32_t)(e >> 32); }
+
+template <bool LDS>
+__device__ __forceinline__ void ssync() {
+    if (LDS) lds_sync();
+    else mem_sync();
+}
+
+// libstdc++ __adjust_heap / __push_heap (one lane)
+__device__ void adjust_heap(uint64_t* a, int hole, int len, uint64_t value) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (skey(a[second]) > skey(a[second - 1])) second--;
+        a[hole] = a[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        a[hole] = a[second - 1];
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && skey(a[parent]) > skey(value)) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = value;
+}
+// __partial_sort(first, last, last) = __make_heap + __sort_heap
+__device__ void heap_sort(uint64_t* a, int len) {
+    if (len >= 2) {
+        for (int parent = (len - 2) / 2;; --parent) {
+            adjust_heap(a, parent, len, a[parent]);
+            if (parent == 0) break;
+        }
+    }
+    while (len > 1) {
+        --len;
+        const uint64_t v = a[len];
+        a[len] = a[0];
+        adjust_heap(a, 0, len, v);
+    }
+}
+
+// __unguarded_partition_pivot(a + f, a + l) by the wave; returns the cut
+template <bool LDS>
+__device__ int partition_pivot(uint64_t* a, int f, int l, int* Lp, int* Rp) {
+    const int lane = lane_id();
+    const int mid = f + (l - f) / 2;
+    // __move_median_to_first(f, f + 1, mid, l - 1)
+    const uint32_t ka = skey(a[f + 1]), kb = skey(a[mid]), kc = skey(a[l - 1]);
+    int sel;
+    if (ka > kb) sel = kb > kc ? mid : (ka > kc ? l - 1 : f + 1);
+    else sel = ka > kc ? f + 1 : (kb > kc ? l - 1 : mid);
+    const uint64_t pv = a[sel], old = a[f];
+    ssync<LDS>();
+    if (lane == 0) {
+        a[sel] = old;
+        a[f] = pv;
+    }
+    ssync<LDS>();
+    const uint32_t pk = skey(pv);
+    // __unguarded_partition(f + 1, l, f): the stoppers of both scans, ranked
+    int cl = 0, cr = 0;
+    for (int base = f + 1; base < l; base += 64) {
+        const int pos = base + lane;
+        const bool v = pos < l;
+        const uint32_t k = v ? skey(a[pos]) : 0;
+        const bool isl = v && k <= pk, isr = v && k >= pk;
+        const unsigned long long ml = __ballot(isl), mr = __ballot(isr);
+        if (isl) Lp[cl + below(ml)] = pos;
+        if (isr) Rp[cr + below(mr)] = pos;
+        cl += __popcll(ml);
+        cr += __popcll(mr);
+    }
+    ssync<LDS>();
+    // K = #k with L[k] < R[k] (L ascending, R[k] = Rp[cr - 1 - k] descending): 64-ary search
+    int lo = 0, hi = min(cl, cr);
+    while (hi > lo) {
+        const int step = (hi - lo + 63) >> 6;
+        const int k = lo + lane * step;
+        const bool inr = k < hi;
+        const bool p = inr && Lp[k] < Rp[cr - 1 - k];
+        const int t = __popcll(__ballot(p)), nv = __popcll(__ballot(inr));
+        if (step == 1 || t == 0) {
+            lo += t * step;   // t == 0: K = lo
+            break;
+        }
+        const int nlo = lo + (t - 1) * step + 1;
+        hi = t < nv ? lo + t * step : hi;
+        lo = nlo;
+    }
+    const int K = lo;
+    for (int base = 0; base < K; base += 64) {
+        const int k = base + lane;
+        if (k < K) {
+            const int pl = Lp[k], pr = Rp[cr - 1 - k];
+            const uint64_t x = a[pl], y = a[pr];
+            a[pl] = y;
+            a[pr] = x;
+        }
+    }
+    const int cL = K < cl ? Lp[K] : INT_MAX;
+    const int cR = K >= 1 ? Rp[cr - K] : INT_MAX;
+    ssync<LDS>();
+    return min(cL, cR);
+}
+
+struct SortLds {
+    uint64_t buf[LSD_SORT_LDS];
+    int lp[LSD_SORT_LDS], rp[LSD_SORT_LDS];
+    int stk[3 * 64];
+    int leaf[2 * 64];
+};
+
+// the final insertion sort, one leaf (<= 16 elements, disjoint) per lane
+template <bool LDS>
+__device__ void flush_leaves(uint64_t* a, int* leaf, int& nleaf) {
+    const int lane = lane_id();
+    if (nleaf == 0) return;
+    ssync<LDS>();
+    if (lane < nleaf) {
+        const int f = leaf[2 * lane], n = leaf[2 * lane + 1];
+        for (int i = 1; i < n; ++i) {
+            const uint64_t v = a[f + i];
+            int j = i;
+            while (j > 0 && skey(v) > skey(a[f + j - 1])) {
+                a[f + j] = a[f + j - 1];
+                --j;
+            }
+            a[f + j] = v;
+        }
+    }
+    ssync<LDS>();
+    nleaf = 0;
+}
+
+template <bool LDS>
+__device__ void add_leaf(uint64_t* a, int* leaf, int& nleaf, int f, int l) {
+    if (l - f < 2) return;
+    if (lane_id() == 0) {
+        leaf[2 * nleaf] = f;
+        leaf[2 * nleaf + 1] = l - f;
+    }
+    lds_sync();
+    if (++nleaf == 64) flush_leaves<LDS>(a, leaf, nleaf);
+}
+
+// __introsort_loop over [0, n) of an LDS array with the given depth budget, then the
+// final insertion sort of its leaves
+__device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
+    const int lane = lane_id();
+    int* stk = S.stk;
+    int* leaf = S.leaf;
+    int nleaf = 0;
+    if (lane == 0) {
+        stk[0] = 0;
+        stk[1] = n;
+        stk[2] = depth;
+    }
+    lds_sync();
+    int sp = 1;
+    while (sp > 0) {
+        --sp;
+        int f = stk[3 * sp], l = stk[3 * sp + 1], d = stk[3 * sp + 2];
+        bool done = false;
+        while (l - f > 16) {
+            if (d == 0) {
+                if (lane == 0) heap_sort(a + f, l - f);
+                lds_sync();
+                done = true;
+                break;
+            }
+            --d;
+            const int cut = partition_pivot<true>(a, f, l, S.lp, S.rp);
+            if (lane == 0) {
+                stk[3 * sp] = cut;
+                stk[3 * sp + 1] = l;
+                stk[3 * sp + 2] = d;
+            }
+            lds_sync();
+            ++sp;
+            l = cut;
+        }
+        if (!done) add_leaf<true>(a, leaf, nleaf, f, l);
+    }
+    flush_leaves<true>(a, leaf, nleaf);
+}
+
+}  // namespace
+
+// the global-memory sort keeps its stack and leaves in the lower half of SortLds' small
+// arrays while a nested LDS sort runs: give the nested call its own copies
+struct SortLdsPair {
+    SortLds inner;
+    int stk[3 * 64];
+    int leaf[2 * 64];
+};
+
+namespace {
+// std::sort of a[0, n) by descending key (S2), the wave of the calling workgroup
+__device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) {
+    if (n < 2) return;
+    const int depth = 2 * (31 - __clz(n));
+    if (n <= LSD_SORT_LDS) {
+        const int lane = lane_id();
+        for (int i = lane; i < n; i += 64) P.inner.buf[i] = a[i];
+        lds_sync();
+        introsort_lds(P.inner.buf, n, depth, P.inner);
+        for (int i = lane; i < n; i += 64) a[i] = P.inner.buf[i];
+        mem_sync();
+        return;
+    }
+    // outer loop in global memory with its own stack / leaf arrays
+    SortLds& S = P.inner;
+    const int lane = lane_id();
+    int* stk = P.stk;
+    int* leaf = P.leaf;
+    int nleaf = 0;
+    if (lane == 0) {
+        stk[0] = 0;
+        stk[1] = n;
+        stk[2] = depth;
+    }
+    lds_sync();
+    int sp = 1;
+    while (sp > 0) {
+        --sp;
+        int f = stk[3 * sp], l = stk[3 * sp + 1], d = stk[3 * sp + 2];
+        bool done = false;
+        while (l - f > 16) {
+            if (l - f <= LSD_SORT_LDS) {
+                const int m = l - f;
+                for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
+                lds_sync();
+                introsort_lds(S.buf, m, d, S);
+                for (int i = lane; i < m; i += 64) a[f + i] = S.buf[i];
+                mem_sync();
+                done = true;
+                break;
+            }
+            if (d == 0) {
+                if (lane == 0) heap_sort(a + f, l - f);
+                mem_sync();
+                done = true;
+                break;
+            }
+            --d;
+            const int cut = partition_pivot<false>(a, f, l, Lp, Rp);
+            if (lane == 0) {
+                stk[3 * sp] = cut;
+                stk[3 * sp + 1] = l;
+                stk[3 * sp + 2] = d;
+            }
+            lds_sync();
+            ++sp;
+            l = cut;
+        }
+        if (!done) add_leaf<false>(a, leaf, nleaf, f, l);
+    }
+    flush_leaves<false>(a, leaf, nleaf);
+}
+}  // namespace
+
+// ------------------------------------------------------------------ ll_angle --
+__global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* images) {
+    const int img = blockIdx.z;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int W = o.W, H = o.H;
+    double norm_def = 0;
+    if (x < W && y < H) {
+        const size_t p = (size_t)img * W * H + (size_t)y * W + x;
+        float a = -1.0f;
+        uint32_t g = 0;
+        float2 cs = make_float2(0.f, 0.f);
+        if (x < W - 1 && y < H - 1) {
+            const uint8_t* I = images + (size_t)img * W * H;
+            const int DA = (int)I[(size_t)(y + 1) * W + x + 1] - (int)I[(size_t)y * W + x];
+            const int BC = (int)I[(size_t)y * W + x + 1] - (int)I[(size_t)(y + 1) * W + x];
+            const int gx = DA + BC, gy = DA - BC;
+            g = (uint32_t)(uint16_t)(int16_t)gx | ((uint32_t)(uint16_t)(int16_t)gy << 16);
+            const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
+            if (norm > o.rho) {
+                a = fast_atan2((float)gx, (float)-gy);
+                const double ad = (double)a * kDeg2Rad;
+                const double af = (double)(float)ad;   // S3: float(angle)
+                cs = make_float2((float)det_cos(af), (float)det_sin(af));
+                norm_def = norm;
+            }
+        }
+        o.ang[p] = a;
+        o.gxy[p] = g;
+        o.csn[p] = cs;
+    }
+    // the image's max norm over defined pixels (norm >= 0: the bits order like the values)
+    unsigned long long b = (unsigned long long)__double_as_longlong(norm_def);
+    for (int off = 32; off; off >>= 1) {
+        const unsigned long long t = __shfl_xor(b, off);
+        b = t > b ? t : b;
+    }
+    if ((threadIdx.x & 63) == 0 && b) atomicMax(&o.maxg[img], b);
+}
+
+__global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
+    const int img = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= o.NP) return;
+    const int W1 = o.W - 1;
+    const int y = i / W1, x = i - y * W1;
+    const double mg = __longlong_as_double((long long)o.maxg[img]);
+    const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
+    const uint32_t g = o.gxy[(size_t)img * o.W * o.H + (size_t)y * o.W + x];
+    const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
+    const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
+    const int bin = (int)(norm * bin_coef);
+    o.keys[(size_t)img * o.NP + i] = ((uint64_t)(uint32_t)bin << 32) | ((uint32_t)y << 16) | (uint32_t)x;
+}
+
+__global__ void __launch_bounds__(64) k_lsd_sort(LsdDev o) {
+    __shared__ SortLdsPair S;
+    const int img = blockIdx.x;
+    wave_sort(o.keys + (size_t)img * o.NP, o.NP, o.lpos + (size_t)img * o.NP, o.rpos + (size_t)img * o.NP, S);
+}
+
+// ---------------------------------------------------------------- the regions --
+namespace {
+
+template <bool LU>
+struct Used {
+    uint32_t* bits;   // LDS bitmap (LU)
+    uint8_t* g;       // global byte map (!LU)
+    int W;
+    __device__ __forceinline__ bool get(int x, int y) const {
+        const int p = y * W + x;
+        if (LU) return (bits[p >> 5] >> (p & 31)) & 1u;
+        return g[p] != 0;
+    }
+    __device__ __forceinline__ void set1(int x, int y) const {   // one lane
+        const int p = y * W + x;
+        if (LU) atomicOr(&bits[p >> 5], 1u << (p & 31));
+        else g[p] = 1;
+    }
+    __device__ __forceinline__ void clr(int x, int y) const {    // any lanes
+        const int p = y * W + x;
+        if (LU) atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
+        else g[p] = 0;
+    }
+    __device__ __forceinline__ void sync() const {
+        if (LU) lds_sync();
+        else mem_sync();
+    }
+};
+
+struct Rect { double x1, y1, x2, y2, width; };
+
+struct Img {
+    const float* ang;
+    const float2* csn;
+    const uint32_t* gxy;
+    uint32_t* reg;
+    uint32_t* tmp;
+    uint32_t* ring;   // LDS
+    int W, H;
+};
+
+__device__ __forceinline__ double modgrad(const Img& I, int x, int y) {
+    const uint32_t g = I.gxy[y * I.W + x];
+    const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
+    return sqrt((double)(gx * gx + gy * gy) / 4.0);
+}
+
+__device__ __forceinline__ uint32_t reg_at(const Img& I, int i, int n) {
+    if (n - i <= LSD_RING) return I.ring[i & (LSD_RING - 1)];
+    mem_sync();
+    return I.reg[i];
+}
+
+// region_grow (lsd.cpp): returns the region size; reg / ring hold the points in push order
+template <bool LU>
+__device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, double prec, double& reg_angle) {
+    const int lane = lane_id();
+    int n = 0;
+    reg_angle = (double)I.ang[sy * I.W + sx] * kDeg2Rad;
+    float sumdx = (float)det_cos(reg_angle), sumdy = (float)det_sin(reg_angle);   // S3
+    const uint32_t s = ((uint32_t)sy << 16) | (uint32_t)sx;
+    if (lane == 0) {
+        I.reg[0] = s;
+        I.ring[0] = s;
+        U.set1(sx, sy);
+    }
+    n = 1;
+    U.sync();
+    lds_sync();
+    const int dxl = lane % 3 - 1, dyl = lane / 3 - 1;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t r = reg_at(I, i, n);
+        const int rx = (int)(r & 0xffff), ry = (int)(r >> 16);
+        const int xx = rx + dxl, yy = ry + dyl;
+        const bool ok = lane < 9 && xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
+        float a = -1.0f;
+        float2 cs = make_float2(0.f, 0.f);
+        if (ok && !U.get(xx, yy)) {
+            a = I.ang[yy * I.W + xx];
+            if (a >= 0.0f) cs = I.csn[yy * I.W + xx];
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float at = rl_f(a, t);
+            if (at < 0.0f) continue;   // out of the image, used, or NOTDEF
+            // isAligned (lsd.cpp)
+            const double ad = (double)at * kDeg2Rad;
+            double nt = reg_angle - ad;
+            if (nt < 0) nt = -nt;
+            if (nt > k32Pi) {
+                nt -= k2Pi;
+                if (nt < 0) nt = -nt;
+            }
+            if (!(nt <= prec)) continue;
+            const int px = rx + t % 3 - 1, py = ry + t / 3 - 1;
+            const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
+            if (lane == 0) {
+                U.set1(px, py);
+                I.reg[n] = e;
+                I.ring[n & (LSD_RING - 1)] = e;
+            }
+            ++n;
+            sumdx += rl_f(cs.x, t);
+            sumdy += rl_f(cs.y, t);
+            reg_angle = (double)fast_atan2(sumdy, sumdx) * kDeg2Rad;
+        }
+        lds_sync();
+        if (!LU) mem_sync();
+    }
+    mem_sync();   // the region list (global) is read by every lane next
+    return n;
+}
+
+// region2rect + get_theta (lsd.cpp), sums in list order
+__device__ void region2rect(const Img& I, int n, double reg_angle, double prec, Rect& rec) {
+    const int lane = lane_id();
+    double X = 0, Y = 0, S = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        double px = 0, py = 0, w = 0;
+        if (i < n) {
+            const uint32_t r = I.reg[i];
+            const int x = (int)(r & 0xffff), y = (int)(r >> 16);
+            w = modgrad(I, x, y);
+            px = (double)x * w;
+            py = (double)y * w;
+        }
+        const int m = min(64, n - b);
+        for (int t = 0; t < m; ++t) {
+            X += rl_d(px, t);
+            Y += rl_d(py, t);
+            S += rl_d(w, t);
+        }
+    }
+    const double x = X / S, y = Y / S;
+    double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        double txx = 0, tyy = 0, txy = 0;
+        if (i < n) {
+            const uint32_t r = I.reg[i];
+            const int rx = (int)(r & 0xffff), ry = (int)(r >> 16);
+            const double w = modgrad(I, rx, ry);
+            const double dx = (double)rx - x, dy = (double)ry - y;
+            txx = dy * dy * w;
+            tyy = dx * dx * w;
+            txy = dx * dy * w;
+        }
+        const int m = min(64, n - b);
+        for (int t = 0; t < m; ++t) {
+            Ixx += rl_d(txx, t);
+            Iyy += rl_d(tyy, t);
+            Ixy -= rl_d(txy, t);
+        }
+    }
+    const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+    double theta = (fabs(Ixx) > fabs(Iyy)) ? (double)fast_atan2((float)(lambda - Ixx), (float)Ixy)
+                                           : (double)fast_atan2((float)Ixy, (float)(lambda - Iyy));
+    theta *= kDeg2Rad;
+    if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
+    const double dx = det_cos(theta), dy = det_sin(theta);
+    double lmax = 0, lmin = 0, wmx = 0, wmn = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        if (i < n) {
+            const uint32_t r = I.reg[i];
+            const double rdx = (double)(int)(r & 0xffff) - x, rdy = (double)(int)(r >> 16) - y;
+            const double l = rdx * dx + rdy * dy;
+            const double w = -rdx * dy + rdy * dx;
+            lmax = fmax(lmax, l);
+            lmin = fmin(lmin, l);
+            wmx = fmax(wmx, w);
+            wmn = fmin(wmn, w);
+        }
+    }
+    lmax = wmax(lmax);
+    lmin = wmin(lmin);
+    wmx = wmax(wmx);
+    wmn = wmin(wmn);
+    rec.x1 = x + lmin * dx;
+    rec.y1 = y + lmin * dy;
+    rec.x2 = x + lmax * dx;
+    rec.y2 = y + lmax * dy;
+    rec.width = wmx - wmn;
+    if (rec.width < 1.0) rec.width = 1.0;
+}
+
+__device__ __forceinline__ double rdist(const Rect& r) {
+    return sqrt((r.x2 - r.x1) * (r.x2 - r.x1) + (r.y2 - r.y1) * (r.y2 - r.y1));
+}
+
+// reduce_region_radius (lsd.cpp): each pass's swap-with-last removal = holes (far points
+// below the new size, ascending) filled by the kept points above it, descending
+template <bool LU>
+__device__ bool reduce_region_radius(const Img& I, const Used<LU>& U, int& n, double reg_angle, double prec,
+                                     Rect& rec, double density, double density_th) {
+    const int lane = lane_id();
+    const uint32_t r0 = I.reg[0];
+    const double xc = (double)(int)(r0 & 0xffff), yc = (double)(int)(r0 >> 16);
+    const double rad1 = (rec.x1 - xc) * (rec.x1 - xc) + (rec.y1 - yc) * (rec.y1 - yc);
+    const double rad2 = (rec.x2 - xc) * (rec.x2 - xc) + (rec.y2 - yc) * (rec.y2 - yc);
+    double rad_sq = rad1 > rad2 ? rad1 : rad2;
+    while (density < density_th) {
+        rad_sq *= 0.75 * 0.75;
+        // kept count
+        int nk = 0;
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + lane;
+            bool far = false;
+            if (i < n) {
+                const uint32_t r = I.reg[i];
+                const double px = (double)(int)(r & 0xffff), py = (double)(int)(r >> 16);
+                far = (px - xc) * (px - xc) + (py - yc) * (py - yc) > rad_sq;
+                if (far) U.clr((int)(r & 0xffff), (int)(r >> 16));
+            }
+            nk += __popcll(__ballot(i < n && !far));
+        }
+        // fillers: kept points at positions >= nk, rank from the end -> tmp
+        int cf = 0;
+        for (int b = nk; b < n; b += 64) {
+            const int i = b + lane;
+            bool keep = false;
+            uint32_t r = 0;
+            if (i < n) {
+                r = I.reg[i];
+                const double px = (double)(int)(r & 0xffff), py = (double)(int)(r >> 16);
+                keep = !((px - xc) * (px - xc) + (py - yc) * (py - yc) > rad_sq);
+            }
+            const unsigned long long m = __ballot(keep);
+            if (keep) I.tmp[cf + below(m)] = r;
+            cf += __popcll(m);
+        }
+        mem_sync();
+        // holes: far points at positions < nk, ascending; hole k takes filler cf - 1 - k
+        int ch = 0;
+        for (int b = 0; b < nk; b += 64) {
+            const int i = b + lane;
+            bool far = false;
+            if (i < nk) {
+                const uint32_t r = I.reg[i];
+                const double px = (double)(int)(r & 0xffff), py = (double)(int)(r >> 16);
+                far = (px - xc) * (px - xc) + (py - yc) * (py - yc) > rad_sq;
+            }
+            const unsigned long long m = __ballot(far);
+            if (far) I.reg[i] = I.tmp[cf - 1 - (ch + below(m))];
+            ch += __popcll(m);
+        }
+        n = nk;
+        mem_sync();
+        U.sync();
+        if (n < 2) return false;
+        region2rect(I, n, reg_angle, prec, rec);
+        density = (double)n / (rdist(rec) * rec.width);
+    }
+    return true;
+}
+
+// refine (lsd.cpp, LSD_REFINE_STD)
+template <bool LU>
+__device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle, double prec, Rect& rec,
+                       double density_th) {
+    const int lane = lane_id();
+    double density = (double)n / (rdist(rec) * rec.width);
+    if (density >= density_th) return true;
+    const uint32_t r0 = I.reg[0];
+    const int sx = (int)(r0 & 0xffff), sy = (int)(r0 >> 16);
+    const double xc = (double)sx, yc = (double)sy;
+    const double ang_c = (double)I.ang[sy * I.W + sx] * kDeg2Rad;
+    double sum = 0, s_sum = 0;
+    int cnt = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        double ad = 0;
+        bool in = false;
+        if (i < n) {
+            const uint32_t r = I.reg[i];
+            const int x = (int)(r & 0xffff), y = (int)(r >> 16);
+            U.clr(x, y);
+            in = sqrt(((double)x - xc) * ((double)x - xc) + ((double)y - yc) * ((double)y - yc)) < rec.width;
+            if (in) ad = angle_diff_signed((double)I.ang[y * I.W + x] * kDeg2Rad, ang_c);
+        }
+        const unsigned long long m = __ballot(in);
+        const int c = min(64, n - b);
+        for (int t = 0; t < c; ++t) {
+            if (!((m >> t) & 1ull)) continue;
+            const double v = rl_d(ad, t);
+            sum += v;
+            s_sum += v * v;
+        }
+        cnt += __popcll(m);
+    }
+    U.sync();
+    const double mean_angle = sum / (double)cnt;
+    const double tau = 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / (double)cnt + mean_angle * mean_angle);
+    n = region_grow<LU>(I, U, sx, sy, tau, reg_angle);
+    if (n < 2) return false;
+    region2rect(I, n, reg_angle, prec, rec);
+    density = (double)n / (rdist(rec) * rec.width);
+    if (density < density_th) return reduce_region_radius<LU>(I, U, n, reg_angle, prec, rec, density, density_th);
+    return true;
+}
+
+template <bool LU>
+__device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ring) {
+    const int lane = lane_id();
+    const size_t off = (size_t)img * o.W * o.H;
+    Img I{o.ang + off, o.csn + off, o.gxy + off, o.reg + off, o.tmp + off, ring, o.W, o.H};
+    Used<LU> U{bits, o.used_g + off, o.W};
+    if (LU) {
+        const int nw = (o.W * o.H + 31) >> 5;
+        for (int i = lane; i < nw; i += 64) bits[i] = 0;
+        lds_sync();
+    } else {
+        for (int i = lane; i < o.W * o.H; i += 64) U.g[i] = 0;
+        mem_sync();
+    }
+    const uint64_t* keys = o.keys + (size_t)img * o.NP;
+    int nseg = 0;
+    for (int base = 0; base < o.NP; base += 64) {
+        const int i = base + lane;
+        int px = 0, py = 0;
+        bool cand = false;
+        if (i < o.NP) {
+            const uint64_t e = keys[i];
+            px = (int)(e & 0xffff);
+            py = (int)((e >> 16) & 0xffff);
+            cand = I.ang[py * o.W + px] >= 0.0f;
+        }
+        for (;;) {
+            const unsigned long long m = __ballot(cand && !U.get(px, py));
+            if (!m) break;
+            const int j = __ffsll((long long)m) - 1;
+            if (lane <= j) cand = false;
+            const int sx = rl_i(px, j), sy = rl_i(py, j);
+            double reg_angle;
+            int n = region_grow<LU>(I, U, sx, sy, o.prec, reg_angle);
+            if (n < o.min_reg_size) continue;
+            Rect rec;
+            region2rect(I, n, reg_angle, o.prec, rec);
+            if (!refine<LU>(I, U, n, reg_angle, o.prec, rec, o.density_th)) continue;
+            if (lane == 0) {
+                if (nseg < o.seg_cap)
+                    o.segs[(size_t)img * o.seg_cap + nseg] =
+                        make_float4((float)(rec.x1 + 0.5), (float)(rec.y1 + 0.5), (float)(rec.x2 + 0.5),
+                                    (float)(rec.y2 + 0.5));
+                else
+                    atomicOr(o.err, 1);
+            }
+            ++nseg;
+        }
+    }
+    if (lane == 0) o.nseg[img] = min(nseg, o.seg_cap);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_lsd_grow_lds(LsdDev o) {
+    extern __shared__ uint32_t lds[];
+    lsd_image<true>(o, blockIdx.x, lds + LSD_RING, lds);
+}
+__global__ void __launch_bounds__(64) k_lsd_grow_glb(LsdDev o) {
+    __shared__ uint32_t ring[LSD_RING];
+    lsd_image<false>(o, blockIdx.x, nullptr, ring);
+}
+
+// std::sort of one device array (test hook of the S2 restatement)
+__global__ void __launch_bounds__(64) k_lsd_sort_one(uint64_t* a, int n, int* lp, int* rp) {
+    __shared__ SortLdsPair S;
+    wave_sort(a, n, lp, rp, S);
+}
+
+// ------------------------------------------------------------------ keylines --
+// LSDDetector_custom.cpp:266-306 and src/stereoFrame.cpp:1177-1185
+__global__ void __launch_bounds__(64) k_lsd_keylines(LsdDev o, gfpl_keyline* kl_out, int* n_kl, float* rsp_out) {
+    __shared__ SortLdsPair S;
+    const int img = blockIdx.x, lane = lane_id();
+    const int ns = o.nseg[img];
+    const float fw = (float)o.W, fh = (float)o.H;
+    const float mx = (float)max(o.W, o.H);
+    float* kt = o.kl_tmp + (size_t)img * o.seg_cap * 6;
+    int m = 0;
+    for (int b = 0; b < ns; b += 64) {
+        const int i = b + lane;
+        bool keep = false;
+        float e0 = 0, e1 = 0, e2 = 0, e3 = 0, ang = 0, rsp = 0;
+        if (i < ns) {
+            const float4 s = o.segs[(size_t)img * o.seg_cap + i];
+            e0 = s.x; e1 = s.y; e2 = s.z; e3 = s.w;
+            // checkLineExtremes (:78-103)
+            if (e0 < 0) e0 = 0;
+            if (e0 >= fw) e0 = fw - 1.0f;
+            if (e2 < 0) e2 = 0;
+            if (e2 >= fw) e2 = fw - 1.0f;
+            if (e1 < 0) e1 = 0;
+            if (e1 >= fh) e1 = fh - 1.0f;
+            if (e3 < 0) e3 = 0;
+            if (e3 >= fh) e3 = fh - 1.0f;
+            const float d0 = e0 - e2, d1 = e1 - e3;
+            const double length = (double)(float)sqrt((double)d0 * (double)d0 + (double)d1 * (double)d1);
+            keep = length > o.min_length;
+            ang = (float)fd_atan2((double)(e3 - e1), (double)(e2 - e0));   // S4
+            rsp = __fdiv_rn((float)length, mx);
+        }
+        const unsigned long long mk = __ballot(keep);
+        if (keep) {
+            float* d = kt + 6 * (m + below(mk));
+            d[0] = e0; d[1] = e1; d[2] = e2; d[3] = e3; d[4] = ang; d[5] = rsp;
+        }
+        m += __popcll(mk);
+    }
+    mem_sync();
+    const bool cut = m > o.n_features && o.n_features != 0;
+    const int nout = cut ? o.n_features : m;
+    if (nout > o.kl_cap) {
+        if (lane == 0) {
+            atomicOr(o.err, 2);
+            n_kl[img] = 0;
+        }
+        return;
+    }
+    uint64_t* rk = o.rkeys + (size_t)img * o.seg_cap;
+    if (cut) {
+        for (int i = lane; i < m; i += 64)
+            rk[i] = ((uint64_t)__float_as_uint(kt[6 * i + 5]) << 32) | (uint32_t)i;
+        mem_sync();
+        wave_sort(rk, m, o.rl + (size_t)img * o.seg_cap, o.rr + (size_t)img * o.seg_cap, S);   // S7
+    }
+    for (int k = lane; k < nout; k += 64) {
+        const int i = cut ? (int)(uint32_t)rk[k] : k;
+        const float* d = kt + 6 * i;
+        gfpl_keyline q;
+        q.sx = d[0]; q.sy = d[1]; q.ex = d[2]; q.ey = d[3]; q.angle = d[4]; q.octave = 0;
+        kl_out[(size_t)img * o.kl_cap + k] = q;
+        if (rsp_out) rsp_out[(size_t)img * o.kl_cap + k] = d[5];
+    }
+    if (lane == 0) n_kl[img] = nout;
+}
+
+}  // namespace gfpl
+
+// ======================================================================= ABI ==
+using namespace gfpl;
+
+struct gfpl_lsd {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int max_images = 0;
+    bool lds_used = false;
+    size_t lds_bytes = 0;
+    LsdDev d{};
+    void* base = nullptr;
+};
+
+extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int width, int height, int max_images,
+                               int kl_cap, int seg_cap, gfpl_lsd** out) {
+    if (!ctx || !prm || !out || max_images < 1 || kl_cap < 1 || seg_cap < 1 || width < 8 || height < 8 ||
+        width > 2048 || height > 2048 || prm->n_bins < 1 || prm->n_features < 0)
+        return GFPL_E_INVALID;
+    if (prm->refine != 1 || prm->scale != 1.0) return GFPL_E_UNSUPPORTED;
+    const int dev = gfpl_ctx_device(ctx);
+    if (hipSetDevice(dev) != hipSuccess) return GFPL_E_HIP;
+    gfpl_lsd* o = new gfpl_lsd();
+    o->device = dev;
+    o->stream = (hipStream_t)gfpl_ctx_stream(ctx);
+    o->max_images = max_images;
+    LsdDev& d = o->d;
+    d.W = width;
+    d.H = height;
+    d.NP = (width - 1) * (height - 1);
+    d.n_bins = prm->n_bins;
+    d.seg_cap = seg_cap;
+    d.kl_cap = kl_cap;
+    d.n_features = prm->n_features;
+    d.density_th = prm->density_th;
+    d.min_length = prm->min_length;
+    {   // flsd's constants (S5), host libm as the oracle computes them
+        const double pi = 3.1415926535897932384626433832795;
+        d.prec = pi * prm->ang_th / 180;
+        const double p = prm->ang_th / 180;
+        d.rho = prm->quant / std::sin(d.prec);
+        const double log_nt = 5 * (std::log10((double)width) + std::log10((double)height)) / 2 + std::log10(11.0);
+        d.min_reg_size = (int)(size_t)(-log_nt / std::log10(p));
+    }
+    const size_t px = (size_t)width * height, M = (size_t)max_images, NP = (size_t)d.NP, SC = (size_t)seg_cap;
+    o->lds_used = (px + 31) / 32 * 4 <= LSD_USED_LDS_MAX;
+    o->lds_bytes = (px + 31) / 32 * 4 + 4 * LSD_RING;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_ang = al(4 * M * px), b_csn = al(8 * M * px), b_gxy = al(4 * M * px), b_max = al(8 * M),
+                 b_keys = al(8 * M * NP), b_pos = al(4 * M * NP), b_reg = al(4 * M * px),
+                 b_used = o->lds_used ? 0 : al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
+                 b_klt = al(24 * M * SC), b_rk = al(8 * M * SC), b_rl = al(4 * M * SC);
+    const size_t total = b_ang + b_csn + b_gxy + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
+                         b_klt + b_rk + 2 * b_rl + 256;
+    if (hipMalloc(&o->base, total) != hipSuccess) { delete o; return GFPL_E_HIP; }
+    char* p = (char*)o->base;
+    d.ang = (float*)p; p += b_ang;
+    d.csn = (float2*)p; p += b_csn;
+    d.gxy = (uint32_t*)p; p += b_gxy;
+    d.maxg = (unsigned long long*)p; p += b_max;
+    d.keys = (uint64_t*)p; p += b_keys;
+    d.lpos = (int*)p; p += b_pos;
+    d.rpos = (int*)p; p += b_pos;
+    d.reg = (uint32_t*)p; p += b_reg;
+    d.tmp = (uint32_t*)p; p += b_reg;
+    d.used_g = b_used ? (uint8_t*)p : nullptr; p += b_used;
+    d.segs = (float4*)p; p += b_segs;
+    d.nseg = (int*)p; p += b_nseg;
+    d.kl_tmp = (float*)p; p += b_klt;
+    d.rkeys = (uint64_t*)p; p += b_rk;
+    d.rl = (int*)p; p += b_rl;
+    d.rr = (int*)p; p += b_rl;
+    d.err = (int*)p;
+    if (o->lds_used &&
+        hipFuncSetAttribute((const void*)k_lsd_grow_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)o->lds_bytes) != hipSuccess) {
+        (void)hipFree(o->base);
+        delete o;
+        return GFPL_E_HIP;
+    }
+    *out = o;
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_lsd_sort_desc(gfpl_lsd* o, uint64_t* a, int n) {
+    if (!o || !a || n < 0 || n > o->d.NP) return GFPL_E_INVALID;
+    if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
+    hipLaunchKernelGGL(k_lsd_sort_one, dim3(1), dim3(64), 0, o->stream, a, n, o->d.lpos, o->d.rpos);
+    if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
+    return hipStreamSynchronize(o->stream) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
+}
+
+extern "C" int gfpl_lsd_destroy(gfpl_lsd* o) {
+    if (!o) return GFPL_E_INVALID;
+    if (o->base) (void)hipFree(o->base);
+    delete o;
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
+                               float* response) {
+    if (!o || !images || n < 1 || n > o->max_images || !keylines || !n_kl) return GFPL_E_INVALID;
+    if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
+    const LsdDev& d = o->d;
+    hipStream_t s = o->stream;
+    if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
+    if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess) return GFPL_E_HIP;
+    hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + 3) / 4, n), dim3(256), 0, s, d, images);
+    hipLaunchKernelGGL(k_lsd_keys, dim3((d.NP + 255) / 256, n), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64), 0, s, d);
+    if (o->lds_used)
+        hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
+    else
+        hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_keylines, dim3(n), dim3(64), 0, s, d, keylines, n_kl, response);
+    if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
+    int err = 0;
+    if (hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return GFPL_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return GFPL_E_HIP;
+    return err ? GFPL_E_CAPACITY : GFPL_OK;
+}

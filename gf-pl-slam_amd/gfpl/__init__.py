@@ -209,6 +209,19 @@ class OrbParams(C.Structure):
                 ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
 
 
+class LsdParams(C.Structure):
+    """gfpl_lsd_params: LSDDetectorC::LSDOptions + Config::lsdNFeatures as StereoFrame builds
+    them (src/stereoFrame.cpp:1163-1172; defaults src/config.cpp:143-152, min_length =
+    Config::minLineLength 0.025 * min(W, H), src/stereoFrame.cpp:151)."""
+    _fields_ = [("refine", C.c_int), ("scale", C.c_double), ("quant", C.c_double), ("ang_th", C.c_double),
+                ("density_th", C.c_double), ("n_bins", C.c_int), ("min_length", C.c_double),
+                ("n_features", C.c_int)]
+
+    @classmethod
+    def reference(cls, width: int, height: int, n_features: int = 300, min_line_length: float = 0.025):
+        return cls(1, 1.0, 2.0, 22.5, 0.6, 1024, min_line_length * min(width, height), n_features)
+
+
 class SynthParams(C.Structure):
     _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
                 ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
@@ -296,6 +309,10 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_kernel_bytes": ([P, P], C.c_int),
             "gfpl_last_step_bytes": ([P, P], C.c_int),
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
+            "gfpl_lsd_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_lsd_destroy": ([P], C.c_int),
+            "gfpl_lsd_detect": ([P, P, C.c_int, P, P, P], C.c_int),
+            "gfpl_lsd_sort_desc": ([P, P, C.c_int], C.c_int),
             "gfpl_strerror": ([C.c_int], C.c_char_p),
             "gfpl_orb_create": ([P, C.c_int, C.c_int, P, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_orb_destroy": ([P], C.c_int),
@@ -943,6 +960,73 @@ class ORBextractor:
     def close(self):
         if getattr(self, "h", None):
             self.L.gfpl_orb_destroy(self.h)
+            self.h = None
+        if getattr(self, "_own", None):
+            self.L.gfpl_destroy(self._own)
+            self._own = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LSDDetector:
+    """line_descriptor::LSDDetectorC on the GPU, the detect(image, keylines, scale, numOctaves,
+    opts) path StereoFrame uses (3rdparty/line_descriptor/src/LSDDetector_custom.cpp:218-316,
+    src/stereoFrame.cpp:1160-1186: LSD_REFINE_STD at scale 1, one octave, the min-length
+    filter, the response sort + resize to Config::lsdNFeatures) for images of one size.
+    detect() takes one host image like the reference; detect_batch() device buffers (the
+    product path's form, writing keylines where gfpl_lbd_compute / gfpl_frames read them)."""
+
+    def __init__(self, width: int, height: int, params: Optional["LsdParams"] = None, max_images: int = 1,
+                 kl_cap: int = 512, seg_cap: int = 4096, ctx: Optional[Context] = None, device: int = 0):
+        self.L = hiplib()
+        self.width, self.height, self.max_images, self.kl_cap, self.seg_cap = width, height, max_images, kl_cap, seg_cap
+        self.params = params if params is not None else LsdParams.reference(width, height)
+        self._own = None
+        if ctx is None:
+            h = C.c_void_p()
+            check(self.L.gfpl_create(device, None, C.byref(h)), "gfpl_create")
+            self._own = h
+            ch = h
+        else:
+            ch = ctx.h
+        self._ctx = ctx
+        o = C.c_void_p()
+        check(self.L.gfpl_lsd_create(ch, C.byref(self.params), width, height, max_images, kl_cap, seg_cap,
+                                     C.byref(o)), "lsd_create")
+        self.h = o
+
+    def detect_batch(self, images_dev, n: int, keylines_dev, n_kl_dev, response_dev=None) -> None:
+        check(self.L.gfpl_lsd_detect(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
+                                     _ptr(response_dev) if response_dev is not None else None), "lsd_detect")
+
+    def sort_desc(self, a_dev, n: int) -> None:
+        """ledger S2 test hook: std::sort by descending high 32 bits of a device u64 array."""
+        check(self.L.gfpl_lsd_sort_desc(self.h, _ptr(a_dev), n), "lsd_sort_desc")
+
+    def detect(self, image: np.ndarray):
+        """detect(image, keylines, ...) on one HOST image: (keylines KEYLINE_DT, response f32)."""
+        import torch
+        image = np.ascontiguousarray(image, np.uint8)
+        if image.shape != (self.height, self.width):
+            raise ValueError(f"image {image.shape} != ({self.height}, {self.width})")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        d_img = torch.from_numpy(image).to(dev)
+        d_kl = torch.zeros(self.kl_cap * KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
+        d_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        d_r = torch.zeros(self.kl_cap, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        self.detect_batch(d_img, 1, d_kl, d_n, d_r)
+        n = int(d_n.cpu()[0])
+        kl = d_kl.cpu().numpy().view(KEYLINE_DT)[:n].copy()
+        return kl, d_r.cpu().numpy()[:n].copy()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_lsd_destroy(self.h)
             self.h = None
         if getattr(self, "_own", None):
             self.L.gfpl_destroy(self._own)

@@ -360,6 +360,42 @@ int  gfpl_lbd_destroy(gfpl_lbd* lbd);
 int  gfpl_lbd_compute(gfpl_lbd* lbd, const uint8_t* images, int n, const gfpl_keyline* keylines,
                       const int* n_kl, uint8_t* desc);
 
+/* ---------------------------------------- LSD line detection (§8(f)2) ---- */
+/* line_descriptor::LSDDetectorC::detect(image, keylines, scale, numOctaves, opts)
+ * (3rdparty/line_descriptor/src/LSDDetector_custom.cpp:218-316) as
+ * StereoFrame::detectLineFeatures calls it (src/stereoFrame.cpp:1160-1186): one octave,
+ * cv::createLineSegmentDetector(opts...) ->detect (OpenCV 3.4.1 lsd.cpp, LSD_REFINE_STD,
+ * scale 1), the keylines' extremes clamped, segments not longer than min_length dropped,
+ * then, when more than n_features remain and n_features != 0, std::sort by response
+ * (include/auxiliar.h:149-154) and the first n_features kept (:1177-1185).  Arithmetic
+ * pinned as the CPU oracle's ledger S1-S7 (oracle/gfpl_lsd_oracle.cpp).   */
+typedef struct gfpl_lsd_params {
+    int    refine;        /* Config::lsdRefine 1 (= LSD_REFINE_STD; only value supported)  */
+    double scale;         /* Config::lsdScale 1 (only value supported)                     */
+    double quant;         /* Config::lsdQuant 2.0                                          */
+    double ang_th;        /* Config::lsdAngTh 22.5                                         */
+    double density_th;    /* Config::lsdDensityTh 0.6                                      */
+    int    n_bins;        /* Config::lsdNBins 1024                                         */
+    double min_length;    /* Config::minLineLength * min(W, H) (src/stereoFrame.cpp:151)   */
+    int    n_features;    /* Config::lsdNFeatures 300 (0 = keep all)                       */
+} gfpl_lsd_params;
+typedef struct gfpl_lsd gfpl_lsd;
+/* images up to 2048 x 2048 (and >= 8 x 8), up to max_images per call; kl_cap keylines out
+ * per image; seg_cap raw segments per image (GFPL_E_CAPACITY beyond).                       */
+int  gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int width, int height, int max_images,
+                     int kl_cap, int seg_cap, gfpl_lsd** out);
+int  gfpl_lsd_destroy(gfpl_lsd* lsd);
+/* all pointers DEVICE: images [n][height][width] u8; keylines [n][kl_cap] receives image j's
+ * keylines (sx sy ex ey angle octave) in the reference's output order, n_kl [n] their count,
+ * response [n][kl_cap] (nullable) KeyLine::response.  Keylines beyond kl_cap are an error
+ * (GFPL_E_CAPACITY).  Synchronises.                                                        */
+int  gfpl_lsd_detect(gfpl_lsd* lsd, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
+                     float* response);
+/* test hook of ledger S2: std::sort(a, a + n, key(x) > key(y)) with key = the high 32 bits of
+ * each element, on DEVICE memory (n <= (width-1)(height-1)); the permutation the seed order
+ * and the response sort use.  Synchronises.                                                 */
+int  gfpl_lsd_sort_desc(gfpl_lsd* lsd, uint64_t* a, int n);
+
 /* ------------------------------------------------- keyframe consumers ---- */
 /* One keyframe's stereo features as KeyFrame::stereo_frame exposes them
  * (src/keyFrame.cpp:26-58, include/stereoFrame.h public members): row i of

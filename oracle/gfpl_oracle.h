@@ -81,6 +81,20 @@ int gfplo_lbd_coefs(float* coef_l, float* coef_g);
 /* LSDDetectorC's numOfPixels of a keyline (cv::LineIterator count, 8-connectivity) */
 int gfplo_lbd_num_pixels(const gfpl_keyline* kl, int width, int height);
 
+/* line_descriptor::LSDDetectorC::detect as StereoFrame::detectLineFeatures calls it
+ * (3rdparty/line_descriptor/src/LSDDetector_custom.cpp:218-316, src/stereoFrame.cpp:1160-1186;
+ * gfpl_lsd_oracle.cpp, ledger S1-S7) on one grey image: keylines (nullable) in the reference's
+ * output order, response (nullable), n_kl; segs (nullable) [seg_cap][4] the raw LSD segments
+ * (after the 0.5 offset, before checkLineExtremes), n_seg their count (nullable). */
+int gfplo_lsd_detect(const gfpl_lsd_params* prm, const uint8_t* image, int width, int height, int kl_cap,
+                     gfpl_keyline* kls, float* response, int* n_kl, float* segs, int seg_cap, int* n_seg);
+/* flsd's per-image constants (S5): prec, rho = quant / sin(prec), min_reg_size */
+int gfplo_lsd_constants(const gfpl_lsd_params* prm, int width, int height, double* prec, double* rho,
+                        int* min_reg_size);
+double gfplo_atan2(double y, double x);                                                  /* S4 */
+/* S2: std::sort(a, a + n) by descending high 32 bits (the library's introsort) */
+int gfplo_sort_desc(uint64_t* a, int n);
+
 /* MapHandler::lookForCommonMatches keyframe-pair stage (src/mapHandler.cpp:
  * 199-470); same contract as gfpl_kf_common_matches but every pointer of the
  * views and outputs is HOST memory. */

@@ -64,6 +64,11 @@ def lib() -> C.CDLL:
         L.gfplo_lbd_gradients.argtypes = [P, C.c_int, C.c_int, P, P, P]; L.gfplo_lbd_gradients.restype = C.c_int
         L.gfplo_lbd_coefs.argtypes = [P, P]; L.gfplo_lbd_coefs.restype = C.c_int
         L.gfplo_lbd_num_pixels.argtypes = [P, C.c_int, C.c_int]; L.gfplo_lbd_num_pixels.restype = C.c_int
+        L.gfplo_lsd_detect.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, P, P, C.c_int, P]
+        L.gfplo_lsd_detect.restype = C.c_int
+        L.gfplo_lsd_constants.argtypes = [P, C.c_int, C.c_int, P, P, P]; L.gfplo_lsd_constants.restype = C.c_int
+        L.gfplo_atan2.argtypes = [C.c_double, C.c_double]; L.gfplo_atan2.restype = C.c_double
+        L.gfplo_sort_desc.argtypes = [P, C.c_int]; L.gfplo_sort_desc.restype = C.c_int
         _L = L
     return _L
 
@@ -314,3 +319,40 @@ def lbd_coefs():
 def lbd_num_pixels(kl) -> int:
     k = np.ascontiguousarray(np.asarray(kl, gfpl.KEYLINE_DT).reshape(1))
     return lib().gfplo_lbd_num_pixels(_p(k), 0, 0)
+
+
+# ---- LSD line detection (gfpl_lsd_oracle.cpp, ledger S1-S7)
+def lsd_detect(image: np.ndarray, params=None, kl_cap: int = 0, seg_cap: int = 8192):
+    """LSDDetectorC::detect + StereoFrame's response filter on one grey image:
+    (keylines KEYLINE_DT, response f32, raw segments [n_seg][4] f32)."""
+    image = np.ascontiguousarray(image, np.uint8)
+    h, w = image.shape
+    prm = params if params is not None else gfpl.LsdParams.reference(w, h)
+    kl_cap = kl_cap or max(seg_cap, 1)
+    kl = np.zeros(kl_cap, gfpl.KEYLINE_DT)
+    rsp = np.zeros(kl_cap, np.float32)
+    segs = np.zeros((seg_cap, 4), np.float32)
+    n = C.c_int(0); ns = C.c_int(0)
+    rc = lib().gfplo_lsd_detect(C.byref(prm), _p(image), w, h, kl_cap, _p(kl), _p(rsp), C.byref(n), _p(segs),
+                                seg_cap, C.byref(ns))
+    if rc != 0:
+        raise RuntimeError(f"gfplo_lsd_detect -> {rc}")
+    return kl[:n.value].copy(), rsp[:n.value].copy(), segs[:min(ns.value, seg_cap)].copy()
+
+
+def lsd_constants(width: int, height: int, params=None):
+    prm = params if params is not None else gfpl.LsdParams.reference(width, height)
+    pr = C.c_double(0); rho = C.c_double(0); mrs = C.c_int(0)
+    lib().gfplo_lsd_constants(C.byref(prm), width, height, C.byref(pr), C.byref(rho), C.byref(mrs))
+    return pr.value, rho.value, mrs.value
+
+
+def atan2(y: float, x: float) -> float:
+    return lib().gfplo_atan2(y, x)
+
+
+def sort_desc(a: np.ndarray) -> np.ndarray:
+    """std::sort of u64 elements by descending high 32 bits (ledger S2)."""
+    a = np.ascontiguousarray(a, np.uint64).copy()
+    lib().gfplo_sort_desc(_p(a), len(a))
+    return a

@@ -1,0 +1,127 @@
+"""GPU LSD line detection (gfpl_lsd_detect, k_lsd.hip) vs the CPU oracle (gfplo_lsd_detect),
+SURVEY.md §8(f)2 (detector part).  Bar: bit-exact keylines (sx sy ex ey angle octave),
+responses and counts for every image of a batch; the std::sort restatement (S2) equal to the
+library's permutation on tie-heavy keys."""
+import numpy as np
+import pytest
+
+import gfpl
+import oracle as O
+from gfpl import pipeline as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _detect(det, imgs):
+    import torch
+    n, h, w = imgs.shape
+    dev = torch.device("cuda", 0)
+    cap = det.kl_cap
+    d_img = torch.from_numpy(np.ascontiguousarray(imgs)).to(dev)
+    d_kl = torch.zeros(n * cap * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_r = torch.zeros(n * cap, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    det.detect_batch(d_img, n, d_kl, d_n, d_r)
+    kl = d_kl.cpu().numpy().view(gfpl.KEYLINE_DT).reshape(n, cap)
+    return kl, d_n.cpu().numpy(), d_r.cpu().numpy().reshape(n, cap)
+
+
+def _check(imgs, params=None, kl_cap=512):
+    n, h, w = imgs.shape
+    prm = params if params is not None else gfpl.LsdParams.reference(w, h)
+    det = gfpl.LSDDetector(w, h, prm, max_images=n, kl_cap=kl_cap)
+    kl, cnt, rsp = _detect(det, imgs)
+    tot = 0
+    for i in range(n):
+        rk, rr, _ = O.lsd_detect(imgs[i], prm)
+        assert cnt[i] == len(rk), (i, cnt[i], len(rk))
+        g = kl[i, :cnt[i]]
+        bad = np.argwhere(g.view(np.uint8).reshape(-1, 24) != rk.view(np.uint8).reshape(-1, 24))
+        assert len(bad) == 0, (i, bad[:5], g[bad[0, 0]], rk[bad[0, 0]])
+        assert (rsp[i, :cnt[i]].view(np.uint32) == rr.view(np.uint32)).all()
+        tot += cnt[i]
+    det.close()
+    return tot
+
+
+def test_lsd_parity_vga_batch():
+    imgs = [gfpl.synth_image(20 + i, i, 640, 480) for i in range(2)]
+    left, right, _, _ = P.synth_stereo_steps(1, 0, 640, 480)
+    l2, r2, _, _ = P.synth_stereo_scene(2, 3, 640, 480)
+    tot = _check(np.stack(imgs + [left, right, l2, r2]))
+    assert tot > 100
+
+
+@pytest.mark.parametrize("cam", ["euroc", "kitti"])
+def test_lsd_parity_cameras(cam):
+    c = gfpl.CAMERAS[cam]
+    w, h = c["width"], c["height"]
+    left, right, _, _ = P.synth_stereo_steps(3, 1, w, h)
+    _check(np.stack([left, right, gfpl.synth_image(5, 0, w, h)]))
+
+
+def test_lsd_parity_global_used_map():
+    """1280 x 720: the used map does not fit the LDS bitmap (global byte map path)."""
+    w, h = 1280, 720
+    left, _, _, _ = P.synth_stereo_steps(4, 0, w, h)
+    _check(np.stack([left]), kl_cap=600)
+
+
+def test_lsd_keep_all_and_small_budget():
+    w, h = 640, 480
+    left, right, _, _ = P.synth_stereo_steps(5, 2, w, h)
+    imgs = np.stack([left, gfpl.synth_image(6, 0, w, h)])
+    _check(imgs, gfpl.LsdParams.reference(w, h, n_features=0), kl_cap=2048)
+    _check(imgs, gfpl.LsdParams.reference(w, h, n_features=5), kl_cap=8)
+
+
+def test_lsd_edge_images():
+    w, h = 64, 48
+    img = np.full((h, w), 90, np.uint8)
+    img2 = img.copy()
+    img2[10:40, 20:50] = 200
+    _check(np.stack([img, img2, np.zeros((h, w), np.uint8)]), kl_cap=16)
+    _check(np.stack([np.full((8, 8), 3, np.uint8)]), kl_cap=4)
+
+
+@pytest.mark.parametrize("n,nkeys", [(17, 2), (700, 3), (2048, 1024), (2049, 7), (30000, 40), (150000, 1024),
+                                     (100000, 1)])
+def test_lsd_sort_matches_std_sort(n, nkeys):
+    import torch
+    rng = np.random.default_rng(n + nkeys)
+    keys = rng.integers(0, nkeys, n).astype(np.uint64)
+    a = (keys << np.uint64(32)) | np.arange(n, dtype=np.uint64)
+    det = gfpl.LSDDetector(640, 480, max_images=1)
+    d = torch.from_numpy(a.view(np.int64).copy()).to("cuda")
+    det.sort_desc(d, n)
+    got = d.cpu().numpy().view(np.uint64)
+    assert (got == O.sort_desc(a)).all()
+    det.close()
+
+
+def test_lsd_feeds_lbd_on_device():
+    """LSD keylines written straight where gfpl_lbd_compute reads them, bit-exact against the
+    oracle LSD -> oracle LBD chain (StereoFrame::detectLineFeatures, src/stereoFrame.cpp:1175-1194)."""
+    import torch
+    w, h = 640, 480
+    left, right, _, _ = P.synth_stereo_steps(7, 0, w, h)
+    imgs = np.stack([left, right])
+    n, cap = 2, 320
+    det = gfpl.LSDDetector(w, h, max_images=n, kl_cap=cap)
+    lbd = gfpl.BinaryDescriptor(w, h, max_images=n, kl_cap=cap)
+    dev = torch.device("cuda", 0)
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_kl = torch.zeros(n * cap * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_desc = torch.zeros(n * cap * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    det.detect_batch(d_img, n, d_kl, d_n)
+    lbd.compute_batch(d_img, n, d_kl, d_n, d_desc)
+    desc = d_desc.cpu().numpy().reshape(n, cap, 32)
+    cnt = d_n.cpu().numpy()
+    for i in range(n):
+        rk, _, _ = O.lsd_detect(imgs[i])
+        rd, _ = O.lbd_compute(imgs[i], rk)
+        assert cnt[i] == len(rk)
+        assert (desc[i, :cnt[i]] == rd).all()
