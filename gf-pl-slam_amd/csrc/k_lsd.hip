@@ -33,16 +33,16 @@
 namespace gfpl {
 
 #define LSD_SORT_LDS 2048          // ranges up to this many elements are sorted in LDS
-#define LSD_RING 1024              // region list entries mirrored in LDS
+#define LSD_RING 256               // region list entries mirrored in LDS
+#define LSD_SMALL 128              // ranges up to this size: one lane runs libstdc++'s serial loop
 #define LSD_USED_LDS_MAX (64 * 1024)   // bytes of LDS bitmap (W*H <= 524288 px)
 
 struct LsdDev {
     int W, H, NP;                  // NP = (W-1)(H-1) sorted pixels
     int n_bins, min_reg_size, seg_cap, kl_cap, n_features;
     double prec, rho, density_th, min_length;
-    float* ang;                    // [n][W*H] fastAtan2 degrees, -1 = NOTDEF
-    float2* csn;                   // [n][W*H] (cos, sin) of float(angle)
-    uint32_t* gxy;                 // [n][W*H] gx (low 16) | gy (high 16), int16 each
+    float4* px;                    // [n][W*H] per pixel: fastAtan2 degrees (-1 = NOTDEF), cos and
+                                   // sin of float(angle), gx (low 16) | gy (high 16) as bits
     unsigned long long* maxg;      // [n] bits of the max norm of defined pixels
     uint64_t* keys;                // [n][NP]
     int* lpos;                     // [n][NP] partition scratch
@@ -68,7 +68,10 @@ constexpr double kDeg2Rad = kPi / 180;
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void mem_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+// global-memory writes of one lane read by others of the same workgroup: a workgroup-scope
+// fence (the workgroup's waves share the CU's write-through L1; an agent-scope fence would
+// write back / invalidate the L2 every time)
+__device__ __forceinline__ void mem_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 __device__ __forceinline__ int below(unsigned long long m) { return __popcll(m & ((1ull << lane_id()) - 1ull)); }
 __device__ __forceinline__ double rl_d(double v, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
@@ -224,8 +227,8 @@ __device__ void heap_sort(uint64_t* a, int len) {
 }
 
 // __unguarded_partition_pivot(a + f, a + l) by the wave; returns the cut
-template <bool LDS>
-__device__ int partition_pivot(uint64_t* a, int f, int l, int* Lp, int* Rp) {
+template <bool LDS, typename IT>
+__device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     const int lane = lane_id();
     const int mid = f + (l - f) / 2;
     // __move_median_to_first(f, f + 1, mid, l - 1)
@@ -243,16 +246,24 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, int* Lp, int* Rp) {
     const uint32_t pk = skey(pv);
     // __unguarded_partition(f + 1, l, f): the stoppers of both scans, ranked
     int cl = 0, cr = 0;
-    for (int base = f + 1; base < l; base += 64) {
-        const int pos = base + lane;
-        const bool v = pos < l;
-        const uint32_t k = v ? skey(a[pos]) : 0;
-        const bool isl = v && k <= pk, isr = v && k >= pk;
-        const unsigned long long ml = __ballot(isl), mr = __ballot(isr);
-        if (isl) Lp[cl + below(ml)] = pos;
-        if (isr) Rp[cr + below(mr)] = pos;
-        cl += __popcll(ml);
-        cr += __popcll(mr);
+    for (int base = f + 1; base < l; base += 256) {   // four chunks' loads in flight
+        uint32_t k4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int pos = base + 64 * c + lane;
+            k4[c] = pos < l ? skey(a[pos]) : 0;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int pos = base + 64 * c + lane;
+            const bool v = pos < l;
+            const bool isl = v && k4[c] <= pk, isr = v && k4[c] >= pk;
+            const unsigned long long ml = __ballot(isl), mr = __ballot(isr);
+            if (isl) Lp[cl + below(ml)] = (IT)pos;
+            if (isr) Rp[cr + below(mr)] = (IT)pos;
+            cl += __popcll(ml);
+            cr += __popcll(mr);
+        }
     }
     ssync<LDS>();
     // K = #k with L[k] < R[k] (L ascending, R[k] = Rp[cr - 1 - k] descending): 64-ary search
@@ -272,14 +283,29 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, int* Lp, int* Rp) {
         lo = nlo;
     }
     const int K = lo;
-    for (int base = 0; base < K; base += 64) {
-        const int k = base + lane;
-        if (k < K) {
-            const int pl = Lp[k], pr = Rp[cr - 1 - k];
-            const uint64_t x = a[pl], y = a[pr];
-            a[pl] = y;
-            a[pr] = x;
+    for (int base = 0; base < K; base += 256) {
+        int pl[4], pr[4];
+        uint64_t x[4], y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int k = base + 64 * c + lane;
+            if (k < K) {
+                pl[c] = Lp[k];
+                pr[c] = Rp[cr - 1 - k];
+            }
         }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (base + 64 * c + lane < K) {
+                x[c] = a[pl[c]];
+                y[c] = a[pr[c]];
+            }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (base + 64 * c + lane < K) {
+                a[pl[c]] = y[c];
+                a[pr[c]] = x[c];
+            }
     }
     const int cL = K < cl ? Lp[K] : INT_MAX;
     const int cR = K >= 1 ? Rp[cr - K] : INT_MAX;
@@ -289,10 +315,80 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, int* Lp, int* Rp) {
 
 struct SortLds {
     uint64_t buf[LSD_SORT_LDS];
-    int lp[LSD_SORT_LDS], rp[LSD_SORT_LDS];
+    uint16_t lp[LSD_SORT_LDS], rp[LSD_SORT_LDS];
     int stk[3 * 64];
     int leaf[2 * 64];
+    int small[3 * 64];
+    int lstk[64 * 3 * 8];   // per-lane stacks of lane_introsort
 };
+
+// libstdc++'s __introsort_loop + final insertion sort of one range [f, l) of an LDS array by
+// one lane (ranges <= LSD_SORT_LDS; the lanes of a wave sort disjoint ranges).  The smaller
+// part of each partition is pushed (ranges are independent, so the order they are finished
+// in does not change the result) and the stack stays <= 8 deep.
+__device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
+    const int F0 = f, L0 = l;
+    int sp = 0;
+    for (;;) {
+        while (l - f > 16) {
+            if (d == 0) {
+                heap_sort(a + f, l - f);
+                break;
+            }
+            --d;
+            const int mid = f + (l - f) / 2;
+            const uint32_t ka = skey(a[f + 1]), kb = skey(a[mid]), kc = skey(a[l - 1]);
+            int sel;
+            if (ka > kb) sel = kb > kc ? mid : (ka > kc ? l - 1 : f + 1);
+            else sel = ka > kc ? f + 1 : (kb > kc ? l - 1 : mid);
+            const uint64_t pv = a[sel];
+            a[sel] = a[f];
+            a[f] = pv;
+            const uint32_t pk = skey(pv);
+            int first = f + 1, last = l;
+            for (;;) {
+                while (skey(a[first]) > pk) ++first;
+                --last;
+                while (pk > skey(a[last])) --last;
+                if (!(first < last)) break;
+                const uint64_t t = a[first];
+                a[first] = a[last];
+                a[last] = t;
+                ++first;
+            }
+            const int cut = first;
+            if (cut - f < l - cut) {
+                st[3 * sp] = f; st[3 * sp + 1] = cut; st[3 * sp + 2] = d;
+                f = cut;
+            } else {
+                st[3 * sp] = cut; st[3 * sp + 1] = l; st[3 * sp + 2] = d;
+                l = cut;
+            }
+            ++sp;
+        }
+        if (sp == 0) break;
+        --sp;
+        f = st[3 * sp]; l = st[3 * sp + 1]; d = st[3 * sp + 2];
+    }
+    for (int i = F0 + 1; i < L0; ++i) {   // stable: equals the final insertion sort here
+        const uint64_t v = a[i];
+        int j = i;
+        while (j > F0 && skey(v) > skey(a[j - 1])) {
+            a[j] = a[j - 1];
+            --j;
+        }
+        a[j] = v;
+    }
+}
+
+__device__ void flush_small(uint64_t* a, SortLds& S, int& ns) {
+    const int lane = lane_id();
+    if (ns == 0) return;
+    lds_sync();
+    if (lane < ns) lane_introsort(a, S.small[3 * lane], S.small[3 * lane + 1], S.small[3 * lane + 2], S.lstk + 24 * lane);
+    lds_sync();
+    ns = 0;
+}
 
 // the final insertion sort, one leaf (<= 16 elements, disjoint) per lane
 template <bool LDS>
@@ -332,8 +428,7 @@ __device__ void add_leaf(uint64_t* a, int* leaf, int& nleaf, int f, int l) {
 __device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
     const int lane = lane_id();
     int* stk = S.stk;
-    int* leaf = S.leaf;
-    int nleaf = 0;
+    int ns = 0;
     if (lane == 0) {
         stk[0] = 0;
         stk[1] = n;
@@ -345,7 +440,7 @@ __device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
         --sp;
         int f = stk[3 * sp], l = stk[3 * sp + 1], d = stk[3 * sp + 2];
         bool done = false;
-        while (l - f > 16) {
+        while (l - f > LSD_SMALL) {
             if (d == 0) {
                 if (lane == 0) heap_sort(a + f, l - f);
                 lds_sync();
@@ -363,9 +458,17 @@ __device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
             ++sp;
             l = cut;
         }
-        if (!done) add_leaf<true>(a, leaf, nleaf, f, l);
+        if (!done && l - f > 1) {
+            if (lane == 0) {
+                S.small[3 * ns] = f;
+                S.small[3 * ns + 1] = l;
+                S.small[3 * ns + 2] = d;
+            }
+            lds_sync();
+            if (++ns == 64) flush_small(a, S, ns);
+        }
     }
-    flush_leaves<true>(a, leaf, nleaf);
+    flush_small(a, S, ns);
 }
 
 }  // namespace
@@ -469,9 +572,7 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
                 norm_def = norm;
             }
         }
-        o.ang[p] = a;
-        o.gxy[p] = g;
-        o.csn[p] = cs;
+        o.px[p] = make_float4(a, cs.x, cs.y, __uint_as_float(g));
     }
     // the image's max norm over defined pixels (norm >= 0: the bits order like the values)
     unsigned long long b = (unsigned long long)__double_as_longlong(norm_def);
@@ -490,7 +591,7 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
     const int y = i / W1, x = i - y * W1;
     const double mg = __longlong_as_double((long long)o.maxg[img]);
     const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
-    const uint32_t g = o.gxy[(size_t)img * o.W * o.H + (size_t)y * o.W + x];
+    const uint32_t g = __float_as_uint(o.px[(size_t)img * o.W * o.H + (size_t)y * o.W + x].w);
     const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
     const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
     const int bin = (int)(norm * bin_coef);
@@ -535,9 +636,7 @@ struct Used {
 struct Rect { double x1, y1, x2, y2, width; };
 
 struct Img {
-    const float* ang;
-    const float2* csn;
-    const uint32_t* gxy;
+    const float4* px;
     uint32_t* reg;
     uint32_t* tmp;
     uint32_t* ring;   // LDS
@@ -545,7 +644,7 @@ struct Img {
 };
 
 __device__ __forceinline__ double modgrad(const Img& I, int x, int y) {
-    const uint32_t g = I.gxy[y * I.W + x];
+    const uint32_t g = __float_as_uint(I.px[y * I.W + x].w);
     const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
     return sqrt((double)(gx * gx + gy * gy) / 4.0);
 }
@@ -561,7 +660,7 @@ template <bool LU>
 __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, double prec, double& reg_angle) {
     const int lane = lane_id();
     int n = 0;
-    reg_angle = (double)I.ang[sy * I.W + sx] * kDeg2Rad;
+    reg_angle = (double)I.px[sy * I.W + sx].x * kDeg2Rad;
     float sumdx = (float)det_cos(reg_angle), sumdy = (float)det_sin(reg_angle);   // S3
     const uint32_t s = ((uint32_t)sy << 16) | (uint32_t)sx;
     if (lane == 0) {
@@ -572,45 +671,62 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, doub
     n = 1;
     U.sync();
     lds_sync();
-    const int dxl = lane % 3 - 1, dyl = lane / 3 - 1;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t r = reg_at(I, i, n);
-        const int rx = (int)(r & 0xffff), ry = (int)(r >> 16);
-        const int xx = rx + dxl, yy = ry + dyl;
-        const bool ok = lane < 9 && xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
-        float a = -1.0f;
-        float2 cs = make_float2(0.f, 0.f);
-        if (ok && !U.get(xx, yy)) {
-            a = I.ang[yy * I.W + xx];
-            if (a >= 0.0f) cs = I.csn[yy * I.W + xx];
+    // the region list is expanded in batches of up to 7 points: lanes 9g..9g+8 load point
+    // i+g's 3x3 neighbour records in one round trip, then the points are processed in list
+    // order, each reading the used map as the earlier points of the batch left it
+    const int g = lane / 9, t9 = lane - 9 * g;
+    const int dxl = t9 % 3 - 1, dyl = t9 / 3 - 1;
+    for (int i = 0; i < n;) {
+        const int nb = min(7, n - i);
+        if (n - i > LSD_RING) mem_sync();
+        int rx = 0, ry = 0, xx = 0, yy = 0;
+        bool ok = false;
+        if (g < nb) {
+            const int idx = i + g;
+            const uint32_t r = (n - idx <= LSD_RING) ? I.ring[idx & (LSD_RING - 1)] : I.reg[idx];
+            rx = (int)(r & 0xffff);
+            ry = (int)(r >> 16);
+            xx = rx + dxl;
+            yy = ry + dyl;
+            ok = xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
         }
+        float4 q = make_float4(-1.0f, 0.f, 0.f, 0.f);
+        if (ok) q = I.px[yy * I.W + xx];
+        for (int k = 0; k < nb; ++k) {
+            const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy);
+            const unsigned long long m = __ballot(av) >> (9 * k);
+            if (!m) continue;
+            const int b = 9 * k;
+            const int prx = rl_i(rx, b), pry = rl_i(ry, b);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            const float at = rl_f(a, t);
-            if (at < 0.0f) continue;   // out of the image, used, or NOTDEF
-            // isAligned (lsd.cpp)
-            const double ad = (double)at * kDeg2Rad;
-            double nt = reg_angle - ad;
-            if (nt < 0) nt = -nt;
-            if (nt > k32Pi) {
-                nt -= k2Pi;
+            for (int t = 0; t < 9; ++t) {
+                if (!((m >> t) & 1ull)) continue;   // out of the image, used, or NOTDEF
+                const float at = rl_f(q.x, b + t);
+                // isAligned (lsd.cpp)
+                const double ad = (double)at * kDeg2Rad;
+                double nt = reg_angle - ad;
                 if (nt < 0) nt = -nt;
+                if (nt > k32Pi) {
+                    nt -= k2Pi;
+                    if (nt < 0) nt = -nt;
+                }
+                if (!(nt <= prec)) continue;
+                const int px = prx + t % 3 - 1, py = pry + t / 3 - 1;
+                const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
+                if (lane == 0) {
+                    U.set1(px, py);
+                    I.reg[n] = e;
+                    I.ring[n & (LSD_RING - 1)] = e;
+                }
+                ++n;
+                sumdx += rl_f(q.y, b + t);
+                sumdy += rl_f(q.z, b + t);
+                reg_angle = (double)fast_atan2(sumdy, sumdx) * kDeg2Rad;
             }
-            if (!(nt <= prec)) continue;
-            const int px = rx + t % 3 - 1, py = ry + t / 3 - 1;
-            const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
-            if (lane == 0) {
-                U.set1(px, py);
-                I.reg[n] = e;
-                I.ring[n & (LSD_RING - 1)] = e;
-            }
-            ++n;
-            sumdx += rl_f(cs.x, t);
-            sumdy += rl_f(cs.y, t);
-            reg_angle = (double)fast_atan2(sumdy, sumdx) * kDeg2Rad;
+            lds_sync();
+            if (!LU) mem_sync();
         }
-        lds_sync();
-        if (!LU) mem_sync();
+        i += nb;
     }
     mem_sync();   // the region list (global) is read by every lane next
     return n;
@@ -770,7 +886,7 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
     const uint32_t r0 = I.reg[0];
     const int sx = (int)(r0 & 0xffff), sy = (int)(r0 >> 16);
     const double xc = (double)sx, yc = (double)sy;
-    const double ang_c = (double)I.ang[sy * I.W + sx] * kDeg2Rad;
+    const double ang_c = (double)I.px[sy * I.W + sx].x * kDeg2Rad;
     double sum = 0, s_sum = 0;
     int cnt = 0;
     for (int b = 0; b < n; b += 64) {
@@ -782,7 +898,7 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
             const int x = (int)(r & 0xffff), y = (int)(r >> 16);
             U.clr(x, y);
             in = sqrt(((double)x - xc) * ((double)x - xc) + ((double)y - yc) * ((double)y - yc)) < rec.width;
-            if (in) ad = angle_diff_signed((double)I.ang[y * I.W + x] * kDeg2Rad, ang_c);
+            if (in) ad = angle_diff_signed((double)I.px[y * I.W + x].x * kDeg2Rad, ang_c);
         }
         const unsigned long long m = __ballot(in);
         const int c = min(64, n - b);
@@ -809,7 +925,7 @@ template <bool LU>
 __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ring) {
     const int lane = lane_id();
     const size_t off = (size_t)img * o.W * o.H;
-    Img I{o.ang + off, o.csn + off, o.gxy + off, o.reg + off, o.tmp + off, ring, o.W, o.H};
+    Img I{o.px + off, o.reg + off, o.tmp + off, ring, o.W, o.H};
     Used<LU> U{bits, o.used_g + off, o.W};
     if (LU) {
         const int nw = (o.W * o.H + 31) >> 5;
@@ -820,17 +936,17 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
         mem_sync();
     }
     const uint64_t* keys = o.keys + (size_t)img * o.NP;
+    const float* pxf = (const float*)I.px;
     int nseg = 0;
+    // chunk c's keys and angles are loaded while chunk c-1 is processed
+    uint64_t e_next = lane < o.NP ? keys[lane] : 0;
     for (int base = 0; base < o.NP; base += 64) {
         const int i = base + lane;
-        int px = 0, py = 0;
-        bool cand = false;
-        if (i < o.NP) {
-            const uint64_t e = keys[i];
-            px = (int)(e & 0xffff);
-            py = (int)((e >> 16) & 0xffff);
-            cand = I.ang[py * o.W + px] >= 0.0f;
-        }
+        const uint64_t e = e_next;
+        int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0xffff);
+        const float a0 = i < o.NP ? pxf[4 * (py * o.W + px)] : -1.0f;
+        e_next = base + 64 + lane < o.NP ? keys[base + 64 + lane] : 0;
+        bool cand = a0 >= 0.0f;
         for (;;) {
             const unsigned long long m = __ballot(cand && !U.get(px, py));
             if (!m) break;
@@ -990,17 +1106,15 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     o->lds_used = (px + 31) / 32 * 4 <= LSD_USED_LDS_MAX;
     o->lds_bytes = (px + 31) / 32 * 4 + 4 * LSD_RING;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_ang = al(4 * M * px), b_csn = al(8 * M * px), b_gxy = al(4 * M * px), b_max = al(8 * M),
+    const size_t b_px = al(16 * M * px), b_max = al(8 * M),
                  b_keys = al(8 * M * NP), b_pos = al(4 * M * NP), b_reg = al(4 * M * px),
                  b_used = o->lds_used ? 0 : al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
                  b_klt = al(24 * M * SC), b_rk = al(8 * M * SC), b_rl = al(4 * M * SC);
-    const size_t total = b_ang + b_csn + b_gxy + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
+    const size_t total = b_px + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
                          b_klt + b_rk + 2 * b_rl + 256;
     if (hipMalloc(&o->base, total) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
-    d.ang = (float*)p; p += b_ang;
-    d.csn = (float2*)p; p += b_csn;
-    d.gxy = (uint32_t*)p; p += b_gxy;
+    d.px = (float4*)p; p += b_px;
     d.maxg = (unsigned long long*)p; p += b_max;
     d.keys = (uint64_t*)p; p += b_keys;
     d.lpos = (int*)p; p += b_pos;
