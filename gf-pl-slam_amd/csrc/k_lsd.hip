@@ -323,9 +323,9 @@ struct SortLds {
 };
 
 // libstdc++'s __introsort_loop + final insertion sort of one range [f, l) of an LDS array by
-// one lane (ranges <= LSD_SORT_LDS; the lanes of a wave sort disjoint ranges).  The smaller
-// part of each partition is pushed (ranges are independent, so the order they are finished
-// in does not change the result) and the stack stays <= 8 deep.
+// one lane (ranges <= LSD_SMALL; the lanes of a wave sort disjoint ranges).  The larger part
+// of each partition is pushed and the smaller one continued (ranges are independent, so the
+// order they are finished in does not change the result): the stack stays <= 8 deep.
 __device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
     const int F0 = f, L0 = l;
     int sp = 0;
@@ -357,14 +357,15 @@ __device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
                 ++first;
             }
             const int cut = first;
-            if (cut - f < l - cut) {
-                st[3 * sp] = f; st[3 * sp + 1] = cut; st[3 * sp + 2] = d;
+            // push the larger part (if it needs work), continue with the smaller one: every
+            // stacked range is at least twice the current one, so the stack stays <= 5 deep
+            if (cut - f >= l - cut) {
+                if (cut - f > 16) { st[3 * sp] = f; st[3 * sp + 1] = cut; st[3 * sp + 2] = d; ++sp; }
                 f = cut;
             } else {
-                st[3 * sp] = cut; st[3 * sp + 1] = l; st[3 * sp + 2] = d;
+                if (l - cut > 16) { st[3 * sp] = cut; st[3 * sp + 1] = l; st[3 * sp + 2] = d; ++sp; }
                 l = cut;
             }
-            ++sp;
         }
         if (sp == 0) break;
         --sp;
@@ -938,14 +939,17 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
     const uint64_t* keys = o.keys + (size_t)img * o.NP;
     const float* pxf = (const float*)I.px;
     int nseg = 0;
-    // chunk c's keys and angles are loaded while chunk c-1 is processed
-    uint64_t e_next = lane < o.NP ? keys[lane] : 0;
+    // software pipeline: chunk c+2's keys and chunk c+1's angles load while chunk c is processed
+    uint64_t e1 = lane < o.NP ? keys[lane] : 0;
+    float a1 = lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+    uint64_t e2 = 64 + lane < o.NP ? keys[64 + lane] : 0;
     for (int base = 0; base < o.NP; base += 64) {
-        const int i = base + lane;
-        const uint64_t e = e_next;
+        const uint64_t e = e1;
         int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0xffff);
-        const float a0 = i < o.NP ? pxf[4 * (py * o.W + px)] : -1.0f;
-        e_next = base + 64 + lane < o.NP ? keys[base + 64 + lane] : 0;
+        const float a0 = a1;
+        e1 = e2;
+        a1 = base + 64 + lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+        e2 = base + 128 + lane < o.NP ? keys[base + 128 + lane] : 0;
         bool cand = a0 >= 0.0f;
         for (;;) {
             const unsigned long long m = __ballot(cand && !U.get(px, py));
