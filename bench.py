@@ -355,14 +355,42 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
                   "keylines_per_image": n_lines,
                   "parity_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
     lbd.close()
+    # LSD (gfpl_lsd_detect, the reference's LSDOptions, 300 keylines kept): its per-image chain
+    # (sort + region growing) is latency-bound, so it is measured at 4 images per CU
+    n_lsd = 1024
+    from gfpl.pipeline import synth_stereo_steps
+    li = np.stack([synth_stereo_steps(i // 2, 0, W, H)[i % 2] for i in range(8)]
+                  + [imgs[i % n_img] for i in range(n_lsd - 8)])
+    d_li = torch.from_numpy(li).to(dev)
+    lsd = gfpl.LSDDetector(W, H, max_images=n_lsd, kl_cap=320)
+    d_kl = torch.zeros(n_lsd * 320 * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(n_lsd, dtype=torch.int32, device=dev)
+    lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
+    t = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
+        t.append(time.perf_counter() - t0)
+    kl_all = d_kl.cpu().numpy().view(gfpl.KEYLINE_DT).reshape(n_lsd, 320)
+    cnt = d_n.cpu().numpy()
+    par = True
+    for i in (0, 1, 8):
+        rk, _, _ = O.lsd_detect(li[i])
+        par = par and int(cnt[i]) == len(rk) and kl_all[i, :cnt[i]].tobytes() == rk.tobytes()
+    out["lsd"] = {"images_per_s": n_lsd / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
+                  "images_per_call": n_lsd, "keylines_per_image": float(cnt.mean()),
+                  "parity_images_0_1_8": bool(par),
+                  "data": "8 staircase stereo images + gfpl_synth_image textures"}
+    lsd.close()
     # with detection on the GPU a host-fed pipeline uploads the two grey images of a stereo
     # frame instead of the pyramid + features: the PCIe ceiling derived from the measured rate
     out["host_fed_images_ceiling"] = {"value": upload_Bps / (2.0 * W * H), "unit": "stereo frames/s",
-                                      "note": "derived: measured upload GB/s / (2 x W x H bytes); LSD stays on the host"}
+                                      "note": "derived: measured upload GB/s / (2 x W x H bytes); every detector on the GPU"}
     return out
 
 
-def pipeline_rate(cam, cfg, B=1024, steps=3):
+def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False):
     """Images in HBM to poses on one device (gfpl.pipeline), measured after the
     timed tracking steps (not part of `value`): per step ORB on both images of B stereo frames,
     LBD of the given keylines, one StereoFrameHandler step; staircase scene
@@ -374,8 +402,9 @@ def pipeline_rate(cam, cfg, B=1024, steps=3):
     W, H, KL = int(cam.width), int(cam.height), 320
     dev = torch.device("cuda", torch.cuda.current_device())
     ctx = gfpl.Context(cam, cfg)
-    pipe = ImagePipeline(ctx, cam, B, KL)
+    pipe = ImagePipeline(ctx, cam, B, KL, lsd=lsd)
     g = gfpl.StereoFrameHandler(ctx, B, pipe.kp_cap, KL)
+    det = (lambda f: pipe.detect_images(f[0], f[1], f[6])) if lsd else (lambda f: pipe.detect(*f))
     frames = []
     for k in range(steps + 2):
         sc = [synth_stereo_steps(b, k, W, H) for b in range(B)]
@@ -389,13 +418,13 @@ def pipeline_rate(cam, cfg, B=1024, steps=3):
         frames.append((to(np.stack([x[0] for x in sc])), to(np.stack([x[1] for x in sc])),
                        to(kl[0].view(np.uint8).reshape(-1)), to(n[0]), to(kl[1].view(np.uint8).reshape(-1)), to(n[1]),
                        torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev)))
-    g.initialize(pipe.detect(*frames[0]))
-    g.frameStep(pipe.detect(*frames[1]))
+    g.initialize(det(frames[0]))
+    g.frameStep(det(frames[1]))
     t_det = t_trk = 0.0
     for k in range(2, steps + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        fr = pipe.detect(*frames[k])
+        fr = det(frames[k])
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         g.frameStep(fr)
@@ -407,7 +436,8 @@ def pipeline_rate(cam, cfg, B=1024, steps=3):
     return {"value": B * steps / (t_det + t_trk), "unit": "stereo frames/s", "sequences": B, "steps": steps,
             "detect_ms_per_step": 1e3 * t_det / steps, "track_ms_per_step": 1e3 * t_trk / steps,
             "matched_pt_seq0": len(tr["matched_pt"]), "matched_ls_seq0": len(tr["matched_ls"]),
-            "scene": "staircase bands at disparity 2/12/20/8 px, 2000 ORB, 300 keylines per side (LSD on the host)"}
+            "scene": "staircase bands at disparity 2/12/20/8 px, 2000 ORB, " +
+                     ("LSD on the device (<= 300 keylines per side)" if lsd else "300 given keylines per side")}
 
 
 def main():
@@ -584,6 +614,7 @@ def main():
             det = detection_rates(cam, in_bytes * K / up_total)
             try:
                 det["images_to_poses"] = pipeline_rate(cam, cfg)
+                det["images_to_poses_lsd"] = pipeline_rate(cam, cfg, lsd=True)
             except Exception as e:   # reported, never fatal to the contract line
                 det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}
         out = {

@@ -1,11 +1,11 @@
 """Images -> detection -> tracking on one device (SURVEY.md §8(f)1-2 feeding rows a-e).
 
 StereoFrame's detectFeatures (src/stereoFrame.cpp:1145-1200) runs ORB_SLAM2::ORBextractor on
-both images and BinaryDescriptor::compute on the LSD keylines of both; here both run on the
-GPU (gfpl_orb_extract, gfpl_lbd_compute) straight into the device buffers a gfpl_frames view
-points at — keypoints, descriptors, the right pyramid for the sub-pixel SAD — so the tracker
-(StereoFrameHandler) reads them without a copy.  LSD line detection stays on the host: the
-keylines are an input.
+both images, LSDDetectorC::detect and BinaryDescriptor::compute on both; here all three run on
+the GPU (gfpl_orb_extract, gfpl_lsd_detect, gfpl_lbd_compute) straight into the device buffers a
+gfpl_frames view points at — keypoints, descriptors, keylines, the right pyramid for the
+sub-pixel SAD — so the tracker (StereoFrameHandler) reads them without a copy.
+detect_images() is that whole path; detect() takes the keylines as an input instead.
 
 The synthetic scene helper renders what a calibrated rig would see while translating along
 x over a fronto-parallel textured plane: every pixel has the same disparity, the right image is
@@ -17,8 +17,8 @@ import functools
 
 import numpy as np
 
-from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, ORBextractor, make_frames, synth_image,
-               synth_keylines)
+from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, LSDDetector, LsdParams, ORBextractor,
+               make_frames, synth_image, synth_keylines)
 
 
 @functools.lru_cache(maxsize=4096)
@@ -102,14 +102,16 @@ def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparitie
 
 class ImagePipeline:
     """Detection for B sequences on the device, as gfpl_frames for StereoFrameHandler:
-    ORB (nfeatures, scale 1.2, the camera's levels, FAST 20 / 7) and LBD of given keylines."""
+    ORB (nfeatures, scale 1.2, the camera's levels, FAST 20 / 7), LSD (lsd=True: the reference's
+    LSDOptions, Config::lsdNFeatures = 300, min length 0.025 * min(W, H)) and LBD."""
 
-    def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000):
+    def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000, lsd: bool = False):
         import torch
         self.cam, self.B, self.kl_cap = cam, batch, kl_cap
         W, H = int(cam.width), int(cam.height)
         self.orb = ORBextractor(nfeatures, 1.2, int(cam.n_levels), 20, 7, W, H, max_images=batch, ctx=ctx)
         self.lbd = BinaryDescriptor(W, H, max_images=batch, kl_cap=kl_cap, ctx=ctx)
+        self.lsd = LSDDetector(W, H, LsdParams.reference(W, H), max_images=batch, kl_cap=kl_cap, ctx=ctx) if lsd else None
         self.kp_cap = self.orb.kp_cap
         dev = torch.device("cuda", torch.cuda.current_device())
         B, kc = batch, self.kp_cap
@@ -127,13 +129,27 @@ class ImagePipeline:
     def detect(self, left, right, kl_left, n_kl_left, kl_right, n_kl_right, time_stamp):
         """left / right: device u8 [B][H][W]; kl_*: device KEYLINE_DT rows [B][kl_cap];
         n_kl_*: device int32 [B]; time_stamp: device f64 [B].  Returns the gfpl_frames."""
+        for side, (kl, n) in enumerate(((kl_left, n_kl_left), (kl_right, n_kl_right))):
+            self.kl[side].copy_(kl.view(-1))
+            self.n_kl[side].copy_(n)
+        return self._describe(left, right, time_stamp)
+
+    def detect_images(self, left, right, time_stamp):
+        """StereoFrame::detectFeatures with every detector on the device: LSD keylines of both
+        images (detectLineFeatures, src/stereoFrame.cpp:1160-1186) written where LBD and the
+        tracker read them, then ORB and LBD.  Needs lsd=True."""
+        if self.lsd is None:
+            raise RuntimeError("ImagePipeline(lsd=True) runs LSD on the device")
+        for side, img in ((0, left), (1, right)):
+            self.lsd.detect_batch(img, self.B, self.kl[side], self.n_kl[side])
+        return self._describe(left, right, time_stamp)
+
+    def _describe(self, left, right, time_stamp):
         B, pb = self.B, int(self.cam.pyr_bytes)
         for side, img in ((0, left), (1, right)):
             pyr = self.pyr_l if side == 0 else self.pyr_r
             self.orb.extract(img, B, self.kps[side], self.pdesc[side], self.n_kp[side], None, None, pyr, pb)
-        for side, (kl, n) in enumerate(((kl_left, n_kl_left), (kl_right, n_kl_right))):
-            self.kl[side].copy_(kl.view(-1))
-            self.n_kl[side].copy_(n)
+        for side in range(2):
             self.lbd.compute_batch(left if side == 0 else right, B, self.kl[side], self.n_kl[side], self.ldesc[side])
         self.ts.copy_(time_stamp)
         arrs = [self.n_kp[0], self.n_kp[1], self.kps[0], self.kps[1], self.pdesc[0], self.pdesc[1],
@@ -143,3 +159,5 @@ class ImagePipeline:
     def close(self):
         self.orb.close()
         self.lbd.close()
+        if self.lsd is not None:
+            self.lsd.close()

@@ -112,3 +112,57 @@ def test_images_to_poses_match_the_oracle_pipeline(disparity):
     else:
         assert all((c[0] if disparity == 3 else c[1]) > 100 for c in counts), counts
     pipe.close()
+
+
+def test_images_to_poses_with_lsd_on_device():
+    """Every detector on the device (ImagePipeline.detect_images: LSD -> LBD, ORB) against the
+    oracle chain (LSD oracle -> LBD oracle, ORB oracle, tracker oracle) on the staircase scene."""
+    import torch
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    B, F, KL = 2, 4, 320
+    W, H = int(cam.width), int(cam.height)
+    ctx = gfpl.Context(cam, cfg)
+    pipe = ImagePipeline(ctx, cam, B, KL, lsd=True)
+    KP = pipe.kp_cap
+    g = gfpl.StereoFrameHandler(ctx, B, KP, KL)
+    orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(B)]
+    dev = torch.device("cuda", 0)
+    bad, counts = [], []
+    for k in range(F):
+        imgs = [synth_stereo_steps(b, k, W, H)[:2] for b in range(B)]
+        scenes = [(L, R, O.lsd_detect(L)[0], O.lsd_detect(R)[0]) for L, R in imgs]
+        left = torch.from_numpy(np.stack([s[0] for s in scenes])).to(dev)
+        right = torch.from_numpy(np.stack([s[1] for s in scenes])).to(dev)
+        fr = pipe.detect_images(left, right, torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
+        hfr, harr = _host_frames(cam, scenes, KP, KL, 0.05 * k)
+        d = [t.cpu().numpy() for t in fr._keep]
+        for side in range(2):
+            nl_d = d[6 + side]
+            assert (nl_d == harr[6 + side]).all(), (k, side, nl_d, harr[6 + side])
+            kld = d[8 + side].view(gfpl.KEYLINE_DT).reshape(B, KL)
+            ldd = d[10 + side].reshape(B, KL, 32)
+            for b in range(B):
+                n2 = int(nl_d[b])
+                assert kld[b, :n2].tobytes() == harr[8 + side][b, :n2].tobytes(), (k, side, b)
+                assert (ldd[b, :n2] == harr[10 + side][b, :n2]).all(), (k, side, b)
+        torch.cuda.synchronize()
+        if k == 0:
+            g.initialize(fr)
+            for b, o in enumerate(orc):
+                o.initialize(hfr, b)
+            continue
+        g.frameStep(fr)
+        for b, o in enumerate(orc):
+            o.insertStereoPair(hfr, b)
+            o.optimizePose()
+            tr = o.read_track()
+            counts.append((len(tr["matched_pt"]), len(tr["matched_ls"])))
+            o.updateFrame()
+            gp, op = g.read_frame(gfpl.PREV, b), o.read_frame(gfpl.PREV)
+            bad += compare_core(gp, op, f"f{k} s{b} ")
+            bad += compare_pose(gp, op, what=f"f{k} s{b} ")[0]
+            bad += compare_track(g.read_last_track(b), tr, f"f{k} s{b} ")
+    assert not bad, "\n".join(bad[:30])
+    assert all(c[1] > 5 for c in counts), counts
+    pipe.close()
