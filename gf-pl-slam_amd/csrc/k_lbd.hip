@@ -45,6 +45,9 @@ __device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i : (i >= n
 // LDS written by some lanes of a wave and read by others: the wave's DS operations complete
 // in order; the clobber keeps the compiler from moving accesses across
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// L5: correctly rounded float sqrt.  __fsqrt_rn lowers to the bare v_sqrt_f32 (1 ulp); the f64
+// sqrt is correctly rounded (N1) and rounding its result to float is exact for sqrt (53 >= 2*24+2)
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
 }  // namespace
 
 // L1 + L2 fused: GaussianBlur 5x5 (rows exact, columns (s + 2^15) >> 16, REFLECT_101) and
@@ -218,7 +221,7 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
         const int sm = (k < 2 ? 0 : 4) + (k & 1), s2 = sm + 2;
         const float t = S72[8 * b + sm] * invN;
         D[8 * b + k] = t;
-        D[8 * b + 4 + k] = __fsqrt_rn(S72[8 * b + s2] * invN - t * t);
+        D[8 * b + 4 + k] = sqrt_rn(S72[8 * b + s2] * invN - t * t);
     }
     lds_sync();
     // normalisation (sequential sums in the reference's order), clamp, renormalisation
@@ -229,8 +232,8 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
 #pragma unroll
         for (int k = 4; k < 8; ++k) ts += D[8 * b + k] * D[8 * b + k];
     }
-    tm = __fdiv_rn(1.0f, __fsqrt_rn(tm));
-    ts = __fdiv_rn(1.0f, __fsqrt_rn(ts));
+    tm = __fdiv_rn(1.0f, sqrt_rn(tm));
+    ts = __fdiv_rn(1.0f, sqrt_rn(ts));
     float e[2];
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -248,7 +251,7 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
     lds_sync();
     float t2 = 0.0f;
     for (int i = 0; i < LBD_BANDS * 8; ++i) t2 += D[i] * D[i];
-    t2 = __fdiv_rn(1.0f, __fsqrt_rn(t2));
+    t2 = __fdiv_rn(1.0f, sqrt_rn(t2));
     if (lane < 32) {
         const int pi = o.pairs[lane] & 15, pj = o.pairs[lane] >> 4;
         uint32_t r = 0;
@@ -337,6 +340,17 @@ extern "C" int gfpl_lbd_destroy(gfpl_lbd* o) {
     if (o->base) (void)hipFree(o->base);
     delete o;
     return GFPL_OK;
+}
+
+extern "C" int gfpl_lbd_gradients(gfpl_lbd* o, const uint8_t* image, uint32_t* grad) {
+    if (!o || !image || !grad) return GFPL_E_INVALID;
+    if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
+    const LbdDev& d = o->d;
+    hipLaunchKernelGGL(k_lbd_grad, dim3((d.W + LBD_TW - 1) / LBD_TW, (d.H + LBD_TH - 1) / LBD_TH, 1), dim3(256), 0,
+                       o->stream, d, image);
+    if (hipMemcpyAsync(grad, d.grad, 4 * (size_t)d.W * d.H, hipMemcpyDeviceToDevice, o->stream) != hipSuccess)
+        return GFPL_E_HIP;
+    return hipStreamSynchronize(o->stream) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
 }
 
 extern "C" int gfpl_lbd_compute(gfpl_lbd* o, const uint8_t* images, int n, const gfpl_keyline* keylines,

@@ -321,6 +321,7 @@ def hiplib() -> C.CDLL:
             "gfpl_lbd_create": ([P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_lbd_destroy": ([P], C.c_int),
             "gfpl_lbd_compute": ([P, P, C.c_int, P, P, P], C.c_int),
+            "gfpl_lbd_gradients": ([P, P, P], C.c_int),
         }
         for n, (a, r) in sigs.items():
             try:

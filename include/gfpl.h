@@ -359,6 +359,9 @@ int  gfpl_lbd_destroy(gfpl_lbd* lbd);
  * 32-byte LBD for keyline i < n_kl[j].  Synchronises.                                      */
 int  gfpl_lbd_compute(gfpl_lbd* lbd, const uint8_t* images, int n, const gfpl_keyline* keylines,
                       const int* n_kl, uint8_t* desc);
+/* test hook of ledger L1-L2: the Gaussian-blurred image's Sobel derivatives of one DEVICE image,
+ * grad [height][width] (DEVICE) = dx (low 16 bits) | dy (high 16 bits).  Synchronises.      */
+int  gfpl_lbd_gradients(gfpl_lbd* lbd, const uint8_t* image, uint32_t* grad);
 
 /* ---------------------------------------- LSD line detection (§8(f)2) ---- */
 /* line_descriptor::LSDDetectorC::detect(image, keylines, scale, numOctaves, opts)
