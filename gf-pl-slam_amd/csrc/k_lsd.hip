@@ -246,15 +246,16 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     const uint32_t pk = skey(pv);
     // __unguarded_partition(f + 1, l, f): the stoppers of both scans, ranked
     int cl = 0, cr = 0;
-    for (int base = f + 1; base < l; base += 256) {   // four chunks' loads in flight
-        uint32_t k4[4];
+    constexpr int CH = LDS ? 4 : 16;   // chunks' loads in flight (HBM: sixteen)
+    for (int base = f + 1; base < l; base += 64 * CH) {
+        uint32_t k4[CH];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < CH; ++c) {
             const int pos = base + 64 * c + lane;
             k4[c] = pos < l ? skey(a[pos]) : 0;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < CH; ++c) {
             const int pos = base + 64 * c + lane;
             const bool v = pos < l;
             const bool isl = v && k4[c] <= pk, isr = v && k4[c] >= pk;
@@ -283,11 +284,12 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
         lo = nlo;
     }
     const int K = lo;
-    for (int base = 0; base < K; base += 256) {
-        int pl[4], pr[4];
-        uint64_t x[4], y[4];
+    constexpr int SW = LDS ? 4 : 8;
+    for (int base = 0; base < K; base += 64 * SW) {
+        int pl[SW], pr[SW];
+        uint64_t x[SW], y[SW];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < SW; ++c) {
             const int k = base + 64 * c + lane;
             if (k < K) {
                 pl[c] = Lp[k];
@@ -295,13 +297,13 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
             }
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < SW; ++c)
             if (base + 64 * c + lane < K) {
                 x[c] = a[pl[c]];
                 y[c] = a[pr[c]];
             }
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < SW; ++c)
             if (base + 64 * c + lane < K) {
                 a[pl[c]] = y[c];
                 a[pr[c]] = x[c];
@@ -489,6 +491,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) 
     const int depth = 2 * (31 - __clz(n));
     if (n <= LSD_SORT_LDS) {
         const int lane = lane_id();
+#pragma unroll 8
         for (int i = lane; i < n; i += 64) P.inner.buf[i] = a[i];
         lds_sync();
         introsort_lds(P.inner.buf, n, depth, P.inner);
@@ -516,6 +519,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) 
         while (l - f > 16) {
             if (l - f <= LSD_SORT_LDS) {
                 const int m = l - f;
+#pragma unroll 8
                 for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
                 lds_sync();
                 introsort_lds(S.buf, m, d, S);
@@ -658,10 +662,12 @@ __device__ __forceinline__ uint32_t reg_at(const Img& I, int i, int n) {
 
 // region_grow (lsd.cpp): returns the region size; reg / ring hold the points in push order
 template <bool LU>
-__device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, double prec, double& reg_angle) {
+// (seed_deg: the seed's angle record; the caller fences before reading the list from HBM)
+__device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, float seed_deg, double prec,
+                           double& reg_angle) {
     const int lane = lane_id();
     int n = 0;
-    reg_angle = (double)I.px[sy * I.W + sx].x * kDeg2Rad;
+    reg_angle = (double)seed_deg * kDeg2Rad;
     float sumdx = (float)det_cos(reg_angle), sumdy = (float)det_sin(reg_angle);   // S3
     const uint32_t s = ((uint32_t)sy << 16) | (uint32_t)sx;
     if (lane == 0) {
@@ -729,7 +735,6 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, doub
         }
         i += nb;
     }
-    mem_sync();   // the region list (global) is read by every lane next
     return n;
 }
 
@@ -914,7 +919,8 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
     U.sync();
     const double mean_angle = sum / (double)cnt;
     const double tau = 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / (double)cnt + mean_angle * mean_angle);
-    n = region_grow<LU>(I, U, sx, sy, tau, reg_angle);
+    n = region_grow<LU>(I, U, sx, sy, I.px[sy * I.W + sx].x, tau, reg_angle);
+    mem_sync();   // the region list (HBM) is read by every lane next
     if (n < 2) return false;
     region2rect(I, n, reg_angle, prec, rec);
     density = (double)n / (rdist(rec) * rec.width);
@@ -942,6 +948,8 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
     // software pipeline: chunk c+2's keys and chunk c+1's angles load while chunk c is processed
     uint64_t e1 = lane < o.NP ? keys[lane] : 0;
     float a1 = lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+    // (a candidate's angle record comes with the scan: a region's first round trip is its
+    // seed's neighbourhood)
     uint64_t e2 = 64 + lane < o.NP ? keys[64 + lane] : 0;
     for (int base = 0; base < o.NP; base += 64) {
         const uint64_t e = e1;
@@ -958,8 +966,9 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
             if (lane <= j) cand = false;
             const int sx = rl_i(px, j), sy = rl_i(py, j);
             double reg_angle;
-            int n = region_grow<LU>(I, U, sx, sy, o.prec, reg_angle);
+            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle);
             if (n < o.min_reg_size) continue;
+            mem_sync();   // the region list (HBM) is read by every lane next
             Rect rec;
             region2rect(I, n, reg_angle, o.prec, rec);
             if (!refine<LU>(I, U, n, reg_angle, o.prec, rec, o.density_th)) continue;
