@@ -664,7 +664,7 @@ __device__ __forceinline__ uint32_t reg_at(const Img& I, int i, int n) {
 template <bool LU>
 // (seed_deg: the seed's angle record; the caller fences before reading the list from HBM)
 __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, float seed_deg, double prec,
-                           double& reg_angle) {
+                           double& reg_angle, bool has_pre = false, float4 pre = float4{}) {
     const int lane = lane_id();
     int n = 0;
     reg_angle = (double)seed_deg * kDeg2Rad;
@@ -698,7 +698,7 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
             ok = xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
         }
         float4 q = make_float4(-1.0f, 0.f, 0.f, 0.f);
-        if (ok) q = I.px[yy * I.W + xx];
+        if (ok) q = (i == 0 && has_pre) ? pre : I.px[yy * I.W + xx];   // pre: the seed's 3x3, prefetched
         for (int k = 0; k < nb; ++k) {
             const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy);
             const unsigned long long m = __ballot(av) >> (9 * k);
@@ -959,14 +959,27 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
         a1 = base + 64 + lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
         e2 = base + 128 + lane < o.NP ? keys[base + 128 + lane] : 0;
         bool cand = a0 >= 0.0f;
+        int pre_j = -1;   // the candidate whose 3x3 records `pre` holds (lanes 0-8)
+        float4 pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
         for (;;) {
             const unsigned long long m = __ballot(cand && !U.get(px, py));
             if (!m) break;
             const int j = __ffsll((long long)m) - 1;
             if (lane <= j) cand = false;
             const int sx = rl_i(px, j), sy = rl_i(py, j);
+            // the next candidate's neighbourhood loads while this region grows (records are
+            // static; whether it is still a seed is decided from the used map later)
+            const bool has_pre = pre_j == j;
+            const float4 cur = pre;
+            const unsigned long long m2 = m & ~((2ull << j) - 1ull);
+            pre_j = m2 ? __ffsll((long long)m2) - 1 : -1;
+            pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
+            if (pre_j >= 0 && lane < 9) {
+                const int xx = rl_i(px, pre_j) + lane % 3 - 1, yy = rl_i(py, pre_j) + lane / 3 - 1;
+                if (xx >= 0 && yy >= 0 && xx < o.W && yy < o.H) pre = I.px[yy * o.W + xx];
+            }
             double reg_angle;
-            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle);
+            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle, has_pre, cur);
             if (n < o.min_reg_size) continue;
             mem_sync();   // the region list (HBM) is read by every lane next
             Rect rec;
