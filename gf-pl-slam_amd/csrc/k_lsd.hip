@@ -41,6 +41,7 @@ struct LsdDev {
     int W, H, NP;                  // NP = (W-1)(H-1) sorted pixels
     int n_bins, min_reg_size, seg_cap, kl_cap, n_features;
     double prec, rho, density_th, min_length;
+    float2* cs_tab;                // [1021][1021] (cos, sin) of float(angle(gx, gy)), gx, gy in +-510
     float4* px;                    // [n][W*H] per pixel: fastAtan2 degrees (-1 = NOTDEF), cos and
                                    // sin of float(angle), gx (low 16) | gy (high 16) as bits
     unsigned long long* maxg;      // [n] bits of the max norm of defined pixels
@@ -552,18 +553,22 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) 
 }  // namespace
 
 // ------------------------------------------------------------------ ll_angle --
+#define LSD_GRAD_ROWS 64   // rows per workgroup (16 passes of 4): one max-norm atomic per 4096 px
 __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* images) {
+    __shared__ unsigned long long wmaxv[4];
     const int img = blockIdx.z;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int W = o.W, H = o.H;
-    double norm_def = 0;
-    if (x < W && y < H) {
+    const uint8_t* I = images + (size_t)img * W * H;
+    unsigned long long b = 0;   // bits of the max norm of defined pixels (norm >= 0 orders like its bits)
+    for (int r = 0; r < LSD_GRAD_ROWS; r += 4) {
+        const int y = blockIdx.y * LSD_GRAD_ROWS + r + (threadIdx.x >> 6);
+        if (x >= W || y >= H) continue;
         const size_t p = (size_t)img * W * H + (size_t)y * W + x;
         float a = -1.0f;
         uint32_t g = 0;
         float2 cs = make_float2(0.f, 0.f);
         if (x < W - 1 && y < H - 1) {
-            const uint8_t* I = images + (size_t)img * W * H;
             const int DA = (int)I[(size_t)(y + 1) * W + x + 1] - (int)I[(size_t)y * W + x];
             const int BC = (int)I[(size_t)y * W + x + 1] - (int)I[(size_t)(y + 1) * W + x];
             const int gx = DA + BC, gy = DA - BC;
@@ -571,21 +576,36 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
             const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
             if (norm > o.rho) {
                 a = fast_atan2((float)gx, (float)-gy);
-                const double ad = (double)a * kDeg2Rad;
-                const double af = (double)(float)ad;   // S3: float(angle)
-                cs = make_float2((float)det_cos(af), (float)det_sin(af));
-                norm_def = norm;
+                cs = o.cs_tab[(gx + 510) * 1021 + (gy + 510)];   // S3, tabulated per (gx, gy)
+                const unsigned long long nb = (unsigned long long)__double_as_longlong(norm);
+                b = nb > b ? nb : b;
             }
         }
         o.px[p] = make_float4(a, cs.x, cs.y, __uint_as_float(g));
     }
-    // the image's max norm over defined pixels (norm >= 0: the bits order like the values)
-    unsigned long long b = (unsigned long long)__double_as_longlong(norm_def);
     for (int off = 32; off; off >>= 1) {
         const unsigned long long t = __shfl_xor(b, off);
         b = t > b ? t : b;
     }
-    if ((threadIdx.x & 63) == 0 && b) atomicMax(&o.maxg[img], b);
+    if ((threadIdx.x & 63) == 0) wmaxv[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmaxv[0];
+        for (int w = 1; w < 4; ++w) m = wmaxv[w] > m ? wmaxv[w] : m;
+        if (m) atomicMax(&o.maxg[img], m);
+    }
+}
+
+// S3 for every gradient an 8-bit image can give: the cos / sin of float(angle) depend on
+// (gx, gy) only, so the f64 fdlibm evaluations run once per detector, not per pixel
+__global__ void __launch_bounds__(256) k_lsd_cs_table(float2* tab) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 1021 * 1021) return;
+    const int gx = i / 1021 - 510, gy = i % 1021 - 510;
+    const float a = fast_atan2((float)gx, (float)-gy);
+    const double ad = (double)a * kDeg2Rad;
+    const double af = (double)(float)ad;   // float(angle)
+    tab[i] = make_float2((float)det_cos(af), (float)det_sin(af));
 }
 
 __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
@@ -1132,14 +1152,15 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     o->lds_used = (px + 31) / 32 * 4 <= LSD_USED_LDS_MAX;
     o->lds_bytes = (px + 31) / 32 * 4 + 4 * LSD_RING;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_px = al(16 * M * px), b_max = al(8 * M),
+    const size_t b_tab = al(8 * 1021 * 1021), b_px = al(16 * M * px), b_max = al(8 * M),
                  b_keys = al(8 * M * NP), b_pos = al(4 * M * NP), b_reg = al(4 * M * px),
                  b_used = o->lds_used ? 0 : al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
                  b_klt = al(24 * M * SC), b_rk = al(8 * M * SC), b_rl = al(4 * M * SC);
-    const size_t total = b_px + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
+    const size_t total = b_tab + b_px + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
                          b_klt + b_rk + 2 * b_rl + 256;
     if (hipMalloc(&o->base, total) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
+    d.cs_tab = (float2*)p; p += b_tab;
     d.px = (float4*)p; p += b_px;
     d.maxg = (unsigned long long*)p; p += b_max;
     d.keys = (uint64_t*)p; p += b_keys;
@@ -1158,6 +1179,12 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     if (o->lds_used &&
         hipFuncSetAttribute((const void*)k_lsd_grow_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)o->lds_bytes) != hipSuccess) {
+        (void)hipFree(o->base);
+        delete o;
+        return GFPL_E_HIP;
+    }
+    hipLaunchKernelGGL(k_lsd_cs_table, dim3((1021 * 1021 + 255) / 256), dim3(256), 0, o->stream, d.cs_tab);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(o->stream) != hipSuccess) {
         (void)hipFree(o->base);
         delete o;
         return GFPL_E_HIP;
@@ -1189,7 +1216,8 @@ extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_k
     hipStream_t s = o->stream;
     if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
     if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess) return GFPL_E_HIP;
-    hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + 3) / 4, n), dim3(256), 0, s, d, images);
+    hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
+                       d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.NP + 255) / 256, n), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64), 0, s, d);
     if (o->lds_used)
