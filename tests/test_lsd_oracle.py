@@ -239,3 +239,20 @@ def test_lines_of_the_staircase_scene():
         kl, rsp, segs = O.lsd_detect(img)
         assert 20 <= len(kl) <= 300
         assert (np.diff(rsp) <= 0).all() or len(kl) < 300
+
+
+def test_lsd_params_match_reference_config():
+    """gfpl.LsdParams.reference = StereoFrame's LSDOptions from Config (src/config.cpp:107,
+    143-152; src/stereoFrame.cpp:151, 1163-1172)."""
+    p = gfpl.LsdParams.reference(640, 480)
+    assert (p.refine, p.scale, p.quant, p.ang_th, p.density_th, p.n_bins) == (1, 1.0, 2.0, 22.5, 0.6, 1024)
+    assert p.n_features == 300 and p.min_length == 0.025 * 480
+
+
+def test_unsupported_lsd_options_refused():
+    img = np.zeros((16, 16), np.uint8)
+    for f, v in (("refine", 2), ("scale", 0.8)):
+        prm = gfpl.LsdParams.reference(16, 16)
+        setattr(prm, f, v)
+        with pytest.raises(RuntimeError):
+            O.lsd_detect(img, prm)
