@@ -32,7 +32,8 @@
 
 namespace gfpl {
 
-#define LSD_SORT_LDS 2048          // ranges up to this many elements are sorted in LDS
+// ranges up to CAP elements are sorted in LDS: CAP 2048 (34 KB, 4 images per CU) for batches up to
+// 4 images per CU, CAP 1024 (19 KB, 8 images per CU) above
 #define LSD_RING 256               // region list entries mirrored in LDS
 #define LSD_SMALL 128              // ranges up to this size: one lane runs libstdc++'s serial loop
 #define LSD_USED_LDS_MAX (64 * 1024)   // bytes of LDS bitmap (W*H <= 524288 px)
@@ -316,19 +317,21 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     return min(cL, cR);
 }
 
+template <int CAP>
 struct SortLds {
-    uint64_t buf[LSD_SORT_LDS];
-    uint16_t lp[LSD_SORT_LDS], rp[LSD_SORT_LDS];
+    uint64_t buf[CAP];
+    uint16_t lp[CAP], rp[CAP];
     int stk[3 * 64];
     int leaf[2 * 64];
     int small[3 * 64];
-    int lstk[64 * 3 * 8];   // per-lane stacks of lane_introsort
+    int lstk[64 * 3 * 5];   // per-lane stacks of lane_introsort (depth <= 3, see there)
 };
 
 // libstdc++'s __introsort_loop + final insertion sort of one range [f, l) of an LDS array by
 // one lane (ranges <= LSD_SMALL; the lanes of a wave sort disjoint ranges).  The larger part
 // of each partition is pushed and the smaller one continued (ranges are independent, so the
-// order they are finished in does not change the result): the stack stays <= 8 deep.
+// order they are finished in does not change the result): a range stacked at depth i is at most
+// 128 / 2^(i-1) elements and only ranges > 16 are partitioned, so the stack stays <= 3 deep.
 __device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
     const int F0 = f, L0 = l;
     int sp = 0;
@@ -385,11 +388,12 @@ __device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
     }
 }
 
-__device__ void flush_small(uint64_t* a, SortLds& S, int& ns) {
+template <int CAP>
+__device__ void flush_small(uint64_t* a, SortLds<CAP>& S, int& ns) {
     const int lane = lane_id();
     if (ns == 0) return;
     lds_sync();
-    if (lane < ns) lane_introsort(a, S.small[3 * lane], S.small[3 * lane + 1], S.small[3 * lane + 2], S.lstk + 24 * lane);
+    if (lane < ns) lane_introsort(a, S.small[3 * lane], S.small[3 * lane + 1], S.small[3 * lane + 2], S.lstk + 15 * lane);
     lds_sync();
     ns = 0;
 }
@@ -429,7 +433,8 @@ __device__ void add_leaf(uint64_t* a, int* leaf, int& nleaf, int f, int l) {
 
 // __introsort_loop over [0, n) of an LDS array with the given depth budget, then the
 // final insertion sort of its leaves
-__device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
+template <int CAP>
+__device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds<CAP>& S) {
     const int lane = lane_id();
     int* stk = S.stk;
     int ns = 0;
@@ -479,18 +484,20 @@ __device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds& S) {
 
 // the global-memory sort keeps its stack and leaves in the lower half of SortLds' small
 // arrays while a nested LDS sort runs: give the nested call its own copies
+template <int CAP>
 struct SortLdsPair {
-    SortLds inner;
+    SortLds<CAP> inner;
     int stk[3 * 64];
     int leaf[2 * 64];
 };
 
 namespace {
 // std::sort of a[0, n) by descending key (S2), the wave of the calling workgroup
-__device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) {
+template <int CAP>
+__device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair<CAP>& P) {
     if (n < 2) return;
     const int depth = 2 * (31 - __clz(n));
-    if (n <= LSD_SORT_LDS) {
+    if (n <= CAP) {
         const int lane = lane_id();
 #pragma unroll 8
         for (int i = lane; i < n; i += 64) P.inner.buf[i] = a[i];
@@ -501,7 +508,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) 
         return;
     }
     // outer loop in global memory with its own stack / leaf arrays
-    SortLds& S = P.inner;
+    SortLds<CAP>& S = P.inner;
     const int lane = lane_id();
     int* stk = P.stk;
     int* leaf = P.leaf;
@@ -518,7 +525,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair& P) 
         int f = stk[3 * sp], l = stk[3 * sp + 1], d = stk[3 * sp + 2];
         bool done = false;
         while (l - f > 16) {
-            if (l - f <= LSD_SORT_LDS) {
+            if (l - f <= CAP) {
                 const int m = l - f;
 #pragma unroll 8
                 for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
@@ -623,8 +630,9 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
     o.keys[(size_t)img * o.NP + i] = ((uint64_t)(uint32_t)bin << 32) | ((uint32_t)y << 16) | (uint32_t)x;
 }
 
+template <int CAP>
 __global__ void __launch_bounds__(64) k_lsd_sort(LsdDev o) {
-    __shared__ SortLdsPair S;
+    __shared__ SortLdsPair<CAP> S;
     const int img = blockIdx.x;
     wave_sort(o.keys + (size_t)img * o.NP, o.NP, o.lpos + (size_t)img * o.NP, o.rpos + (size_t)img * o.NP, S);
 }
@@ -1032,14 +1040,14 @@ __global__ void __launch_bounds__(64) k_lsd_grow_glb(LsdDev o) {
 
 // std::sort of one device array (test hook of the S2 restatement)
 __global__ void __launch_bounds__(64) k_lsd_sort_one(uint64_t* a, int n, int* lp, int* rp) {
-    __shared__ SortLdsPair S;
+    __shared__ SortLdsPair<1024> S;
     wave_sort(a, n, lp, rp, S);
 }
 
 // ------------------------------------------------------------------ keylines --
 // LSDDetector_custom.cpp:266-306 and src/stereoFrame.cpp:1177-1185
 __global__ void __launch_bounds__(64) k_lsd_keylines(LsdDev o, gfpl_keyline* kl_out, int* n_kl, float* rsp_out) {
-    __shared__ SortLdsPair S;
+    __shared__ SortLdsPair<1024> S;
     const int img = blockIdx.x, lane = lane_id();
     const int ns = o.nseg[img];
     const float fw = (float)o.W, fh = (float)o.H;
@@ -1219,7 +1227,12 @@ extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_k
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.NP + 255) / 256, n), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64), 0, s, d);
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o->device);
+    if (n > 4 * cus)
+        hipLaunchKernelGGL(k_lsd_sort<1024>, dim3(n), dim3(64), 0, s, d);
+    else
+        hipLaunchKernelGGL(k_lsd_sort<2048>, dim3(n), dim3(64), 0, s, d);
     if (o->lds_used)
         hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
     else

@@ -111,7 +111,9 @@ class ImagePipeline:
         W, H = int(cam.width), int(cam.height)
         self.orb = ORBextractor(nfeatures, 1.2, int(cam.n_levels), 20, 7, W, H, max_images=batch, ctx=ctx)
         self.lbd = BinaryDescriptor(W, H, max_images=batch, kl_cap=kl_cap, ctx=ctx)
-        self.lsd = LSDDetector(W, H, LsdParams.reference(W, H), max_images=batch, kl_cap=kl_cap, ctx=ctx) if lsd else None
+        # both images of the B stereo frames go through LSD in one call (2B images in flight)
+        self.lsd = LSDDetector(W, H, LsdParams.reference(W, H), max_images=2 * batch, kl_cap=kl_cap,
+                               ctx=ctx) if lsd else None
         self.kp_cap = self.orb.kp_cap
         dev = torch.device("cuda", torch.cuda.current_device())
         B, kc = batch, self.kp_cap
@@ -119,8 +121,11 @@ class ImagePipeline:
         self.n_kp = [z(B, torch.int32), z(B, torch.int32)]
         self.kps = [z(B * kc * KEYPOINT_DT.itemsize), z(B * kc * KEYPOINT_DT.itemsize)]
         self.pdesc = [z(B * kc * DESC), z(B * kc * DESC)]
-        self.n_kl = [z(B, torch.int32), z(B, torch.int32)]
-        self.kl = [z(B * kl_cap * KEYLINE_DT.itemsize), z(B * kl_cap * KEYLINE_DT.itemsize)]
+        self.n_kl_lr = z(2 * B, torch.int32)
+        self.kl_lr = z(2 * B * kl_cap * KEYLINE_DT.itemsize)
+        self.n_kl = [self.n_kl_lr[:B], self.n_kl_lr[B:]]
+        self.kl = [self.kl_lr[:B * kl_cap * KEYLINE_DT.itemsize], self.kl_lr[B * kl_cap * KEYLINE_DT.itemsize:]]
+        self.img_lr = z(2 * B * W * H) if lsd else None
         self.ldesc = [z(B * kl_cap * DESC), z(B * kl_cap * DESC)]
         self.pyr_l = z(B * int(cam.pyr_bytes))   # the left pyramid (not read by the tracker)
         self.pyr_r = z(B * int(cam.pyr_bytes))
@@ -140,8 +145,10 @@ class ImagePipeline:
         tracker read them, then ORB and LBD.  Needs lsd=True."""
         if self.lsd is None:
             raise RuntimeError("ImagePipeline(lsd=True) runs LSD on the device")
-        for side, img in ((0, left), (1, right)):
-            self.lsd.detect_batch(img, self.B, self.kl[side], self.n_kl[side])
+        n = self.B * int(self.cam.width) * int(self.cam.height)
+        self.img_lr[:n].copy_(left.reshape(-1))
+        self.img_lr[n:].copy_(right.reshape(-1))
+        self.lsd.detect_batch(self.img_lr, 2 * self.B, self.kl_lr, self.n_kl_lr)
         return self._describe(left, right, time_stamp)
 
     def _describe(self, left, right, time_stamp):
