@@ -152,7 +152,7 @@ __device__ double fd_atan2(double y, double x) {
     const int hx = __double2hiint(x), hy = __double2hiint(y);
     const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
     const unsigned lx = (unsigned)__double2loint(x), ly = (unsigned)__double2loint(y);
-    if (((unsigned)(hx - 0x3ff00000) | lx) == 0) return fd_atan(y);
+    if ((((unsigned)hx - 0x3ff00000u) | lx) == 0) return fd_atan(y);
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
     if (((unsigned)iy | ly) == 0) {
         if (m <= 1) return y;

@@ -129,10 +129,40 @@ int run_helpers() {
     return 0;
 }
 
+// LSD (+ LBD on its keylines) on drawn shapes and a ramp: every region / refine branch, the
+// response sort (n_features below the count), the std::sort hook
+int run_lines() {
+    const int w = 160, h = 120;
+    std::vector<uint8_t> img((size_t)w * h);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            int v = 30 + (x * 7 + y * 3) % 11;
+            if (x > 30 && x < 120 && y > 25 && y < 90) v = 200;
+            if ((x - 60) * (x - 60) + (y - 60) * (y - 60) < 300) v = 90;
+            if (x + y > 200) v = 140;
+            img[(size_t)y * w + x] = (uint8_t)v;
+        }
+    gfpl_lsd_params prm{1, 1.0, 2.0, 22.5, 0.6, 1024, 0.025 * h, 3};
+    std::vector<gfpl_keyline> kl(64);
+    std::vector<float> rsp(64), segs(4 * 256);
+    int n = 0, ns = 0;
+    CHECK(gfplo_lsd_detect(&prm, img.data(), w, h, 64, kl.data(), rsp.data(), &n, segs.data(), 256, &ns));
+    prm.n_features = 0;
+    CHECK(gfplo_lsd_detect(&prm, img.data(), w, h, 64, kl.data(), rsp.data(), &n, segs.data(), 256, &ns));
+    std::vector<uint8_t> desc((size_t)32 * (n > 0 ? n : 1));
+    CHECK(gfplo_lbd_compute(img.data(), w, h, kl.data(), n, desc.data(), nullptr));
+    std::vector<uint64_t> a(5000);
+    for (size_t i = 0; i < a.size(); ++i) a[i] = ((uint64_t)((i * 2654435761u) % 37) << 32) | i;
+    CHECK(gfplo_sort_desc(a.data(), (int)a.size()));
+    (void)gfplo_atan2(-1.5, -0.25);
+    return 0;
+}
+
 }  // namespace
 
 int main() {
     if (run_helpers()) return 1;
+    if (run_lines()) return 1;
     for (const CamDef& d : kCams)
         if (run_camera(d)) return 1;
     std::printf("oracle sanitizer run: clean\n");

@@ -96,7 +96,7 @@ double fd_atan2(double y, double x) {
     const int32_t hx = (int32_t)hi_word(x), hy = (int32_t)hi_word(y);
     const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
     const uint32_t lx = lo_word(x), ly = lo_word(y);
-    if (((uint32_t)(hx - 0x3ff00000) | lx) == 0) return fd_atan(y);   // x = 1.0
+    if ((((uint32_t)hx - 0x3ff00000u) | lx) == 0) return fd_atan(y);   // x = 1.0 (unsigned: no overflow)
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
     if ((iy | ly) == 0) {
         switch (m) {
