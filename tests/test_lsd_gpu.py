@@ -125,3 +125,38 @@ def test_lsd_feeds_lbd_on_device():
         rd, _ = O.lbd_compute(imgs[i], rk)
         assert cnt[i] == len(rk)
         assert (desc[i, :cnt[i]] == rd).all()
+
+
+def _dense_image(seed, w, h):
+    """Random rectangles, discs and ramps over noise: many regions, refinements and
+    radius reductions."""
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, 12, (h, w)).astype(np.int32) + 40
+    yy, xx = np.mgrid[0:h, 0:w]
+    for _ in range(40):
+        x0, y0 = rng.integers(0, w), rng.integers(0, h)
+        a, b = rng.integers(4, w // 3), rng.integers(4, h // 3)
+        v = int(rng.integers(0, 200))
+        k = rng.integers(0, 3)
+        if k == 0:
+            img[y0:y0 + b, x0:x0 + a] += v // 2
+        elif k == 1:
+            img[(xx - x0) ** 2 + (yy - y0) ** 2 < a * a] = v
+        else:
+            img += ((xx * int(rng.integers(-3, 4)) + yy * int(rng.integers(-3, 4))) // 7 % 3)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def test_lsd_parity_dense_scenes():
+    w, h = 640, 480
+    _check(np.stack([_dense_image(s, w, h) for s in range(3)]), gfpl.LsdParams.reference(w, h, n_features=0),
+           kl_cap=4096)
+
+
+def test_lsd_parity_large_batch_small_lds_sort():
+    """More than 4 images per CU: the sort runs with the 1024-element LDS capacity (8 per CU)."""
+    w, h = 96, 72
+    n = 1100
+    imgs = np.stack([_dense_image(1000 + i, w, h) if i % 50 == 0 else gfpl.synth_image(i, 0, w, h)
+                     for i in range(n)])
+    assert _check(imgs, kl_cap=64) > 0
