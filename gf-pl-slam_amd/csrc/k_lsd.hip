@@ -35,7 +35,7 @@ namespace gfpl {
 // ranges up to CAP elements are sorted in LDS: CAP 2048 (34 KB, 4 images per CU) for batches up to
 // 4 images per CU, CAP 1024 (19 KB, 8 images per CU) above
 #define LSD_RING 256               // region list entries mirrored in LDS
-#define LSD_SMALL 128              // ranges up to this size: one lane runs libstdc++'s serial loop
+#define LSD_SMALL 96               // ranges up to this size: one lane runs libstdc++'s serial loop
 #define LSD_USED_LDS_MAX (64 * 1024)   // bytes of LDS bitmap (W*H <= 524288 px)
 
 struct LsdDev {
