@@ -12,12 +12,17 @@ updateFrame, app/plslam_mod.cpp:387-477) for every one of the B independent
 sequences resident on a GPU (B = 16384 by default, independent of --steps).
 
 Input ring: before each step the host generates the next input frame of all B
-sequences (splitmix64, deterministic; gfpl_synth) into pinned memory and
-uploads it into the seqbatch's device staging area (gfpl_upload_frames), both
-outside the timed brackets.  Each step is timed on its own, bracketed by
-barrier + device synchronize on both sides with the inputs resident in HBM;
-the reported time is the sum over the K timed steps (MAX over ranks).  The
-upload is timed separately: `host_fed` is the PCIe-inclusive rate.
+sequences (splitmix64, deterministic; gfpl_synth) chunk by chunk into a ring of
+two pinned chunks and uploads each chunk with gfpl_upload_frames_async into the
+seqbatch's device staging buffer (the next chunk is generated while the last one
+is copied), all outside the timed brackets.  Each step is timed on its own,
+bracketed by barrier + device synchronize on both sides with the inputs resident
+in HBM; the reported time is the sum over the K timed steps (MAX over ranks).
+The synthetic scene is stationary (landmarks re-spawn in the frustum, gfpl_synth
+`respawn`), so per-step work does not drift with --steps; the bench line carries
+the per-step mean feature counts.  `host_fed` is measured after the timed steps:
+two frames held in pinned host memory are uploaded on the copy stream into the
+two staging buffers while the step on the other one runs (PCIe-inclusive rate).
 
 Parity at the operating point: `parity_sampled` replays a sample of the timed
 sequences (same ids, same frames) on the CPU oracle after every step and
@@ -55,18 +60,23 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # per SIMD (MI355X_MICROARCH.md §Wave scheduling) = 1228.8 G wave-instructions/s
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2
 
+# Every workload re-spawns its landmarks (gfpl_synth `respawn`: each pool slot is re-sampled in
+# the current frustum every `respawn` frames, phases spread), so 90 % of the detections observe a
+# landmark at every frame (10 % distractors) and the per-step work is stationary.
 WORKLOADS = {
     # name: (camera, synth overrides, description)
-    "cfg2": ("vga", {}, "cfg2: synthetic VGA 640x480 stereo (gazebo rig), 2000 ORB + 500 LBD per side, 10+10 GN iters"),
-    "cfg3": ("kitti", dict(dt=0.1, v_fwd=8.0, z_min=4.0, z_max=40.0),
+    "cfg2": ("vga", dict(respawn=16),
+             "cfg2: synthetic VGA 640x480 stereo (gazebo rig), 2000 ORB + 500 LBD per side, 10+10 GN iters"),
+    # KITTI moves 0.8 m per frame: landmarks live 4 frames, from a larger pool
+    "cfg3": ("kitti", dict(dt=0.1, v_fwd=8.0, z_min=4.0, z_max=40.0, respawn=4, n_world_pts=3200, n_world_lines=900),
              "cfg3: KITTI-00 1241x376 stream (synthetic detections), 2000 ORB + 500 LBD, 10+10 GN iters"),
     # BASELINE configs[3]: the EuRoC rig following the ground-truth motion of the 8 EuRoC
     # sequences (config/asl/gt-ass/*), sequence (rank mod 8) on rank r
-    "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0),
+    "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0, respawn=16),
              "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
              "2000 ORB + 500 LBD, 10+10 GN iters"),
     # BASELINE configs[4]: stress, 8000 ORB + 2000 LBD per 1920x1080 frame, line cut on
-    "cfg5": ("stress", dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=2800, z_max=12.0),
+    "cfg5": ("stress", dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=3200, z_max=12.0, respawn=16),
              "cfg5: stress 1920x1080 stereo (gazebo x3), 8000 ORB + 2000 LBD per side, good-line-cut on, "
              "10+10 GN iters"),
 }
@@ -75,12 +85,16 @@ WORKLOADS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16384, help="sequences per GPU (reduced only if HBM is short)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-detect", action="store_true", help="skip the ORB / LBD detection rates")
-    ap.add_argument("--gen-threads", type=int, default=16, help="host threads generating the input frames")
+    ap.add_argument("--gen-threads", type=int, default=16,
+                    help="host threads generating the input frames (capped by this rank's share of the cores)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="sequences per pinned host chunk of the input ring (0: B/8, at least 256)")
+    ap.add_argument("--no-host-fed", action="store_true", help="skip the pipelined host-fed (PCIe) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
@@ -88,8 +102,6 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (gloo): launcher, broadcast, sharding, input generation and reductions; "
                          "no tracking step is run and value is null")
-    ap.add_argument("--diag-every-step", action="store_true",
-                    help="read the per-stage / per-kernel HIP-event times after every timed step")
     ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC summary written by tools/pmc_summary.py (HBM traffic, SQ counters)")
@@ -174,17 +186,28 @@ def reduce_sum_ints(vals, dist, device):
     return [int(x) for x in t.tolist()]
 
 
-def load_pmc(path, kernel_name, batch, workload):
-    """Per-launch PMC summary of a kernel (tools/pmc_summary.py), only when it was
-    collected on this workload and batch size."""
+def load_pmc(path, kernel_name, batch, workload, steps, warmup):
+    """Per-launch PMC summary of a kernel (tools/pmc_summary.py) over the same window of
+    launches as this run's timed steps: only when it was collected on this workload,
+    batch size, --steps and --warmup (else None, and the line says why)."""
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("batch") != batch or d.get("workload", "cfg2") != workload:
-            return None
-        return d["kernels"].get(kernel_name)
-    except Exception:
-        return None
+    except Exception as e:
+        return None, f"no PMC summary ({type(e).__name__})"
+    want = {"batch": batch, "workload": workload, "steps": steps, "warmup": warmup}
+    got = {k: d.get(k) for k in want}
+    if got != want:
+        return None, f"PMC summary window {got} != this run {want}"
+    k = d["kernels"].get(kernel_name)
+    return k, None if k else f"{kernel_name} not in the PMC summary"
+
+
+def rank_share(cores: int, world: int) -> int:
+    """Host threads one rank may use: the process's cores (cgroup quota) split over the
+    ranks of this node (the quota is shared by every rank's process)."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world) or world)
+    return max(1, cores // max(1, local))
 
 
 # ------------------------------------------------------- parity at the bench --
@@ -192,7 +215,8 @@ class ParitySampler:
     """Replays sampled sequences of the timed batch on the CPU oracle (the checker)
     and compares them with the GPU state after every step, bit for bit."""
 
-    def __init__(self, cam, cfg, kp_cap, kl_cap, seqs, threads):
+    def __init__(self, cam, cfg, sp, kp_cap, kl_cap, seq0, seqs, threads):
+        self.cam, self.sp, self.kp_cap, self.kl_cap, self.seq0 = cam, sp, kp_cap, kl_cap, seq0
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle as O
@@ -221,21 +245,30 @@ class ParitySampler:
         for t in th:
             t.join()
 
-    def initialize(self, host_frames, h):
-        self._par(lambda i: self.orc[i].initialize(host_frames, self.seqs[i]))
+    def _frames(self, k):
+        """Frame k of every sampled sequence, generated again on the host (the generator is a
+        pure function of (seed, sequence, frame), so these are the bytes the GPU step read)."""
+        import gfpl
+        return [gfpl.HostFrames(self.cam, self.sp, 1, 1, self.kp_cap, self.kl_cap, seq0=self.seq0 + b, frame0=k,
+                                threads=1) for b in self.seqs]
+
+    def initialize(self, h):
+        H = self._frames(0)
+        self._par(lambda i: self.orc[i].initialize(H[i].frames(0), 0))
         for i, b in enumerate(self.seqs):
             self._record(self.PT.compare_core(h.read_frame(0, b), self.orc[i].read_frame(0), f"init s{b} "))
 
-    def step(self, host_frames, h, k):
+    def step(self, h, k):
         # GPU side first (the ABI reads synchronise; the state is the step's result)
         g_new = [h.read_frame(0, b) for b in self.seqs]      # PREV after update = the new frame
         g_old = [h.read_frame(1, b) for b in self.seqs]      # CURR slot = the old prev (cut results)
         g_tr = [h.read_last_track(b) for b in self.seqs]
         res = [None] * len(self.seqs)
+        H = self._frames(k)
 
         def run(i):
             o = self.orc[i]
-            o.insertStereoPair(host_frames, self.seqs[i])
+            o.insertStereoPair(H[i].frames(0), 0)
             o.optimizePose()
             res[i] = (o.read_frame(1), o.read_frame(0), o.read_track())
             o.updateFrame()
@@ -335,7 +368,7 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     d0 = desc.cpu().numpy().reshape(n_img, kc, 32)[0, :n0]
     out["orb"] = {"images_per_s": n_img / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
                   "kp_per_image": float(nkp.float().mean().item()),
-                  "parity_image0": bool(int(nkp[0].item()) == n0 and (k0 == o["kps"]).all() and (d0 == o["desc"]).all())}
+                  "parity_vs_oracle_image0": bool(int(nkp[0].item()) == n0 and (k0 == o["kps"]).all() and (d0 == o["desc"]).all())}
     orb.close()
     # LBD
     kls = np.stack([gfpl.synth_keylines(n_lines, W, H, 1000 + i, max_len=150.0) for i in range(n_img)])
@@ -353,7 +386,7 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     ref, _ = O.lbd_compute(imgs[0], kls[0])
     out["lbd"] = {"images_per_s": n_img / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
                   "keylines_per_image": n_lines,
-                  "parity_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
+                  "parity_vs_oracle_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
     lbd.close()
     # LSD (gfpl_lsd_detect, the reference's LSDOptions, 300 keylines kept): its per-image chain
     # (sort + region growing) is latency-bound, so it is measured at 4 images per CU
@@ -380,7 +413,7 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
         par = par and int(cnt[i]) == len(rk) and kl_all[i, :cnt[i]].tobytes() == rk.tobytes()
     out["lsd"] = {"images_per_s": n_lsd / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
                   "images_per_call": n_lsd, "keylines_per_image": float(cnt.mean()),
-                  "parity_images_0_1_8": bool(par),
+                  "parity_vs_oracle_images_0_1_8": bool(par),
                   "data": "8 staircase stereo images + gfpl_synth_image textures"}
     lsd.close()
     # with detection on the GPU a host-fed pipeline uploads the two grey images of a stereo
@@ -432,7 +465,9 @@ def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False):
         t_det += t1 - t0
         t_trk += time.perf_counter() - t1
     tr = g.read_last_track(0)
+    g.close()
     pipe.close()
+    ctx.close()
     return {"value": B * steps / (t_det + t_trk), "unit": "stereo frames/s", "sequences": B, "steps": steps,
             "detect_ms_per_step": 1e3 * t_det / steps, "track_ms_per_step": 1e3 * t_trk / steps,
             "matched_pt_seq0": len(tr["matched_pt"]), "matched_ls_seq0": len(tr["matched_ls"]),
@@ -482,8 +517,13 @@ def main():
     B, W, K = args.batch, args.warmup, args.steps
     KP, KL = (8192, 2048) if args.workload == "cfg5" else (2048, 512)
     keep = []
+    n_frames_needed = W + K + 3   # init + warmup + timed + the two host-fed frames
     if args.workload == "cfg4":
-        T, t = gfpl.euroc_traj(gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)], 64)
+        if n_frames_needed > gfpl.EUROC_MAX_POSES:
+            print(f"error: cfg4 needs {n_frames_needed} ground-truth poses, {gfpl.EUROC_MAX_POSES} stored",
+                  file=sys.stderr)
+            sys.exit(2)
+        T, t = gfpl.euroc_traj(gfpl.EUROC_SEQS[rank % len(gfpl.EUROC_SEQS)], n_frames_needed)
         keep += [T, t]   # the generator reads them through raw pointers
         synth_over = dict(synth_over, traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data)
         desc = desc + f" [rank 0: {gfpl.EUROC_SEQS[0]}]"
@@ -505,15 +545,43 @@ def main():
         B = reduce_min_int(B, dist, dev)   # one B on every rank: shards [r*B, (r+1)*B)
     seq0 = shard_first_seq(rank, B)
 
+    # host resources of this rank: its share of the process cores, a ring of two pinned
+    # chunks of the input batch (not a whole batch: 8 ranks share one host)
     cores, cores_info = host_cores()
-    gen_threads = max(1, min(args.gen_threads, cores))
-    hb = gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=not dry)
+    share = rank_share(cores, world)
+    gen_threads = max(1, min(args.gen_threads, share))
+    chunk = args.chunk or max(256, (B // 8 + 63) // 64 * 64)
+    chunk = min(chunk, B)
+    ring = [gfpl.HostBatch(cam, sp, chunk, KP, KL, seq0=seq0, pinned=not dry) for _ in range(2)]
+    pinned_bytes = 0 if dry else sum(r.nbytes() for r in ring)
     t_gen = 0.0
-    t0 = time.perf_counter()
-    hb.fill(0, gen_threads)
-    t_gen += time.perf_counter() - t0
 
+    h = None if dry else gfpl.StereoFrameHandler(ctx, B, KP, KL)
+
+    def stage_frame(k, slot=0):
+        """Generate frame k of this rank's B sequences chunk by chunk into the pinned ring and
+        copy each chunk into staging buffer `slot` (gfpl_upload_frames_async); the next chunk
+        is generated while the previous one is copied.  Returns the staged device view."""
+        tick = []
+        for ci, s0 in enumerate(range(0, B, chunk)):
+            n = min(chunk, B - s0)
+            hb = ring[ci % 2]
+            if ci >= 2 and h is not None:
+                h.upload_wait(tick[ci - 2])   # the chunk's host buffer is free again
+            hb.fill(k, gen_threads, seq0=seq0 + s0, n=n)
+            if h is not None:
+                tick.append(h.upload_async(hb.frames(n), s0, slot))
+        if h is None:
+            return None
+        h.upload_wait(tick[-1])
+        return h.staged_frames(slot)
+
+    host_info = {"pinned_bytes_per_rank": int(pinned_bytes), "chunk_sequences": int(chunk),
+                 "gen_threads_per_rank": int(gen_threads), "cores_share_per_rank": int(share)}
     if dry:
+        t0 = time.perf_counter()
+        stage_frame(0)
+        t_gen += time.perf_counter() - t0
         frames_total = B * K
         if world > 1:
             _, frames_total = reduce_job(0.0, B * K, dist, dev)
@@ -523,62 +591,64 @@ def main():
                               "dry_run": True, "frames_sharded": frames_total,
                               "config": {"workload": desc, "sequences_per_gpu": B,
                                          "parallelism": f"sequences sharded 1/{world} per GPU"},
-                              "input_bytes_per_step": int(hb.nbytes())}))
+                              "input_bytes_per_step": int(per_in * B), "host": host_info,
+                              "pinned_bytes_per_rank_if_gpu": int(sum(r.nbytes() for r in ring)),
+                              "gen_s": round(t_gen, 2)}))
         if world > 1:
             dist.destroy_process_group()
         return
 
-    h = gfpl.StereoFrameHandler(ctx, B, KP, KL)
     sampler = None
     if args.parity_seqs > 0:
         n = min(args.parity_seqs, B)
-        sampler = ParitySampler(cam, cfg, KP, KL, [int(x) for x in np.linspace(0, B - 1, n)], cores)
+        sampler = ParitySampler(cam, cfg, sp, KP, KL, seq0, [int(x) for x in np.linspace(0, B - 1, n)], share)
 
     def sync_all():
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
 
-    dv = h.upload_frames(hb.frames())
+    t0 = time.perf_counter()
+    dv = stage_frame(0)
+    t_gen += time.perf_counter() - t0
     h.initialize(dv)
     if sampler:
-        sampler.initialize(hb.frames(), h)
-    step_s, up_s = [], []
-    stage_ms, stage_bytes, kern_ms, kern_bytes = [], [], [], []
+        sampler.initialize(h)
+    step_s = []
+    stage_ms, stage_bytes, kern_ms, kern_bytes, counts = [], [], [], [], []
     ctx.set_timing(True)
     for k in range(1, 1 + W + K):
         t0 = time.perf_counter()
-        hb.fill(k, gen_threads)                       # host input generation (untimed)
+        dv = stage_frame(k)                           # host generation + upload (untimed)
         t_gen += time.perf_counter() - t0
-        sync_all()
-        tu0 = time.perf_counter()
-        dv = h.upload_frames(hb.frames())             # PCIe: synchronous, timed separately
-        tu1 = time.perf_counter()
         sync_all()
         ts0 = time.perf_counter()
         h.frameStep(dv)                               # the step: inputs resident in HBM
         sync_all()
         ts1 = time.perf_counter()
-        timed = k > W
-        if timed:
+        if k > W:
+            # the timed window: HIP-event stage / kernel times and the algorithmic bytes and
+            # counts of every timed step (the PMC summary averages the same launches)
             step_s.append(ts1 - ts0)
-            up_s.append(tu1 - tu0)
-            if args.diag_every_step or k == W + K:
-                stage_ms.append(ctx.stage_times())
-                stage_bytes.append(h.last_step_stage_bytes())
-                kern_ms.append(ctx.kernel_times())
-                kern_bytes.append(h.last_step_kernel_bytes())
+            stage_ms.append(ctx.stage_times())
+            stage_bytes.append(h.last_step_stage_bytes())
+            kern_ms.append(ctx.kernel_times())
+            kern_bytes.append(h.last_step_kernel_bytes())
+            counts.append(h.last_step_counts())
         if sampler:
-            sampler.step(hb.frames(), h, k)
-    elapsed, up_total = float(np.sum(step_s)), float(np.sum(up_s))
+            sampler.step(h, k)
+    elapsed = float(np.sum(step_s))
     lost = sum(h.read_track(b)["num_frame_loss"] > 0 for b in range(0, B, max(1, B // 16)))
     par = [sampler.frames, sampler.mismatch_frames] if sampler else [0, 0]
     if world > 1:
         t_max, frames_total = reduce_job(elapsed, B * K, dist, dev)
-        t_up_max, _ = reduce_job(elapsed + up_total, 0, dist, dev)
         par = reduce_sum_ints(par, dist, dev)
     else:
-        t_max, frames_total, t_up_max = elapsed, B * K, elapsed + up_total
+        t_max, frames_total = elapsed, B * K
+
+    host_fed = None
+    if world == 1 and not args.no_host_fed:
+        host_fed = host_fed_rate(h, cam, sp, B, KP, KL, seq0, W + K + 1, gen_threads, per_in, dev)
 
     if rank == 0:
         sm = np.mean(np.array(stage_ms, dtype=np.float64)[:, :6], axis=0)
@@ -595,7 +665,8 @@ def main():
         achieved = k_bytes / (k_ms * 1e-3) / 1e9
         step_bytes = float(np.mean(np.array(stage_bytes)[:, 6]))
         value = frames_total / t_max
-        pmc = load_pmc(args.pmc, kname, B, args.workload) or {}
+        pmc, pmc_note = load_pmc(args.pmc, kname, B, args.workload, K, W)
+        pmc = pmc or {}
         traffic = pmc.get("hbm_bytes_per_launch")
         roof_valu = None
         if pmc.get("SQ_INSTS_VALU"):
@@ -608,15 +679,18 @@ def main():
         if world == 1 and not args.no_cpu:
             nt = args.cpu_threads or cores
             cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads, W + K)
-        in_bytes = hb.nbytes()
         det = None
         if world == 1 and not args.no_detect:
-            det = detection_rates(cam, in_bytes * K / up_total)
+            up_Bps = host_fed["upload_GBps"] * 1e9 if host_fed and host_fed.get("upload_GBps") else 0.0
+            det = detection_rates(cam, up_Bps)
             try:
                 det["images_to_poses"] = pipeline_rate(cam, cfg)
                 det["images_to_poses_lsd"] = pipeline_rate(cam, cfg, lsd=True)
             except Exception as e:   # reported, never fatal to the contract line
                 det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}
+        cmean = {n: round(float(np.mean([c[n] for c in counts])), 1) for n in gfpl.StereoFrameHandler.STEP_COUNTS}
+        crange = {n: [round(float(min(c[n] for c in counts)), 1), round(float(max(c[n] for c in counts)), 1)]
+                  for n in ("S_p", "S_l", "M_o", "M_p", "M_l")}
         out = {
             "metric": "stereo frames/sec (2k ORB + 500 LBD, 10 GN iters)",
             "value": value,
@@ -629,39 +703,86 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth), "
-                    "generated per step on the host and uploaded to HBM before each timed step",
+            "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth; "
+                    "stationary scene: landmarks re-spawn in the frustum), generated per step on the host and "
+                    "uploaded to HBM before each timed step",
             "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": int(sp.n_kp),
                        "kl_per_side": int(sp.n_kl), "gn_iters": "10+10",
                        "parallelism": f"sequences sharded 1/{world} per GPU",
                        "timing": "sum of K per-step brackets (barrier + device sync both sides), MAX over ranks"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": float(achieved), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": float(achieved / HBM_PEAK_GBS), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": float(k_bytes), "avg_launch_ms": float(k_ms)},
+                         "traffic_note": pmc_note,
+                         "algorithmic_bytes_per_launch": float(k_bytes), "avg_launch_ms": float(k_ms),
+                         "window": f"the {K} timed steps (launches {W + 1}..{W + K} of each step kernel)"},
             "roofline_valu": roof_valu,
             "hbm_frac_step": float(step_bytes / (t_max / K) / 1e9 / HBM_PEAK_GBS),
+            "counts_per_seq_step": cmean,
+            "counts_range_over_steps": crange,
             "parity_sampled": {"sequences": len(sampler.seqs) * world if sampler else 0,
                                "frames": par[0], "mismatches": par[1],
                                "compared": "stereo features, matched lists, inlier counts, cut ratios, invCovPose, "
-                                           "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise",
+                                           "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise "
+                                           "vs the CPU oracle (oracle/)",
                                "first": sampler.msgs[:3] if sampler else []},
-            "host_fed": {"value": frames_total / t_up_max, "unit": "stereo frames/s",
-                         "upload_ms_per_step": up_total / K * 1e3,
-                         "upload_GBps": in_bytes * K / up_total / 1e9,
-                         "input_bytes_per_step": int(in_bytes),
-                         "note": "each step's inputs copied from pinned host memory through gfpl_upload_frames "
-                                 "(PCIe) then the step; detection / generation excluded"},
+            "host_fed": host_fed,
             "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES, sm)},
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
             "stage_bytes_per_step": {n: int(v) for n, v in zip(STAGES, sb)},
             "cpu_baseline": cpu,
             "detection": det,
+            "host": host_info,
             "gen_s": round(t_gen, 2),
             "lost_sampled": int(lost),
         }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, steps=4):
+    """PCIe-inclusive rate of a host-fed pipeline (rank 0 at N=1, after the timed steps):
+    two input frames (f0, f0 + 1) of all B sequences held in pinned host memory are uploaded
+    with gfpl_upload_frames_async into the two staging buffers in turn — the copy of step
+    j + 1 on the seqbatch's copy stream, the step j on the context stream, ordered by the
+    staging events — for `steps` steps (the frames alternate), wall clock from the first
+    copy to the last step.  Generation excluded.  Needs two pinned input frames on the host
+    and a second staging buffer in HBM; skipped (with the reason) when they do not fit."""
+    import torch
+    import gfpl
+    in_bytes = per_in * B
+    try:
+        import psutil
+        avail = psutil.virtual_memory().available
+    except Exception:
+        avail = None
+    free, _ = torch.cuda.mem_get_info(dev)
+    if (avail is not None and avail < 2.6 * in_bytes) or free < 1.1 * in_bytes:
+        return {"skipped": f"needs 2 x {in_bytes / 1e9:.1f} GB pinned host memory and a second staging buffer"}
+    hb = [gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=True) for _ in range(2)]
+    for i, x in enumerate(hb):
+        x.fill(f0 + i, gen_threads)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    h.upload_async(hb[0].frames(), 0, 1)
+    for j in range(steps):
+        if j + 1 < steps:
+            h.upload_async(hb[(j + 1) % 2].frames(), 0, (j + 2) % 2)
+        h.frameStep(h.staged_frames((j + 1) % 2))
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    # the copy alone, for the upload rate
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    h.upload_wait(h.upload_async(hb[0].frames(), 0, 1))
+    up = time.perf_counter() - t1
+    del hb
+    return {"value": B * steps / wall, "unit": "stereo frames/s", "steps": steps,
+            "ms_per_step": wall / steps * 1e3, "upload_ms_per_step": up * 1e3, "upload_GBps": in_bytes / up / 1e9,
+            "input_bytes_per_step": int(in_bytes),
+            "note": "frames f0, f0+1 of every sequence in pinned host memory, uploaded (gfpl_upload_frames_async, "
+                    "copy stream, two staging buffers) while the step on the other buffer runs; the frames "
+                    "alternate; generation / detection excluded"}
 
 
 if __name__ == "__main__":

@@ -37,8 +37,17 @@ struct gfpl_seqbatch {
     bool has_curr = false;
     DevTrack tr{};
     DevScratch scr{};
-    void* stage = nullptr;   // device staging of one uploaded input batch (gfpl_upload_frames)
-    size_t stage_bytes = 0;
+    // two device staging buffers of uploaded input batches (gfpl_upload_frames[_async]),
+    // filled on a copy stream: a step reading slot s waits for ev_ready[s]; a copy into
+    // slot s waits for ev_free[s], recorded after the last call that read it
+    void* stage[2] = {nullptr, nullptr};
+    size_t stage_bytes[2] = {0, 0};
+    gfpl_frames stage_view[2]{};
+    hipStream_t copy = nullptr;
+    hipEvent_t ev_ready[2]{}, ev_free[2]{};
+    bool ready_pending[2] = {false, false}, free_recorded[2] = {false, false};
+    hipEvent_t ev_ticket[16]{};   // ticket t of gfpl_upload_frames_async -> ev_ticket[t % 16]
+    int64_t n_tickets = 0;
     int32_t* last_n_pt = nullptr;   // [B] list lengths before the last gfpl_update_frame
     int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
 };
@@ -113,7 +122,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cut_rec = c.take<double>(B * sb->mls_cap * CUT_REC);
     sb->scr.knn = c.take<int32_t>(B * 2 * (size_t)sb->kp_cap * 3);
     sb->scr.proj = reinterpret_cast<double*>(sb->scr.knn);
-    sb->scr.bytes = c.take<int64_t>(B * 8);
+    sb->scr.bytes = c.take<int64_t>(B * STEP_REC);
     sb->scr.n_subpix = c.take<int32_t>(B);
     sb->scr.cut_sum = c.take<double>(B * 24);
     sb->scr.cut_dtinv = c.take<double>(B * 16);
@@ -169,6 +178,23 @@ int check_in(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (!in->n_kp_l || !in->n_kp_r || !in->kp_l || !in->kp_r || !in->pdesc_l || !in->pdesc_r || !in->n_kl_l ||
         !in->n_kl_r || !in->kl_l || !in->kl_r || !in->ldesc_l || !in->ldesc_r || !in->pyr_r || !in->time_stamp)
         return GFPL_E_INVALID;
+    return GFPL_OK;
+}
+
+// A call that reads `in` from a staging slot waits (on the context stream) for that
+// slot's uploads; after enqueueing its work it marks the slot free for the next copy.
+int in_acquire(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    for (int s = 0; s < 2; ++s)
+        if (sb->stage[s] && in->n_kp_l == sb->stage_view[s].n_kp_l) {
+            if (sb->ready_pending[s] && hipStreamWaitEvent(sb->ctx->stream, sb->ev_ready[s], 0) != hipSuccess) return -2;
+            return s;
+        }
+    return -1;
+}
+int in_release(gfpl_seqbatch* sb, int slot) {
+    if (slot < 0) return GFPL_OK;
+    if (hipEventRecord(sb->ev_free[slot], sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+    sb->free_recorded[slot] = true;
     return GFPL_OK;
 }
 
@@ -293,8 +319,16 @@ int gfpl_seqbatch_destroy(gfpl_seqbatch* sb) {
     (void)hipStreamSynchronize(sb->ctx->stream);
     auto& v = sb->ctx->sbs;
     v.erase(std::remove(v.begin(), v.end(), sb), v.end());
+    if (sb->copy) (void)hipStreamSynchronize(sb->copy);
     if (sb->base) (void)hipFree(sb->base);
-    if (sb->stage) (void)hipFree(sb->stage);
+    for (int k = 0; k < 2; ++k) {
+        if (sb->stage[k]) (void)hipFree(sb->stage[k]);
+        if (sb->ev_ready[k]) (void)hipEventDestroy(sb->ev_ready[k]);
+        if (sb->ev_free[k]) (void)hipEventDestroy(sb->ev_free[k]);
+    }
+    for (hipEvent_t e : sb->ev_ticket)
+        if (e) (void)hipEventDestroy(e);
+    if (sb->copy) (void)hipStreamDestroy(sb->copy);
     delete sb;
     return GFPL_OK;
 }
@@ -305,12 +339,14 @@ int gfpl_initialize(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (!sb) return GFPL_E_INVALID;
     int e = check_in(sb, in);
     if (e) return e;
+    const int slot = in_acquire(sb, in);
+    if (slot == -2) return GFPL_E_HIP;
     KParams p = params(sb, in);
     p.curr = sb->slot[sb->prev_slot];   // the initial frame becomes prev_frame
     HIPCHK(launch_init(p, sb->ctx->stream));
     sb->initialized = true;
     sb->has_curr = false;
-    return GFPL_OK;
+    return in_release(sb, slot);
 }
 
 int gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in) {
@@ -318,9 +354,11 @@ int gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (!sb->initialized) return GFPL_E_STATE;
     int e = check_in(sb, in);
     if (e) return e;
+    const int slot = in_acquire(sb, in);
+    if (slot == -2) return GFPL_E_HIP;
     HIPCHK(launch_stereo_points(params(sb, in), sb->ctx->stream));
     sb->has_curr = true;
-    return GFPL_OK;
+    return in_release(sb, slot);
 }
 
 int gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in) {
@@ -328,9 +366,11 @@ int gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (!sb->initialized) return GFPL_E_STATE;
     int e = check_in(sb, in);
     if (e) return e;
+    const int slot = in_acquire(sb, in);
+    if (slot == -2) return GFPL_E_HIP;
     HIPCHK(launch_stereo_lines(params(sb, in), sb->ctx->stream));
     sb->has_curr = true;
-    return GFPL_OK;
+    return in_release(sb, slot);
 }
 
 int gfpl_line_uncertainty(gfpl_seqbatch* sb) {
@@ -367,6 +407,8 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
     int e = check_in(sb, in);
     if (e) return e;
     gfpl_ctx* c = sb->ctx;
+    const int slot = in_acquire(sb, in);
+    if (slot == -2) return GFPL_E_HIP;
     KParams p = params(sb, in);
     tmark(c, 0);
     HIPCHK(launch_stereo_points(p, c->stream));
@@ -384,7 +426,7 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
     HIPCHK(launch_step_bytes(p, c->stream));
     tmark(c, 5);
     sb->has_curr = true;
-    return GFPL_OK;
+    return in_release(sb, slot);
 }
 
 int gfpl_optimize_pose(gfpl_seqbatch* sb) {
@@ -451,42 +493,102 @@ int gfpl_optimize_pose_ini(gfpl_seqbatch* sb, const double* dt_ini) {
     return GFPL_OK;
 }
 
-int gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* dev) {
-    if (!sb || !host || !dev) return GFPL_E_INVALID;
-    if (host->batch != sb->B || host->kp_cap != sb->kp_cap || host->kl_cap != sb->kl_cap) return GFPL_E_INVALID;
+}  // extern "C"
+
+namespace {
+// device layout of one staged input batch of B sequences (the gfpl_frames [B][cap] layout)
+void stage_layout(Carver& c, const gfpl_seqbatch* sb, gfpl_frames& f) {
     const size_t B = sb->B, P = B * sb->kp_cap, L = B * sb->kl_cap;
     const size_t pyr = B * (size_t)sb->ctx->cam.pyr_bytes;
-    Carver c;
-    auto layout = [&](gfpl_frames& f) {
-        f.batch = host->batch; f.kp_cap = host->kp_cap; f.kl_cap = host->kl_cap;
-        f.n_kp_l = c.take<int>(B); f.n_kp_r = c.take<int>(B);
-        f.kp_l = c.take<gfpl_keypoint>(P); f.kp_r = c.take<gfpl_keypoint>(P);
-        f.pdesc_l = c.take<uint8_t>(P * 32); f.pdesc_r = c.take<uint8_t>(P * 32);
-        f.n_kl_l = c.take<int>(B); f.n_kl_r = c.take<int>(B);
-        f.kl_l = c.take<gfpl_keyline>(L); f.kl_r = c.take<gfpl_keyline>(L);
-        f.ldesc_l = c.take<uint8_t>(L * 32); f.ldesc_r = c.take<uint8_t>(L * 32);
-        f.pyr_r = c.take<uint8_t>(pyr); f.time_stamp = c.take<double>(B);
-    };
-    gfpl_frames d{};
-    layout(d);   // sizing pass (base == nullptr)
-    if (sb->stage_bytes < c.off) {
-        if (sb->stage) (void)hipFree(sb->stage);
-        sb->stage = nullptr;
-        sb->stage_bytes = 0;
-        HIPCHK(hipMalloc(&sb->stage, c.off));
-        sb->stage_bytes = c.off;
+    f.batch = sb->B; f.kp_cap = sb->kp_cap; f.kl_cap = sb->kl_cap;
+    f.n_kp_l = c.take<int>(B); f.n_kp_r = c.take<int>(B);
+    f.kp_l = c.take<gfpl_keypoint>(P); f.kp_r = c.take<gfpl_keypoint>(P);
+    f.pdesc_l = c.take<uint8_t>(P * 32); f.pdesc_r = c.take<uint8_t>(P * 32);
+    f.n_kl_l = c.take<int>(B); f.n_kl_r = c.take<int>(B);
+    f.kl_l = c.take<gfpl_keyline>(L); f.kl_r = c.take<gfpl_keyline>(L);
+    f.ldesc_l = c.take<uint8_t>(L * 32); f.ldesc_r = c.take<uint8_t>(L * 32);
+    f.pyr_r = c.take<uint8_t>(pyr); f.time_stamp = c.take<double>(B);
+}
+
+int stage_alloc(gfpl_seqbatch* sb, int slot) {
+    if (!sb->copy) {
+        HIPCHK(hipStreamCreateWithFlags(&sb->copy, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            HIPCHK(hipEventCreateWithFlags(&sb->ev_ready[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&sb->ev_free[k], hipEventDisableTiming));
+        }
+        for (hipEvent_t& e : sb->ev_ticket) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    if (sb->stage[slot]) return GFPL_OK;
+    Carver c;
+    gfpl_frames f{};
+    stage_layout(c, sb, f);   // sizing pass (base == nullptr)
+    HIPCHK(hipMalloc(&sb->stage[slot], c.off));
+    sb->stage_bytes[slot] = c.off;
     c.off = 0;
-    c.base = (char*)sb->stage;
-    layout(d);
-    hipStream_t s = sb->ctx->stream;
-#define UP(field, n) HIPCHK(hipMemcpyAsync((void*)d.field, host->field, sizeof(*d.field) * (n), hipMemcpyHostToDevice, s))
-    UP(n_kp_l, B); UP(n_kp_r, B); UP(kp_l, P); UP(kp_r, P); UP(pdesc_l, P * 32); UP(pdesc_r, P * 32);
-    UP(n_kl_l, B); UP(n_kl_r, B); UP(kl_l, L); UP(kl_r, L); UP(ldesc_l, L * 32); UP(ldesc_r, L * 32);
-    UP(pyr_r, pyr); UP(time_stamp, B);
+    c.base = (char*)sb->stage[slot];
+    stage_layout(c, sb, sb->stage_view[slot]);
+    return GFPL_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t* ticket) {
+    if (!sb || !host || (slot != 0 && slot != 1) || !sb->ctx->has_cam) return GFPL_E_INVALID;
+    const int n = host->batch;
+    if (n < 1 || s0 < 0 || s0 + n > sb->B || host->kp_cap != sb->kp_cap || host->kl_cap != sb->kl_cap)
+        return GFPL_E_INVALID;
+    if (!host->n_kp_l || !host->n_kp_r || !host->kp_l || !host->kp_r || !host->pdesc_l || !host->pdesc_r ||
+        !host->n_kl_l || !host->n_kl_r || !host->kl_l || !host->kl_r || !host->ldesc_l || !host->ldesc_r ||
+        !host->pyr_r || !host->time_stamp)
+        return GFPL_E_INVALID;
+    int e = stage_alloc(sb, slot);
+    if (e) return e;
+    const gfpl_frames& d = sb->stage_view[slot];
+    hipStream_t s = sb->copy;
+    if (sb->free_recorded[slot]) HIPCHK(hipStreamWaitEvent(s, sb->ev_free[slot], 0));
+    const size_t N = n, P = N * sb->kp_cap, L = N * sb->kl_cap, S = s0;
+    const size_t kp0 = S * sb->kp_cap, kl0 = S * sb->kl_cap, pyr = (size_t)sb->ctx->cam.pyr_bytes;
+#define UP(field, off, cnt) \
+    HIPCHK(hipMemcpyAsync((void*)(d.field + (off)), host->field, sizeof(*d.field) * (cnt), hipMemcpyHostToDevice, s))
+    UP(n_kp_l, S, N); UP(n_kp_r, S, N); UP(kp_l, kp0, P); UP(kp_r, kp0, P);
+    UP(pdesc_l, kp0 * 32, P * 32); UP(pdesc_r, kp0 * 32, P * 32);
+    UP(n_kl_l, S, N); UP(n_kl_r, S, N); UP(kl_l, kl0, L); UP(kl_r, kl0, L);
+    UP(ldesc_l, kl0 * 32, L * 32); UP(ldesc_r, kl0 * 32, L * 32);
+    UP(pyr_r, S * pyr, N * pyr); UP(time_stamp, S, N);
 #undef UP
-    HIPCHK(hipStreamSynchronize(s));
-    *dev = d;
+    HIPCHK(hipEventRecord(sb->ev_ready[slot], s));
+    sb->ready_pending[slot] = true;
+    const int64_t t = sb->n_tickets++;
+    HIPCHK(hipEventRecord(sb->ev_ticket[t % 16], s));
+    if (ticket) *ticket = t;
+    return GFPL_OK;
+}
+
+int gfpl_upload_wait(gfpl_seqbatch* sb, int64_t ticket) {
+    if (!sb || ticket < 0 || ticket >= sb->n_tickets) return GFPL_E_INVALID;
+    // the event may since have been re-recorded by a newer copy on the same in-order stream:
+    // waiting for that one is later than needed, never earlier
+    HIPCHK(hipEventSynchronize(sb->ev_ticket[ticket % 16]));
+    return GFPL_OK;
+}
+
+int gfpl_staged_frames(gfpl_seqbatch* sb, int slot, gfpl_frames* dev) {
+    if (!sb || !dev || (slot != 0 && slot != 1) || !sb->stage[slot]) return GFPL_E_INVALID;
+    *dev = sb->stage_view[slot];
+    return GFPL_OK;
+}
+
+int gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* dev) {
+    if (!sb || !host || !dev) return GFPL_E_INVALID;
+    if (host->batch != sb->B) return GFPL_E_INVALID;
+    int64_t t = 0;
+    int e = gfpl_upload_frames_async(sb, host, 0, 0, &t);
+    if (e) return e;
+    e = gfpl_upload_wait(sb, t);
+    if (e) return e;
+    *dev = sb->stage_view[0];
     return GFPL_OK;
 }
 
@@ -881,34 +983,52 @@ int gfpl_get_kernel_times(gfpl_ctx* c, float* ms4) {
     return GFPL_OK;
 }
 
-int gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4) {
-    if (!sb || !bytes4) return GFPL_E_INVALID;
-    std::vector<int64_t> v((size_t)sb->B * 8);
+}  // extern "C"
+
+namespace {
+// column sums over the B per-sequence step records (k_step_bytes)
+int step_rec_sums(gfpl_seqbatch* sb, int64_t* sums) {
+    std::vector<int64_t> v((size_t)sb->B * STEP_REC);
     HIPCHK(hipStreamSynchronize(sb->ctx->stream));
     HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost));
-    int64_t t = 0;
-    for (int b = 0; b < sb->B; ++b) t += v[(size_t)b * 8 + 7];
-    // k_cut_search bytes are recorded per sequence; the other three are the
-    // stage bytes split as documented in k_step_bytes
-    bytes4[1] = t;
-    int64_t st[7];
-    int e = gfpl_last_step_stage_bytes(sb, st);
+    for (int s = 0; s < STEP_REC; ++s) {
+        int64_t t = 0;
+        for (int b = 0; b < sb->B; ++b) t += v[(size_t)b * STEP_REC + s];
+        sums[s] = t;
+    }
+    return GFPL_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4) {
+    if (!sb || !bytes4) return GFPL_E_INVALID;
+    int64_t v[STEP_REC];
+    int e = step_rec_sums(sb, v);
     if (e) return e;
+    // k_cut_search bytes are recorded per sequence; k_pose's are the pose stage's
     bytes4[0] = bytes4[2] = -1;   // not split out
-    bytes4[3] = st[5];
+    bytes4[1] = v[7];
+    bytes4[3] = v[5];
     return GFPL_OK;
 }
 
 int gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7) {
     if (!sb || !bytes7) return GFPL_E_INVALID;
-    std::vector<int64_t> v((size_t)sb->B * 8);
-    HIPCHK(hipStreamSynchronize(sb->ctx->stream));
-    HIPCHK(hipMemcpy(v.data(), sb->scr.bytes, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost));
-    for (int s = 0; s < 7; ++s) {
-        int64_t t = 0;
-        for (int b = 0; b < sb->B; ++b) t += v[(size_t)b * 8 + s];
-        bytes7[s] = t;
-    }
+    int64_t v[STEP_REC];
+    int e = step_rec_sums(sb, v);
+    if (e) return e;
+    for (int s = 0; s < 7; ++s) bytes7[s] = v[s];
+    return GFPL_OK;
+}
+
+int gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8) {
+    if (!sb || !counts8) return GFPL_E_INVALID;
+    int64_t v[STEP_REC];
+    int e = step_rec_sums(sb, v);
+    if (e) return e;
+    for (int s = 0; s < 8; ++s) counts8[s] = v[8 + s];
     return GFPL_OK;
 }
 

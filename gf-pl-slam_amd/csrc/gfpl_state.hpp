@@ -72,6 +72,8 @@ struct DevTrack {
     int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
+#define STEP_REC 16   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
+                      // [8..15] counts N_o N_k M_o S_p' S_l' M_p M_l n_inliers (gfpl_last_step_counts)
 #define CUT_FAST 48   // doubles of per-line comparison polynomials (k_cut.hip, PD_*)
 #define CUT_REC 72    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (576 B)
 
@@ -80,7 +82,7 @@ struct DevScratch {
                       // coefficients, geometry flag, list index of the next line | lower-triangle r = 0 info
     int32_t* knn;     // [B*6*kcap] initial-frame knn results (idx0, d0, d1, ...)
     double* proj;     // [B*kcap*2] cross-points projections (aliases knn: init never overlaps)
-    int64_t* bytes;   // [B] algorithmic bytes of the last step
+    int64_t* bytes;   // [B*STEP_REC] algorithmic bytes of the last step per stage | feature counts
     int32_t* n_subpix; // [B] left keypoints that reached the sub-pixel SAD (M_o)
     double* cut_sum;   // [B*24] invCov_sum (lower triangle) after the r=0 pass
     double* cut_dtinv; // [B*16] DT_inv of the line cut

@@ -797,9 +797,9 @@ __global__ void __launch_bounds__(256) k_line_uncertainty(KParams p) {
 
 // Algorithmic HBM bytes of one step of one sequence, per stage (DESIGN.md
 // §Roofline): the bytes each stage must read or write at minimum, from the
-// runtime counts.  bytes[b*8 + s], s = 0 stereo_points, 1 stereo_lines,
+// runtime counts.  bytes[b*STEP_REC + s], s = 0 stereo_points, 1 stereo_lines,
 // 2 cross_points (+ prev line uncertainty), 3 cross_lines, 4 line_cut, 5 pose,
-// 6 total.
+// 6 total, 7 k_cut_search; 8-15 the counts they are priced on.
 __global__ void k_step_bytes(KParams p) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.B) return;
@@ -817,12 +817,16 @@ __global__ void k_step_bytes(KParams p) {
     st[4] = 608 * Ml + 44 * Mp;                              // cut: line/point info inputs, cut endpoints + invCov
     st[5] = 54 * Mp + 86 * Ml + 1504;                        // GN inputs once, inlier flags, pose + covariances
     int64_t tot = 0;
-    for (int i = 0; i < 6; ++i) { p.scr.bytes[8 * b + i] = st[i]; tot += st[i]; }
-    p.scr.bytes[8 * b + 6] = tot;
+    int64_t* rec = p.scr.bytes + (size_t)STEP_REC * b;
+    for (int i = 0; i < 6; ++i) { rec[i] = st[i]; tot += st[i]; }
+    rec[6] = tot;
     // k_cut_search alone: per matched line its cut inputs (sP eP covS covE le_obs
     // 208 B + index 4 B), its r = 0 info from k_cut_prep (168 B), the cut ratio
     // written (16 B); per sequence invCov_sum + metric + DT_inv (272 B)
-    p.scr.bytes[8 * b + 7] = (p.cfg.use_line_conf_cut && Ml > 0) ? 396 * Ml + 272 : 0;
+    rec[7] = (p.cfg.use_line_conf_cut && Ml > 0) ? 396 * Ml + 272 : 0;
+    // the counts the bytes are priced on (the bench's per-step means)
+    rec[8] = No; rec[9] = Nk; rec[10] = Mo; rec[11] = Sp2; rec[12] = Sl2; rec[13] = Mp; rec[14] = Ml;
+    rec[15] = p.tr.n_inliers[b];
     // insertStereoPair's last statement, numFrameSinceKeyframe++ (src/stereoFrameHandler.cpp:150):
     // this per-sequence kernel closes every gfpl_insert_stereo_pair
     p.tr.kf_nsince[b] = p.tr.kf_nsince[b] + 1;

@@ -228,7 +228,7 @@ class SynthParams(C.Structure):
                 ("yaw_rate", C.c_double), ("z_min", C.c_double), ("z_max", C.c_double),
                 ("px_noise", C.c_double), ("distractor_frac", C.c_double),
                 ("margin", C.c_int), ("seed", C.c_uint64),
-                ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp)]
+                ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp), ("respawn", C.c_int)]
 
 
 # ------------------------------------------------------------- libraries --
@@ -286,6 +286,9 @@ def hiplib() -> C.CDLL:
             "gfpl_update_frame": ([P], C.c_int),
             "gfpl_frame_step": ([P, P], C.c_int),
             "gfpl_upload_frames": ([P, P, P], C.c_int),
+            "gfpl_upload_frames_async": ([P, P, C.c_int, C.c_int, P], C.c_int),
+            "gfpl_upload_wait": ([P, C.c_int64], C.c_int),
+            "gfpl_staged_frames": ([P, C.c_int, P], C.c_int),
             "gfpl_stereo_points": ([P, P], C.c_int),
             "gfpl_stereo_lines": ([P, P], C.c_int),
             "gfpl_line_uncertainty": ([P], C.c_int),
@@ -309,6 +312,7 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_kernel_bytes": ([P, P], C.c_int),
             "gfpl_last_step_bytes": ([P, P], C.c_int),
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
+            "gfpl_last_step_counts": ([P, P], C.c_int),
             "gfpl_lsd_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_lsd_destroy": ([P], C.c_int),
             "gfpl_lsd_detect": ([P, P, C.c_int, P, P, P], C.c_int),
@@ -345,6 +349,8 @@ def synthlib() -> C.CDLL:
         L.gfpl_synth_batch.restype = C.c_int
         L.gfpl_synth_image.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P]
         L.gfpl_synth_image.restype = C.c_int
+        L.gfpl_synth_frame_ex.argtypes = [P, P, C.c_int, C.c_int, C.c_int, C.c_int] + [P] * 16
+        L.gfpl_synth_frame_ex.restype = C.c_int
         L._gfpl_typed = True
     return L
 
@@ -379,13 +385,19 @@ CAMERAS = {
 EUROC_SEQS = ["mh_01", "mh_02", "mh_03", "mh_04", "mh_05", "v1_01", "v1_02", "v1_03"]
 
 
+EUROC_MAX_POSES = 512
+
+
 def euroc_traj(seq: str = "mh_01", n: int = 64):
     """First n ground-truth camera poses (3x4 row-major T_w<-c) and timestamps [s] of a
-    EuRoC sequence, from the reference's config/asl/gt-ass/<seq> files (data/euroc_gt.json)."""
-    with open(os.path.join(os.path.dirname(LIB_DIR), "data", "euroc_gt.json")) as f:
-        d = json.load(f)["seqs"][seq]
-    T = np.ascontiguousarray(np.array(d["T_wc_3x4"][:n], np.float64))
-    t = np.ascontiguousarray(np.array(d["t"][:n], np.float64))
+    EuRoC sequence, from the reference's config/asl/gt-ass/<seq> files (data/euroc_gt.npz,
+    the first 512 poses of each; tests/golden/make_euroc_fixture.py).  n beyond the stored
+    poses raises: the generator never wraps a trajectory around."""
+    if n > EUROC_MAX_POSES:
+        raise ValueError(f"euroc_traj: {n} poses requested, {EUROC_MAX_POSES} stored for {seq}")
+    with np.load(os.path.join(os.path.dirname(LIB_DIR), "data", "euroc_gt.npz")) as d:
+        T = np.ascontiguousarray(d[seq + "_T"][:n])
+        t = np.ascontiguousarray(d[seq + "_t"][:n])
     return T, t
 
 
@@ -428,6 +440,27 @@ def synth_keylines(n: int, w: int, h: int, seed: int, min_len: float = 2.0, max_
         gx, gy = np.float32(ex), np.float32(ey)
         kl[i] = (fs, fe, gx, gy, np.arctan2(gy - fe, gx - fs).astype(np.float32), 0)
     return kl
+
+
+def synth_true_counts(cam: Camera, sp: SynthParams, seq: int, frame: int, kp_cap: int = 0, kl_cap: int = 0):
+    """(true keypoints, true keylines) per side in frame `frame` of sequence `seq`: the
+    detections that observe a landmark / 3-D segment (the rest are distractors)."""
+    kp_cap, kl_cap = kp_cap or sp.n_kp, kl_cap or sp.n_kl
+    n = np.zeros(6, np.int32)
+    kp = np.zeros((2, kp_cap), KEYPOINT_DT)
+    kl = np.zeros((2, kl_cap), KEYLINE_DT)
+    pd = np.zeros((2, kp_cap, DESC), np.uint8)
+    ld = np.zeros((2, kl_cap, DESC), np.uint8)
+    pyr = np.zeros(cam.pyr_bytes, np.uint8)
+    ts = np.zeros(1, np.float64)
+    nt = np.zeros(2, np.int32)
+    a = n.ctypes.data
+    check(synthlib().gfpl_synth_frame_ex(C.byref(sp), C.byref(cam), seq, frame, kp_cap, kl_cap, a, a + 4,
+                                         kp[0].ctypes.data, kp[1].ctypes.data, pd[0].ctypes.data, pd[1].ctypes.data,
+                                         a + 8, a + 12, kl[0].ctypes.data, kl[1].ctypes.data, ld[0].ctypes.data,
+                                         ld[1].ctypes.data, pyr.ctypes.data, ts.ctypes.data, None, nt.ctypes.data),
+          "synth_frame_ex")
+    return int(nt[0]), int(nt[1])
 
 
 def synth_params(**over) -> SynthParams:
@@ -517,16 +550,23 @@ class HostBatch:
     def arrays(self):
         return self._arrs
 
-    def fill(self, frame_idx: int, threads: int = 0):
-        """Generate frame `frame_idx` of sequences [seq0, seq0 + B) (gfpl_synth_batch)."""
+    def fill(self, frame_idx: int, threads: int = 0, seq0: Optional[int] = None, n: Optional[int] = None):
+        """Generate frame `frame_idx` of sequences [seq0, seq0 + n) (gfpl_synth_batch) into
+        the first n rows (default: the batch's own seq0 and all B rows)."""
         threads = threads or min(16, os.cpu_count() or 1)
+        seq0 = self.seq0 if seq0 is None else seq0
+        n = self.B if n is None else n
+        if not 0 < n <= self.B:
+            raise ValueError(f"fill: {n} sequences into a batch of {self.B}")
         check(synthlib().gfpl_synth_batch(
-            C.byref(self.sp), C.byref(self.cam), self.seq0, self.B, frame_idx, 1, self.kp_cap, self.kl_cap,
+            C.byref(self.sp), C.byref(self.cam), seq0, n, frame_idx, 1, self.kp_cap, self.kl_cap,
             *[_ptr(a) for a in self._arrs], threads), "synth_batch")
-        self.frame_idx = frame_idx
+        self.frame_idx, self.n = frame_idx, n
 
-    def frames(self) -> Frames:
-        return make_frames(self.B, self.kp_cap, self.kl_cap, self._arrs)
+    def frames(self, n: Optional[int] = None) -> Frames:
+        """gfpl_frames (HOST pointers) of the first n rows (default all B)."""
+        n = self.B if n is None else n
+        return make_frames(n, self.kp_cap, self.kl_cap, [a[:n] for a in self._arrs])
 
     def nbytes(self) -> int:
         return sum(a.nbytes for a in self._arrs)
@@ -775,6 +815,23 @@ class StereoFrameHandler:
         dev._keep = [host]
         return dev
 
+    def upload_async(self, host: Frames, s0: int, slot: int) -> int:
+        """gfpl_upload_frames_async: enqueue the copy of host.batch sequences of HOST frames
+        into sequences [s0, s0 + host.batch) of staging buffer `slot` on the seqbatch's copy
+        stream; returns the ticket for upload_wait (host memory untouched until then)."""
+        t = C.c_int64()
+        check(self.L.gfpl_upload_frames_async(self.h, C.byref(host), s0, slot, C.byref(t)), "upload_frames_async")
+        return t.value
+
+    def upload_wait(self, ticket: int):
+        check(self.L.gfpl_upload_wait(self.h, ticket), "upload_wait")
+
+    def staged_frames(self, slot: int) -> Frames:
+        """Device view of staging buffer `slot` (every tracker call reading it waits for its copies)."""
+        dev = Frames()
+        check(self.L.gfpl_staged_frames(self.h, slot, C.byref(dev)), "staged_frames")
+        return dev
+
     def read_frame(self, which: int, seq: int) -> FrameHost:
         fh = FrameHost(self.kp_cap, self.kl_cap)
         check(self.L.gfpl_read_frame(self.h, which, seq, fh.ptr()), "read_frame")
@@ -828,6 +885,16 @@ class StereoFrameHandler:
         v = np.zeros(7, np.int64)
         check(self.L.gfpl_last_step_stage_bytes(self.h, v.ctypes.data), "last_step_stage_bytes")
         return v
+
+    STEP_COUNTS = ["N_o", "N_k", "M_o", "S_p", "S_l", "M_p", "M_l", "n_inliers"]
+
+    def last_step_counts(self) -> dict:
+        """Per-sequence means of the counts the last step's bytes are priced on
+        (gfpl_last_step_counts): keypoints / keylines (both sides), SAD keypoints,
+        stereo points / lines of the new frame, matched points / lines, inliers."""
+        v = np.zeros(8, np.int64)
+        check(self.L.gfpl_last_step_counts(self.h, v.ctypes.data), "last_step_counts")
+        return {n: float(x) / self.B for n, x in zip(self.STEP_COUNTS, v)}
 
     def last_step_kernel_bytes(self) -> np.ndarray:
         v = np.zeros(4, np.int64)

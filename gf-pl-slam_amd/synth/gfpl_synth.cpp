@@ -51,7 +51,7 @@ struct Pose { double R[9]; double t[3]; };   // T_w<-c : X_w = R X_c + t
 
 void pose_at(const gfpl_synth_params* p, int k, Pose* T, double* ts) {
     if (p->traj && p->n_traj > 0) {
-        int kk = k % p->n_traj;
+        int kk = std::min(std::max(k, 0), p->n_traj - 1);   // callers refuse k >= n_traj
         const double* r = p->traj + 12 * kk;
         // rebase on the first pose so the sequence starts at identity
         const double* r0 = p->traj;
@@ -122,51 +122,89 @@ struct World {
     std::vector<Segment> lines;
 };
 
-void build_world(const gfpl_synth_params* p, const gfpl_camera* cam, int seq, World* W) {
-    Rng r(mix(p->seed, 0x1000000ull + (uint64_t)seq));
-    // ORB per-level quotas (src/ORBextractor.cc:433-446)
+// ORB per-level quotas (src/ORBextractor.cc:433-446), normalised to probabilities
+std::vector<double> level_quota(const gfpl_synth_params* p, const gfpl_camera* cam) {
     int nl = cam->n_levels;
     std::vector<double> quota(nl);
-    {
-        double factor = 1.0 / (double)cam->scale[1 < nl ? 1 : 0];
-        double nd = p->n_kp * (1 - factor) / (1 - std::pow(factor, (double)nl));
-        double sum = 0;
-        for (int l = 0; l < nl - 1; ++l) { quota[l] = std::round(nd); sum += quota[l]; nd *= factor; }
-        quota[nl - 1] = std::max(p->n_kp - sum, 0.0);
-        double tot = 0; for (double q : quota) tot += q;
-        for (double& q : quota) q /= tot;
-    }
-    Pose T0; double ts;
-    pose_at(p, 0, &T0, &ts);
-    double m = p->margin;
+    double factor = 1.0 / (double)cam->scale[1 < nl ? 1 : 0];
+    double nd = p->n_kp * (1 - factor) / (1 - std::pow(factor, (double)nl));
+    double sum = 0;
+    for (int l = 0; l < nl - 1; ++l) { quota[l] = std::round(nd); sum += quota[l]; nd *= factor; }
+    quota[nl - 1] = std::max(p->n_kp - sum, 0.0);
+    double tot = 0; for (double q : quota) tot += q;
+    for (double& q : quota) q /= tot;
+    return quota;
+}
+
+void sample_landmark(Rng& r, const gfpl_synth_params* p, const gfpl_camera* cam, const std::vector<double>& quota,
+                     const Pose& T, Landmark& L) {
+    const int nl = cam->n_levels;
+    const double m = p->margin;
+    double u = r.uni(m, cam->width - m), v = r.uni(m, cam->height - m);
+    double iz = r.uni(1.0 / p->z_max, 1.0 / p->z_min);   // uniform in inverse depth
+    double z = 1.0 / iz;
+    double Xc[3] = {(u - cam->cx) * z / cam->fx, (v - cam->cy) * z / cam->fy, z};
+    c2w(T, Xc, L.X);
+    double a = r.uni(), acc = 0; L.octave = nl - 1;
+    for (int l = 0; l < nl; ++l) { acc += quota[l]; if (a < acc) { L.octave = l; break; } }
+    rand_code(r, L.code);
+    L.key = r.next();
+}
+
+void sample_segment(Rng& r, const gfpl_synth_params* p, const gfpl_camera* cam, const Pose& T, Segment& S) {
+    const double m = p->margin;
+    double u = r.uni(m, cam->width - m), v = r.uni(m, cam->height - m);
+    double z = r.uni(p->z_min * 1.5, p->z_max * 0.8);
+    double Xc[3] = {(u - cam->cx) * z / cam->fx, (v - cam->cy) * z / cam->fy, z};
+    double d[3] = {r.gauss(), r.gauss(), 0.3 * r.gauss()};
+    double n = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-12;
+    double len = r.uni(0.3, 1.5) * z / 4.0;
+    double Sc[3], Ec[3];
+    for (int k = 0; k < 3; ++k) { Sc[k] = Xc[k] - 0.5 * len * d[k] / n; Ec[k] = Xc[k] + 0.5 * len * d[k] / n; }
+    c2w(T, Sc, S.S);
+    c2w(T, Ec, S.E);
+    rand_code(r, S.code);
+    S.key = r.next();
+}
+
+// The world seen at frame k.  respawn == 0: one pool sampled in the first camera's
+// frustum, fixed for the whole sequence (it drains as the camera moves on).
+// respawn == L > 0: every pool slot lives L frames and is re-sampled in the frustum of
+// the camera at its spawn frame, with a per-slot phase, so at any frame the pool's ages
+// are spread uniformly over 0..L-1 and the share of visible landmarks (hence the
+// true-keypoint count) is stationary.  Slot i at frame k: epoch e = (k + phase_i) / L,
+// spawn frame k - (k + phase_i) % L; everything drawn from (seed, seq, slot, epoch).
+void build_world(const gfpl_synth_params* p, const gfpl_camera* cam, int seq, int k, World* W) {
+    const std::vector<double> quota = level_quota(p, cam);
     W->pts.resize(p->n_world_pts);
-    for (int i = 0; i < p->n_world_pts; ++i) {
-        Landmark& L = W->pts[i];
-        double u = r.uni(m, cam->width - m), v = r.uni(m, cam->height - m);
-        double iz = r.uni(1.0 / p->z_max, 1.0 / p->z_min);   // uniform in inverse depth
-        double z = 1.0 / iz;
-        double Xc[3] = {(u - cam->cx) * z / cam->fx, (v - cam->cy) * z / cam->fy, z};
-        c2w(T0, Xc, L.X);
-        double a = r.uni(), acc = 0; L.octave = nl - 1;
-        for (int l = 0; l < nl; ++l) { acc += quota[l]; if (a < acc) { L.octave = l; break; } }
-        rand_code(r, L.code);
-        L.key = r.next();
-    }
     W->lines.resize(p->n_world_lines);
-    for (int i = 0; i < p->n_world_lines; ++i) {
-        Segment& S = W->lines[i];
-        double u = r.uni(m, cam->width - m), v = r.uni(m, cam->height - m);
-        double z = r.uni(p->z_min * 1.5, p->z_max * 0.8);
-        double Xc[3] = {(u - cam->cx) * z / cam->fx, (v - cam->cy) * z / cam->fy, z};
-        double d[3] = {r.gauss(), r.gauss(), 0.3 * r.gauss()};
-        double n = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-12;
-        double len = r.uni(0.3, 1.5) * z / 4.0;
-        double Sc[3], Ec[3];
-        for (int k = 0; k < 3; ++k) { Sc[k] = Xc[k] - 0.5 * len * d[k] / n; Ec[k] = Xc[k] + 0.5 * len * d[k] / n; }
-        c2w(T0, Sc, S.S);
-        c2w(T0, Ec, S.E);
-        rand_code(r, S.code);
-        S.key = r.next();
+    if (p->respawn <= 0) {
+        Rng r(mix(p->seed, 0x1000000ull + (uint64_t)seq));
+        Pose T0; double ts;
+        pose_at(p, 0, &T0, &ts);
+        for (int i = 0; i < p->n_world_pts; ++i) sample_landmark(r, p, cam, quota, T0, W->pts[i]);
+        for (int i = 0; i < p->n_world_lines; ++i) sample_segment(r, p, cam, T0, W->lines[i]);
+        return;
+    }
+    const int L = p->respawn;
+    std::vector<Pose> spawn(L);   // spawn[a] = pose of frame k - a (trajectories: clamped at frame 0)
+    for (int a = 0; a < L; ++a) {
+        double ts;
+        pose_at(p, k - a, &spawn[a], &ts);   // synthetic motion extends to negative times
+    }
+    const uint64_t sk = mix(p->seed, 0x5000000ull + (uint64_t)seq);
+    for (int kind = 0; kind < 2; ++kind) {
+        const int n = kind == 0 ? p->n_world_pts : p->n_world_lines;
+        for (int i = 0; i < n; ++i) {
+            const uint64_t slot = mix(sk, ((uint64_t)kind << 32) | (uint64_t)i);
+            const int phase = (int)(slot % (uint64_t)L);
+            const int64_t t = (int64_t)k + phase;
+            const uint64_t epoch = (uint64_t)(t / L);
+            const int age = (int)(t % L);
+            Rng r(mix(slot, epoch));
+            if (kind == 0) sample_landmark(r, p, cam, quota, spawn[age], W->pts[i]);
+            else sample_segment(r, p, cam, spawn[age], W->lines[i]);
+        }
     }
 }
 
@@ -200,16 +238,17 @@ extern "C" void gfpl_synth_default(gfpl_synth_params* p) {
     p->seed = 0x9E3779B97F4A7C15ull;
 }
 
-extern "C" int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* cam,
-                                int seq, int k, int kp_cap, int kl_cap,
-                                int* n_kp_l, int* n_kp_r, gfpl_keypoint* kp_l, gfpl_keypoint* kp_r,
-                                uint8_t* pdesc_l, uint8_t* pdesc_r,
-                                int* n_kl_l, int* n_kl_r, gfpl_keyline* kl_l, gfpl_keyline* kl_r,
-                                uint8_t* ldesc_l, uint8_t* ldesc_r,
-                                uint8_t* pyr_r, double* time_stamp, double* T_wc_out) {
-    if (!p || !cam || p->n_kp > kp_cap || p->n_kl > kl_cap) return GFPL_E_INVALID;
+extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera* cam,
+                                   int seq, int k, int kp_cap, int kl_cap,
+                                   int* n_kp_l, int* n_kp_r, gfpl_keypoint* kp_l, gfpl_keypoint* kp_r,
+                                   uint8_t* pdesc_l, uint8_t* pdesc_r,
+                                   int* n_kl_l, int* n_kl_r, gfpl_keyline* kl_l, gfpl_keyline* kl_r,
+                                   uint8_t* ldesc_l, uint8_t* ldesc_r,
+                                   uint8_t* pyr_r, double* time_stamp, double* T_wc_out, int* n_true_out) {
+    if (!p || !cam || p->n_kp > kp_cap || p->n_kl > kl_cap || k < 0) return GFPL_E_INVALID;
+    if (p->traj && k >= p->n_traj) return GFPL_E_INVALID;   // past the loaded trajectory: no wrap-around
     World W;
-    build_world(p, cam, seq, &W);
+    build_world(p, cam, seq, k, &W);
     Pose T; double ts;
     pose_at(p, k, &T, &ts);
     if (time_stamp) *time_stamp = ts;
@@ -307,6 +346,8 @@ extern "C" int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* c
         *n_kp_l = (int)L.size(); *n_kp_r = (int)R.size();
     }
 
+    if (n_true_out) n_true_out[0] = (int)vis.size();
+
     // ---- lines
     std::vector<gfpl_keyline> LL, LR;
     std::vector<std::array<uint8_t, 32>> LDL, LDR;
@@ -336,6 +377,7 @@ extern "C" int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* c
         observe_code(ro, sg.code, dr.data());
         LL.push_back(a); LR.push_back(c); LDL.push_back(dl); LDR.push_back(dr);
     }
+    if (n_true_out) n_true_out[1] = (int)LL.size();
     {
         Rng rd(mix(mix(p->seed, 0x4000000ull + (uint64_t)seq), (uint64_t)k));
         auto distractor_kl = [&](Rng& rr) {
@@ -363,6 +405,17 @@ extern "C" int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* c
         *n_kl_l = (int)LL.size(); *n_kl_r = (int)LR.size();
     }
     return 0;
+}
+
+extern "C" int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* cam,
+                                int seq, int k, int kp_cap, int kl_cap,
+                                int* n_kp_l, int* n_kp_r, gfpl_keypoint* kp_l, gfpl_keypoint* kp_r,
+                                uint8_t* pdesc_l, uint8_t* pdesc_r,
+                                int* n_kl_l, int* n_kl_r, gfpl_keyline* kl_l, gfpl_keyline* kl_r,
+                                uint8_t* ldesc_l, uint8_t* ldesc_r,
+                                uint8_t* pyr_r, double* time_stamp, double* T_wc_out) {
+    return gfpl_synth_frame_ex(p, cam, seq, k, kp_cap, kl_cap, n_kp_l, n_kp_r, kp_l, kp_r, pdesc_l, pdesc_r,
+                               n_kl_l, n_kl_r, kl_l, kl_r, ldesc_l, ldesc_r, pyr_r, time_stamp, T_wc_out, nullptr);
 }
 
 extern "C" int gfpl_synth_batch(const gfpl_synth_params* p, const gfpl_camera* cam,

@@ -32,6 +32,10 @@ typedef struct gfpl_synth_params {
     const double* traj;       /* optional [n_traj*12] T_w<-c rows (3x4 row-major); NULL = synthetic motion */
     int      n_traj;
     const double* traj_t;     /* optional [n_traj] timestamps [s]                          */
+    int      respawn;         /* 0: one landmark pool per sequence, sampled at frame 0 (it
+                                 drains as the camera moves); L > 0: each pool slot is
+                                 re-sampled in the current frustum every L frames (per-slot
+                                 phase), so the true-keypoint share is stationary          */
 } gfpl_synth_params;
 
 /* Default parameters for a camera (cfg 2 counts: 2000 ORB + 500 LBD). */
@@ -47,6 +51,16 @@ int gfpl_synth_frame(const gfpl_synth_params* p, const gfpl_camera* cam,
                      int* n_kl_l, int* n_kl_r, gfpl_keyline* kl_l, gfpl_keyline* kl_r,
                      uint8_t* ldesc_l, uint8_t* ldesc_r,
                      uint8_t* pyr_r, double* time_stamp, double* T_wc_out);
+
+/* gfpl_synth_frame + n_true[2] (when non-NULL): the true (landmark) keypoints and
+ * keylines per side in the frame; the rest are distractors.                   */
+int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera* cam,
+                        int seq_id, int frame_idx, int kp_cap, int kl_cap,
+                        int* n_kp_l, int* n_kp_r, gfpl_keypoint* kp_l, gfpl_keypoint* kp_r,
+                        uint8_t* pdesc_l, uint8_t* pdesc_r,
+                        int* n_kl_l, int* n_kl_r, gfpl_keyline* kl_l, gfpl_keyline* kl_r,
+                        uint8_t* ldesc_l, uint8_t* ldesc_r,
+                        uint8_t* pyr_r, double* time_stamp, double* T_wc_out, int* n_true);
 
 /* Generate frames [f0, f0+nf) for sequences [s0, s0+ns) into batched host
  * arrays laid out [frame][seq][cap] using up to n_threads threads.          */

@@ -273,10 +273,24 @@ int  gfpl_optimize_pose(gfpl_seqbatch* sb);
  * sequence: dt_ini = HOST array [B*16] row-major (NULL = prev_frame->DT).  Synchronises. */
 int  gfpl_optimize_pose_ini(gfpl_seqbatch* sb, const double* dt_ini);
 /* Copy one batch of HOST input frames (host->* are host pointers, same layout)
- * into a device staging area owned by the seqbatch and return its device view
- * in *dev (valid until the next upload).  Synchronous; for FFI callers without a
- * HIP runtime of their own.  The rate through this path includes PCIe.        */
+ * into staging buffer 0 of the seqbatch and return its device view in *dev
+ * (valid until the next upload into that buffer).  Synchronous; for FFI callers
+ * without a HIP runtime of their own.  The rate through this path includes PCIe. */
 int  gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames* dev);
+/* Stream-ordered upload, no host synchronisation: copy the host->batch sequences of
+ * a HOST input batch (pinned memory for an asynchronous DMA) into sequences
+ * [s0, s0 + host->batch) of staging buffer `slot` (0 or 1; each holds one input
+ * frame of all B sequences, allocated on first use) on the seqbatch's own copy
+ * stream.  The copy waits for the last tracker call that read the slot, and every
+ * tracker call that reads the slot (gfpl_staged_frames view) waits for the copies
+ * enqueued before it — so uploading frame k+1 into one slot overlaps the step on
+ * frame k in the other.  *ticket (nullable) names the copy for gfpl_upload_wait;
+ * the host memory must stay unchanged until then.                              */
+int  gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t* ticket);
+/* Block the host until the copy `ticket` (and every copy enqueued before it) is done. */
+int  gfpl_upload_wait(gfpl_seqbatch* sb, int64_t ticket);
+/* Device view (all B sequences) of staging buffer `slot` (GFPL_E_INVALID before its first upload). */
+int  gfpl_staged_frames(gfpl_seqbatch* sb, int slot, gfpl_frames* dev);
 /* StereoFrameHandler::updateFrame_ECCV18 state swap (src/stereoFrameHandler.cpp:864-922):
  * prev <- curr, matched lists cleared.  (FAST-threshold adaptation is out of scope;
  * the T_base trajectory log lives in the host mirror, gf-pl-slam_amd/host/stvo.h.) */
@@ -496,6 +510,11 @@ int  gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes);
 /* ... per stage: [stereo_points, stereo_lines, cross_points, cross_lines,
  * line_cut, pose, total] (DESIGN.md §Roofline gives each stage's formula). */
 int  gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7);
+/* The counts those bytes are priced on, summed over the batch: [N_o (keypoints, both
+ * sides), N_k (keylines, both sides), M_o (left keypoints reaching the sub-pixel SAD),
+ * S_p (stereo points of the new frame), S_l (its stereo lines), M_p (matched_pt), M_l
+ * (matched_ls), n_inliers] of the last insert.  Synchronises.                   */
+int  gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
  * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same

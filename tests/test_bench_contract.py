@@ -34,5 +34,8 @@ def test_bench_json_contract():
     assert ps["sequences"] == 4 and ps["frames"] == 4 * 4 and ps["mismatches"] == 0, ps
     hf = d["host_fed"]
     assert 0 < hf["value"] < d["value"] and hf["upload_GBps"] > 0
+    c = d["counts_per_seq_step"]
+    assert c["S_p"] > 0 and c["S_l"] > 0 and c["M_p"] > 0 and c["M_o"] >= c["S_p"]
+    assert d["roofline"]["window"] and "traffic_note" in d["roofline"]
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0 and cb["sample"]

@@ -30,6 +30,33 @@ def test_launcher_spawns_two_ranks():
     assert d["config"]["sequences_per_gpu"] == 4
 
 
+def test_launcher_eight_ranks_fit_one_host():
+    """The N=8 launch (the driver's scaling run) rehearsed on CPU: 8 gloo ranks, each with its
+    share of the host cores and a ring of two pinned chunks of its batch (not the whole
+    batch: 8 ranks x 16.5 GB pinned would not fit a host), stated in the line."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run", "--batch", "1024",
+                        "--steps", "2", "--warmup", "0", "--no-cpu", "--master-port", str(29900 + os.getpid() % 90)],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["frames_sharded"] == 8 * 1024 * 2
+    h = d["host"]
+    per_seq = d["input_bytes_per_step"] / 1024
+    assert h["chunk_sequences"] == 256                       # B / 8, at least 256
+    assert d["pinned_bytes_per_rank_if_gpu"] == 2 * 256 * per_seq   # two chunks, not the batch
+    cores = len(os.sched_getaffinity(0))
+    assert h["cores_share_per_rank"] == max(1, cores // 8) and h["gen_threads_per_rank"] <= h["cores_share_per_rank"]
+
+
+def test_cfg4_refuses_frames_past_the_trajectory():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "cfg4",
+                        "--steps", "600", "--batch", "4", "--no-cpu"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 2 and "ground-truth poses" in r.stderr
+
+
 def test_world_size_mismatch_refused():
     r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

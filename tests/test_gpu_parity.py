@@ -299,14 +299,67 @@ def test_optimize_pose_explicit_initial_guess():
             o.updateFrame()
 
 
-def test_euroc_ground_truth_trajectory_parity():
-    """BASELINE configs[3] shape: the EuRoC rig on a ground-truth trajectory (MH_03)."""
-    T, t = gfpl.euroc_traj("mh_03", 6)
-    rep = _run_sequence("euroc", {}, n_seq=2, n_frames=6, kp_cap=2048, kl_cap=512,
-                        synth_over=dict(z_min=2.0, z_max=12.0, traj=T.ctypes.data, n_traj=len(t),
-                                        traj_t=t.ctypes.data), seed=31)
+@pytest.mark.parametrize("seq", gfpl.EUROC_SEQS)
+def test_euroc_ground_truth_trajectory_parity(seq):
+    """BASELINE configs[3]: the EuRoC rig on each of the eight ground-truth trajectories
+    (config/asl/gt-ass/{mh_01..mh_05, v1_01..v1_03}), bench cfg4's scene (re-spawned
+    landmarks), 10+10 GN iterations."""
+    T, t = gfpl.euroc_traj(seq, 6)
+    rep = _run_sequence("euroc", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
+                        n_seq=2, n_frames=6, kp_cap=2048, kl_cap=512,
+                        synth_over=dict(z_min=2.0, z_max=12.0, respawn=16, traj=T.ctypes.data, n_traj=len(t),
+                                        traj_t=t.ctypes.data), seed=31 + gfpl.EUROC_SEQS.index(seq))
     _check(rep)
     assert all(rep["pose_exact"])
+
+
+@pytest.mark.parametrize("wl", ["cfg2", "cfg3"])
+def test_bench_workload_parity(wl):
+    """The bench's own scenes (stationary, landmarks re-spawned: bench.WORKLOADS) over
+    frames 0..7, so re-spawned landmarks enter and leave the matched sets."""
+    import bench
+    cam_name, over, _ = bench.WORKLOADS[wl]
+    rep = _run_sequence(cam_name, dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
+                        n_seq=2, n_frames=8, kp_cap=2048, kl_cap=512, synth_over=over, seed=41)
+    _check(rep)
+    assert all(rep["pose_exact"])
+
+
+def test_async_double_buffered_upload_parity():
+    """gfpl_upload_frames_async: frames uploaded chunk by chunk from host memory into the two
+    staging buffers on the copy stream, frame k + 1 copied while the step on frame k runs
+    (the staging events order them); poses and matched lists equal the oracle's."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    B, F, KP, KL = 5, 5, 2048, 512
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=43, respawn=16), B, F, KP, KL)
+    g = gfpl.StereoFrameHandler(gfpl.Context(cam, cfg), B, KP, KL)
+    orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(B)]
+
+    def upload(k, slot):
+        # two chunks of 3 + 2 sequences
+        ts = [g.upload_async(gfpl.make_frames(n, KP, KL, [a[k, s0:s0 + n] for a in H.arrays()]), s0, slot)
+              for s0, n in ((0, 3), (3, 2))]
+        return ts[-1]
+
+    g.upload_wait(upload(0, 0))
+    g.initialize(g.staged_frames(0))
+    upload(1, 1)
+    for k in range(1, F):
+        if k + 1 < F:
+            upload(k + 1, (k + 1) % 2)   # waits (on the GPU) for the step that last read that buffer
+        g.frameStep(g.staged_frames(k % 2))
+        for b, o in enumerate(orc):
+            if k == 1:
+                o.initialize(H.frames(0), b)
+            o.insertStereoPair(H.frames(k), b)
+            o.optimizePose()
+            tr = o.read_track()
+            o.updateFrame()
+            gp, op = g.read_frame(gfpl.PREV, b), o.read_frame(gfpl.PREV)
+            bad = compare_core(gp, op, f"f{k} s{b} ") + compare_track(g.read_last_track(b), tr, f"f{k} s{b} ")
+            pb, exact = compare_pose(gp, op, what=f"f{k} s{b} ")
+            assert not bad and not pb and exact, (bad + pb)[:10]
 
 
 # ---- certified line-cut search (DESIGN.md §4): the chosen ratios are the reference's

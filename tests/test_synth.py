@@ -2,6 +2,7 @@
 inside the margins the sub-pixel SAD needs, descriptors with the intended
 Hamming statistics."""
 import numpy as np
+import pytest
 
 import gfpl
 
@@ -50,3 +51,54 @@ def test_frames_independent_of_chunking():
     for a, b in zip(whole.arrays(), one.arrays()):
         assert np.array_equal(a[2], b[0])
     assert gfpl.input_bytes_per_frame(cam, 512, 128) == sum(a[0].nbytes for a in one.arrays()) // 3
+
+
+def test_respawn_keeps_the_scene_stationary():
+    """bench.py's workloads re-spawn landmarks (gfpl_synth `respawn`): the true (landmark)
+    detections stay at 90 % of the budget at every frame (10 % distractors),
+    where the fixed pool of respawn = 0 drains as the camera moves on."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    cfg = gfpl.default_config()
+    for wl, (cam_name, over, _) in bench.WORKLOADS.items():
+        cam = gfpl.make_camera(cam_name, cfg)
+        keep = []
+        if wl == "cfg4":
+            T, t = gfpl.euroc_traj("mh_02", 61)
+            keep += [T, t]
+            over = dict(over, traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data)
+        sp = gfpl.synth_params(**over)
+        for k in (0, 1, 7, 20, 33, 60):
+            for s in (0, 5):
+                n_kp, n_kl = gfpl.synth_true_counts(cam, sp, s, k)
+                assert n_kp >= 0.9 * sp.n_kp - 1 and n_kl >= 0.9 * sp.n_kl - 1, (wl, k, s, n_kp, n_kl)
+    # the fixed pool drains (the round-2 bench workload: 1800 -> < 1000 true keypoints by frame 25)
+    cam = gfpl.make_camera("vga", cfg)
+    assert gfpl.synth_true_counts(cam, gfpl.synth_params(), 0, 25)[0] < 1000
+
+
+def test_respawn_zero_is_the_fixed_pool():
+    """respawn = 0 keeps the round-1/2 generator bit for bit (the golden fixtures depend on it)."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    sp = gfpl.synth_params(seed=3, n_kp=300, n_kl=60, n_world_pts=400, n_world_lines=90)
+    assert sp.respawn == 0
+    A = gfpl.HostFrames(cam, sp, 2, 3, 512, 128)
+    sp2 = gfpl.synth_params(seed=3, n_kp=300, n_kl=60, n_world_pts=400, n_world_lines=90, respawn=4)
+    R = gfpl.HostFrames(cam, sp2, 2, 3, 512, 128)
+    assert not np.array_equal(A.kp_l, R.kp_l)
+
+
+def test_trajectory_frames_are_not_wrapped():
+    """A frame past the loaded ground-truth trajectory is refused (it used to wrap to pose 0)."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("euroc", cfg)
+    T, t = gfpl.euroc_traj("v1_03", 4)
+    sp = gfpl.synth_params(traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data, respawn=16)
+    gfpl.HostFrames(cam, sp, 1, 4, 2048, 512)
+    with pytest.raises(gfpl.GfplError):
+        gfpl.HostFrames(cam, sp, 1, 5, 2048, 512)
+    with pytest.raises(ValueError):
+        gfpl.euroc_traj("mh_01", gfpl.EUROC_MAX_POSES + 1)
