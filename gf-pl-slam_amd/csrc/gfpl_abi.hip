@@ -17,6 +17,7 @@ using namespace gfpl;
 struct gfpl_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = false;   // gfpl_create_async: the context created (and destroys) its stream
     gfpl_camera cam{};
     gfpl_config cfg{};
     bool has_cam = false, has_cfg = false;
@@ -52,9 +53,16 @@ struct gfpl_seqbatch {
     int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
 };
 
+struct gfpl_event {
+    int device = 0;
+    hipEvent_t ev = nullptr;
+};
+
 // for the other extern "C" objects built on a context (k_orb.hip)
 int gfpl_ctx_device(const gfpl_ctx* c) { return c->device; }
 void* gfpl_ctx_stream(const gfpl_ctx* c) { return (void*)c->stream; }
+const gfpl_camera* gfpl_ctx_camera(const gfpl_ctx* c) { return c->has_cam ? &c->cam : nullptr; }
+
 
 namespace {
 
@@ -178,12 +186,16 @@ int check_in(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (!in->n_kp_l || !in->n_kp_r || !in->kp_l || !in->kp_r || !in->pdesc_l || !in->pdesc_r || !in->n_kl_l ||
         !in->n_kl_r || !in->kl_l || !in->kl_r || !in->ldesc_l || !in->ldesc_r || !in->pyr_r || !in->time_stamp)
         return GFPL_E_INVALID;
+    // the sub-pixel SAD reads pyramid rows as aligned dwords relative to each sequence's pyramid
+    if (((uintptr_t)in->pyr_r & 3) != 0) return GFPL_E_INVALID;
     return GFPL_OK;
 }
 
 // A call that reads `in` from a staging slot waits (on the context stream) for that
 // slot's uploads; after enqueueing its work it marks the slot free for the next copy.
+// Frames with a producer event (gfpl_frames.ready / consumed) are ordered the same way.
 int in_acquire(gfpl_seqbatch* sb, const gfpl_frames* in) {
+    if (in->ready && hipStreamWaitEvent(sb->ctx->stream, in->ready->ev, 0) != hipSuccess) return -2;
     for (int s = 0; s < 2; ++s)
         if (sb->stage[s] && in->n_kp_l == sb->stage_view[s].n_kp_l) {
             if (sb->ready_pending[s] && hipStreamWaitEvent(sb->ctx->stream, sb->ev_ready[s], 0) != hipSuccess) return -2;
@@ -191,7 +203,8 @@ int in_acquire(gfpl_seqbatch* sb, const gfpl_frames* in) {
         }
     return -1;
 }
-int in_release(gfpl_seqbatch* sb, int slot) {
+int in_release(gfpl_seqbatch* sb, const gfpl_frames* in, int slot) {
+    if (in->consumed && hipEventRecord(in->consumed->ev, sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
     if (slot < 0) return GFPL_OK;
     if (hipEventRecord(sb->ev_free[slot], sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
     sb->free_recorded[slot] = true;
@@ -232,12 +245,67 @@ int gfpl_create(int device, void* stream, gfpl_ctx** out) {
     return GFPL_OK;
 }
 
+int gfpl_create_async(int device, gfpl_ctx** out) {
+    if (!out) return GFPL_E_INVALID;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return GFPL_E_NO_DEVICE;
+    if (device < 0 || device >= n) return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int e = gfpl_create(device, (void*)s, out);
+    if (e) { (void)hipStreamDestroy(s); return e; }
+    (*out)->own_stream = true;
+    return GFPL_OK;
+}
+
 int gfpl_destroy(gfpl_ctx* c) {
     if (!c) return GFPL_E_INVALID;
     if (!c->sbs.empty()) return GFPL_E_STATE;   // its seqbatches use the context's stream and config
     for (int i = 0; i < GFPL_NEV; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->own_stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
     delete c;
+    return GFPL_OK;
+}
+
+void* gfpl_get_stream(const gfpl_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int gfpl_event_create(gfpl_ctx* c, gfpl_event** out) {
+    if (!c || !out) return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    gfpl_event* e = new gfpl_event();
+    e->device = c->device;
+    if (hipEventCreateWithFlags(&e->ev, hipEventDisableTiming) != hipSuccess) { delete e; return GFPL_E_HIP; }
+    *out = e;
+    return GFPL_OK;
+}
+
+int gfpl_event_destroy(gfpl_event* e) {
+    if (!e) return GFPL_E_INVALID;
+    (void)hipEventDestroy(e->ev);
+    delete e;
+    return GFPL_OK;
+}
+
+int gfpl_event_record(gfpl_event* e, gfpl_ctx* c) {
+    if (!e || !c || e->device != c->device) return GFPL_E_INVALID;
+    HIPCHK(hipEventRecord(e->ev, c->stream));
+    return GFPL_OK;
+}
+
+int gfpl_event_wait(gfpl_ctx* c, gfpl_event* e) {
+    if (!e || !c || e->device != c->device) return GFPL_E_INVALID;
+    HIPCHK(hipStreamWaitEvent(c->stream, e->ev, 0));
+    return GFPL_OK;
+}
+
+int gfpl_event_synchronize(gfpl_event* e) {
+    if (!e) return GFPL_E_INVALID;
+    HIPCHK(hipEventSynchronize(e->ev));
     return GFPL_OK;
 }
 
@@ -251,6 +319,7 @@ int gfpl_set_camera(gfpl_ctx* c, const gfpl_camera* cam) {
         need = std::max<int64_t>(need, cam->lvl_offset[i] + (int64_t)cam->lvl_cols[i] * cam->lvl_rows[i]);
     }
     if (cam->pyr_bytes < need + GFPL_PYR_TAIL) return GFPL_E_INVALID;   // window loads read past the last row
+    if (cam->pyr_bytes % 4 != 0) return GFPL_E_INVALID;                 // every sequence's pyramid dword-aligned
     c->cam = *cam;
     c->has_cam = true;
     return GFPL_OK;
@@ -346,7 +415,7 @@ int gfpl_initialize(gfpl_seqbatch* sb, const gfpl_frames* in) {
     HIPCHK(launch_init(p, sb->ctx->stream));
     sb->initialized = true;
     sb->has_curr = false;
-    return in_release(sb, slot);
+    return in_release(sb, in, slot);
 }
 
 int gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in) {
@@ -358,7 +427,7 @@ int gfpl_stereo_points(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (slot == -2) return GFPL_E_HIP;
     HIPCHK(launch_stereo_points(params(sb, in), sb->ctx->stream));
     sb->has_curr = true;
-    return in_release(sb, slot);
+    return in_release(sb, in, slot);
 }
 
 int gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in) {
@@ -370,7 +439,7 @@ int gfpl_stereo_lines(gfpl_seqbatch* sb, const gfpl_frames* in) {
     if (slot == -2) return GFPL_E_HIP;
     HIPCHK(launch_stereo_lines(params(sb, in), sb->ctx->stream));
     sb->has_curr = true;
-    return in_release(sb, slot);
+    return in_release(sb, in, slot);
 }
 
 int gfpl_line_uncertainty(gfpl_seqbatch* sb) {
@@ -426,7 +495,7 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
     HIPCHK(launch_step_bytes(p, c->stream));
     tmark(c, 5);
     sb->has_curr = true;
-    return in_release(sb, slot);
+    return in_release(sb, in, slot);
 }
 
 int gfpl_optimize_pose(gfpl_seqbatch* sb) {

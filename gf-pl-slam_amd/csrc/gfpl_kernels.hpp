@@ -52,3 +52,51 @@ hipError_t launch_kf_map_filter(const DevCam& cam, const double* T1, const doubl
 // context accessors for the other extern "C" objects built on a context (gfpl_abi.hip)
 int gfpl_ctx_device(const gfpl_ctx* c);
 void* gfpl_ctx_stream(const gfpl_ctx* c);
+const gfpl_camera* gfpl_ctx_camera(const gfpl_ctx* c);   // NULL before gfpl_set_camera
+
+namespace gfpl {
+// Deferred error status of the stream-ordered detector calls (gfpl_*_async): the kernels
+// OR error bits into a device word; each call ends with a copy of it into pinned host
+// memory and an event, so the call returns without synchronising; *_status waits for
+// the event, reports the bits of every call since the previous status and clears them.
+struct AsyncStatus {
+    int* dev = nullptr;
+    int* host = nullptr;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    hipError_t init(int* dev_word, hipStream_t s) {
+        dev = dev_word;
+        hipError_t e = hipHostMalloc((void**)&host, sizeof(int), hipHostMallocDefault);
+        if (e == hipSuccess) { *host = 0; e = hipEventCreateWithFlags(&ev, hipEventDisableTiming); }
+        if (e == hipSuccess) e = hipMemsetAsync(dev, 0, sizeof(int), s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    }
+    hipError_t enqueue(hipStream_t s) {
+        hipError_t e = hipMemcpyAsync(host, dev, sizeof(int), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(ev, s);
+        if (e == hipSuccess) pending = true;
+        return e;
+    }
+    // bits of the calls since the last wait (0 when none is pending)
+    hipError_t wait(hipStream_t s, int* bits) {
+        *bits = 0;
+        if (!pending) return hipSuccess;
+        hipError_t e = hipEventSynchronize(ev);
+        if (e != hipSuccess) return e;
+        *bits = *host;
+        pending = false;
+        if (*bits) {
+            *host = 0;
+            e = hipMemsetAsync(dev, 0, sizeof(int), s);   // ordered before the next call's kernels
+        }
+        return e;
+    }
+    void destroy() {
+        if (host) (void)hipHostFree(host);
+        if (ev) (void)hipEventDestroy(ev);
+        host = nullptr;
+        ev = nullptr;
+    }
+};
+}  // namespace gfpl

@@ -132,6 +132,8 @@ __global__ void __launch_bounds__(256) k_lbd_describe(LbdDev o, const gfpl_keyli
     __shared__ float dv[4][LBD_BANDS * 8];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int img = blockIdx.y, li = blockIdx.x * 4 + wave;
+    // the reference describes every keyline: more than kl_cap is an error, not a truncation
+    if (li == 0 && lane == 0 && n_kl[img] > o.kl_cap) atomicOr(o.err, 2);
     if (li >= min(n_kl[img], o.kl_cap)) return;
     const gfpl_keyline kl = kls[(size_t)img * o.kl_cap + li];
     uint8_t* out = desc + ((size_t)img * o.kl_cap + li) * 32;
@@ -272,6 +274,7 @@ using namespace gfpl;
 struct gfpl_lbd {
     int device = 0;
     hipStream_t stream = nullptr;
+    AsyncStatus st;
     int max_images = 0;
     LbdDev d{};
     void* base = nullptr;
@@ -331,12 +334,15 @@ extern "C" int gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_ima
     char* p = (char*)o->base;
     d.grad = (uint32_t*)p; p += b_g;
     d.err = (int*)p;
+    if (o->st.init(d.err, o->stream) != hipSuccess) { o->st.destroy(); (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
     *out = o;
     return GFPL_OK;
 }
 
 extern "C" int gfpl_lbd_destroy(gfpl_lbd* o) {
     if (!o) return GFPL_E_INVALID;
+    (void)hipStreamSynchronize(o->stream);
+    o->st.destroy();
     if (o->base) (void)hipFree(o->base);
     delete o;
     return GFPL_OK;
@@ -353,19 +359,30 @@ extern "C" int gfpl_lbd_gradients(gfpl_lbd* o, const uint8_t* image, uint32_t* g
     return hipStreamSynchronize(o->stream) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
 }
 
-extern "C" int gfpl_lbd_compute(gfpl_lbd* o, const uint8_t* images, int n, const gfpl_keyline* keylines,
-                                const int* n_kl, uint8_t* desc) {
+extern "C" int gfpl_lbd_compute_async(gfpl_lbd* o, const uint8_t* images, int n, const gfpl_keyline* keylines,
+                                      const int* n_kl, uint8_t* desc) {
     if (!o || !images || n < 1 || n > o->max_images || !keylines || !n_kl || !desc) return GFPL_E_INVALID;
     if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
     const LbdDev& d = o->d;
     hipStream_t s = o->stream;
-    if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
     hipLaunchKernelGGL(k_lbd_grad, dim3((d.W + LBD_TW - 1) / LBD_TW, (d.H + LBD_TH - 1) / LBD_TH, n), dim3(256), 0, s, d,
                        images);
     hipLaunchKernelGGL(k_lbd_describe, dim3((d.kl_cap + 3) / 4, n), dim3(256), 0, s, d, keylines, n_kl, desc);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
-    int err = 0;
-    if (hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return GFPL_E_HIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return GFPL_E_HIP;
-    return err ? GFPL_E_UNSUPPORTED : GFPL_OK;
+    return o->st.enqueue(s) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
+}
+
+extern "C" int gfpl_lbd_status(gfpl_lbd* o) {
+    if (!o) return GFPL_E_INVALID;
+    int bits = 0;
+    if (o->st.wait(o->stream, &bits) != hipSuccess) return GFPL_E_HIP;
+    if (bits & 1) return GFPL_E_UNSUPPORTED;   // a keyline of another octave
+    return (bits & 2) ? GFPL_E_CAPACITY : GFPL_OK;   // more keylines than kl_cap
+}
+
+extern "C" int gfpl_lbd_compute(gfpl_lbd* o, const uint8_t* images, int n, const gfpl_keyline* keylines,
+                                const int* n_kl, uint8_t* desc) {
+    const int e = gfpl_lbd_compute_async(o, images, n, keylines, n_kl, desc);
+    if (e) return e;
+    return gfpl_lbd_status(o);
 }

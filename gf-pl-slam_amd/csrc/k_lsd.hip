@@ -1119,6 +1119,7 @@ using namespace gfpl;
 struct gfpl_lsd {
     int device = 0;
     hipStream_t stream = nullptr;
+    AsyncStatus st;
     int max_images = 0;
     bool lds_used = false;
     size_t lds_bytes = 0;
@@ -1192,7 +1193,8 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
         return GFPL_E_HIP;
     }
     hipLaunchKernelGGL(k_lsd_cs_table, dim3((1021 * 1021 + 255) / 256), dim3(256), 0, o->stream, d.cs_tab);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(o->stream) != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || o->st.init(d.err, o->stream) != hipSuccess) {
+        o->st.destroy();
         (void)hipFree(o->base);
         delete o;
         return GFPL_E_HIP;
@@ -1211,18 +1213,19 @@ extern "C" int gfpl_lsd_sort_desc(gfpl_lsd* o, uint64_t* a, int n) {
 
 extern "C" int gfpl_lsd_destroy(gfpl_lsd* o) {
     if (!o) return GFPL_E_INVALID;
+    (void)hipStreamSynchronize(o->stream);
+    o->st.destroy();
     if (o->base) (void)hipFree(o->base);
     delete o;
     return GFPL_OK;
 }
 
-extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
-                               float* response) {
+extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
+                                     float* response) {
     if (!o || !images || n < 1 || n > o->max_images || !keylines || !n_kl) return GFPL_E_INVALID;
     if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
     const LsdDev& d = o->d;
     hipStream_t s = o->stream;
-    if (hipMemsetAsync(d.err, 0, 4, s) != hipSuccess) return GFPL_E_HIP;
     if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess) return GFPL_E_HIP;
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
@@ -1239,8 +1242,19 @@ extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_k
         hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_lsd_keylines, dim3(n), dim3(64), 0, s, d, keylines, n_kl, response);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
-    int err = 0;
-    if (hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return GFPL_E_HIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return GFPL_E_HIP;
-    return err ? GFPL_E_CAPACITY : GFPL_OK;
+    return o->st.enqueue(s) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
+}
+
+extern "C" int gfpl_lsd_status(gfpl_lsd* o) {
+    if (!o) return GFPL_E_INVALID;
+    int bits = 0;
+    if (o->st.wait(o->stream, &bits) != hipSuccess) return GFPL_E_HIP;
+    return bits ? GFPL_E_CAPACITY : GFPL_OK;
+}
+
+extern "C" int gfpl_lsd_detect(gfpl_lsd* o, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
+                               float* response) {
+    const int e = gfpl_lsd_detect_async(o, images, n, keylines, n_kl, response);
+    if (e) return e;
+    return gfpl_lsd_status(o);
 }

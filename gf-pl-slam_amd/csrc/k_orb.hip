@@ -1007,6 +1007,8 @@ using namespace gfpl;
 struct gfpl_orb {
     int device = 0;
     hipStream_t stream = nullptr;
+    const gfpl_ctx* ctx = nullptr;  // its camera checks the pyramid layout the tracker will read
+    AsyncStatus st;
     gfpl_orb_params prm{};
     int max_images = 0, kp_cap = 0;
     OrbDev d{};
@@ -1047,6 +1049,7 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
     gfpl_orb* o = new gfpl_orb();
     o->device = dev;
     o->stream = (hipStream_t)gfpl_ctx_stream(ctx);
+    o->ctx = ctx;
     o->prm = *prm;
     o->max_images = max_images;
     o->kp_cap = kp_cap;
@@ -1243,13 +1246,15 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
         ok = ok && hipMemcpy(bp, beta_h.data(), 2 * beta_h.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_orb_pattern), kOrbPattern, sizeof(kOrbPattern)) == hipSuccess;
-    if (!ok) { (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
+    if (!ok || o->st.init(d.err, o->stream) != hipSuccess) { o->st.destroy(); (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
     *out = o;
     return GFPL_OK;
 }
 
 extern "C" int gfpl_orb_destroy(gfpl_orb* o) {
     if (!o) return GFPL_E_INVALID;
+    (void)hipStreamSynchronize(o->stream);
+    o->st.destroy();
     if (o->base) (void)hipFree(o->base);
     delete o;
     return GFPL_OK;
@@ -1261,10 +1266,23 @@ extern "C" int gfpl_orb_pyramid_bytes(const gfpl_orb* o, int64_t* bytes) {
     return GFPL_OK;
 }
 
-extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_keypoint* kps, uint8_t* desc,
-                                int* n_kp, float* angle, float* response, uint8_t* pyramid, int64_t pyr_stride) {
+extern "C" int gfpl_orb_extract_async(gfpl_orb* o, const uint8_t* images, int n, gfpl_keypoint* kps, uint8_t* desc,
+                                      int* n_kp, float* angle, float* response, uint8_t* pyramid, int64_t pyr_stride) {
     if (!o || !images || n < 1 || n > o->max_images || !kps || !desc || !n_kp) return GFPL_E_INVALID;
     if (pyramid && pyr_stride < o->pyr_bytes) return GFPL_E_INVALID;
+    if (pyramid) {
+        // a pyramid written at the stride of the context camera's pyramids, for images of its
+        // size, is the tracker's input (gfpl_frames.pyr_r): its level geometry must be the
+        // camera's, else the sub-pixel SAD would read other pixels than the reference's
+        const gfpl_camera* cam = gfpl_ctx_camera(o->ctx);
+        if (cam && cam->width == o->d.W && cam->height == o->d.H && pyr_stride == cam->pyr_bytes) {
+            if (cam->n_levels != o->d.nlevels) return GFPL_E_INVALID;
+            for (int l = 0; l < o->d.nlevels; ++l)
+                if (cam->lvl_cols[l] != o->d.lv[l].w || cam->lvl_rows[l] != o->d.lv[l].h ||
+                    cam->lvl_offset[l] != o->d.lv[l].off)
+                    return GFPL_E_INVALID;
+        }
+    }
     ORB_HIPCHK(hipSetDevice(o->device));
     OrbDev d = o->d;   // this call's view: the caller's pyramid array is the working pyramid
     if (pyramid) {
@@ -1272,7 +1290,6 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
         d.pyr_stride = pyr_stride;
     }
     hipStream_t s = o->stream;
-    ORB_HIPCHK(hipMemsetAsync(d.err, 0, 4, s));
     hipLaunchKernelGGL(k_orb_copy0, dim3(128, n), dim3(256), 0, s, d, images, n);
     for (int l = 1; l < d.nlevels; ++l)
         hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].h + RESIZE_ROWS - 1) / RESIZE_ROWS, n), dim3(RESIZE_T),
@@ -1289,8 +1306,20 @@ extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_
     hipLaunchKernelGGL(k_orb_describe, dim3((std::min(max_tot, o->kp_cap) + 7) / 8, n), dim3(256), 0, s, d, n, kps,
                        desc, n_kp, angle, response, o->kp_cap);
     ORB_HIPCHK(hipGetLastError());
-    int err = 0;
-    ORB_HIPCHK(hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, s));
-    ORB_HIPCHK(hipStreamSynchronize(s));
-    return err ? GFPL_E_CAPACITY : GFPL_OK;
+    ORB_HIPCHK(o->st.enqueue(s));
+    return GFPL_OK;
+}
+
+extern "C" int gfpl_orb_status(gfpl_orb* o) {
+    if (!o) return GFPL_E_INVALID;
+    int bits = 0;
+    ORB_HIPCHK(o->st.wait(o->stream, &bits));
+    return bits ? GFPL_E_CAPACITY : GFPL_OK;
+}
+
+extern "C" int gfpl_orb_extract(gfpl_orb* o, const uint8_t* images, int n, gfpl_keypoint* kps, uint8_t* desc,
+                                int* n_kp, float* angle, float* response, uint8_t* pyramid, int64_t pyr_stride) {
+    const int e = gfpl_orb_extract_async(o, images, n, kps, desc, n_kp, angle, response, pyramid, pyr_stride);
+    if (e) return e;
+    return gfpl_orb_status(o);
 }

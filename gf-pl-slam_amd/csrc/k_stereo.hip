@@ -63,7 +63,8 @@ __device__ __forceinline__ int clamp_level(int o, int n) { return o < 0 ? 0 : (o
 // in flight, consecutive in row order, so its window rows stay in L1/L2 across
 // neighbouring keypoints instead of being re-fetched from HBM per keypoint.
 struct SadJob {
-    const uint8_t* img;
+    const uint8_t* img;   // the pyramid of the sequence (256-B aligned)
+    int64_t lvl;          // byte offset of level o in it
     int cols, o, vL, uL, uR;
     float scaleduR0;
 };
@@ -83,7 +84,8 @@ __device__ __forceinline__ bool sad_setup(const KParams& p, int b, const gfpl_ke
     if (iniu < 0 || endu >= cols) return false;
     const int vL = (int)scaledvL, uL = (int)scaleduL, uR = (int)scaleduR0;
     if (vL - 5 < 0 || vL + 5 >= rows || uL - 5 < 0 || uL + 5 >= cols || uR - 10 < 0 || uR + 10 >= cols) return false;
-    J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[o];
+    J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes;
+    J.lvl = p.cam.lvl_offset[o];
     J.cols = cols; J.o = o; J.vL = vL; J.uL = uL; J.uR = uR; J.scaleduR0 = scaleduR0;
     return true;
 }
@@ -94,11 +96,13 @@ __device__ __forceinline__ bool sad_setup(const KParams& p, int b, const gfpl_ke
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ void sad_load_row(const SadJob& J, int y, uint32_t* il4, uint32_t* ir6) {
-    const uint8_t* rowp = J.img + (size_t)y * J.cols;
-    const uintptr_t pl = (uintptr_t)(rowp + (J.uL - 5)), pr = (uintptr_t)(rowp + (J.uR - 10));
-    const uint32_t* wl = reinterpret_cast<const uint32_t*>(pl & ~(uintptr_t)3);
-    const uint32_t* wr = reinterpret_cast<const uint32_t*>(pr & ~(uintptr_t)3);
-    const uint32_t shl = (uint32_t)(pl & 3u), shr = (uint32_t)(pr & 3u);
+    // byte offsets from the (256-B aligned) pyramid base: their low 2 bits are the misalignment
+    // (integer offsets keep the loads global_load, not flat)
+    const int64_t rowo = J.lvl + (int64_t)y * J.cols;
+    const int64_t pl = rowo + (J.uL - 5), pr = rowo + (J.uR - 10);
+    const uint32_t* wl = reinterpret_cast<const uint32_t*>(J.img + (pl & ~(int64_t)3));
+    const uint32_t* wr = reinterpret_cast<const uint32_t*>(J.img + (pr & ~(int64_t)3));
+    const uint32_t shl = (uint32_t)(pl & 3), shr = (uint32_t)(pr & 3);
     // dword-aligned 16-B / 8-B vector loads (one load instruction per 4 / 2 dwords)
     const u32x4a4 a = *reinterpret_cast<const u32x4a4*>(wl);
     const u32x4a4 c0 = *reinterpret_cast<const u32x4a4*>(wr);
@@ -114,12 +118,27 @@ __device__ __forceinline__ void sad_load_row(const SadJob& J, int y, uint32_t* i
 
 __device__ __forceinline__ int byte_at(const uint32_t* w, int k) { return (int)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu); }
 
+// bytes c and c + 1 of a little-endian dword array as the two 16-bit halves of one register
+// (one v_perm_b32; selector 0x0C yields a zero byte).  c is a compile-time constant.
+__device__ __forceinline__ uint32_t pair16(const uint32_t* w, int c) {
+    const uint32_t b = (uint32_t)(c & 3);
+    if (b < 3) return __builtin_amdgcn_perm(0u, w[c >> 2], 0x0C000C00u | ((b + 1) << 16) | b);
+    return __builtin_amdgcn_perm(w[(c >> 2) + 1], w[c >> 2], 0x0C040C03u);   // byte 3 | next dword's byte 0
+}
+// byte c in both 16-bit halves
+__device__ __forceinline__ uint32_t dup16(const uint32_t* w, int c) {
+    const uint32_t b = (uint32_t)(c & 3);
+    return __builtin_amdgcn_perm(0u, w[c >> 2], 0x0C000C00u | (b << 16) | b);
+}
+
 // partial SADs of the window rows q, q+4, q+8 (q = lane within the quad; lane 3
 // has no third row: it re-reads the centre row and drops that row's sums).  All
 // four rows are loaded before any SAD so their latencies overlap.
+// SAD_s = sum |(IL - cL) - (IR_s - cR_s)| = sum |(IL + cR_s) - (IR_s + cL)|, both sides
+// <= 510: two columns per v_sad_u16.  Per row the right pairs (IR_c + cL, IR_c+1 + cL) are
+// formed once for every column c and the left pairs once; per shift only the left pairs
+// take cR_s (the centre pixels cR_s are shared by the lane's rows).
 __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) {
-    // centre row: the centre pixels of the 11 shifted right windows are bytes 5..15 of
-    // its right row (kept as the 6 row dwords, expanded where used)
     uint32_t irc[6];
     int cL;
     {
@@ -133,29 +152,29 @@ __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) 
         const int r = q + 4 * i;
         sad_load_row(J, J.vL - 5 + (r < 11 ? r : 5), il4[i], ir6[i]);
     }
-    // SAD = sum |(IL - cL) - (IR_s - cR[s])| = sum |(IL + cR[s]) - (IR_s + cL)|, both
-    // sides <= 510: two columns per v_sad_u16 (16-bit lanes of one register)
     const uint32_t cLL = (uint32_t)cL * 0x10001u;
+    uint32_t cRR[11];
+#pragma unroll
+    for (int s = 0; s < 11; ++s) cRR[s] = dup16(irc, 5 + s);   // (cR_s, cR_s)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (q + 4 * i >= 11) break;
         const uint32_t* L = il4[i];
         const uint32_t* R = ir6[i];
-        uint32_t ILp[5];
+        uint32_t ILp[5], RP[19];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) ILp[k] = (uint32_t)byte_at(L, 2 * k) | ((uint32_t)byte_at(L, 2 * k + 1) << 16);
-        const int il10 = byte_at(L, 10);
+        for (int k = 0; k < 5; ++k) ILp[k] = pair16(L, 2 * k);
+#pragma unroll
+        for (int c = 0; c < 19; ++c) RP[c] = pair16(R, c) + cLL;   // (IR_c + cL, IR_c+1 + cL)
+        const uint32_t il10 = (uint32_t)byte_at(L, 10);
 #pragma unroll
         for (int s = 0; s < 11; ++s) {
-            const uint32_t cRRs = (uint32_t)byte_at(irc, 5 + s) * 0x10001u;
             uint32_t a = acc[s];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const int c = s + 2 * k;   // right window column pair (c, c + 1)
-                const uint32_t ir = ((uint32_t)byte_at(R, c) | ((uint32_t)byte_at(R, c + 1) << 16)) + cLL;
-                a = __builtin_amdgcn_sad_u16(ILp[k] + cRRs, ir, a);
-            }
-            a += (uint32_t)abs((il10 + (int)(cRRs & 0xFFFFu)) - (byte_at(R, 10 + s) + cL));
+            for (int k = 0; k < 5; ++k) a = __builtin_amdgcn_sad_u16(ILp[k] + cRR[s], RP[s + 2 * k], a);
+            // column 10: one 16-bit half (IR_{10+s} + cL is the low half of pair 10 + s)
+            const uint32_t rt = (s + 10 < 19 ? RP[s + 10] : pair16(R, s + 10) + cLL) & 0xFFFFu;
+            a = __builtin_amdgcn_sad_u16(il10 + (cRR[s] & 0xFFFFu), rt, a);
             acc[s] = a;
         }
     }
@@ -184,17 +203,22 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 }
 
 // ------------------------------------------------------- stereo points --
-#ifndef GFPL_SP_SEG
-#define GFPL_SP_SEG 1
-#endif
 #ifndef GFPL_SL_WAVES
 #define GFPL_SL_WAVES 1
 #endif
 #ifndef GFPL_SP_WAVES
-#define GFPL_SP_WAVES 7   // waves per SIMD: 72 VGPRs, no spill (8 waves spilled 28 B/lane: 10.59 vs 10.72 ms, within noise)
+#define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
+#define SP_CHUNK 32
+#ifndef GFPL_SP_PROBE
+#define GFPL_SP_PROBE 0
+#endif       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
+
+// LDS-only wave sync: the wave's earlier LDS writes / reads have completed (LDS executes a
+// wave's accesses in order; the clobber keeps the compiler from moving accesses across it)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // dynamic LDS: rkey[KP2] u32 | order[KP2] u32 | pairs[KP2] u32 | recx[KP2] f32 |
-//              recm[KP2] u16 | rowlo[nRows] u16 | misc[64] i32
+//              recm[KP2] u16 | rowlo[nRows] u16 | misc[64] i32 | (SEG) stage[waves][SP_CHUNK][32 B]
 // Right keypoints are sorted by their row band start (the reference's
 // vRowIndices buckets, src/stereoFrame.cpp:459-485) and their x, octave and band
 // height are copied next to the sorted keys, so the band scan of a left keypoint
@@ -224,6 +248,8 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     const int nlev = p.cam.n_levels;
     const int nrl = SEG ? nlev * nRows : nRows;
     int* misc = (int*)(rowlo + ((nrl + 1) & ~1));   // SEG: [22 + seg] band heights, [31] out-of-range count
+    // SEG: per-wave staging of right descriptors, SP_CHUNK x 32 B per wave (16-B aligned)
+    uint32_t* stg = (uint32_t*)(((uintptr_t)(misc + 32) + 15) & ~(uintptr_t)15);
     // mvDepth of the sub-pixel pass lives in recx: the right keypoints' x are dead once the
     // band scan is over (LDS, no scattered 4-B global stores)
     float* depth = recx;
@@ -267,7 +293,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         pairs[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    bitonic_sort2(rkey, order, KP2);
+    if (GFPL_SP_PROBE != 5) bitonic_sort2(rkey, order, KP2);
     const int D = misc[0];
     // records in sorted order: x, band height maxr - minr (<= 16), octave (int8;
     // -128 = out of range, read from HBM)
@@ -301,11 +327,104 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     // per left keypoint: band search + Hamming (src/stereoFrame.cpp:502-545).  A match
     // leaves (bestDist, bestIdxR) in pairs[iL] and iL in order[t] for the sub-pixel pass;
     // order[t] / pairs[iL] are private to the thread that owns slot t.
+    auto finish_kp = [&](int t, int iL, const gfpl_keypoint& kpL, int bestDist, int bestIdxR) {
+        uint32_t job = 0xFFFFFFFFu;
+        if (bestDist < 80) {
+            atomicAdd(&misc[2], 1);
+            SadJob J;
+            // job: iL | uL << 16 (order[t]); bestDist | o << 7 | vL << 10 | uR << 21
+            // (pairs[iL]); failed window checks keep only bestDist (disparity -1)
+            if (sad_setup(p, b, kpL, KR[bestIdxR], J)) {
+                pairs[iL] = (uint32_t)bestDist | ((uint32_t)J.o << 7) | ((uint32_t)J.vL << 10) |
+                            ((uint32_t)J.uR << 21);
+                job = (uint32_t)iL | ((uint32_t)J.uL << 16);
+            }
+        }
+        order[t] = job;
+    };
+    if (SEG) {
+        // Staged scan: a wave takes 64 row-consecutive left keypoints; per octave segment their
+        // candidate ranges [rowlo, first minr > row) are walked in chunks of 32 sorted entries
+        // whose right descriptors the wave first copies into its own LDS buffer (one 16-B load
+        // per lane, all in flight together), so each distance reads LDS instead of a dependent
+        // 32-B HBM gather.  Every lane still visits its candidates in ascending sorted order
+        // with the same tests: the lexicographic (dist, iR) minimum is unchanged.
+        const int lane = tid & 63;
+        // explicitly LDS-qualified (a generic pointer here compiled to flat_load / flat_store)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+        lds_u32x4* wst = (lds_u32x4*)(stg + (tid >> 6) * (SP_CHUNK * 8));
+        for (int base = tid & ~63; base < N; base += BLOCK) {
+            const int t = base + lane;
+            const int iL = t < N ? (int)(order[t] & 0xFFFFu) : 0;
+            const gfpl_keypoint kpL = KL[iL];
+            const int levelL = kpL.octave;
+            const float vL = kpL.y, uL = kpL.x;
+            const float minU = uL - maxD, maxU = uL - minD;
+            const bool act = t < N && vL >= 0.0f && (unsigned)(int)vL < (unsigned)nRows && !(maxU < 0);
+            const int row = act ? (int)vL : 0;
+            uint32_t dl[8];
+            load_desc(DL + (size_t)iL * 32, dl);
+            // lexicographic (dist, iR) minimum as one packed key (iR < 2^16 on this layout);
+            // the start value keeps bestDist = 100 (no candidate below it: no match)
+            uint32_t best = (100u << 16) | 0xFFFFu;
+#if GFPL_SP_PROBE == 1
+            if (t < N) finish_kp(t, iL, kpL, 100, 0);
+            continue;
+#endif
+            for (int o = 0; o <= nlev; ++o) {   // wave-uniform
+                const bool need = act && (o < nlev ? ((long long)o >= (long long)levelL - 1 &&
+                                                      (long long)o <= (long long)levelL + 1)
+                                                   : misc[31] > 0);
+                if (!__any(need)) continue;
+                int j = need ? (o < nlev ? (int)rowlo[o * nRows + row] : lower(seg_key(nlev, row))) : 0x7FFFFFFF;
+                bool more = need && j < Nr;
+                while (__any(more)) {
+                    int c0 = more ? j : 0x7FFFFFFF;
+#pragma unroll
+                    for (int sh = 1; sh < 64; sh <<= 1) c0 = min(c0, __shfl_xor(c0, sh));
+                    {
+                        const int je = c0 + (lane >> 1);
+                        if (GFPL_SP_PROBE != 3 && je < Nr && (rkey[je] >> 28) == (uint32_t)o) {
+                            const int iR = (int)(rkey[je] & 0xFFFFu);
+                            wst[lane] = *reinterpret_cast<const u32x4*>(DR + (size_t)iR * 32 + 16 * (lane & 1));   // entry lane >> 1, half lane & 1
+                        }
+                    }
+                    wave_lds_sync();
+                    const int cend = min(c0 + SP_CHUNK, Nr);
+                    while (more && j < cend) {
+                        // every LDS read of the entry issued together (the stop test is folded into
+                        // `pass`, not a branch ahead of the reads): one round trip per candidate
+                        const uint32_t k = rkey[j];
+                        const uint32_t m = recm[j];
+                        const float uR = recx[j];
+                        const u32x4 a = wst[2 * (j - c0)], c = wst[2 * (j - c0) + 1];
+                        const int minr = (int)((k >> 16) & 0xFFFu) - 1024;
+                        const bool stop = (k >> 28) != (uint32_t)o || minr > row;
+                        const int iR = (int)(k & 0xFFFFu);
+                        int octR = (int)(int8_t)(uint8_t)(m & 0xFFu);
+                        if (octR == -128 && !stop) octR = KR[iR].octave;
+                        const uint32_t dr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+                        const uint32_t key = ((uint32_t)hamming8<1>(dl, dr) << 16) | (uint32_t)iR;
+                        const bool pass = !stop && minr + (int)(m >> 8) >= row &&   // maxr >= row
+                                          octR >= levelL - 1 && octR <= levelL + 1 && uR >= minU && uR <= maxU;
+                        best = (pass && key < best) ? key : best;
+                        if (stop) { more = false; break; }
+                        ++j;
+                    }
+                    if (j >= Nr) more = false;
+                    wave_lds_sync();   // the chunk is read before the next one overwrites it
+                }
+            }
+            const int bestDist = (int)(best >> 16), bestIdxR = (int)(best & 0xFFFFu);
+            if (t < N) finish_kp(t, iL, kpL, bestDist, bestIdxR);
+        }
+    } else {
     for (int t = tid; t < N; t += blockDim.x) {
         const int iL = (int)(order[t] & 0xFFFFu);
-        uint32_t job = 0xFFFFFFFFu;
+        const gfpl_keypoint kpL = KL[iL];
+        int bestDist = 100, bestIdxR = 0x7FFFFFFF;
         {
-            const gfpl_keypoint kpL = KL[iL];
             const int levelL = kpL.octave;
             const float vL = kpL.y, uL = kpL.x;
             const float minU = uL - maxD, maxU = uL - minD;
@@ -313,12 +432,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                 const int row = (int)vL;
                 uint32_t dl[8];
                 load_desc(DL + (size_t)iL * 32, dl);
-                int bestDist = 100, bestIdxR = 0x7FFFFFFF;
-                auto scan = [&](int j0, int seg) {
-                for (int j = j0; j < Nr; ++j) {
+                for (int j = rowlo[row]; j < Nr; ++j) {
                     const uint32_t k = rkey[j];
-                    if (SEG && (k >> 28) != (uint32_t)seg) break;
-                    const int minr = SEG ? (int)((k >> 16) & 0xFFFu) - 1024 : (int)(k >> 16) - 32768;
+                    const int minr = (int)(k >> 16) - 32768;
                     if (minr > row) break;
                     const uint32_t m = recm[j];
                     if (minr + (int)(m >> 8) < row) continue;   // maxr < row
@@ -336,29 +452,10 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                         if (dist < bestDist || (dist == bestDist && iR < bestIdxR)) { bestDist = dist; bestIdxR = iR; }
                     }
                 }
-                };
-                if (SEG) {
-                    const int olo = (int)max((long long)levelL - 1, 0LL);
-                    const int ohi = (int)min((long long)levelL + 1, (long long)nlev - 1);
-                    for (int o = olo; o <= ohi; ++o) scan(rowlo[o * nRows + row], o);
-                    if (misc[31] > 0) scan(lower(seg_key(nlev, row)), nlev);
-                } else {
-                    scan(rowlo[row], 0);
-                }
-                if (bestDist < 80) {
-                    atomicAdd(&misc[2], 1);
-                    SadJob J;
-                    // job: iL | uL << 16 (order[t]); bestDist | o << 7 | vL << 10 | uR << 21
-                    // (pairs[iL]); failed window checks keep only bestDist (disparity -1)
-                    if (sad_setup(p, b, kpL, KR[bestIdxR], J)) {
-                        pairs[iL] = (uint32_t)bestDist | ((uint32_t)J.o << 7) | ((uint32_t)J.vL << 10) |
-                                    ((uint32_t)J.uR << 21);
-                        job = (uint32_t)iL | ((uint32_t)J.uL << 16);
-                    }
-                }
             }
         }
-        order[t] = job;
+        finish_kp(t, iL, kpL, bestDist, bestIdxR);
+    }
     }
     __syncthreads();
     // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
@@ -372,7 +469,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         SadJob J;
         float xL = 0.0f;
         uint32_t pr = 0;
-        if (job != 0xFFFFFFFFu) {
+        if (GFPL_SP_PROBE != 2 && job != 0xFFFFFFFFu) {
             const int iL = (int)(job & 0xFFFFu);
             xL = KL[iL].x;
             pr = pairs[iL];
@@ -381,7 +478,8 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             J.uR = (int)(pr >> 21);
             J.uL = (int)(job >> 16);
             J.cols = p.cam.lvl_cols[J.o];
-            J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes + p.cam.lvl_offset[J.o];
+            J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes;
+            J.lvl = p.cam.lvl_offset[J.o];
             J.scaleduR0 = (float)J.uR;
             sad_rows(J, q, acc);
         }
@@ -407,7 +505,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     __syncthreads();
     // sort(vDistIdx) (src/stereoFrame.cpp:585)
-    bitonic_sort(pairs, KP2);
+    if (GFPL_SP_PROBE != 4) bitonic_sort(pairs, KP2);
     for (int i = tid; i < KP2; i += blockDim.x) {
         bool v = pairs[i] != 0xFFFFFFFFu;
         bool vn = (i + 1 < KP2) ? (pairs[i + 1] != 0xFFFFFFFFu) : false;
@@ -838,11 +936,12 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
-    const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((p.cam.n_levels * p.cam.height + 1) & ~1) * 2 + 32 * 4;
+    const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((p.cam.n_levels * p.cam.height + 1) & ~1) * 2 + 32 * 4 + 16 +
+                           (size_t)(512 / 64) * SP_CHUNK * 32;
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
     if (p.kp_cap > 2048)
         hipLaunchKernelGGL((k_stereo_points<1024, false>), dim3(p.B), dim3(1024), lds, s, p, KP2);
-    else if (GFPL_SP_SEG && lds_seg <= 40960)   // four workgroups per CU
+    else if (lds_seg <= 54 * 1024)   // three workgroups per CU
         hipLaunchKernelGGL((k_stereo_points<512, true>), dim3(p.B), dim3(512), lds_seg, s, p, KP2);
     else
         hipLaunchKernelGGL((k_stereo_points<512, false>), dim3(p.B), dim3(512), lds, s, p, KP2);

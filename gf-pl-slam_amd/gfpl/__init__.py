@@ -87,7 +87,8 @@ class Frames(C.Structure):
                 ("n_kp_l", _vp), ("n_kp_r", _vp), ("kp_l", _vp), ("kp_r", _vp),
                 ("pdesc_l", _vp), ("pdesc_r", _vp),
                 ("n_kl_l", _vp), ("n_kl_r", _vp), ("kl_l", _vp), ("kl_r", _vp),
-                ("ldesc_l", _vp), ("ldesc_r", _vp), ("pyr_r", _vp), ("time_stamp", _vp)]
+                ("ldesc_l", _vp), ("ldesc_r", _vp), ("pyr_r", _vp), ("time_stamp", _vp),
+                ("ready", _vp), ("consumed", _vp)]
 
 
 # (name, dtype, per-feature shape) of gfpl_frame_host arrays, in struct order
@@ -270,6 +271,19 @@ def hiplib() -> C.CDLL:
             "gfpl_camera_init": ([P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                   C.c_double, C.c_double, P], C.c_int),
             "gfpl_create": ([C.c_int, P, C.POINTER(P)], C.c_int),
+            "gfpl_create_async": ([C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_get_stream": ([P], C.c_void_p),
+            "gfpl_event_create": ([P, C.POINTER(P)], C.c_int),
+            "gfpl_event_destroy": ([P], C.c_int),
+            "gfpl_event_record": ([P, P], C.c_int),
+            "gfpl_event_wait": ([P, P], C.c_int),
+            "gfpl_event_synchronize": ([P], C.c_int),
+            "gfpl_orb_extract_async": ([P, P, C.c_int, P, P, P, P, P, P, C.c_int64], C.c_int),
+            "gfpl_orb_status": ([P], C.c_int),
+            "gfpl_lsd_detect_async": ([P, P, C.c_int, P, P, P], C.c_int),
+            "gfpl_lsd_status": ([P], C.c_int),
+            "gfpl_lbd_compute_async": ([P, P, C.c_int, P, P, P], C.c_int),
+            "gfpl_lbd_status": ([P], C.c_int),
             "gfpl_destroy": ([P], C.c_int),
             "gfpl_set_camera": ([P, P], C.c_int),
             "gfpl_set_config": ([P, P], C.c_int),
@@ -678,19 +692,36 @@ class FrameHost:
 
 # ---------------------------------------------------------- GPU handles --
 class Context:
-    """gfpl_ctx: one HIP device + stream + camera + config."""
+    """gfpl_ctx: one HIP device + stream + camera + config.  stream: a hipStream_t handle
+    (0 = the default stream); own_stream=True gives the context its own non-blocking stream
+    (gfpl_create_async), e.g. for detection beside a tracking context."""
 
-    def __init__(self, cam: Camera, cfg: Config, device: int = 0, stream: int = 0):
+    def __init__(self, cam: Camera, cfg: Config, device: int = 0, stream: int = 0, own_stream: bool = False):
         self.L = hiplib()
         h = C.c_void_p()
-        check(self.L.gfpl_create(device, C.c_void_p(stream), C.byref(h)), "gfpl_create")
+        if own_stream:
+            check(self.L.gfpl_create_async(device, C.byref(h)), "gfpl_create_async")
+        else:
+            check(self.L.gfpl_create(device, C.c_void_p(stream), C.byref(h)), "gfpl_create")
         self.h = h
+        self.device = device
         check(self.L.gfpl_set_camera(h, C.byref(cam)), "set_camera")
         check(self.L.gfpl_set_config(h, C.byref(cfg)), "set_config")
         self.cam, self.cfg = cam, cfg
 
     def synchronize(self):
         check(self.L.gfpl_synchronize(self.h), "synchronize")
+
+    @property
+    def stream(self) -> int:
+        """the hipStream_t handle the context enqueues on (0: the default stream)"""
+        return int(self.L.gfpl_get_stream(self.h) or 0)
+
+    def torch_stream(self):
+        """the context's stream as a torch stream (torch work ordered with the gfpl calls)"""
+        import torch
+        dev = torch.device("cuda", self.device)
+        return torch.cuda.ExternalStream(self.stream, device=dev) if self.stream else torch.cuda.default_stream(dev)
 
     def set_timing(self, on: bool):
         check(self.L.gfpl_set_timing(self.h, int(on)), "set_timing")
@@ -742,8 +773,41 @@ class Context:
                 lp[: 2 * nls.value].cpu().numpy().reshape(-1, 2))
 
     def close(self):
+        """gfpl_destroy.  Refused (GfplError, the handle kept) while a StereoFrameHandler
+        created on this context is still open: close those first."""
         if getattr(self, "h", None):
-            self.L.gfpl_destroy(self.h)
+            check(self.L.gfpl_destroy(self.h), "gfpl_destroy (close the StereoFrameHandlers of this context first)")
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Event:
+    """gfpl_event: record on one context's stream, make another context's stream wait."""
+
+    def __init__(self, ctx: Context):
+        self.L = ctx.L
+        h = C.c_void_p()
+        check(self.L.gfpl_event_create(ctx.h, C.byref(h)), "gfpl_event_create")
+        self.h = h
+
+    def record(self, ctx: Context):
+        check(self.L.gfpl_event_record(self.h, ctx.h), "gfpl_event_record")
+
+    def wait(self, ctx: Context):
+        """ctx's stream waits for the last record"""
+        check(self.L.gfpl_event_wait(ctx.h, self.h), "gfpl_event_wait")
+
+    def synchronize(self):
+        check(self.L.gfpl_event_synchronize(self.h), "gfpl_event_synchronize")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_event_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -992,6 +1056,16 @@ class ORBextractor:
                                       _ptr(angle_dev), _ptr(response_dev), _ptr(pyramid_dev), pyr_stride),
               "orb_extract")
 
+    def extract_async(self, images_dev, n: int, kps_dev, desc_dev, n_kp_dev, angle_dev=None, response_dev=None,
+                      pyramid_dev=None, pyr_stride: int = 0) -> None:
+        """gfpl_orb_extract_async: enqueued on the context's stream; status() reports capacity errors."""
+        check(self.L.gfpl_orb_extract_async(self.h, _ptr(images_dev), n, _ptr(kps_dev), _ptr(desc_dev),
+                                            _ptr(n_kp_dev), _ptr(angle_dev), _ptr(response_dev), _ptr(pyramid_dev),
+                                            pyr_stride), "orb_extract_async")
+
+    def status(self) -> None:
+        check(self.L.gfpl_orb_status(self.h), "orb_status")
+
     def __call__(self, image: np.ndarray):
         """operator()(image, noArray(), keypoints, descriptors) on one HOST grey image:
         returns (keypoints [CV_KEYPOINT_DT], descriptors [n][32] u8); mvImagePyramid holds
@@ -1071,6 +1145,14 @@ class LSDDetector:
         check(self.L.gfpl_lsd_detect(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
                                      _ptr(response_dev) if response_dev is not None else None), "lsd_detect")
 
+    def detect_async(self, images_dev, n: int, keylines_dev, n_kl_dev, response_dev=None) -> None:
+        """gfpl_lsd_detect_async: enqueued on the context's stream; status() reports capacity errors."""
+        check(self.L.gfpl_lsd_detect_async(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
+                                           _ptr(response_dev) if response_dev is not None else None), "lsd_detect_async")
+
+    def status(self) -> None:
+        check(self.L.gfpl_lsd_status(self.h), "lsd_status")
+
     def sort_desc(self, a_dev, n: int) -> None:
         """ledger S2 test hook: std::sort by descending high 32 bits of a device u64 array."""
         check(self.L.gfpl_lsd_sort_desc(self.h, _ptr(a_dev), n), "lsd_sort_desc")
@@ -1134,6 +1216,14 @@ class BinaryDescriptor:
     def compute_batch(self, images_dev, n: int, keylines_dev, n_kl_dev, desc_dev) -> None:
         check(self.L.gfpl_lbd_compute(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
                                       _ptr(desc_dev)), "lbd_compute")
+
+    def compute_async(self, images_dev, n: int, keylines_dev, n_kl_dev, desc_dev) -> None:
+        """gfpl_lbd_compute_async: enqueued on the context's stream; status() reports errors."""
+        check(self.L.gfpl_lbd_compute_async(self.h, _ptr(images_dev), n, _ptr(keylines_dev), _ptr(n_kl_dev),
+                                            _ptr(desc_dev)), "lbd_compute_async")
+
+    def status(self) -> None:
+        check(self.L.gfpl_lbd_status(self.h), "lbd_status")
 
     def compute(self, image: np.ndarray, keylines: np.ndarray) -> np.ndarray:
         """compute(image, keylines, descriptors) on one HOST image; keylines: KEYLINE_DT rows.

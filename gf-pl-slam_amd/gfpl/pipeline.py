@@ -2,9 +2,10 @@
 
 StereoFrame's detectFeatures (src/stereoFrame.cpp:1145-1200) runs ORB_SLAM2::ORBextractor on
 both images, LSDDetectorC::detect and BinaryDescriptor::compute on both; here all three run on
-the GPU (gfpl_orb_extract, gfpl_lsd_detect, gfpl_lbd_compute) straight into the device buffers a
-gfpl_frames view points at — keypoints, descriptors, keylines, the right pyramid for the
-sub-pixel SAD — so the tracker (StereoFrameHandler) reads them without a copy.
+the GPU (gfpl_orb_extract_async, gfpl_lsd_detect_async, gfpl_lbd_compute_async) straight into
+the device buffers a gfpl_frames view points at — keypoints, descriptors, keylines, the right
+pyramid for the sub-pixel SAD — so the tracker (StereoFrameHandler) reads them without a copy,
+on a detection stream of its own, ordered with the tracker by events (no host synchronisation).
 detect_images() is that whole path; detect() takes the keylines as an input instead.
 
 The synthetic scene helper renders what a calibrated rig would see while translating along
@@ -17,8 +18,8 @@ import functools
 
 import numpy as np
 
-from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, LSDDetector, LsdParams, ORBextractor,
-               make_frames, synth_image, synth_keylines)
+from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, Event, LSDDetector, LsdParams,
+               ORBextractor, make_frames, synth_image, synth_keylines)
 
 
 @functools.lru_cache(maxsize=4096)
@@ -102,69 +103,140 @@ def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparitie
 
 class ImagePipeline:
     """Detection for B sequences on the device, as gfpl_frames for StereoFrameHandler:
-    ORB (nfeatures, scale 1.2, the camera's levels, FAST 20 / 7), LSD (lsd=True: the reference's
-    LSDOptions, Config::lsdNFeatures = 300, min length 0.025 * min(W, H)) and LBD."""
+    ORB (nfeatures, Config::orbScaleFactor / orbNLevels of the configuration, FAST 20 / 7),
+    LSD (lsd=True: the reference's LSDOptions, Config::lsdNFeatures = 300, min length
+    0.025 * min(W, H)) and LBD.
 
-    def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000, lsd: bool = False):
+    Detection runs on its own context (its own stream, gfpl_create_async) into `sets`
+    buffer sets in turn, through the stream-ordered detector calls (gfpl_*_async).  Every
+    gfpl_frames it returns carries two events: `ready` (its detection is done) and
+    `consumed` (recorded by the tracker call that reads it, gfpl_frames.ready / consumed),
+    so a tracker call on another context waits for exactly that detection and the next
+    detection into the same set waits for exactly that read: detecting frame k + 1 while
+    frame k is tracked needs no host synchronisation.  Capacity / octave errors of the
+    asynchronous detectors are reported by status()."""
+
+    def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000, lsd: bool = False,
+                 cfg=None, sets: int = 2):
         import torch
-        self.cam, self.B, self.kl_cap = cam, batch, kl_cap
+        cfg = cfg if cfg is not None else ctx.cfg
+        self.ctx, self.cam, self.B, self.kl_cap, self.sets = ctx, cam, batch, kl_cap, sets
         W, H = int(cam.width), int(cam.height)
-        self.orb = ORBextractor(nfeatures, 1.2, int(cam.n_levels), 20, 7, W, H, max_images=batch, ctx=ctx)
-        self.lbd = BinaryDescriptor(W, H, max_images=batch, kl_cap=kl_cap, ctx=ctx)
+        self.det = Context(cam, cfg, device=ctx.device, own_stream=True)
+        self.orb = ORBextractor(nfeatures, float(cfg.orb_scale_factor), int(cfg.orb_n_levels), 20, 7, W, H,
+                                max_images=batch, ctx=self.det)
+        # the extractor writes the tracker's right pyramid (gfpl_frames.pyr_r): its levels must
+        # be the camera's (gfpl_orb_extract checks it as well)
+        geo = [(int(cam.lvl_cols[l]), int(cam.lvl_rows[l])) for l in range(int(cam.n_levels))]
+        if self.orb.level_sizes() != geo or self.orb.pyramid_bytes > int(cam.pyr_bytes):
+            raise ValueError(f"ORB pyramid {self.orb.level_sizes()} ({self.orb.pyramid_bytes} B) does not match the "
+                             f"camera's {geo} ({int(cam.pyr_bytes)} B): build both from the same config")
+        self.lbd = BinaryDescriptor(W, H, max_images=batch, kl_cap=kl_cap, ctx=self.det)
         # both images of the B stereo frames go through LSD in one call (2B images in flight)
         self.lsd = LSDDetector(W, H, LsdParams.reference(W, H), max_images=2 * batch, kl_cap=kl_cap,
-                               ctx=ctx) if lsd else None
+                               ctx=self.det) if lsd else None
         self.kp_cap = self.orb.kp_cap
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", ctx.device)
         B, kc = batch, self.kp_cap
         z = lambda n, dt=torch.uint8: torch.zeros(n, dtype=dt, device=dev)
-        self.n_kp = [z(B, torch.int32), z(B, torch.int32)]
-        self.kps = [z(B * kc * KEYPOINT_DT.itemsize), z(B * kc * KEYPOINT_DT.itemsize)]
-        self.pdesc = [z(B * kc * DESC), z(B * kc * DESC)]
-        self.n_kl_lr = z(2 * B, torch.int32)
-        self.kl_lr = z(2 * B * kl_cap * KEYLINE_DT.itemsize)
-        self.n_kl = [self.n_kl_lr[:B], self.n_kl_lr[B:]]
-        self.kl = [self.kl_lr[:B * kl_cap * KEYLINE_DT.itemsize], self.kl_lr[B * kl_cap * KEYLINE_DT.itemsize:]]
-        self.img_lr = z(2 * B * W * H) if lsd else None
-        self.ldesc = [z(B * kl_cap * DESC), z(B * kl_cap * DESC)]
-        self.pyr_l = z(B * int(cam.pyr_bytes))   # the left pyramid (not read by the tracker)
-        self.pyr_r = z(B * int(cam.pyr_bytes))
-        self.ts = torch.zeros(B, dtype=torch.float64, device=dev)
+        kls = B * kl_cap * KEYLINE_DT.itemsize
+        self.bufs = []
+        for _ in range(sets):
+            n_kl_lr, kl_lr = z(2 * B, torch.int32), z(2 * kls)
+            self.bufs.append({
+                "n_kp": [z(B, torch.int32), z(B, torch.int32)],
+                "kps": [z(B * kc * KEYPOINT_DT.itemsize), z(B * kc * KEYPOINT_DT.itemsize)],
+                "pdesc": [z(B * kc * DESC), z(B * kc * DESC)],
+                "n_kl_lr": n_kl_lr, "kl_lr": kl_lr,
+                "n_kl": [n_kl_lr[:B], n_kl_lr[B:]], "kl": [kl_lr[:kls], kl_lr[kls:]],
+                "img_lr": z(2 * B * W * H) if lsd else None,
+                "ldesc": [z(B * kl_cap * DESC), z(B * kl_cap * DESC)],
+                "pyr_l": z(B * int(cam.pyr_bytes)),   # the left pyramid (not read by the tracker)
+                "pyr_r": z(B * int(cam.pyr_bytes)),
+                "ts": torch.zeros(B, dtype=torch.float64, device=dev)})
+        self.ready = [Event(self.det) for _ in range(sets)]
+        self.consumed = [Event(ctx) for _ in range(sets)]
+        self.k = 0
+        torch.cuda.synchronize(dev)   # the buffers' zero fills (default stream) before any detection
+
+    def _begin(self, inputs):
+        """next buffer set; the detection stream waits for the tracker's last read of it and for
+        the caller's stream (which produced the inputs)"""
+        import torch
+        s = self.k % self.sets
+        self.k += 1
+        self.consumed[s].wait(self.det)
+        ts = self.det.torch_stream()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(ts.device))
+        ts.wait_event(ev)
+        for t in inputs:
+            t.record_stream(ts)   # the caching allocator keeps them until the detection ran
+        return s, ts
 
     def detect(self, left, right, kl_left, n_kl_left, kl_right, n_kl_right, time_stamp):
         """left / right: device u8 [B][H][W]; kl_*: device KEYLINE_DT rows [B][kl_cap];
-        n_kl_*: device int32 [B]; time_stamp: device f64 [B].  Returns the gfpl_frames."""
-        for side, (kl, n) in enumerate(((kl_left, n_kl_left), (kl_right, n_kl_right))):
-            self.kl[side].copy_(kl.view(-1))
-            self.n_kl[side].copy_(n)
-        return self._describe(left, right, time_stamp)
+        n_kl_*: device int32 [B]; time_stamp: device f64 [B].  Returns the gfpl_frames
+        (asynchronous: a tracker call on it waits for its `ready` event)."""
+        import torch
+        s, ts = self._begin([left, right, kl_left, n_kl_left, kl_right, n_kl_right, time_stamp])
+        b = self.bufs[s]
+        with torch.cuda.stream(ts):
+            for side, (kl, n) in enumerate(((kl_left, n_kl_left), (kl_right, n_kl_right))):
+                b["kl"][side].copy_(kl.view(-1))
+                b["n_kl"][side].copy_(n)
+        return self._describe(s, ts, left, right, time_stamp)
 
     def detect_images(self, left, right, time_stamp):
         """StereoFrame::detectFeatures with every detector on the device: LSD keylines of both
         images (detectLineFeatures, src/stereoFrame.cpp:1160-1186) written where LBD and the
         tracker read them, then ORB and LBD.  Needs lsd=True."""
+        import torch
         if self.lsd is None:
             raise RuntimeError("ImagePipeline(lsd=True) runs LSD on the device")
+        s, ts = self._begin([left, right, time_stamp])
+        b = self.bufs[s]
         n = self.B * int(self.cam.width) * int(self.cam.height)
-        self.img_lr[:n].copy_(left.reshape(-1))
-        self.img_lr[n:].copy_(right.reshape(-1))
-        self.lsd.detect_batch(self.img_lr, 2 * self.B, self.kl_lr, self.n_kl_lr)
-        return self._describe(left, right, time_stamp)
+        with torch.cuda.stream(ts):
+            b["img_lr"][:n].copy_(left.reshape(-1))
+            b["img_lr"][n:].copy_(right.reshape(-1))
+        self.lsd.detect_async(b["img_lr"], 2 * self.B, b["kl_lr"], b["n_kl_lr"])
+        return self._describe(s, ts, left, right, time_stamp)
 
-    def _describe(self, left, right, time_stamp):
-        B, pb = self.B, int(self.cam.pyr_bytes)
+    def _describe(self, s, ts, left, right, time_stamp):
+        import torch
+        B, pb, b = self.B, int(self.cam.pyr_bytes), self.bufs[s]
         for side, img in ((0, left), (1, right)):
-            pyr = self.pyr_l if side == 0 else self.pyr_r
-            self.orb.extract(img, B, self.kps[side], self.pdesc[side], self.n_kp[side], None, None, pyr, pb)
+            pyr = b["pyr_l"] if side == 0 else b["pyr_r"]
+            self.orb.extract_async(img, B, b["kps"][side], b["pdesc"][side], b["n_kp"][side], None, None, pyr, pb)
         for side in range(2):
-            self.lbd.compute_batch(left if side == 0 else right, B, self.kl[side], self.n_kl[side], self.ldesc[side])
-        self.ts.copy_(time_stamp)
-        arrs = [self.n_kp[0], self.n_kp[1], self.kps[0], self.kps[1], self.pdesc[0], self.pdesc[1],
-                self.n_kl[0], self.n_kl[1], self.kl[0], self.kl[1], self.ldesc[0], self.ldesc[1], self.pyr_r, self.ts]
-        return make_frames(B, self.kp_cap, self.kl_cap, arrs)
+            self.lbd.compute_async(left if side == 0 else right, B, b["kl"][side], b["n_kl"][side], b["ldesc"][side])
+        with torch.cuda.stream(ts):
+            b["ts"].copy_(time_stamp)
+        self.ready[s].record(self.det)
+        arrs = [b["n_kp"][0], b["n_kp"][1], b["kps"][0], b["kps"][1], b["pdesc"][0], b["pdesc"][1],
+                b["n_kl"][0], b["n_kl"][1], b["kl"][0], b["kl"][1], b["ldesc"][0], b["ldesc"][1], b["pyr_r"], b["ts"]]
+        fr = make_frames(B, self.kp_cap, self.kl_cap, arrs)
+        fr.ready, fr.consumed = self.ready[s].h, self.consumed[s].h
+        fr._events = (self.ready[s], self.consumed[s])
+        return fr
+
+    def status(self):
+        """capacity / octave errors of the detections since the last status (waits for them)"""
+        self.orb.status()
+        self.lbd.status()
+        if self.lsd is not None:
+            self.lsd.status()
+
+    def synchronize(self):
+        self.det.synchronize()
 
     def close(self):
+        self.det.synchronize()
         self.orb.close()
         self.lbd.close()
         if self.lsd is not None:
             self.lsd.close()
+        for e in self.ready + self.consumed:
+            e.close()
+        self.det.close()

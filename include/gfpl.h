@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GFPL_ABI_VERSION 2
+#define GFPL_ABI_VERSION 3
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
@@ -72,7 +72,8 @@ typedef struct gfpl_camera {
     int    lvl_rows[GFPL_MAX_LEVELS];         /* cvRound(H * inv_scale)        */
     int64_t lvl_offset[GFPL_MAX_LEVELS];      /* byte offset of level in packed pyramid */
     int64_t pyr_bytes;                        /* bytes of one packed pyramid: sum of the
-                                                 levels + >= GFPL_PYR_TAIL, 256-aligned   */
+                                                 levels + >= GFPL_PYR_TAIL, a multiple of 4
+                                                 (gfpl_camera_init: of 256)               */
     double sigma2_pt[GFPL_MAX_LEVELS];        /* PointFeature::sigma2 per level (src/stereoFeatures.cpp:41-47) */
     double sigma2_ln[GFPL_MAX_LEVELS];        /* LineFeature::sigma2 per level  (src/stereoFeatures.cpp:96-101) */
 } gfpl_camera;
@@ -132,6 +133,8 @@ typedef struct gfpl_orb_params {
 /* line_descriptor::KeyLine subset (3rdparty/line_descriptor/include/line_descriptor/descriptor_custom.hpp:105-170) */
 typedef struct gfpl_keyline { float sx, sy, ex, ey, angle; int octave; } gfpl_keyline;
 
+typedef struct gfpl_event gfpl_event;   /* stream-ordering event (gfpl_event_*) */
+
 /* One batch of input stereo frames (detections already done — detection is out
  * of scope).  All pointers are DEVICE pointers.     */
 typedef struct gfpl_frames {
@@ -149,8 +152,13 @@ typedef struct gfpl_frames {
     const gfpl_keyline*  kl_r;         /* [B*kl_cap]                          */
     const uint8_t*       ldesc_l;      /* [B*kl_cap*32]                       */
     const uint8_t*       ldesc_r;      /* [B*kl_cap*32]                       */
-    const uint8_t*       pyr_r;        /* [B*cam.pyr_bytes] right ORB pyramid */
+    const uint8_t*       pyr_r;        /* [B*cam.pyr_bytes] right ORB pyramid (4-byte aligned) */
     const double*        time_stamp;   /* [B]                                 */
+    /* optional stream ordering with a producer on another context (e.g. the detectors):
+     * a tracker call that reads these frames makes its stream wait for `ready` first and
+     * records `consumed` once its reads are enqueued.  NULL (zero-initialised): none.   */
+    gfpl_event*          ready;
+    gfpl_event*          consumed;
 } gfpl_frames;
 
 /* Host view of one frame's state (StereoFrame public members the path
@@ -237,6 +245,20 @@ int  gfpl_camera_init(gfpl_camera* cam, int width, int height, double fx, double
 /* context: device + stream + camera + config (replaces the Config singleton
  * src/config.cpp:158-162 and the PinholeStereoCamera* each frame holds).   */
 int  gfpl_create(int device, void* hip_stream, gfpl_ctx** out);
+/* A context on its own non-blocking stream (created here, destroyed with the context):
+ * for a caller without a HIP runtime that wants, e.g., detection and tracking on two
+ * contexts ordered by gfpl_event_* instead of one serial stream.                      */
+int  gfpl_create_async(int device, gfpl_ctx** out);
+/* the hipStream_t (as void*) the context enqueues on */
+void* gfpl_get_stream(const gfpl_ctx* ctx);
+
+/* Stream-ordering events between contexts (all asynchronous but synchronize):
+ * record on a context's stream, make another context's stream wait for it.           */
+int  gfpl_event_create(gfpl_ctx* ctx, gfpl_event** out);
+int  gfpl_event_destroy(gfpl_event* ev);
+int  gfpl_event_record(gfpl_event* ev, gfpl_ctx* ctx);
+int  gfpl_event_wait(gfpl_ctx* ctx, gfpl_event* ev);
+int  gfpl_event_synchronize(gfpl_event* ev);
 /* GFPL_E_STATE while seqbatches created on the context are still alive.       */
 int  gfpl_destroy(gfpl_ctx* ctx);
 int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
@@ -352,11 +374,21 @@ int  gfpl_orb_pyramid_bytes(const gfpl_orb* orb, int64_t* bytes);
  * kps / desc (32 B) / angle (degrees) / response (FAST score) hold the keypoints
  * in the reference's order (level by level, DistributeOctTree node order),
  * coordinates scaled to level 0.  angle, response, pyramid may be NULL; pyramid
- * receives each image's level images at pyr_stride bytes apart.  Synchronises;
- * GFPL_E_CAPACITY when an internal or kp_cap capacity was exceeded.            */
+ * receives each image's level images at pyr_stride bytes apart.  When the context has
+ * a camera of this image size and pyr_stride is its pyr_bytes (the tracker's
+ * gfpl_frames.pyr_r), the extractor's level geometry must be the camera's
+ * (GFPL_E_INVALID otherwise).  Synchronises; GFPL_E_CAPACITY when an internal or
+ * kp_cap capacity was exceeded.                                                */
 int  gfpl_orb_extract(gfpl_orb* orb, const uint8_t* images, int n, gfpl_keypoint* kps,
                       uint8_t* desc, int* n_kp, float* angle, float* response,
                       uint8_t* pyramid, int64_t pyr_stride);
+/* The same, stream-ordered: returns after enqueueing on the context's stream (argument
+ * errors are still returned at once); the capacity status of every async call since the
+ * last status is returned by gfpl_orb_status (which waits for the last of them).      */
+int  gfpl_orb_extract_async(gfpl_orb* orb, const uint8_t* images, int n, gfpl_keypoint* kps,
+                            uint8_t* desc, int* n_kp, float* angle, float* response,
+                            uint8_t* pyramid, int64_t pyr_stride);
+int  gfpl_orb_status(gfpl_orb* orb);
 
 /* ---------------------------------------- LBD descriptors (§8(f)2 part) ---- */
 /* line_descriptor::BinaryDescriptor::compute(image, keylines, descriptors)
@@ -370,9 +402,14 @@ int  gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_images, int k
 int  gfpl_lbd_destroy(gfpl_lbd* lbd);
 /* all pointers DEVICE: images [n][height][width] u8, keylines [n][kl_cap] (sx sy ex ey angle
  * octave, LSDDetectorC's fields), n_kl [n]; desc [n][kl_cap][32] receives row i of image j's
- * 32-byte LBD for keyline i < n_kl[j].  Synchronises.                                      */
+ * 32-byte LBD for keyline i < n_kl[j].  Synchronises; GFPL_E_CAPACITY when some n_kl[j] >
+ * kl_cap (the first kl_cap are described), GFPL_E_UNSUPPORTED for a keyline of octave != 0. */
 int  gfpl_lbd_compute(gfpl_lbd* lbd, const uint8_t* images, int n, const gfpl_keyline* keylines,
                       const int* n_kl, uint8_t* desc);
+/* stream-ordered form; gfpl_lbd_status reports (and waits for) the async calls since the last */
+int  gfpl_lbd_compute_async(gfpl_lbd* lbd, const uint8_t* images, int n, const gfpl_keyline* keylines,
+                            const int* n_kl, uint8_t* desc);
+int  gfpl_lbd_status(gfpl_lbd* lbd);
 /* test hook of ledger L1-L2: the Gaussian-blurred image's Sobel derivatives of one DEVICE image,
  * grad [height][width] (DEVICE) = dx (low 16 bits) | dy (high 16 bits).  Synchronises.      */
 int  gfpl_lbd_gradients(gfpl_lbd* lbd, const uint8_t* image, uint32_t* grad);
@@ -408,6 +445,10 @@ int  gfpl_lsd_destroy(gfpl_lsd* lsd);
  * (GFPL_E_CAPACITY).  Synchronises.                                                        */
 int  gfpl_lsd_detect(gfpl_lsd* lsd, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
                      float* response);
+/* stream-ordered form; gfpl_lsd_status reports (and waits for) the async calls since the last */
+int  gfpl_lsd_detect_async(gfpl_lsd* lsd, const uint8_t* images, int n, gfpl_keyline* keylines, int* n_kl,
+                           float* response);
+int  gfpl_lsd_status(gfpl_lsd* lsd);
 /* test hook of ledger S2: std::sort(a, a + n, key(x) > key(y)) with key = the high 32 bits of
  * each element, on DEVICE memory (n <= (width-1)(height-1)); the permutation the seed order
  * and the response sort use.  Synchronises.                                                 */

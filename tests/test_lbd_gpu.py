@@ -73,3 +73,29 @@ def test_lbd_host_call_and_octave_refusal():
     kl["octave"][10] = 1
     with pytest.raises(gfpl.GfplError):
         lbd.compute(img, kl)
+
+
+def test_lbd_more_keylines_than_capacity_is_an_error():
+    """The reference describes every keyline: n_kl > kl_cap is GFPL_E_CAPACITY (the first kl_cap
+    rows are still described), like LSD's and ORB's capacity errors; the asynchronous form
+    reports it through gfpl_lbd_status, and the status clears after it is read."""
+    import torch
+    w, h = 320, 240
+    img = gfpl.synth_image(7, 0, w, h)
+    kl = synth_keylines(40, w, h, 3)
+    lbd = gfpl.BinaryDescriptor(w, h, max_images=1, kl_cap=40)
+    dev = torch.device("cuda", 0)
+    d_img = torch.from_numpy(img).to(dev)
+    d_kl = torch.from_numpy(kl.view(np.uint8).reshape(-1)).to(dev)
+    d_desc = torch.zeros(40 * 32, dtype=torch.uint8, device=dev)
+    over = torch.tensor([41], dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    with pytest.raises(gfpl.GfplError) as e:
+        lbd.compute_batch(d_img, 1, d_kl, over, d_desc)
+    assert e.value.code == -5
+    assert (d_desc.cpu().numpy().reshape(40, 32) == O.lbd_compute(img, kl)[0]).all()
+    lbd.compute_async(d_img, 1, d_kl, over, d_desc)
+    with pytest.raises(gfpl.GfplError):
+        lbd.status()
+    lbd.status()   # cleared
+    lbd.compute_batch(d_img, 1, d_kl, torch.tensor([40], dtype=torch.int32, device=dev), d_desc)

@@ -161,3 +161,34 @@ def test_orb_pyramid_is_the_trackers_right_pyramid():
     rep = _run_sequence("vga", {}, n_seq=2, n_frames=3, kp_cap=2048, kl_cap=512, mutate=host_pyr, dev_hook=dev_hook)
     assert seen.get("ok")
     _check(rep)
+
+
+def test_orb_pyramid_for_the_tracker_must_match_the_camera():
+    """gfpl_orb_extract refuses to write the tracker's right pyramid (a context camera of the
+    image size, stride = its pyr_bytes) with other level geometry (e.g. another scale factor):
+    the sub-pixel SAD would silently read other pixels (GFPL_E_INVALID)."""
+    import torch
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    ctx = gfpl.Context(cam, cfg)
+    W, H = int(cam.width), int(cam.height)
+    dev = torch.device("cuda", 0)
+    img = torch.from_numpy(gfpl.synth_image(1, 0, W, H)).to(dev)
+    for scale, ok in ((1.2, True), (1.3, False)):
+        orb = gfpl.ORBextractor(1000, scale, int(cam.n_levels), 20, 7, W, H, ctx=ctx)
+        kc = orb.kp_cap
+        kps = torch.zeros(kc * gfpl.KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+        desc = torch.zeros(kc * 32, dtype=torch.uint8, device=dev)
+        nkp = torch.zeros(1, dtype=torch.int32, device=dev)
+        pyr = torch.zeros(int(cam.pyr_bytes), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        if ok:
+            orb.extract(img, 1, kps, desc, nkp, None, None, pyr, int(cam.pyr_bytes))
+        else:
+            with pytest.raises(gfpl.GfplError) as e:
+                orb.extract(img, 1, kps, desc, nkp, None, None, pyr, int(cam.pyr_bytes))
+            assert e.value.code == -1
+            # any other stride is a pyramid for some other consumer: not checked
+            orb.extract(img, 1, kps, desc, nkp, None, None, torch.zeros(orb.pyramid_bytes + 256, dtype=torch.uint8,
+                                                                          device=dev), orb.pyramid_bytes + 256)
+        orb.close()

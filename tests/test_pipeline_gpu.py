@@ -74,6 +74,7 @@ def test_images_to_poses_match_the_oracle_pipeline(disparity):
         fr = pipe.detect(left, right, to(kl[0]), torch.from_numpy(n[0]).to(dev), to(kl[1]),
                          torch.from_numpy(n[1]).to(dev), torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
         hfr, harr = _host_frames(cam, scenes, KP, KL, 0.05 * k)
+        pipe.status()   # waits for the detection stream; capacity errors raise
         # the device detections are the oracle's, byte for byte (valid rows; the device
         # buffers keep stale rows past each count)
         d = [t.cpu().numpy() for t in fr._keep]
@@ -136,6 +137,7 @@ def test_images_to_poses_with_lsd_on_device():
         right = torch.from_numpy(np.stack([s[1] for s in scenes])).to(dev)
         fr = pipe.detect_images(left, right, torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
         hfr, harr = _host_frames(cam, scenes, KP, KL, 0.05 * k)
+        pipe.status()
         d = [t.cpu().numpy() for t in fr._keep]
         for side in range(2):
             nl_d = d[6 + side]
@@ -165,4 +167,65 @@ def test_images_to_poses_with_lsd_on_device():
             bad += compare_track(g.read_last_track(b), tr, f"f{k} s{b} ")
     assert not bad, "\n".join(bad[:30])
     assert all(c[1] > 5 for c in counts), counts
+    pipe.close()
+
+
+def test_detection_overlapped_with_tracking_parity():
+    """The bench's order: the detection of frame k + 1 is enqueued (its own stream, the other
+    buffer set) before the tracking step of frame k, with no host synchronisation between
+    them — the gfpl_frames ready / consumed events alone order them.  Poses, stereo features
+    and matched lists equal the oracle chain's, frame by frame."""
+    import torch
+    cfg = gfpl.default_config(max_iters=10, max_iters_ref=10)
+    cam = gfpl.make_camera("vga", cfg)
+    B, F, KL = 3, 6, 320
+    W, H = int(cam.width), int(cam.height)
+    ctx = gfpl.Context(cam, cfg)
+    pipe = ImagePipeline(ctx, cam, B, KL)
+    KP = pipe.kp_cap
+    g = gfpl.StereoFrameHandler(ctx, B, KP, KL)
+    orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(B)]
+    dev = torch.device("cuda", 0)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    def inputs(k):
+        scenes = [synth_stereo_steps(b, k, W, H) for b in range(B)]
+        kl = [np.zeros((B, KL), gfpl.KEYLINE_DT) for _ in range(2)]
+        n = [np.zeros(B, np.int32) for _ in range(2)]
+        for b, sc in enumerate(scenes):
+            for side in range(2):
+                n[side][b] = len(sc[2 + side])
+                kl[side][b, :n[side][b]] = sc[2 + side]
+        dev_in = (to(np.stack([x[0] for x in scenes])), to(np.stack([x[1] for x in scenes])),
+                  to(kl[0].view(np.uint8).reshape(-1)), to(n[0]), to(kl[1].view(np.uint8).reshape(-1)), to(n[1]),
+                  torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
+        return scenes, dev_in
+
+    sc0, in0 = inputs(0)
+    g.initialize(pipe.detect(*in0))
+    hfr0, _ = _host_frames(cam, sc0, KP, KL, 0.0)
+    for b, o in enumerate(orc):
+        o.initialize(hfr0, b)
+    scenes, nxt = inputs(1)
+    fr_next = pipe.detect(*nxt)
+    bad = []
+    for k in range(1, F):
+        cur, cur_scenes = fr_next, scenes
+        if k + 1 < F:
+            scenes, nxt = inputs(k + 1)
+            fr_next = pipe.detect(*nxt)     # enqueued before the step on frame k
+        g.frameStep(cur)
+        hfr, _ = _host_frames(cam, cur_scenes, KP, KL, 0.05 * k)
+        for b, o in enumerate(orc):
+            o.insertStereoPair(hfr, b)
+            o.optimizePose()
+            tr = o.read_track()
+            o.updateFrame()
+            gp, op = g.read_frame(gfpl.PREV, b), o.read_frame(gfpl.PREV)
+            bad += compare_core(gp, op, f"f{k} s{b} ")
+            bad += compare_pose(gp, op, what=f"f{k} s{b} ")[0]
+            bad += compare_track(g.read_last_track(b), tr, f"f{k} s{b} ")
+    pipe.status()
+    assert not bad, "\n".join(bad[:30])
+    g.close()
     pipe.close()
