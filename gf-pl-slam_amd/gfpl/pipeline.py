@@ -107,7 +107,7 @@ class ImagePipeline:
     LSD (lsd=True: the reference's LSDOptions, Config::lsdNFeatures = 300, min length
     0.025 * min(W, H)) and LBD.
 
-    Detection runs on its own context (its own stream, gfpl_create_async) into `sets`
+    Detection runs on its own context (its own stream) into `sets`
     buffer sets in turn, through the stream-ordered detector calls (gfpl_*_async).  Every
     gfpl_frames it returns carries two events: `ready` (its detection is done) and
     `consumed` (recorded by the tracker call that reads it, gfpl_frames.ready / consumed),
@@ -122,7 +122,10 @@ class ImagePipeline:
         cfg = cfg if cfg is not None else ctx.cfg
         self.ctx, self.cam, self.B, self.kl_cap, self.sets = ctx, cam, batch, kl_cap, sets
         W, H = int(cam.width), int(cam.height)
-        self.det = Context(cam, cfg, device=ctx.device, own_stream=True)
+        # the detection stream is a torch stream (pooled by torch, never destroyed), so torch's
+        # allocator may record the inputs' use on it (Tensor.record_stream)
+        self._tstream = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+        self.det = Context(cam, cfg, device=ctx.device, stream=self._tstream.cuda_stream)
         self.orb = ORBextractor(nfeatures, float(cfg.orb_scale_factor), int(cfg.orb_n_levels), 20, 7, W, H,
                                 max_images=batch, ctx=self.det)
         # the extractor writes the tracker's right pyramid (gfpl_frames.pyr_r): its levels must
@@ -166,7 +169,7 @@ class ImagePipeline:
         s = self.k % self.sets
         self.k += 1
         self.consumed[s].wait(self.det)
-        ts = self.det.torch_stream()
+        ts = self._tstream
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(ts.device))
         ts.wait_event(ev)

@@ -192,3 +192,39 @@ def test_orb_pyramid_for_the_tracker_must_match_the_camera():
             orb.extract(img, 1, kps, desc, nkp, None, None, torch.zeros(orb.pyramid_bytes + 256, dtype=torch.uint8,
                                                                           device=dev), orb.pyramid_bytes + 256)
         orb.close()
+
+
+def test_orb_async_on_own_stream_context_with_events():
+    """The FFI form of stream ordering: a context with its own stream (gfpl_create_async),
+    ORB extraction enqueued there (gfpl_orb_extract_async), an event recorded on it and
+    waited for by a second context's stream; the host waits on the event only."""
+    import torch
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    det = gfpl.Context(cam, cfg, own_stream=True)
+    trk = gfpl.Context(cam, cfg)
+    assert det.stream != 0 and det.stream != trk.stream
+    W, H = int(cam.width), int(cam.height)
+    img_np = gfpl.synth_image(4, 2, W, H)
+    dev = torch.device("cuda", 0)
+    img = torch.from_numpy(img_np).to(dev)
+    orb = gfpl.ORBextractor(2000, 1.2, 4, 20, 7, W, H, ctx=det)
+    kc = orb.kp_cap
+    kps = torch.zeros(kc * gfpl.KEYPOINT_DT.itemsize, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(kc * 32, dtype=torch.uint8, device=dev)
+    nkp = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ev = gfpl.Event(det)
+    orb.extract_async(img, 1, kps, desc, nkp)
+    ev.record(det)
+    ev.wait(trk)
+    ev.synchronize()
+    orb.status()
+    o = O.orb_extract(img_np, kp_cap=kc)
+    n = int(nkp.cpu()[0])
+    assert n == len(o["kps"])
+    assert (kps.cpu().numpy().view(gfpl.KEYPOINT_DT)[:n] == o["kps"]).all()
+    assert (desc.cpu().numpy().reshape(kc, 32)[:n] == o["desc"]).all()
+    orb.close()
+    ev.close()
+    det.close()
