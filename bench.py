@@ -656,6 +656,8 @@ def main():
             counts.append(h.last_step_counts())
         if sampler:
             sampler.step(h, k)
+        if rank == 0:   # progress (stderr): long runs under a watchdog keep writing
+            print(f"[bench] step {k}/{W + K}: {1e3 * (ts1 - ts0):.2f} ms", file=sys.stderr, flush=True)
     elapsed = float(np.sum(step_s))
     lost = sum(h.read_track(b)["num_frame_loss"] > 0 for b in range(0, B, max(1, B // 16)))
     par = [sampler.frames, sampler.mismatch_frames] if sampler else [0, 0]
@@ -759,7 +761,7 @@ def main():
         dist.destroy_process_group()
 
 
-def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, steps=4):
+def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, steps=8):
     """PCIe-inclusive rate of a host-fed pipeline (rank 0 at N=1, after the timed steps):
     two input frames (f0, f0 + 1) of all B sequences held in pinned host memory are uploaded
     with gfpl_upload_frames_async into the two staging buffers in turn — the copy of step

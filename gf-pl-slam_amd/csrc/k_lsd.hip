@@ -682,12 +682,6 @@ __device__ __forceinline__ double modgrad(const Img& I, int x, int y) {
     return sqrt((double)(gx * gx + gy * gy) / 4.0);
 }
 
-__device__ __forceinline__ uint32_t reg_at(const Img& I, int i, int n) {
-    if (n - i <= LSD_RING) return I.ring[i & (LSD_RING - 1)];
-    mem_sync();
-    return I.reg[i];
-}
-
 // region_grow (lsd.cpp): returns the region size; reg / ring hold the points in push order
 template <bool LU>
 // (seed_deg: the seed's angle record; the caller fences before reading the list from HBM)

@@ -36,19 +36,11 @@ struct PoseLDS {
 // of the same columns k, k + 1 as 16-B pairs, and a 64-double stride would put
 // every row in the same LDS bank
 #define CH_STRIDE 66
-// register-budget knobs of the GN loop (DESIGN.md §4 k_pose): DT read from LDS and a
-// 4-deep reduction unroll bring the kernel to 149 VGPRs (3 waves / SIMD, which the
-// ~10 KB LDS workgroup now allows): 7.3 -> 6.9 ms measured; without the prefetch
-// (117 VGPRs) it was slower again
-#ifndef GFPL_POSE_DT_LDS
-#define GFPL_POSE_DT_LDS 1
-#endif
-#ifndef GFPL_POSE_PREFETCH
-#define GFPL_POSE_PREFETCH 1
-#endif
-#ifndef GFPL_POSE_RED_UNROLL
+// register budget of the GN loop (DESIGN.md §4 k_pose): DT read from LDS, the next chunk's
+// inputs prefetched into registers and a 4-deep reduction unroll: 149 VGPRs (3 waves /
+// SIMD, which the ~10 KB LDS workgroup allows), 7.3 -> 6.9 ms measured; without the
+// prefetch (117 VGPRs) it was slower again
 #define GFPL_POSE_RED_UNROLL 4
-#endif
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
 // evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w;
@@ -122,15 +114,9 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     const uint8_t* actp = X.act;
     const uint8_t* actl = X.act + X.npt;
     for (int it = 0; it < max_iters; ++it) {
-#if GFPL_POSE_DT_LDS
         // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
         // holding 16 doubles in registers across the chunk loop
         const double* DT = S.DT;
-#else
-        double DT[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) DT[i] = S.DT[i];
-#endif
         double s = 0.0;
         // raw inputs of chunk c + 1 are loaded into registers while chunk c is
         // reduced, so the SoA scratch latency hides behind the LDS reduction
@@ -143,14 +129,9 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
 #pragma unroll
             for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
         };
-#if GFPL_POSE_PREFETCH
         load_chunk(0);
-#endif
         for (int c = 0; c < nch; ++c) {
             const int f = (c << 6) + lane;
-#if !GFPL_POSE_PREFETCH
-            load_chunk(c);
-#endif
             double o[8];
             if (f < X.npt && actp[f]) eval_point(cam, homog, DT, pv, o);
             else {
@@ -166,9 +147,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
-#if GFPL_POSE_PREFETCH
             if (c + 1 < nch) load_chunk(c + 1);
-#endif
             __syncthreads();
             const double* A = buf + ia * CH_STRIDE;
             const double* Bv = buf + ib * CH_STRIDE;

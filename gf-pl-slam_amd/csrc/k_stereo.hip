@@ -210,9 +210,7 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
 #define SP_CHUNK 32
-#ifndef GFPL_SP_PROBE
-#define GFPL_SP_PROBE 0
-#endif       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
+       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
 
 // LDS-only wave sync: the wave's earlier LDS writes / reads have completed (LDS executes a
 // wave's accesses in order; the clobber keeps the compiler from moving accesses across it)
@@ -293,7 +291,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         pairs[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    if (GFPL_SP_PROBE != 5) bitonic_sort2(rkey, order, KP2);
+    bitonic_sort2(rkey, order, KP2);
     const int D = misc[0];
     // records in sorted order: x, band height maxr - minr (<= 16), octave (int8;
     // -128 = out of range, read from HBM)
@@ -368,10 +366,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             // lexicographic (dist, iR) minimum as one packed key (iR < 2^16 on this layout);
             // the start value keeps bestDist = 100 (no candidate below it: no match)
             uint32_t best = (100u << 16) | 0xFFFFu;
-#if GFPL_SP_PROBE == 1
-            if (t < N) finish_kp(t, iL, kpL, 100, 0);
-            continue;
-#endif
             for (int o = 0; o <= nlev; ++o) {   // wave-uniform
                 const bool need = act && (o < nlev ? ((long long)o >= (long long)levelL - 1 &&
                                                       (long long)o <= (long long)levelL + 1)
@@ -385,7 +379,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                     for (int sh = 1; sh < 64; sh <<= 1) c0 = min(c0, __shfl_xor(c0, sh));
                     {
                         const int je = c0 + (lane >> 1);
-                        if (GFPL_SP_PROBE != 3 && je < Nr && (rkey[je] >> 28) == (uint32_t)o) {
+                        if (je < Nr && (rkey[je] >> 28) == (uint32_t)o) {
                             const int iR = (int)(rkey[je] & 0xFFFFu);
                             wst[lane] = *reinterpret_cast<const u32x4*>(DR + (size_t)iR * 32 + 16 * (lane & 1));   // entry lane >> 1, half lane & 1
                         }
@@ -469,7 +463,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         SadJob J;
         float xL = 0.0f;
         uint32_t pr = 0;
-        if (GFPL_SP_PROBE != 2 && job != 0xFFFFFFFFu) {
+        if (job != 0xFFFFFFFFu) {
             const int iL = (int)(job & 0xFFFFu);
             xL = KL[iL].x;
             pr = pairs[iL];
@@ -505,7 +499,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     __syncthreads();
     // sort(vDistIdx) (src/stereoFrame.cpp:585)
-    if (GFPL_SP_PROBE != 4) bitonic_sort(pairs, KP2);
+    bitonic_sort(pairs, KP2);
     for (int i = tid; i < KP2; i += blockDim.x) {
         bool v = pairs[i] != 0xFFFFFFFFu;
         bool vn = (i + 1 < KP2) ? (pairs[i + 1] != 0xFFFFFFFFu) : false;
