@@ -209,8 +209,8 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #ifndef GFPL_SP_WAVES
 #define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
-#define SP_CHUNK 32
-       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
+#define SP_CHUNK 32       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
+#define SP_MINR_PAD 32    // minr bins span [-PAD, H + PAD) (k_stereo_points, SEG): every band is shorter
 
 // LDS-only wave sync: the wave's earlier LDS writes / reads have completed (LDS executes a
 // wave's accesses in order; the clobber keeps the compiler from moving accesses across it)
@@ -242,12 +242,14 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     uint32_t* pairs = order + KP2;
     float* recx = (float*)(pairs + KP2);
     uint16_t* recm = (uint16_t*)(recx + KP2);
-    uint16_t* rowlo = recm + KP2;
+    uint16_t* rowlo = recm + KP2;   // SEG: offr, the bin offsets of the counting sort
     const int nlev = p.cam.n_levels;
-    const int nrl = SEG ? nlev * nRows : nRows;
-    int* misc = (int*)(rowlo + ((nrl + 1) & ~1));   // SEG: [22 + seg] band heights, [31] out-of-range count
-    // SEG: per-wave staging of right descriptors, SP_CHUNK x 32 B per wave (16-B aligned)
-    uint32_t* stg = (uint32_t*)(((uintptr_t)(misc + 32) + 15) & ~(uintptr_t)15);
+    const int NBIN = nRows + 2 * SP_MINR_PAD;   // SEG: minr bins per octave segment
+    const int nrl = SEG ? (nlev + 1) * NBIN + 1 : nRows;
+    int* misc = (int*)(rowlo + ((nrl + 1) & ~1));   // SEG: [22 + seg] band heights
+    // SEG: per-wave staging of right descriptors, SP_CHUNK x 32 B per wave (16-B aligned); an
+    // integer offset from smem keeps the pointer in the LDS address space
+    uint32_t* stg = (uint32_t*)(smem + ((KP2 * 18 + ((nrl + 1) & ~1) * 2 + 32 * 4 + 15) & ~15));
     // mvDepth of the sub-pixel pass lives in recx: the right keypoints' x are dead once the
     // band scan is over (LDS, no scattered 4-B global stores)
     float* depth = recx;
@@ -257,6 +259,96 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
     const uint8_t* DL = p.in.pdesc_l + (size_t)b * cap * 32;
     const uint8_t* DR = p.in.pdesc_r + (size_t)b * cap * 32;
+    if (SEG) {
+        // vRowIndices (src/stereoFrame.cpp:459-485) as a counting sort of the right keypoints
+        // by (octave segment, minr) and of the left ones by row: the scan needs the band
+        // candidates grouped by minr only (it takes the lexicographic (dist, iR) minimum of
+        // every candidate with minr <= row, and stops at the first minr > row), so the order
+        // inside a bin — the LDS atomics' — is immaterial, and the bin offsets are the table
+        // of each row's first candidate.  minr is binned clamped to [-PAD, H + PAD): rows are
+        // in [0, H) and bands are shorter than PAD, so clamping never reorders a candidate
+        // across a row's start or stop.  Left keypoints go in row order (the processing
+        // order, which has no effect on the output).
+        uint32_t* hr = reinterpret_cast<uint32_t*>(rowlo);   // u16 counts, two per word
+        uint32_t* hl = stg;                                  // left row counts (u16), in the stage buffer
+        const int nbr = (nlev + 1) * NBIN, nbl = nRows + 1;
+        for (int w = tid; w < (nbr + 2) / 2; w += BLOCK) hr[w] = 0u;
+        for (int w = tid; w < (nbl + 1) / 2; w += BLOCK) hl[w] = 0u;
+        if (tid < 32) misc[tid] = 0;
+        __syncthreads();
+        constexpr int RMAX = 2048 / BLOCK;   // kp_cap <= 2048 on this layout
+        uint32_t rk[RMAX], rbr[RMAX], lbr[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const int i = tid + r * BLOCK;
+            rk[r] = 0xFFFFFFFFu;
+            rbr[r] = 0u;
+            lbr[r] = 0u;
+            if (i < Nr) {
+                const gfpl_keypoint kp = KR[i];
+                const float rr = 2.0f * p.cam.scale[clamp_level(kp.octave, nlev)];
+                const int maxr = (int)ceilf(kp.y + rr);
+                const int minr = (int)floorf(kp.y - rr);
+                const int seg = (kp.octave >= 0 && kp.octave < nlev) ? kp.octave : nlev;
+                // rows are < 2048 (GFPL_MAX_IMAGE_DIM): the key keeps minr clamped to [-1024, 3071]
+                const int mc = min(max(minr, -1024), 3071);
+                rk[r] = ((uint32_t)seg << 28) | ((uint32_t)(mc + 1024) << 16) | (uint32_t)i;
+                const int bin = seg * NBIN + min(max(minr + SP_MINR_PAD, 0), NBIN - 1);
+                const uint32_t sh = 16u * (uint32_t)(bin & 1);
+                const uint32_t old = atomicAdd(&hr[bin >> 1], 1u << sh);
+                rbr[r] = (uint32_t)bin | (((old >> sh) & 0xFFFFu) << 16);   // bin | rank in bin
+                atomicMax(&misc[22 + seg], maxr - minr);
+            }
+            if (i < N) {
+                const float y = KL[i].y;
+                const int row = (y >= 0.0f && y < (float)nRows) ? (int)y + 1 : 0;
+                const uint32_t sh = 16u * (uint32_t)(row & 1);
+                const uint32_t old = atomicAdd(&hl[row >> 1], 1u << sh);
+                lbr[r] = (uint32_t)row | (((old >> sh) & 0xFFFFu) << 16);
+            }
+            if (i < KP2) pairs[i] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        // exclusive scans of both histograms in place (u16 offsets), block-wide
+        uint16_t* offr = rowlo;
+        uint16_t* offl = reinterpret_cast<uint16_t*>(hl);
+        {
+            const int per = (nbr + BLOCK - 1) / BLOCK, b0 = min(tid * per, nbr), b1 = min(b0 + per, nbr);
+            int sum = 0;
+            for (int x = b0; x < b1; ++x) sum += offr[x];
+            int tot;
+            int run = block_exclusive_scan<BLOCK>(sum, misc + 4, &tot);
+            for (int x = b0; x < b1; ++x) { const int c = offr[x]; offr[x] = (uint16_t)run; run += c; }
+            if (tid == 0) offr[nbr] = (uint16_t)tot;
+        }
+        {
+            const int per = (nbl + BLOCK - 1) / BLOCK, b0 = min(tid * per, nbl), b1 = min(b0 + per, nbl);
+            int sum = 0;
+            for (int x = b0; x < b1; ++x) sum += offl[x];
+            int tot;
+            int run = block_exclusive_scan<BLOCK>(sum, misc + 4, &tot);
+            for (int x = b0; x < b1; ++x) { const int c = offl[x]; offl[x] = (uint16_t)run; run += c; }
+        }
+        __syncthreads();
+        // scatter: keys with their x, band height maxr - minr and octave (int8; -128 = out
+        // of range, read from HBM) side by side; left keypoint indices in row order
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const int i = tid + r * BLOCK;
+            if (i < Nr) {
+                const int j = (int)offr[rbr[r] & 0xFFFFu] + (int)(rbr[r] >> 16);
+                const gfpl_keypoint kp = KR[i];
+                const float rr = 2.0f * p.cam.scale[clamp_level(kp.octave, nlev)];
+                const int band = (int)ceilf(kp.y + rr) - (int)floorf(kp.y - rr);
+                const int oc = (kp.octave >= -127 && kp.octave <= 127) ? kp.octave : -128;
+                rkey[j] = rk[r];
+                recx[j] = kp.x;
+                recm[j] = (uint16_t)(((uint32_t)band << 8) | ((uint32_t)oc & 0xFFu));
+            }
+            if (i < N) order[(int)offl[lbr[r] & 0xFFFFu] + (int)(lbr[r] >> 16)] = (uint32_t)i;
+        }
+        __syncthreads();
+    } else {
     if (tid < 32) misc[tid] = 0;
     __syncthreads();
     // vRowIndices as (minr, iR) keys; left keypoints as (row, iL) keys
@@ -266,18 +358,8 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             const float r = 2.0f * p.cam.scale[clamp_level(kp.octave, p.cam.n_levels)];
             const int maxr = (int)ceilf(kp.y + r);
             const int minr = (int)floorf(kp.y - r);
-            if (SEG) {
-                // rows are < 2048 (GFPL_MAX_IMAGE_DIM): clamping minr to [-1024, 3071]
-                // keeps every key whose band can reach a row exact
-                const int seg = (kp.octave >= 0 && kp.octave < nlev) ? kp.octave : nlev;
-                const int mc = min(max(minr, -1024), 3071);
-                rkey[i] = ((uint32_t)seg << 28) | ((uint32_t)(mc + 1024) << 16) | (uint32_t)i;
-                atomicMax(&misc[22 + seg], maxr - minr);
-                if (seg == nlev) atomicAdd(&misc[31], 1);
-            } else {
-                rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
-                atomicMax(&misc[0], maxr - minr);
-            }
+            rkey[i] = ((uint32_t)(minr + 32768) << 16) | (uint32_t)i;
+            atomicMax(&misc[0], maxr - minr);
         } else {
             rkey[i] = 0xFFFFFFFFu;
         }
@@ -304,21 +386,19 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         recx[j] = kp.x;
         recm[j] = (uint16_t)(((uint32_t)band << 8) | ((uint32_t)oc & 0xFFu));
     }
-    // first candidate of each row: lower bound of minr >= row - D (SEG: per octave)
-    auto seg_key = [&](int seg, int row) {
-        const int r0 = min(max(row - misc[22 + seg], -1024), 3071);
-        return ((uint32_t)seg << 28) | ((uint32_t)(r0 + 1024) << 16);
-    };
-    auto lower = [&](uint32_t lo_key) {
-        int lo = 0, hi = Nr;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
-        return lo;
-    };
+    // first candidate of each row: lower bound of minr >= row - D
     for (int x = tid; x < nrl; x += blockDim.x) {
-        if (SEG) rowlo[x] = (uint16_t)lower(seg_key(x / nRows, x % nRows));
-        else rowlo[x] = (uint16_t)lower((uint32_t)(x - D + 32768) << 16);
+        int lo = 0, hi = Nr;
+        const uint32_t lo_key = (uint32_t)(x - D + 32768) << 16;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (rkey[mid] < lo_key) lo = mid + 1; else hi = mid; }
+        rowlo[x] = (uint16_t)lo;
     }
     __syncthreads();
+    }
+    // SEG: first candidate of segment o for a row: the first bin with minr >= row - D_o
+    auto seg_start = [&](int o, int row) {
+        return (int)rowlo[o * NBIN + min(max(row - misc[22 + o] + SP_MINR_PAD, 0), NBIN - 1)];
+    };
     const float minD = 0;
     const float maxD = (float)p.cam.fx;
     const float mbf = (float)(p.cam.fx * p.cam.b);
@@ -369,9 +449,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             for (int o = 0; o <= nlev; ++o) {   // wave-uniform
                 const bool need = act && (o < nlev ? ((long long)o >= (long long)levelL - 1 &&
                                                       (long long)o <= (long long)levelL + 1)
-                                                   : misc[31] > 0);
+                                                   : rowlo[(nlev + 1) * NBIN] > rowlo[nlev * NBIN]);
                 if (!__any(need)) continue;
-                int j = need ? (o < nlev ? (int)rowlo[o * nRows + row] : lower(seg_key(nlev, row))) : 0x7FFFFFFF;
+                int j = need ? seg_start(o, row) : 0x7FFFFFFF;
                 bool more = need && j < Nr;
                 while (__any(more)) {
                     int c0 = more ? j : 0x7FFFFFFF;
@@ -498,18 +578,82 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         }
     }
     __syncthreads();
-    // sort(vDistIdx) (src/stereoFrame.cpp:585)
-    bitonic_sort(pairs, KP2);
-    for (int i = tid; i < KP2; i += blockDim.x) {
-        bool v = pairs[i] != 0xFFFFFFFFu;
-        bool vn = (i + 1 < KP2) ? (pairs[i + 1] != 0xFFFFFFFFu) : false;
-        if (v && !vn) misc[1] = i + 1;
+    // sort(vDistIdx) (src/stereoFrame.cpp:585): the (dist, iL) keys ascending
+    uint32_t* keys = pairs;
+    if (SEG) {
+        // A stable counting sort by dist (< 128) of the keys in iL order — the order sorting
+        // the (dist, iL) pairs gives.  Ranks among equal dists: within a wave by ballots (a
+        // multisplit on the 7 dist bits), across the waves of a round and across rounds (iL
+        // ascending) by per-dist counters; the sorted keys go to order[] (free after the SAD).
+        constexpr int NW = BLOCK / 64;
+        int* cnt = reinterpret_cast<int*>(stg);   // [128] dist counts -> running offsets
+        int* wcnt = cnt + 128;                    // [NW][128] this round's per-wave counts
+        for (int x = tid; x < 128 * (NW + 1); x += BLOCK) cnt[x] = 0;
+        __syncthreads();
+        for (int i = tid; i < KP2; i += BLOCK) {
+            const uint32_t k = pairs[i];
+            if (k != 0xFFFFFFFFu) atomicAdd(&cnt[k >> 16], 1);
+        }
+        __syncthreads();
+        if (tid < 64) {   // exclusive scan of the 128 counts, two per lane
+            const int c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
+            int x = c0 + c1;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (tid >= o) x += y;
+            }
+            const int ex = x - (c0 + c1);
+            cnt[2 * tid] = ex;
+            cnt[2 * tid + 1] = ex + c0;
+            if (tid == 63) misc[1] = x;   // valid keys
+        }
+        __syncthreads();
+        const int wave = tid >> 6, lane = tid & 63;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        keys = order;
+        for (int r0 = 0; r0 < KP2; r0 += BLOCK) {   // block-uniform
+            const int i = r0 + tid;
+            const uint32_t k = i < KP2 ? pairs[i] : 0xFFFFFFFFu;
+            const bool v = k != 0xFFFFFFFFu;
+            const int d = (int)(k >> 16) & 127;
+            unsigned long long peers = __ballot(v);
+#pragma unroll
+            for (int bit = 0; bit < 7; ++bit) {
+                const bool on = (d >> bit) & 1;
+                const unsigned long long m = __ballot(on);
+                peers &= on ? m : ~m;
+            }
+            const int rnk = __popcll(peers & lt);
+            if (v && rnk == 0) wcnt[wave * 128 + d] = __popcll(peers);
+            __syncthreads();
+            if (v) {
+                int pos = cnt[d] + rnk;
+                for (int w = 0; w < wave; ++w) pos += wcnt[w * 128 + d];
+                keys[pos] = k;
+            }
+            __syncthreads();
+            if (tid < 128) {
+                int sum = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) { sum += wcnt[w * 128 + tid]; wcnt[w * 128 + tid] = 0; }
+                cnt[tid] += sum;
+            }
+            __syncthreads();
+        }
+    } else {
+        bitonic_sort(pairs, KP2);
+        for (int i = tid; i < KP2; i += blockDim.x) {
+            bool v = pairs[i] != 0xFFFFFFFFu;
+            bool vn = (i + 1 < KP2) ? (pairs[i + 1] != 0xFFFFFFFFu) : false;
+            if (v && !vn) misc[1] = i + 1;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const int nv = misc[1];
     float thDist = 0.0f;
     if (nv > 0) {
-        const float median = (float)(pairs[nv / 2] >> 16);
+        const float median = (float)(keys[nv / 2] >> 16);
         thDist = 1.5f * 1.4f * median;
     }
     // emission in sorted order while dist < thDist, skipping negative disparities
@@ -517,13 +661,13 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     DevPoints& C = p.curr.pt;
     const size_t base = (size_t)b * cap;
     int off = 0;
-    for (int c0 = 0; c0 < KP2; c0 += BLOCK) {
+    for (int c0 = 0; c0 < nv; c0 += BLOCK) {   // block-uniform
         const int i = c0 + tid;
         int flag = 0;
         float disparity = 0.0f;
         int iL = 0;
         if (i < nv) {
-            const uint32_t k = pairs[i];
+            const uint32_t k = keys[i];
             const int dist = (int)(k >> 16);
             iL = (int)(k & 0xFFFFu);
             if ((float)dist < thDist) {
@@ -930,12 +1074,13 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
-    const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((p.cam.n_levels * p.cam.height + 1) & ~1) * 2 + 32 * 4 + 16 +
+    const int nrl_seg = (p.cam.n_levels + 1) * (p.cam.height + 2 * SP_MINR_PAD) + 1;
+    const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((nrl_seg + 1) & ~1) * 2 + 32 * 4 + 16 +
                            (size_t)(512 / 64) * SP_CHUNK * 32;
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
     if (p.kp_cap > 2048)
         hipLaunchKernelGGL((k_stereo_points<1024, false>), dim3(p.B), dim3(1024), lds, s, p, KP2);
-    else if (lds_seg <= 54 * 1024)   // three workgroups per CU
+    else if (lds_seg <= 54 * 1024 && p.kp_cap <= 2048)   // three workgroups per CU
         hipLaunchKernelGGL((k_stereo_points<512, true>), dim3(p.B), dim3(512), lds_seg, s, p, KP2);
     else
         hipLaunchKernelGGL((k_stereo_points<512, false>), dim3(p.B), dim3(512), lds, s, p, KP2);
