@@ -42,7 +42,10 @@ struct LsdDev {
     int W, H, NP;                  // NP = (W-1)(H-1) sorted pixels
     int n_bins, min_reg_size, seg_cap, kl_cap, n_features;
     double prec, rho, density_th, min_length;
-    float2* cs_tab;                // [1021][1021] (cos, sin) of float(angle(gx, gy)), gx, gy in +-510
+    float4* cs_tab;                // [1021][1021] per (gx, gy) in +-510: float cos / sin of float(angle)
+                                   // (a pixel joining a region) and of the double angle (a seed)
+    float2* scs;                   // [n][W*H] a defined pixel's seed (cos, sin): cs_tab.zw
+    float* ang;                    // [n][W*H] px.x alone (k_lsd_keys' neighbour reads)
     float4* px;                    // [n][W*H] per pixel: fastAtan2 degrees (-1 = NOTDEF), cos and
                                    // sin of float(angle), gx (low 16) | gy (high 16) as bits
     unsigned long long* maxg;      // [n] bits of the max norm of defined pixels
@@ -229,7 +232,7 @@ __device__ void heap_sort(uint64_t* a, int len) {
 }
 
 // __unguarded_partition_pivot(a + f, a + l) by the wave; returns the cut
-template <bool LDS, typename IT>
+template <bool LDS, typename IT, int CH = (LDS ? 4 : 16), int SW = (LDS ? 4 : 8)>
 __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     const int lane = lane_id();
     const int mid = f + (l - f) / 2;
@@ -247,8 +250,7 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     ssync<LDS>();
     const uint32_t pk = skey(pv);
     // __unguarded_partition(f + 1, l, f): the stoppers of both scans, ranked
-    int cl = 0, cr = 0;
-    constexpr int CH = LDS ? 4 : 16;   // chunks' loads in flight (HBM: sixteen)
+    int cl = 0, cr = 0;   // CH: chunks' loads in flight
     for (int base = f + 1; base < l; base += 64 * CH) {
         uint32_t k4[CH];
 #pragma unroll
@@ -286,7 +288,6 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
         lo = nlo;
     }
     const int K = lo;
-    constexpr int SW = LDS ? 4 : 8;
     for (int base = 0; base < K; base += 64 * SW) {
         int pl[SW], pr[SW];
         uint64_t x[SW], y[SW];
@@ -322,9 +323,8 @@ struct SortLds {
     uint64_t buf[CAP];
     uint16_t lp[CAP], rp[CAP];
     int stk[3 * 64];
-    int leaf[2 * 64];
     int small[3 * 64];
-    int lstk[64 * 3 * 5];   // per-lane stacks of lane_introsort (depth <= 3, see there)
+    int lstk[64 * 3 * 3];   // per-lane stacks of lane_introsort (depth <= 3, see there)
 };
 
 // libstdc++'s __introsort_loop + final insertion sort of one range [f, l) of an LDS array by
@@ -364,7 +364,8 @@ __device__ void lane_introsort(uint64_t* a, int f, int l, int d, int* st) {
             }
             const int cut = first;
             // push the larger part (if it needs work), continue with the smaller one: every
-            // stacked range is at least twice the current one, so the stack stays <= 5 deep
+            // stacked range is at least twice the current one: from <= 96 elements (LSD_SMALL) the stack
+            // holds <= 3 ranges (96 -> 48 -> 24 -> <= 12 stops)
             if (cut - f >= l - cut) {
                 if (cut - f > 16) { st[3 * sp] = f; st[3 * sp + 1] = cut; st[3 * sp + 2] = d; ++sp; }
                 f = cut;
@@ -393,7 +394,7 @@ __device__ void flush_small(uint64_t* a, SortLds<CAP>& S, int& ns) {
     const int lane = lane_id();
     if (ns == 0) return;
     lds_sync();
-    if (lane < ns) lane_introsort(a, S.small[3 * lane], S.small[3 * lane + 1], S.small[3 * lane + 2], S.lstk + 15 * lane);
+    if (lane < ns) lane_introsort(a, S.small[3 * lane], S.small[3 * lane + 1], S.small[3 * lane + 2], S.lstk + 9 * lane);
     lds_sync();
     ns = 0;
 }
@@ -557,6 +558,276 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair<CAP>
     }
     flush_leaves<false>(a, leaf, nleaf);
 }
+
+// ---- std::sort of one image's pixels by the NW waves of a workgroup (k_lsd_sort) ----
+// Introsort's recursion tree has independent subtrees: whichever wave partitions or finishes a
+// range, every element ends where libstdc++ puts it.  The waves share the pending ranges through
+// a LIFO queue in LDS (a lock word; the queue only holds range bounds, the elements stay in HBM):
+// a wave pops a range and walks its introsort_loop spine — while it is > CAP it partitions it in
+// HBM (its stoppers go to Lp / Rp at the range's own offset, so concurrent partitions never share
+// scratch) and pushes the right part; a range <= CAP is sorted in the wave's own LDS buffer; a
+// spent depth budget heap-sorts; leaves (<= 16) are collected for the per-leaf insertion sort.
+#ifndef LSD_SORT_WAVES
+#define LSD_SORT_WAVES 2
+#endif
+#ifndef LSD_SORT_CAP
+#define LSD_SORT_CAP 1024    // 2 waves x ~17 KB + the queue: four images' workgroups per CU
+#endif
+#define LSD_QCAP 192         // shared queue entries (a full queue spills to the wave's own stack)
+// __unguarded_partition_pivot(a + f, a + l) of a range in HBM by one wave, as Hoare's two scans
+// in rounds of up to BT stopper pairs: the left scan gathers the next BT left stoppers (key <=
+// pivot) in position order, the right scan the next BT right stoppers (key >= pivot) from the
+// right, both staged (position and element) in the wave's LDS sort buffer; the pairs with the
+// left stopper still left of its right partner swap (they are a prefix), and a full round moves
+// both scans past the swapped positions, which the next round never reads — every scan reads
+// elements as the serial algorithm leaves them, and no stopper list goes to HBM.  The cut is
+// partition_pivot's: min(next left stopper, last swapped right stopper).
+template <int CAP>
+__device__ int partition_hoare(uint64_t* a, int f, int l, SortLds<CAP>& S) {
+    constexpr int BT = CAP / 2, CH = 8;
+    const int lane = lane_id();
+    const int mid = f + (l - f) / 2;
+    const uint32_t ka = skey(a[f + 1]), kb = skey(a[mid]), kc = skey(a[l - 1]);
+    int sel;
+    if (ka > kb) sel = kb > kc ? mid : (ka > kc ? l - 1 : f + 1);
+    else sel = ka > kc ? f + 1 : (kb > kc ? l - 1 : mid);
+    const uint64_t pv = a[sel], old = a[f];
+    mem_sync();
+    if (lane == 0) {
+        a[sel] = old;
+        a[f] = pv;
+    }
+    mem_sync();
+    const uint32_t pk = skey(pv);
+    uint64_t* LV = S.buf;
+    uint64_t* RV = S.buf + BT;
+    uint32_t* LP = reinterpret_cast<uint32_t*>(S.lp);   // lp | rp: 4 CAP bytes = 2 BT positions
+    uint32_t* RP = LP + BT;
+    int lnext = f + 1, rnext = l - 1;   // next positions the scans read
+    int lbound = l, rbound = f;         // the left scan stays below lbound, the right one above rbound
+    for (;;) {
+        int nL = 0, nR = 0;
+        // both scans advance together: each step issues CH chunks per side before ranking either
+        for (int pl = lnext, pr = rnext;;) {
+            const bool gl = nL < BT && pl < lbound, gr = nR < BT && pr > rbound;   // (uniform)
+            if (!gl && !gr) break;
+            uint64_t vl[CH], vr[CH];
+            if (gl) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    const int pos = pl + 64 * c + lane;
+                    vl[c] = pos < lbound ? a[pos] : 0;
+                }
+            }
+            if (gr) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    const int pos = pr - 64 * c - lane;
+                    vr[c] = pos > rbound ? a[pos] : 0;
+                }
+            }
+            if (gl) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    const int pos = pl + 64 * c + lane;
+                    const bool st = pos < lbound && skey(vl[c]) <= pk;
+                    const unsigned long long m = __ballot(st);
+                    const int r = nL + below(m);
+                    if (st && r < BT) { LP[r] = (uint32_t)pos; LV[r] = vl[c]; }
+                    nL += __popcll(m);
+                }
+                pl += 64 * CH;
+            }
+            if (gr) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    const int pos = pr - 64 * c - lane;
+                    const bool st = pos > rbound && skey(vr[c]) >= pk;
+                    const unsigned long long m = __ballot(st);
+                    const int r = nR + below(m);
+                    if (st && r < BT) { RP[r] = (uint32_t)pos; RV[r] = vr[c]; }
+                    nR += __popcll(m);
+                }
+                pr -= 64 * CH;
+            }
+        }
+        nL = min(nL, BT);
+        nR = min(nR, BT);
+        lds_sync();
+        const int np = min(nL, nR);
+        int kb = 0;   // pairs with L[k] < R[k]: a prefix of the round's ranks
+        for (int k0 = 0; k0 < np; k0 += 64) {
+            const int k = k0 + lane;
+            kb += __popcll(__ballot(k < np && LP[k] < RP[k]));
+        }
+        for (int k = lane; k < kb; k += 64) {
+            a[LP[k]] = RV[k];
+            a[RP[k]] = LV[k];
+        }
+        if (kb == BT) {   // (both scans gathered BT stoppers, every pair swapped)
+            rbound = (int)LP[BT - 1];
+            lbound = (int)RP[BT - 1];
+            lnext = rbound + 1;
+            rnext = lbound - 1;
+            lds_sync();
+            continue;
+        }
+        // the scans have crossed: L[K] is the next left stopper if this round gathered it (else
+        // the left scan reached lbound: L[K] lies beyond the last swapped right stopper and is
+        // not the min)
+        const int cL = kb < nL ? (int)LP[kb] : INT_MAX;
+        const int cR = kb >= 1 ? (int)RP[kb - 1] : (lbound < l ? lbound : INT_MAX);
+        mem_sync();
+        return min(cL, cR);
+    }
+}
+
+template <int CAP, int NW>
+struct SortLdsMW {
+    SortLds<CAP> w[NW];
+    int leaf[NW][2 * 64];
+    int own[NW][3 * 40];     // per-wave overflow stack (depth budget <= 2 log2 n <= 40)
+    int lock, qn, busy;
+    int q[3 * LSD_QCAP];
+};
+
+__device__ __forceinline__ void q_lock(int* lk) {
+    int e = 0;
+    while (!__hip_atomic_compare_exchange_strong(lk, &e, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        e = 0;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ void q_unlock(int* lk) {
+    __hip_atomic_store(lk, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the queue counters are read outside the lock too: relaxed atomics (written under the lock)
+__device__ __forceinline__ int q_get(int* v) { return __hip_atomic_load(v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void q_set(int* v, int x) { __hip_atomic_store(v, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+template <int CAP, int NW>
+__device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsMW<CAP, NW>& M) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        M.lock = 0;
+        M.busy = 0;
+        M.qn = n > 1 ? 1 : 0;
+        M.q[0] = 0;
+        M.q[1] = n;
+        M.q[2] = n > 1 ? 2 * (31 - __clz(n)) : 0;
+    }
+    __syncthreads();
+    SortLds<CAP>& S = M.w[w];
+    int* leaf = M.leaf[w];
+    int* own = M.own[w];
+    int nleaf = 0, nown = 0;
+    int held = 0;   // this wave counts in M.busy (a popped range or its spilled parts are pending)
+#ifdef GFPL_LSD_PROBE
+    long long tp = 0, tl = 0, tf = 0, t0, tall = clock64(); int np = 0, nl = 0;
+#endif
+    for (;;) {
+        int f, l, d;
+        if (nown > 0) {
+            --nown;
+            f = own[3 * nown]; l = own[3 * nown + 1]; d = own[3 * nown + 2];
+        } else {
+            int st = 0;   // 1: a range, 2: every range is done, 0: wait for a push
+            int qf = 0, ql = 0, qd = 0;
+            // an idle wave peeks at the counters and takes the lock only when there is a range
+            // to pop or every wave may be done (idle waves polling under the lock starved the
+            // working waves' pushes)
+            if (lane == 0 && (held || q_get(&M.qn) > 0 || q_get(&M.busy) == 0)) {
+                q_lock(&M.lock);
+                int busy = q_get(&M.busy) - held;
+                const int qn = q_get(&M.qn);
+                if (qn > 0) {
+                    const int k = qn - 1;
+                    qf = M.q[3 * k]; ql = M.q[3 * k + 1]; qd = M.q[3 * k + 2];
+                    q_set(&M.qn, k);
+                    ++busy;
+                    st = 1;
+                } else if (busy == 0) {
+                    st = 2;
+                }
+                q_set(&M.busy, busy);
+                q_unlock(&M.lock);
+            }
+            st = __builtin_amdgcn_readfirstlane(st);
+            held = st == 1;
+            if (st == 2) break;
+            if (st == 0) {
+                __builtin_amdgcn_s_sleep(8);
+                continue;
+            }
+            f = __builtin_amdgcn_readfirstlane(qf);
+            l = __builtin_amdgcn_readfirstlane(ql);
+            d = __builtin_amdgcn_readfirstlane(qd);
+            mem_sync();   // acquire: the elements as the partitioning wave left them
+        }
+        for (;;) {    // one introsort_loop spine
+            const int m = l - f;
+            if (m <= 16) {
+                add_leaf<false>(a, leaf, nleaf, f, l);
+                break;
+            }
+            if (m <= CAP) {
+#pragma unroll 4
+                for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
+                lds_sync();
+#ifdef GFPL_LSD_PROBE
+                t0 = clock64(); ++nl;
+#endif
+                introsort_lds(S.buf, m, d, S);
+#ifdef GFPL_LSD_PROBE
+                tl += clock64() - t0;
+#endif
+                for (int i = lane; i < m; i += 64) a[f + i] = S.buf[i];
+                mem_sync();
+                break;
+            }
+            if (d == 0) {
+                if (lane == 0) heap_sort(a + f, m);
+                mem_sync();
+                break;
+            }
+            --d;
+            // (partition_pivot ends with a fence: its swaps are visible to the wave that pops [cut, l))
+#ifdef GFPL_LSD_PROBE
+            t0 = clock64(); ++np;
+#endif
+            const int cut = partition_hoare(a, f, l, S);
+#ifdef GFPL_LSD_PROBE
+            tp += clock64() - t0;
+#endif
+            if (l - cut > 16) {
+                int pushed = 0;
+                if (lane == 0) {
+                    q_lock(&M.lock);
+                    const int k = q_get(&M.qn);
+                    if (k < LSD_QCAP) {
+                        M.q[3 * k] = cut; M.q[3 * k + 1] = l; M.q[3 * k + 2] = d;
+                        q_set(&M.qn, k + 1);
+                        pushed = 1;
+                    }
+                    q_unlock(&M.lock);
+                }
+                if (!__builtin_amdgcn_readfirstlane(pushed)) {   // queue full: keep it on the own stack
+                    own[3 * nown] = cut; own[3 * nown + 1] = l; own[3 * nown + 2] = d;
+                    ++nown;
+                }
+            } else {
+                add_leaf<false>(a, leaf, nleaf, cut, l);
+            }
+            l = cut;
+        }
+    }
+    flush_leaves<false>(a, leaf, nleaf);
+#ifdef GFPL_LSD_PROBE
+    if (lane == 0 && (blockIdx.x & 255) == 0)
+        printf("MW img=%d w=%d all=%lld part=%lld(%d) lds=%lld(%d)\n", blockIdx.x, w, clock64() - tall, tp, np, tl, nl);
+#endif
+}
 }  // namespace
 
 // ------------------------------------------------------------------ ll_angle --
@@ -574,7 +845,7 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
         const size_t p = (size_t)img * W * H + (size_t)y * W + x;
         float a = -1.0f;
         uint32_t g = 0;
-        float2 cs = make_float2(0.f, 0.f);
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
         if (x < W - 1 && y < H - 1) {
             const int DA = (int)I[(size_t)(y + 1) * W + x + 1] - (int)I[(size_t)y * W + x];
             const int BC = (int)I[(size_t)y * W + x + 1] - (int)I[(size_t)(y + 1) * W + x];
@@ -589,6 +860,8 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
             }
         }
         o.px[p] = make_float4(a, cs.x, cs.y, __uint_as_float(g));
+        o.ang[p] = a;
+        if (a >= 0.0f) o.scs[p] = make_float2(cs.z, cs.w);
     }
     for (int off = 32; off; off >>= 1) {
         const unsigned long long t = __shfl_xor(b, off);
@@ -605,14 +878,15 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
 
 // S3 for every gradient an 8-bit image can give: the cos / sin of float(angle) depend on
 // (gx, gy) only, so the f64 fdlibm evaluations run once per detector, not per pixel
-__global__ void __launch_bounds__(256) k_lsd_cs_table(float2* tab) {
+__global__ void __launch_bounds__(256) k_lsd_cs_table(float4* tab) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= 1021 * 1021) return;
     const int gx = i / 1021 - 510, gy = i % 1021 - 510;
     const float a = fast_atan2((float)gx, (float)-gy);
     const double ad = (double)a * kDeg2Rad;
     const double af = (double)(float)ad;   // float(angle)
-    tab[i] = make_float2((float)det_cos(af), (float)det_sin(af));
+    // region_grow's seed sums: cos / sin of the double angle itself (no float rounding)
+    tab[i] = make_float4((float)det_cos(af), (float)det_sin(af), (float)det_cos(ad), (float)det_sin(ad));
 }
 
 __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
@@ -623,18 +897,45 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
     const int y = i / W1, x = i - y * W1;
     const double mg = __longlong_as_double((long long)o.maxg[img]);
     const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
-    const uint32_t g = __float_as_uint(o.px[(size_t)img * o.W * o.H + (size_t)y * o.W + x].w);
+    const float4* P = o.px + (size_t)img * o.W * o.H;
+    const float* A = o.ang + (size_t)img * o.W * o.H;
+    const float4 c = P[(size_t)y * o.W + x];
+    const uint32_t g = __float_as_uint(c.w);
     const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
     const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
     const int bin = (int)(norm * bin_coef);
-    o.keys[(size_t)img * o.NP + i] = ((uint64_t)(uint32_t)bin << 32) | ((uint32_t)y << 16) | (uint32_t)x;
+    // bit 31 (above y): a defined pixel none of whose 8 neighbours is defined and aligned with
+    // its angle — region_grow from it as a seed stops at the seed (isAligned against the seed's
+    // own angle, lsd.cpp), so k_lsd_grow only marks it used (a one-pixel region never reaches
+    // min_reg_size >= 2).  The sort compares bin only (skey), the payload bits ride along.
+    uint32_t iso = 0;
+    if (c.x >= 0.0f && o.min_reg_size > 1) {
+        const double ra = (double)c.x * kDeg2Rad;
+        bool any = false;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int xx = x + t % 3 - 1, yy = y + t / 3 - 1;
+            if (t == 4 || xx < 0 || yy < 0 || xx >= o.W || yy >= o.H) continue;
+            const float at = A[(size_t)yy * o.W + xx];
+            if (!(at >= 0.0f)) continue;
+            double nt = ra - (double)at * kDeg2Rad;
+            if (nt < 0) nt = -nt;
+            if (nt > k32Pi) {
+                nt -= k2Pi;
+                if (nt < 0) nt = -nt;
+            }
+            any = any || nt <= o.prec;
+        }
+        iso = any ? 0u : 1u;
+    }
+    o.keys[(size_t)img * o.NP + i] =
+        ((uint64_t)(uint32_t)bin << 32) | (iso << 31) | ((uint32_t)y << 16) | (uint32_t)x;
 }
 
-template <int CAP>
-__global__ void __launch_bounds__(64) k_lsd_sort(LsdDev o) {
-    __shared__ SortLdsPair<CAP> S;
-    const int img = blockIdx.x;
-    wave_sort(o.keys + (size_t)img * o.NP, o.NP, o.lpos + (size_t)img * o.NP, o.rpos + (size_t)img * o.NP, S);
+__global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(LSD_SORT_WAVES))) k_lsd_sort(LsdDev o) {
+    __shared__ SortLdsMW<LSD_SORT_CAP, LSD_SORT_WAVES> S;
+    const size_t img = blockIdx.x;
+    mw_sort(o.keys + img * o.NP, o.NP, o.lpos + img * o.NP, o.rpos + img * o.NP, S);
 }
 
 // ---------------------------------------------------------------- the regions --
@@ -682,22 +983,38 @@ __device__ __forceinline__ double modgrad(const Img& I, int x, int y) {
     return sqrt((double)(gx * gx + gy * gy) / 4.0);
 }
 
-// region_grow (lsd.cpp): returns the region size; reg / ring hold the points in push order
+// region_grow (lsd.cpp): returns the region size; the points in push order are in the LDS
+// ring and, once the region nears LSD_RING points (in_hbm), in the HBM list as well: a region
+// that stays small never stores to HBM (a store would hold up the next wait for a load, the
+// prefetch of the next seed's neighbourhood included); ring_to_hbm() completes the list for
+// the callers that read it (region2rect / refine), which fence before reading.
+// has_pre: lanes 0-24 of `pre` hold the records of the seed's 5x5 neighbourhood (lane
+// 5 (dy + 2) + dx + 2) and lane 25 of `pcs` its seed (cos, sin): the first two batches (the
+// seed and the pixels it adds) need no HBM round trip.  (seed_deg: the seed's angle record)
 template <bool LU>
-// (seed_deg: the seed's angle record; the caller fences before reading the list from HBM)
 __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, float seed_deg, double prec,
-                           double& reg_angle, bool has_pre = false, float4 pre = float4{}) {
+                           double& reg_angle, bool& in_hbm, bool has_pre = false, float4 pre = float4{},
+                           float2 pcs = float2{}) {
     const int lane = lane_id();
     int n = 0;
     reg_angle = (double)seed_deg * kDeg2Rad;
-    float sumdx = (float)det_cos(reg_angle), sumdy = (float)det_sin(reg_angle);   // S3
+    float sumdx, sumdy;   // S3
+    if (has_pre) {
+        sumdx = rl_f(pcs.x, 25);
+        sumdy = rl_f(pcs.y, 25);
+    } else {
+        sumdx = (float)det_cos(reg_angle);
+        sumdy = (float)det_sin(reg_angle);
+    }
     const uint32_t s = ((uint32_t)sy << 16) | (uint32_t)sx;
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    lds_u32* ring = (lds_u32*)(uintptr_t)(uint32_t)(uintptr_t)I.ring;
     if (lane == 0) {
-        I.reg[0] = s;
-        I.ring[0] = s;
+        ring[0] = s;
         U.set1(sx, sy);
     }
     n = 1;
+    bool glob = false;   // (uniform) new points go to the HBM list too
     U.sync();
     lds_sync();
     // the region list is expanded in batches of up to 7 points: lanes 9g..9g+8 load point
@@ -707,12 +1024,19 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
     const int dxl = t9 % 3 - 1, dyl = t9 / 3 - 1;
     for (int i = 0; i < n;) {
         const int nb = min(7, n - i);
-        if (n - i > LSD_RING) mem_sync();
         int rx = 0, ry = 0, xx = 0, yy = 0;
         bool ok = false;
+        uint32_t r = 0;
+        if (n - i > LSD_RING) {   // (uniform) the oldest points have left the ring
+            mem_sync();
+            if (g < nb) {
+                const int idx = i + g;
+                r = n - idx > LSD_RING ? I.reg[idx] : (uint32_t)ring[idx & (LSD_RING - 1)];
+            }
+        } else if (g < nb) {
+            r = ring[(i + g) & (LSD_RING - 1)];
+        }
         if (g < nb) {
-            const int idx = i + g;
-            const uint32_t r = (n - idx <= LSD_RING) ? I.ring[idx & (LSD_RING - 1)] : I.reg[idx];
             rx = (int)(r & 0xffff);
             ry = (int)(r >> 16);
             xx = rx + dxl;
@@ -720,8 +1044,20 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
             ok = xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
         }
         float4 q = make_float4(-1.0f, 0.f, 0.f, 0.f);
-        if (ok) q = (i == 0 && has_pre) ? pre : I.px[yy * I.W + xx];   // pre: the seed's 3x3, prefetched
+        bool inwin = false;
+        if (has_pre) {   // (uniform)
+            const int ox = xx - sx + 2, oy = yy - sy + 2;
+            inwin = ok && ox >= 0 && ox < 5 && oy >= 0 && oy < 5;
+            const int src = inwin ? 5 * oy + ox : 0;
+            const float4 w = make_float4(__shfl(pre.x, src), __shfl(pre.y, src), __shfl(pre.z, src), __shfl(pre.w, src));
+            if (inwin) q = w;
+        }
+        if (ok && !inwin) q = I.px[yy * I.W + xx];
         for (int k = 0; k < nb; ++k) {
+            if (!glob && n > LSD_RING - 16) {   // <= 9 points join per step: the ring has not wrapped
+                for (int e = lane; e < n; e += 64) I.reg[e] = ring[e];
+                glob = true;
+            }
             const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy);
             const unsigned long long m = __ballot(av) >> (9 * k);
             if (!m) continue;
@@ -744,8 +1080,8 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
                 const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
                 if (lane == 0) {
                     U.set1(px, py);
-                    I.reg[n] = e;
-                    I.ring[n & (LSD_RING - 1)] = e;
+                    if (glob) I.reg[n] = e;
+                    ring[n & (LSD_RING - 1)] = e;
                 }
                 ++n;
                 sumdx += rl_f(q.y, b + t);
@@ -757,7 +1093,14 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
         }
         i += nb;
     }
+    in_hbm = glob;
     return n;
+}
+
+// the region list of a region_grow that stayed in the ring, copied to HBM (caller fences)
+__device__ __forceinline__ void ring_to_hbm(const Img& I, int n, bool in_hbm) {
+    if (in_hbm) return;
+    for (int e = lane_id(); e < n; e += 64) I.reg[e] = I.ring[e];
 }
 
 // region2rect + get_theta (lsd.cpp), sums in list order
@@ -941,7 +1284,9 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
     U.sync();
     const double mean_angle = sum / (double)cnt;
     const double tau = 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / (double)cnt + mean_angle * mean_angle);
-    n = region_grow<LU>(I, U, sx, sy, I.px[sy * I.W + sx].x, tau, reg_angle);
+    bool in_hbm;
+    n = region_grow<LU>(I, U, sx, sy, I.px[sy * I.W + sx].x, tau, reg_angle, in_hbm);
+    ring_to_hbm(I, n, in_hbm);
     mem_sync();   // the region list (HBM) is read by every lane next
     if (n < 2) return false;
     region2rect(I, n, reg_angle, prec, rec);
@@ -969,40 +1314,58 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
     int nseg = 0;
     // software pipeline: chunk c+2's keys and chunk c+1's angles load while chunk c is processed
     uint64_t e1 = lane < o.NP ? keys[lane] : 0;
-    float a1 = lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+    float a1 = lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
     // (a candidate's angle record comes with the scan: a region's first round trip is its
     // seed's neighbourhood)
     uint64_t e2 = 64 + lane < o.NP ? keys[64 + lane] : 0;
     for (int base = 0; base < o.NP; base += 64) {
         const uint64_t e = e1;
-        int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0xffff);
+        int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0x7fff);
+        const bool iso = (e >> 31) & 1u;   // (k_lsd_keys)
         const float a0 = a1;
         e1 = e2;
-        a1 = base + 64 + lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0xffff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+        a1 = base + 64 + lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
         e2 = base + 128 + lane < o.NP ? keys[base + 128 + lane] : 0;
         bool cand = a0 >= 0.0f;
-        int pre_j = -1;   // the candidate whose 3x3 records `pre` holds (lanes 0-8)
+        int pre_j = -1;   // the candidate whose 5x5 records and seed (cos, sin) `pre` holds
         float4 pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
+        float2 pcs = make_float2(0.f, 0.f);
         for (;;) {
             const unsigned long long m = __ballot(cand && !U.get(px, py));
             if (!m) break;
-            const int j = __ffsll((long long)m) - 1;
+            // isolated seeds ahead of the next one that grows become used, in one step
+            const unsigned long long mg = m & __ballot(!iso);
+            const unsigned long long mi = mg ? m & ((mg & (0ull - mg)) - 1ull) : m;
+            if (mi) {
+                if ((mi >> lane) & 1ull) {
+                    U.set1(px, py);
+                    cand = false;
+                }
+                U.sync();
+            }
+            if (!mg) break;
+            const int j = __ffsll((long long)mg) - 1;
             if (lane <= j) cand = false;
             const int sx = rl_i(px, j), sy = rl_i(py, j);
             // the next candidate's neighbourhood loads while this region grows (records are
             // static; whether it is still a seed is decided from the used map later)
             const bool has_pre = pre_j == j;
             const float4 cur = pre;
-            const unsigned long long m2 = m & ~((2ull << j) - 1ull);
+            const float2 cur_cs = pcs;
+            const unsigned long long m2 = mg & ~((2ull << j) - 1ull);
             pre_j = m2 ? __ffsll((long long)m2) - 1 : -1;
             pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
-            if (pre_j >= 0 && lane < 9) {
-                const int xx = rl_i(px, pre_j) + lane % 3 - 1, yy = rl_i(py, pre_j) + lane / 3 - 1;
-                if (xx >= 0 && yy >= 0 && xx < o.W && yy < o.H) pre = I.px[yy * o.W + xx];
+            if (pre_j >= 0) {   // (separate registers: no wait for one load before the other)
+                const int cx = rl_i(px, pre_j), cy = rl_i(py, pre_j);
+                const int xx = cx + lane % 5 - 2, yy = cy + lane / 5 - 2;
+                if (lane < 25 && xx >= 0 && yy >= 0 && xx < o.W && yy < o.H) pre = I.px[yy * o.W + xx];
+                if (lane == 25) pcs = o.scs[off + (size_t)cy * o.W + cx];
             }
             double reg_angle;
-            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle, has_pre, cur);
+            bool in_hbm;
+            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle, in_hbm, has_pre, cur, cur_cs);
             if (n < o.min_reg_size) continue;
+            ring_to_hbm(I, n, in_hbm);
             mem_sync();   // the region list (HBM) is read by every lane next
             Rect rec;
             region2rect(I, n, reg_angle, o.prec, rec);
@@ -1033,9 +1396,9 @@ __global__ void __launch_bounds__(64) k_lsd_grow_glb(LsdDev o) {
 }
 
 // std::sort of one device array (test hook of the S2 restatement)
-__global__ void __launch_bounds__(64) k_lsd_sort_one(uint64_t* a, int n, int* lp, int* rp) {
-    __shared__ SortLdsPair<1024> S;
-    wave_sort(a, n, lp, rp, S);
+__global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(LSD_SORT_WAVES))) k_lsd_sort_one(uint64_t* a, int n, int* lp, int* rp) {
+    __shared__ SortLdsMW<LSD_SORT_CAP, LSD_SORT_WAVES> S;
+    mw_sort(a, n, lp, rp, S);
 }
 
 // ------------------------------------------------------------------ keylines --
@@ -1155,16 +1518,18 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     o->lds_used = (px + 31) / 32 * 4 <= LSD_USED_LDS_MAX;
     o->lds_bytes = (px + 31) / 32 * 4 + 4 * LSD_RING;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t b_tab = al(8 * 1021 * 1021), b_px = al(16 * M * px), b_max = al(8 * M),
+    const size_t b_tab = al(16 * 1021 * 1021), b_px = al(16 * M * px), b_scs = al(8 * M * px), b_ang = al(4 * M * px), b_max = al(8 * M),
                  b_keys = al(8 * M * NP), b_pos = al(4 * M * NP), b_reg = al(4 * M * px),
                  b_used = o->lds_used ? 0 : al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
                  b_klt = al(24 * M * SC), b_rk = al(8 * M * SC), b_rl = al(4 * M * SC);
-    const size_t total = b_tab + b_px + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
+    const size_t total = b_tab + b_px + b_scs + b_ang + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
                          b_klt + b_rk + 2 * b_rl + 256;
     if (hipMalloc(&o->base, total) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
-    d.cs_tab = (float2*)p; p += b_tab;
+    d.cs_tab = (float4*)p; p += b_tab;
     d.px = (float4*)p; p += b_px;
+    d.scs = (float2*)p; p += b_scs;
+    d.ang = (float*)p; p += b_ang;
     d.maxg = (unsigned long long*)p; p += b_max;
     d.keys = (uint64_t*)p; p += b_keys;
     d.lpos = (int*)p; p += b_pos;
@@ -1200,7 +1565,7 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
 extern "C" int gfpl_lsd_sort_desc(gfpl_lsd* o, uint64_t* a, int n) {
     if (!o || !a || n < 0 || n > o->d.NP) return GFPL_E_INVALID;
     if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
-    hipLaunchKernelGGL(k_lsd_sort_one, dim3(1), dim3(64), 0, o->stream, a, n, o->d.lpos, o->d.rpos);
+    hipLaunchKernelGGL(k_lsd_sort_one, dim3(1), dim3(64 * LSD_SORT_WAVES), 0, o->stream, a, n, o->d.lpos, o->d.rpos);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
     return hipStreamSynchronize(o->stream) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
 }
@@ -1224,12 +1589,7 @@ extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, 
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.NP + 255) / 256, n), dim3(256), 0, s, d);
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o->device);
-    if (n > 4 * cus)
-        hipLaunchKernelGGL(k_lsd_sort<1024>, dim3(n), dim3(64), 0, s, d);
-    else
-        hipLaunchKernelGGL(k_lsd_sort<2048>, dim3(n), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
     if (o->lds_used)
         hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
     else
