@@ -238,6 +238,48 @@ __device__ double stdv_mad(double* buf, int n, int NP2) {
     return 1.4826 * mad;
 }
 
+// k-th smallest (0-based) of the unsigned keys a wave holds in registers (lane l, slot r:
+// list position l + 64 r; slots past the list hold all-ones keys, never selected since
+// k < n).  The answer is built bit by bit from the top: the largest P with
+// #{x < P} <= k is the k-th smallest key, and each bit costs one compare per slot (the
+// compare mask is the ballot) and a scalar popcount — no sort.  For non-negative doubles
+// (floats) the bit patterns order like the values, so this is the element
+// std::sort(...)[k] leaves at k (vector_stdv_mad, src/auxiliar.cpp:521-537); residuals
+// sqrt(.) * sqrt(sigma2) and fabsf(.) are never -0.0.
+template <typename K, int R>
+__device__ __forceinline__ K wave_select(const K* key, int n, int k) {
+    K P = 0;
+    for (int b = 8 * (int)sizeof(K) - 1; b >= 0; --b) {
+        const K T = P | ((K)1 << b);
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r * 64 < n) c += __popcll(__ballot(key[r] < T));
+        if (c <= k) P = T;
+    }
+    return P;
+}
+
+// vector_stdv_mad of n <= 64 R residuals held in registers (r[slot] = list position
+// lane + 64 slot): the median, then the median of (double)fabsf((float)(x - median))
+template <int R>
+__device__ __forceinline__ double stdv_mad_regs(const double* r, int n) {
+    if (n == 0) return 0.0;   // uniform
+    const int lane = threadIdx.x;
+    uint64_t k64[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+        k64[s] = (lane + 64 * s < n) ? (uint64_t)__double_as_longlong(r[s]) : ~0ull;
+    const double median = __longlong_as_double((long long)wave_select<uint64_t, R>(k64, n, n / 2));
+    uint32_t k32[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+        k32[s] = (lane + 64 * s < n) ? __float_as_uint(fabsf((float)(r[s] - median))) : ~0u;
+    const double mad = (double)__uint_as_float(wave_select<uint32_t, R>(k32, n, n / 2));
+    return 1.4826 * mad;
+}
+#define POSE_MAD_R 8   // residuals per lane held in registers (lists of up to 512 entries)
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -337,23 +379,48 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
                 const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
                 return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
             };
-            // the MAD sorts run in the GN chunk region (buf aliases it); the flag pass
-            // re-evaluates each residual (same operands, same bits) instead of keeping
-            // 800 residuals in LDS, which keeps the workgroup at ~10 KB of LDS
-            __syncthreads();
-            for (int k = lane; k < npt; k += 64) buf[k] = res_p(k);
-            __syncthreads();
-            const double th_p = p.cfg.inlier_k * stdv_mad(buf, npt, NP2);
-            for (int k = lane; k < nls; k += 64) buf[k] = res_l(k);
-            __syncthreads();
-            const double th_l = p.cfg.inlier_k * stdv_mad(buf, nls, NP2);
-            // duplicates of one prev point share P, pl_obs and sigma2, hence the residual:
-            // flagging per list position equals the reference's per-feature flag
+            // Lists of up to 512 entries keep their residuals in registers and take both
+            // medians by wave_select (no sort); longer lists sort in the GN chunk region (buf
+            // aliases it) and the flag pass re-evaluates each residual (same operands, same
+            // bits).  Duplicates of one prev point share P, pl_obs and sigma2, hence the
+            // residual: flagging per list position equals the reference's per-feature flag.
             int op = 0, ol = 0;
-            for (int k = lane; k < npt; k += 64)
-                if (res_p(k) > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
-            for (int k = lane; k < nls; k += 64)
-                if (res_l(k) > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+            __syncthreads();
+            if (npt <= 64 * POSE_MAD_R) {
+                double r[POSE_MAD_R];
+#pragma unroll
+                for (int s = 0; s < POSE_MAD_R; ++s) r[s] = (lane + 64 * s < npt) ? res_p(lane + 64 * s) : 0.0;
+                const double th_p = p.cfg.inlier_k * stdv_mad_regs<POSE_MAD_R>(r, npt);
+#pragma unroll
+                for (int s = 0; s < POSE_MAD_R; ++s) {
+                    const int k = lane + 64 * s;
+                    if (k < npt && r[s] > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
+                }
+            } else {
+                for (int k = lane; k < npt; k += 64) buf[k] = res_p(k);
+                __syncthreads();
+                const double th_p = p.cfg.inlier_k * stdv_mad(buf, npt, NP2);
+                for (int k = lane; k < npt; k += 64)
+                    if (res_p(k) > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
+            }
+            __syncthreads();
+            if (nls <= 64 * POSE_MAD_R) {
+                double r[POSE_MAD_R];
+#pragma unroll
+                for (int s = 0; s < POSE_MAD_R; ++s) r[s] = (lane + 64 * s < nls) ? res_l(lane + 64 * s) : 0.0;
+                const double th_l = p.cfg.inlier_k * stdv_mad_regs<POSE_MAD_R>(r, nls);
+#pragma unroll
+                for (int s = 0; s < POSE_MAD_R; ++s) {
+                    const int k = lane + 64 * s;
+                    if (k < nls && r[s] > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+                }
+            } else {
+                for (int k = lane; k < nls; k += 64) buf[k] = res_l(k);
+                __syncthreads();
+                const double th_l = p.cfg.inlier_k * stdv_mad(buf, nls, NP2);
+                for (int k = lane; k < nls; k += 64)
+                    if (res_l(k) > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+            }
             op = wave_sum(op);
             ol = wave_sum(ol);
             // active counts for stage 2

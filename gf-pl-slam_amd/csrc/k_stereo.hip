@@ -446,7 +446,11 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             // lexicographic (dist, iR) minimum as one packed key (iR < 2^16 on this layout);
             // the start value keeps bestDist = 100 (no candidate below it: no match)
             uint32_t best = (100u << 16) | 0xFFFFu;
+#ifdef GFPL_PROBE_SP_NOSCAN
+            for (int o = 0; o < 0; ++o) {
+#else
             for (int o = 0; o <= nlev; ++o) {   // wave-uniform
+#endif
                 const bool need = act && (o < nlev ? ((long long)o >= (long long)levelL - 1 &&
                                                       (long long)o <= (long long)levelL + 1)
                                                    : rowlo[(nlev + 1) * NBIN] > rowlo[nlev * NBIN]);
@@ -532,6 +536,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     }
     __syncthreads();
+#ifdef GFPL_PROBE_SP_SCANONLY
+    if (N > 0) return;
+#endif
     // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
     // per matched keypoint, BLOCK/4 consecutive (row-ordered) keypoints per pass
     for (int base = 0; base < N; base += BLOCK / 4) {

@@ -497,6 +497,18 @@ def test_line_cut_ill_conditioned_s_parity():
         _check(rep)
 
 
+def test_pose_long_match_lists_parity():
+    """Matched lists above 512 entries (the gazebo budget maxPointMatchNum = 1000,
+    src/config.cpp:89; 600 lines) take k_pose's sorted-MAD path (residuals in LDS),
+    lists of up to 512 the register selection (wave_select) — both must give the oracle's
+    std::sort medians, hence the same outlier flags and poses."""
+    rep = _run_sequence("vga", dict(max_point_match_num=1000, max_line_match_num=600),
+                        n_seq=2, n_frames=4, kp_cap=2048, kl_cap=1024,
+                        synth_over=dict(n_kp=2000, n_kl=1000, n_world_pts=2600, n_world_lines=1300), seed=43)
+    _check(rep)
+    assert max(c[2] for c in rep["counts"]) > 512 and max(c[3] for c in rep["counts"]) > 512, rep["counts"]
+
+
 def test_match_budget_raise_after_seqbatch_refused():
     """A seqbatch sizes matched_pt / matched_ls and the cut / pose scratch from the
     config's budgets at creation: a larger budget while it lives is refused
