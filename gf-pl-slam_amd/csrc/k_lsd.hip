@@ -723,9 +723,6 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
     int* own = M.own[w];
     int nleaf = 0, nown = 0;
     int held = 0;   // this wave counts in M.busy (a popped range or its spilled parts are pending)
-#ifdef GFPL_LSD_PROBE
-    long long tp = 0, tl = 0, tf = 0, t0, tall = clock64(); int np = 0, nl = 0;
-#endif
     for (;;) {
         int f, l, d;
         if (nown > 0) {
@@ -775,13 +772,7 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
 #pragma unroll 4
                 for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
                 lds_sync();
-#ifdef GFPL_LSD_PROBE
-                t0 = clock64(); ++nl;
-#endif
                 introsort_lds(S.buf, m, d, S);
-#ifdef GFPL_LSD_PROBE
-                tl += clock64() - t0;
-#endif
                 for (int i = lane; i < m; i += 64) a[f + i] = S.buf[i];
                 mem_sync();
                 break;
@@ -793,13 +784,7 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
             }
             --d;
             // (partition_pivot ends with a fence: its swaps are visible to the wave that pops [cut, l))
-#ifdef GFPL_LSD_PROBE
-            t0 = clock64(); ++np;
-#endif
             const int cut = partition_hoare(a, f, l, S);
-#ifdef GFPL_LSD_PROBE
-            tp += clock64() - t0;
-#endif
             if (l - cut > 16) {
                 int pushed = 0;
                 if (lane == 0) {
@@ -823,10 +808,6 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
         }
     }
     flush_leaves<false>(a, leaf, nleaf);
-#ifdef GFPL_LSD_PROBE
-    if (lane == 0 && (blockIdx.x & 255) == 0)
-        printf("MW img=%d w=%d all=%lld part=%lld(%d) lds=%lld(%d)\n", blockIdx.x, w, clock64() - tall, tp, np, tl, nl);
-#endif
 }
 }  // namespace
 
@@ -889,46 +870,76 @@ __global__ void __launch_bounds__(256) k_lsd_cs_table(float4* tab) {
     tab[i] = make_float4((float)det_cos(af), (float)det_sin(af), (float)det_cos(ad), (float)det_sin(ad));
 }
 
-__global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o) {
-    const int img = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= o.NP) return;
-    const int W1 = o.W - 1;
-    const int y = i / W1, x = i - y * W1;
+// one wave per 64 pixels of a row (4 rows per workgroup, no index division); the gradient
+// is recomputed from the image bytes (S1: the same integers, hence the same norm and bin as
+// k_lsd_grad) instead of read back from the 16-B records, and the angle comes from `ang`
+__global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o, const uint8_t* images) {
+    const int img = blockIdx.z;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int W = o.W, H = o.H, W1 = W - 1;
+    if (x >= W1 || y >= H - 1) return;
+    const uint8_t* I = images + (size_t)img * W * H + (size_t)y * W + x;
+    const int DA = (int)I[W + 1] - (int)I[0];
+    const int BC = (int)I[1] - (int)I[W];
+    const int gx = DA + BC, gy = DA - BC;
     const double mg = __longlong_as_double((long long)o.maxg[img]);
     const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
-    const float4* P = o.px + (size_t)img * o.W * o.H;
-    const float* A = o.ang + (size_t)img * o.W * o.H;
-    const float4 c = P[(size_t)y * o.W + x];
-    const uint32_t g = __float_as_uint(c.w);
-    const int gx = (int16_t)(g & 0xffff), gy = (int16_t)(g >> 16);
     const double norm = sqrt((double)(gx * gx + gy * gy) / 4.0);
     const int bin = (int)(norm * bin_coef);
+    const float* A = o.ang + (size_t)img * W * H;
+    const float ac = A[(size_t)y * W + x];
     // bit 31 (above y): a defined pixel none of whose 8 neighbours is defined and aligned with
     // its angle — region_grow from it as a seed stops at the seed (isAligned against the seed's
     // own angle, lsd.cpp), so k_lsd_grow only marks it used (a one-pixel region never reaches
     // min_reg_size >= 2).  The sort compares bin only (skey), the payload bits ride along.
+    // The 8 tests run unconditionally (clamped reads, selects): no per-neighbour branches.
+    // Each test is taken in float degrees first (|ac - at| wrapped past 270 against the
+    // threshold prec in degrees, both within 1e-4 degrees of the double quantities); only a
+    // lane with a difference within 1e-3 degrees of the threshold repeats its tests in double
+    // as isAligned does.  The 8 tests run unconditionally (clamped reads, selects).
     uint32_t iso = 0;
-    if (c.x >= 0.0f && o.min_reg_size > 1) {
-        const double ra = (double)c.x * kDeg2Rad;
-        bool any = false;
+    if (__any(ac >= 0.0f) && o.min_reg_size > 1) {
+        const float pdeg = (float)(o.prec / kDeg2Rad);
+        float at[8];
+        bool ok[8];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
+        for (int t = 0, k = 0; t < 9; ++t) {
+            if (t == 4) continue;
             const int xx = x + t % 3 - 1, yy = y + t / 3 - 1;
-            if (t == 4 || xx < 0 || yy < 0 || xx >= o.W || yy >= o.H) continue;
-            const float at = A[(size_t)yy * o.W + xx];
-            if (!(at >= 0.0f)) continue;
-            double nt = ra - (double)at * kDeg2Rad;
-            if (nt < 0) nt = -nt;
-            if (nt > k32Pi) {
-                nt -= k2Pi;
-                if (nt < 0) nt = -nt;
-            }
-            any = any || nt <= o.prec;
+            ok[k] = xx >= 0 && yy >= 0 && xx < W && yy < H;
+            at[k] = A[(size_t)min(max(yy, 0), H - 1) * W + min(max(xx, 0), W - 1)];
+            ++k;
         }
-        iso = any ? 0u : 1u;
+        // (the float wrap at 270 may differ from the double one at 3 pi / 2 only where both
+        // 270 and 90 degrees are unaligned: thresholds of 80 degrees and more take the double tests)
+        const bool fast = pdeg < 80.0f;
+        bool any = false, amb = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool v = ok[k] && at[k] >= 0.0f;
+            float d = fabsf(ac - at[k]);
+            d = d > 270.0f ? fabsf(d - 360.0f) : d;
+            any = any || (fast && v && d < pdeg - 1e-3f);
+            amb = amb || (v && (!fast || fabsf(d - pdeg) <= 1e-3f));
+        }
+        if (__any(amb && !any && ac >= 0.0f)) {
+            if (amb && !any) {
+                const double ra = (double)ac * kDeg2Rad;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    double nt = ra - (double)at[k] * kDeg2Rad;
+                    if (nt < 0) nt = -nt;
+                    double nw = nt - k2Pi;
+                    if (nw < 0) nw = -nw;
+                    nt = (nt > k32Pi) ? nw : nt;
+                    any = any || (ok[k] && at[k] >= 0.0f && nt <= o.prec);
+                }
+            }
+        }
+        iso = (ac >= 0.0f && !any) ? 1u : 0u;
     }
-    o.keys[(size_t)img * o.NP + i] =
+    o.keys[(size_t)img * o.NP + (size_t)y * W1 + x] =
         ((uint64_t)(uint32_t)bin << 32) | (iso << 31) | ((uint32_t)y << 16) | (uint32_t)x;
 }
 
@@ -1588,7 +1599,7 @@ extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, 
     if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess) return GFPL_E_HIP;
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
-    hipLaunchKernelGGL(k_lsd_keys, dim3((d.NP + 255) / 256, n), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_keys, dim3((d.W - 1 + 63) / 64, (d.H - 1 + 3) / 4, n), dim3(256), 0, s, d, images);
     hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
     if (o->lds_used)
         hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);

@@ -139,19 +139,19 @@ __device__ __forceinline__ uint32_t dup16(const uint32_t* w, int c) {
 // formed once for every column c and the left pairs once; per shift only the left pairs
 // take cR_s (the centre pixels cR_s are shared by the lane's rows).
 __device__ __forceinline__ void sad_rows(const SadJob& J, int q, uint32_t* acc) {
-    uint32_t irc[6];
-    int cL;
-    {
-        uint32_t il4[3];
-        sad_load_row(J, J.vL, il4, irc);
-        cL = byte_at(il4, 5);
-    }
     uint32_t il4[3][3], ir6[3][6];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int r = q + 4 * i;
         sad_load_row(J, J.vL - 5 + (r < 11 ? r : 5), il4[i], ir6[i]);
     }
+    // the centre row (window row 5) is lane 1's second row: its centre pixels cL (IL byte 5)
+    // and cR_s (IR bytes 5..15, words 1-3) reach the quad by DPP quad_perm(1,1,1,1)
+    uint32_t irc[4];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) irc[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)ir6[1][k], 0x55, 0xF, 0xF, false);
+    irc[0] = 0u;
+    const int cL = (int)(((uint32_t)__builtin_amdgcn_mov_dpp((int)il4[1][1], 0x55, 0xF, 0xF, false) >> 8) & 0xFFu);
     const uint32_t cLL = (uint32_t)cL * 0x10001u;
     uint32_t cRR[11];
 #pragma unroll
@@ -446,17 +446,16 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             // lexicographic (dist, iR) minimum as one packed key (iR < 2^16 on this layout);
             // the start value keeps bestDist = 100 (no candidate below it: no match)
             uint32_t best = (100u << 16) | 0xFFFFu;
-#ifdef GFPL_PROBE_SP_NOSCAN
-            for (int o = 0; o < 0; ++o) {
-#else
             for (int o = 0; o <= nlev; ++o) {   // wave-uniform
-#endif
                 const bool need = act && (o < nlev ? ((long long)o >= (long long)levelL - 1 &&
                                                       (long long)o <= (long long)levelL + 1)
                                                    : rowlo[(nlev + 1) * NBIN] > rowlo[nlev * NBIN]);
                 if (!__any(need)) continue;
-                int j = need ? seg_start(o, row) : 0x7FFFFFFF;
-                bool more = need && j < Nr;
+                // candidates of segment o with minr in [row - D_o, row]: from the bin of row - D_o to
+                // the bin of row + 1 (the counting sort's offsets), so the walk needs no stop test
+                int j = need ? seg_start(o, row) : 0;
+                const int jend = need ? (int)rowlo[o * NBIN + row + 1 + SP_MINR_PAD] : 0;
+                bool more = j < jend;
                 while (__any(more)) {
                     int c0 = more ? j : 0x7FFFFFFF;
 #pragma unroll
@@ -469,28 +468,25 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                         }
                     }
                     wave_lds_sync();
-                    const int cend = min(c0 + SP_CHUNK, Nr);
-                    while (more && j < cend) {
-                        // every LDS read of the entry issued together (the stop test is folded into
-                        // `pass`, not a branch ahead of the reads): one round trip per candidate
+                    const int jl = min(c0 + SP_CHUNK, jend);
+                    for (; j < jl; ++j) {
+                        // every LDS read of the entry issued together: one round trip per candidate
                         const uint32_t k = rkey[j];
                         const uint32_t m = recm[j];
                         const float uR = recx[j];
                         const u32x4 a = wst[2 * (j - c0)], c = wst[2 * (j - c0) + 1];
                         const int minr = (int)((k >> 16) & 0xFFFu) - 1024;
-                        const bool stop = (k >> 28) != (uint32_t)o || minr > row;
                         const int iR = (int)(k & 0xFFFFu);
                         int octR = (int)(int8_t)(uint8_t)(m & 0xFFu);
-                        if (octR == -128 && !stop) octR = KR[iR].octave;
+                        if (octR == -128) octR = KR[iR].octave;
                         const uint32_t dr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
                         const uint32_t key = ((uint32_t)hamming8<1>(dl, dr) << 16) | (uint32_t)iR;
-                        const bool pass = !stop && minr + (int)(m >> 8) >= row &&   // maxr >= row
-                                          octR >= levelL - 1 && octR <= levelL + 1 && uR >= minU && uR <= maxU;
-                        best = (pass && key < best) ? key : best;
-                        if (stop) { more = false; break; }
-                        ++j;
+                        // the tests as one mask and the minimum as a select: no branch around the distance
+                        const bool pass = (minr + (int)(m >> 8) >= row) &   // maxr >= row
+                                          (octR >= levelL - 1) & (octR <= levelL + 1) & (uR >= minU) & (uR <= maxU);
+                        best = min(best, pass ? key : 0xFFFFFFFFu);
                     }
-                    if (j >= Nr) more = false;
+                    more = j < jend;
                     wave_lds_sync();   // the chunk is read before the next one overwrites it
                 }
             }
@@ -536,9 +532,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     }
     __syncthreads();
-#ifdef GFPL_PROBE_SP_SCANONLY
-    if (N > 0) return;
-#endif
     // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
     // per matched keypoint, BLOCK/4 consecutive (row-ordered) keypoints per pass
     for (int base = 0; base < N; base += BLOCK / 4) {
