@@ -532,11 +532,68 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     }
     __syncthreads();
+    // SEG: the SAD jobs counting-sorted by the tile of their window — (level, 8-row band,
+    // 64-px column strip), coarser on large images so the tiles fit 4096 bins — so the 16 quads
+    // of a wave read overlapping window rows (one cache line serves several lanes) instead of
+    // 16 windows spread across the image width.  Each job refines its own keypoint: the order
+    // has no effect on the output.
+    const uint32_t* jobs = order;
+    int njobs = N;
+    if (SEG) {
+        uint32_t* sj = rkey;                 // sorted jobs (rkey is dead after the band scan)
+        uint32_t* hb = stg;                  // u16 tile counts, two per word (the stage buffers are dead)
+        int ty = 3, tx = 6;
+        auto nbins = [&](int a, int c) {
+            return nlev * (((p.cam.lvl_rows[0] - 1) >> a) + 1) * (((p.cam.lvl_cols[0] - 1) >> c) + 1);
+        };
+        while (nbins(ty, tx) > 4094) { if (ty + 3 <= tx) ++ty; else ++tx; }   // (nb + 2) / 2 words <= 2048
+        const int TY = ((p.cam.lvl_rows[0] - 1) >> ty) + 1, TX = ((p.cam.lvl_cols[0] - 1) >> tx) + 1;
+        const int nb = nlev * TY * TX;
+        for (int w = tid; w < (nb + 2) / 2; w += BLOCK) hb[w] = 0u;
+        __syncthreads();
+        constexpr int RMAX = 2048 / BLOCK;
+        uint32_t jb[RMAX], jr[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const int i = tid + r * BLOCK;
+            jb[r] = 0xFFFFFFFFu;
+            jr[r] = 0u;
+            if (i < N) {
+                const uint32_t job = order[i];
+                if (job != 0xFFFFFFFFu) {
+                    const uint32_t pr = pairs[job & 0xFFFFu];
+                    const int o = (int)((pr >> 7) & 7u), vL = (int)((pr >> 10) & 0x7FFu), uL = (int)(job >> 16);
+                    const int bin = (o * TY + min(vL >> ty, TY - 1)) * TX + min(uL >> tx, TX - 1);
+                    const uint32_t sh = 16u * (uint32_t)(bin & 1);
+                    const uint32_t old = atomicAdd(&hb[bin >> 1], 1u << sh);
+                    jb[r] = job;
+                    jr[r] = (uint32_t)bin | (((old >> sh) & 0xFFFFu) << 16);
+                }
+            }
+        }
+        __syncthreads();
+        uint16_t* off = reinterpret_cast<uint16_t*>(hb);
+        {
+            const int per = (nb + BLOCK - 1) / BLOCK, b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+            int sum = 0;
+            for (int x = b0; x < b1; ++x) sum += off[x];
+            int tot;
+            int run = block_exclusive_scan<BLOCK>(sum, misc + 4, &tot);
+            for (int x = b0; x < b1; ++x) { const int c = off[x]; off[x] = (uint16_t)run; run += c; }
+            njobs = tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            if (jb[r] != 0xFFFFFFFFu) sj[(int)off[jr[r] & 0xFFFFu] + (int)(jr[r] >> 16)] = jb[r];
+        __syncthreads();
+        jobs = sj;
+    }
     // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
-    // per matched keypoint, BLOCK/4 consecutive (row-ordered) keypoints per pass
-    for (int base = 0; base < N; base += BLOCK / 4) {
+    // per matched keypoint, BLOCK/4 consecutive (tile- or row-ordered) keypoints per pass
+    for (int base = 0; base < njobs; base += BLOCK / 4) {
         const int t = base + (tid >> 2), q = tid & 3;
-        const uint32_t job = (t < N) ? order[t] : 0xFFFFFFFFu;
+        const uint32_t job = (t < njobs) ? jobs[t] : 0xFFFFFFFFu;
         uint32_t acc[11];
 #pragma unroll
         for (int s = 0; s < 11; ++s) acc[s] = 0;
