@@ -374,8 +374,10 @@ GFPL_DEV double logdet6_lower(double* a /* 21, destroyed */) {
 template <typename T>
 GFPL_DEV void swap_v(T& a, T& b) { T t = a; a = b; b = t; }
 
-// LDLT solve, Eigen 3.3 semantics (see oracle ldlt_solve6)
-GFPL_DEV void ldlt_solve6(const double* H, const double* g, double* x) {
+// LDLT solve, Eigen 3.3 semantics (see oracle ldlt_solve6).  ONE LANE only (k_pose's lane 0):
+// each pivot index is made wave-uniform (readfirstlane), so a pivot swap is one scalar branch
+// to the block of moves for that index instead of selects over every candidate index.
+GFPL_DEV void ldlt_solve6_one_lane(const double* H, const double* g, double* x) {
     double m[36];
 #pragma unroll
     for (int i = 0; i < 36; ++i) m[i] = H[i];
@@ -392,6 +394,7 @@ GFPL_DEV void ldlt_solve6(const double* H, const double* g, double* x) {
             const double v = fabs(m[i * 7]);
             if (v > bv) { bv = v; big = i; }
         }
+        big = __builtin_amdgcn_readfirstlane(big);
         tr[k] = big;
 #pragma unroll
         for (int c = k + 1; c < 6; ++c) {

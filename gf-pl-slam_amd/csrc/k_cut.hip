@@ -437,7 +437,8 @@ struct CutCmp {
     double ns[5], ne[5];     // |W_s(t)|^2, |W_e(t)|^2
     double vs[5], ve[5];     // v'_s, v'_e
     double cc[9];            // C(t0, t1): cc[3 i + k] multiplies t0^i t1^k
-    double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2)
+    double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2); line open only
+    double bnd[3];           // the line's bound terms at |t| = T = max(|rlo|, |rhi|): P1, VsA, VeA
 };
 
 // d at (t0, t1), NaN when not healthy; bound_ok: the forward rounding-error bound of
@@ -445,13 +446,12 @@ struct CutCmp {
 //   40u [(Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2] / D + 16u (VsA / v's + VeA / v'e) + 4u,
 // where Bs^2 bounds the absolute terms of Ns and of the Gram entries behind it, Bs Be
 // those of C, VsA those of v's (Horner with absolute coefficients at |t|).
-__device__ __forceinline__ double cut_dcore(double Ns, double Vs, double Ne, double Ve, double C, double Bs, double Be,
-                                           double VsA, double VeA, double tau, int& bound_ok) {
+// with P1 = (Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2 given
+__device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, double Ve, double C, double P1,
+                                              double VsA, double VeA, double tau, int& bound_ok) {
     const double D = __builtin_fma(Vs + Ns, Ve + Ne, -(C * C));
     const double den = Vs * Ve;
     const double d = D * rcp_fast(den);
-    const double Bs2 = Bs * Bs, Be2 = Be * Be;
-    const double P1 = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
     const double P2 = __builtin_fma(VsA, Ve, VeA * Vs);
     constexpr double u = 0x1p-53;
     const double Dd = D * den;
@@ -459,14 +459,14 @@ __device__ __forceinline__ double cut_dcore(double Ns, double Vs, double Ne, dou
     bound_ok = healthy && __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= (0.25 * tau - 4.0 * u) * Dd;
     return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
+// Bs, Be, VsA, VeA are Horner sums of non-negative terms in |t|, increasing in |t|: their values at
+// T = max(|rlo|, |rhi|) bound them for every valid neighbour (|t0|, |t1| <= T), so the line's P1,
+// VsA, VeA (cmp.bnd, formed when it opens) replace the four per-neighbour evaluations
 __device__ __forceinline__ double cut_dval(const CutCmp& c, double t0, double t1, double tau, int& bound_ok) {
     const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
     const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
                                    h2(c.cc[0], c.cc[3], c.cc[6], t0));
-    const double a0 = fabs(t0), a1 = fabs(t1);
-    const double Bs = h2(c.bs[0], c.bs[1], c.bs[2], a0), Be = h2(c.be[0], c.be[1], c.be[2], a1);
-    const double VsA = h4abs(c.vs, a0), VeA = h4abs(c.ve, a1);
-    return cut_dcore(Ns, Vs, Ne, Ve, C, Bs, Be, VsA, VeA, tau, bound_ok);
+    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], tau, bound_ok);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -746,9 +746,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
         }
         wave_lds_sync();
+        // the line's bound terms at T (lane 7; see cut_dval)
+        if (j == 7) {
+            const double T = fmax(fabs(rlo), fabs(rhi));
+            const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
+            const double VsA = h4abs(cl + 10, T), VeA = h4abs(cl + 15, T);
+            const double Bs2 = Bs * Bs, Be2 = Be * Be;
+            cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+            cl[36] = VsA;
+            cl[37] = VeA;
+        }
+        wave_lds_sync();
         // the centre of the first step: d at (0, 0)
         const double vs0 = cl[10], ve0 = cl[15];
-        dc = cut_dcore(cl[0], vs0, cl[5], ve0, cl[20], cl[29], cl[32], fabs(vs0), fabs(ve0), tau, c_ok);
+        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], tau, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (576 B) from HBM straight into LDS (global_load_lds, no registers); it is

@@ -14,8 +14,10 @@
 //    each add one of the 28 reduction entries (21 H + 6 g + 1 e) over the chunk
 //    in list order — the reference's accumulation order, so H is bit-identical
 //    (a zero row adds +0.0, which leaves a sum that started at +0.0 unchanged);
-//  * lane 0 solves the 6x6 LDLT, applies the SE(3) update and tests convergence.
-// The outlier pass sorts residuals in LDS (bitonic) for the MAD medians.
+//  * lane 0 solves the 6x6 LDLT and tests convergence; the wave applies the SE(3)
+//    update element-parallel (se3_update_wave).
+// The outlier pass takes the MAD medians by bitwise selection over register-held
+// residuals (wave_select; lists above 512 entries sort in LDS).
 #include "gfpl_kernels.hpp"
 
 namespace gfpl {
@@ -25,11 +27,75 @@ struct PoseLDS {
     double DTini[16];
     double H[36];
     double part[64];
+    double inc[6];    // the GN increment (lane 0's LDLT solve)
+    double X[48];     // se3_update_wave scratch: expmap | s, V | inverse
     int brk;
+    int upd;          // apply inc to DT (the error test did not stop the loop)
     int ninl;
     int cnt[2];
     double err;
 };
+
+// DT <- DT * inverse_se3(expmap_se3(inc)) (gaussNewtonOptimization, src/stereoFrameHandler.cpp:
+// 2046-2050) by the wave, element-parallel: every element is formed by the expression the serial
+// helpers use for it (expmap_se3, inverse_se3, mat4_mul in gfpl_device.hpp), so the bits are
+// theirs; theta, sin and cos are computed identically by every lane.  inc, DT, X in LDS.
+// Out of line: inlined into the GN loop it raised k_pose to 172 VGPRs (2 waves / SIMD, 6.31 ms);
+// as a call it costs a 48-B stack save and the kernel keeps 3 waves / SIMD (5.82 ms; the serial
+// lane-0 update ran 5.95 ms)
+__device__ __attribute__((noinline)) void se3_update_wave(const double* inc, double* DT, double* X) {
+    const int lane = threadIdx.x;
+    double* E = X;        // [16] expmap_se3(inc)
+    double* Sm = X + 16;  // [9] skew(w) / theta, then V
+    double* Ei = X + 32;  // [16] inverse_se3(E)
+    const double w0 = inc[3], w1 = inc[4], w2 = inc[5];
+    const double theta = sqrt((w0 * w0 + w1 * w1) + w2 * w2);
+    const int r9 = lane / 3, c9 = lane - 3 * (lane / 3);
+    if (!(theta < 0.000001)) {   // wave-uniform
+        if (lane < 9) {
+            const double sk = lane == 1 ? -w2 : lane == 2 ? w1 : lane == 3 ? w2 : lane == 5 ? -w0
+                            : lane == 6 ? -w1 : lane == 7 ? w0 : 0.0;
+            Sm[lane] = sk / theta;
+        }
+        __syncthreads();
+        const double st = det_sin(theta), ct = det_cos(theta);
+        double Vi = 0.0;
+        if (lane < 9) {
+            const double si = Sm[lane];
+            const double ssi = (Sm[r9 * 3 + 0] * Sm[0 * 3 + c9] + Sm[r9 * 3 + 1] * Sm[1 * 3 + c9]) + Sm[r9 * 3 + 2] * Sm[2 * 3 + c9];
+            const double Ii = (r9 == c9) ? 1.0 : 0.0;
+            const double omc = 1.0 - ct;
+            E[r9 * 4 + c9] = (Ii + si * st) + ssi * omc;
+            const double tms = theta - st;
+            Vi = (Ii + (si * omc) / theta) + (ssi * tms) / theta;
+        }
+        __syncthreads();
+        if (lane < 9) Sm[lane] = Vi;
+        __syncthreads();
+        if (lane < 3) E[lane * 4 + 3] = (Sm[lane * 3 + 0] * inc[0] + Sm[lane * 3 + 1] * inc[1]) + Sm[lane * 3 + 2] * inc[2];
+    } else {
+        if (lane < 9) E[r9 * 4 + c9] = (r9 == c9) ? 1.0 : 0.0;
+        if (lane < 3) E[lane * 4 + 3] = inc[lane];
+    }
+    if (lane >= 12 && lane < 16) E[lane] = (lane == 15) ? 1.0 : 0.0;
+    __syncthreads();
+    const int r = (lane >> 2) & 3, c = lane & 3;
+    if (lane < 16) {
+        double ei;
+        if (r < 3 && c < 3) ei = E[c * 4 + r];
+        else if (r < 3) ei = ((-E[0 * 4 + r]) * E[3] + (-E[1 * 4 + r]) * E[7]) + (-E[2 * 4 + r]) * E[11];
+        else ei = (c == 3) ? 1.0 : 0.0;
+        Ei[lane] = ei;
+    }
+    __syncthreads();
+    double dn = 0.0;
+    if (lane < 16)
+        dn = ((DT[r * 4 + 0] * Ei[0 * 4 + c] + DT[r * 4 + 1] * Ei[1 * 4 + c]) + DT[r * 4 + 2] * Ei[2 * 4 + c]) +
+             DT[r * 4 + 3] * Ei[3 * 4 + c];
+    __syncthreads();
+    if (lane < 16) DT[lane] = dn;
+    __syncthreads();
+}
 
 #define PT_K 6    // X Y Z ox oy sigma2
 // chunk rows are 66 doubles (528 B) apart: the reduction lanes read rows ia, ib
@@ -165,37 +231,38 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
         }
         S.part[lane] = s;
         __syncthreads();
+        // H = H_p + H_l, one element per lane (the symmetric pair gets the same sum)
+        if (lane < 36) {
+            const int r = lane / 6, c = lane - 6 * (lane / 6);
+            const int t = r >= c ? tri(r, c) : tri(c, r);
+            S.H[lane] = S.part[t] + S.part[28 + t];
+        }
+        __syncthreads();
         if (lane == 0) {
             double H[36], g[6];
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j <= i; ++j) {
-                    const double v = S.part[tri(i, j)] + S.part[28 + tri(i, j)];
-                    H[i * 6 + j] = v; H[j * 6 + i] = v;
-                }
+            for (int i = 0; i < 36; ++i) H[i] = S.H[i];
             for (int i = 0; i < 6; ++i) g[i] = S.part[21 + i] + S.part[28 + 21 + i];
             double ee = S.part[27] + S.part[28 + 27];
             ee = ee / (double)(S.cnt[1] + S.cnt[0]);
-            for (int i = 0; i < 36; ++i) S.H[i] = H[i];
             S.err = ee;
-            int brk = 0;
+            int brk = 0, upd = 0;
             if ((fabs(ee - err_prev) < p.cfg.min_error_change) || (ee < p.cfg.min_error)) {
                 brk = 1;
             } else {
-                double inc[6], E[16], Ei[16], Dn[16], DTc[16];
-                ldlt_solve6(H, g, inc);
-                expmap_se3(inc, E);
-                inverse_se3(E, Ei);
-                for (int i = 0; i < 16; ++i) DTc[i] = S.DT[i];
-                mat4_mul(DTc, Ei, Dn);
-                for (int i = 0; i < 16; ++i) S.DT[i] = Dn[i];
+                double inc[6];
+                ldlt_solve6_one_lane(H, g, inc);
+                for (int i = 0; i < 6; ++i) S.inc[i] = inc[i];
+                upd = 1;
                 const double nrm = sqrt(((((inc[0] * inc[0] + inc[1] * inc[1]) + inc[2] * inc[2]) + inc[3] * inc[3]) +
                                          inc[4] * inc[4]) + inc[5] * inc[5]);
                 if (nrm < 2.220446049250313e-16) brk = 1;
                 err_prev = ee;
             }
             S.brk = brk;
+            S.upd = upd;
         }
         __syncthreads();
+        if (S.upd) se3_update_wave(S.inc, S.DT, S.X);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
         if (S.brk) break;
     }
 }
