@@ -117,9 +117,15 @@ __device__ __forceinline__ void knn_stage_soa(uint32_t* T, int stride, const uin
 #ifndef GFPL_KNN_INLINE
 #define GFPL_KNN_INLINE __forceinline__
 #endif
-template <int CELL, bool TOP2>
+// RL (the reverse direction in the same pass): Hamming distance is symmetric, so tile
+// (t, q) also holds the train-side query's distances — for every train row t the
+// lexicographic minimum of (dist << 16 | q) over the queries is taken by a DPP row_ror
+// min over the 16 lanes of each lane row, then one LDS atomicMin per lane row into
+// rl_key[t] (initialised to 0xFFFFFFFF by the caller): the knn-1 of the train rows
+// against the queries, the OpenCV tie rule included, without a second MFMA pass.
+template <int CELL, bool TOP2, bool RL = false>
 __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt, const uint8_t* Q, int nq, uint32_t* out_k0,
-                          uint32_t* out_k1, const uint32_t* lut) {
+                          uint32_t* out_k1, const uint32_t* lut, uint32_t* rl_key = nullptr) {
     constexpr int KS = CELL == 2 ? 16 : 8;   // k-steps of 32
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
@@ -169,6 +175,14 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
                     k1 = min(k1, hi);
                 } else {
                     k0 = min(k0, key);
+                }
+                if (RL) {
+                    uint32_t v = q < nq ? (((uint32_t)acc[r] << 16) | (uint32_t)q) : 0xFFFFFFFFu;
+                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
+                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
+                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
+                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
+                    if ((lane & 15) == 0 && (int)tr < nt) atomicMin(&rl_key[tr], v);
                 }
             }
         }

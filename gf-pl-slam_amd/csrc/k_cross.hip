@@ -245,10 +245,12 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         const uint8_t* DC = Cc.desc + pb * 32;
         knn_stage_soa(tb, cap, DC, Sc);
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
+        for (int j = tid; j < Sc; j += blockDim.x) i21[j] = -1;   // 21 keys (atomicMin)
         knn_lut_fill<1>(lut);
         __syncthreads();
-        // 12: prev queries against curr trains, knn-2 on the matrix cores (gfpl_knn.hpp)
-        knn2_mfma<1, true>(tb, cap, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112, lut);
+        // 12: prev queries against curr trains, knn-2 on the matrix cores (gfpl_knn.hpp);
+        // 21 (curr queries against prev trains, best index only) from the same distance tiles
+        knn2_mfma<1, true, true>(tb, cap, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112, lut, (uint32_t*)i21);
         __syncthreads();
         for (int i = tid; i < Sl; i += blockDim.x) {
             const uint32_t k0 = (uint32_t)i12[i], k1 = (uint32_t)d112[i];
@@ -257,11 +259,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
             atomicAdd(&h12[d1 - d0], 1);
             atomicAdd(&h0[d0], 1);
         }
-        knn_stage_soa(tb, cap, DP, Sl);
-        __syncthreads();
-        // 21: curr queries against prev trains (best index only)
-        knn2_mfma<1, false>(tb, cap, Sl, DC, Sc, (uint32_t*)i21, nullptr, lut);
-        __syncthreads();
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = (int)((uint32_t)i21[j] & 0xFFFFu);
         __syncthreads();
         if (tid == 0) {

@@ -889,10 +889,12 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
     knn_stage_soa(tb, cap, DRg, NR);
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
+    for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = -1;   // R->L keys (atomicMin)
     knn_lut_fill<CELL>(lut);
     __syncthreads();
-    // L->R knn-2 on the matrix cores (gfpl_knn.hpp): keys (dist << 16 | iR)
-    knn2_mfma<CELL, true>(tb, cap, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1, lut);
+    // L->R knn-2 on the matrix cores (gfpl_knn.hpp): keys (dist << 16 | iR); the R->L knn
+    // (only its best index is used) from the same distance tiles (RL)
+    knn2_mfma<CELL, true, true>(tb, cap, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1, lut, (uint32_t*)rl_i);
     __syncthreads();
     for (int i = tid; i < NL; i += blockDim.x) {
         const uint32_t k0 = (uint32_t)lr_i[i], k1 = (uint32_t)lr_d1[i];
@@ -900,11 +902,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
         lr_i[i] = (int)(k0 & 0xFFFFu); lr_d0[i] = d0; lr_d1[i] = d1;
         atomicAdd(&hist[d1 - d0], 1);   // lineDescriptorMAD deviations |d1-d0| (U1 pin)
     }
-    knn_stage_soa(tb, cap, DLg, NL);
-    __syncthreads();
-    // R->L knn (only the best index is used)
-    knn2_mfma<CELL, false>(tb, cap, NL, DRg, NR, (uint32_t*)rl_i, nullptr, lut);
-    __syncthreads();
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = (int)((uint32_t)rl_i[j] & 0xFFFFu);
     __syncthreads();
     if (tid == 0) {
