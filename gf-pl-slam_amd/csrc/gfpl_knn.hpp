@@ -178,10 +178,10 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
                 }
                 if (RL) {
                     uint32_t v = q < nq ? (((uint32_t)acc[r] << 16) | (uint32_t)q) : 0xFFFFFFFFu;
-                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
-                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
-                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
-                    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
+                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
+                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
+                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
+                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
                     if ((lane & 15) == 0 && (int)tr < nt) atomicMin(&rl_key[tr], v);
                 }
             }
