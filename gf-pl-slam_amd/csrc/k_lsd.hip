@@ -234,7 +234,7 @@ __device__ void heap_sort(uint64_t* a, int len) {
 
 // __unguarded_partition_pivot(a + f, a + l) by the wave; returns the cut
 template <bool LDS, typename IT, int CH = (LDS ? 4 : 16), int SW = (LDS ? 4 : 8)>
-__device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
+__device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp, uint32_t* pko = nullptr) {
     const int lane = lane_id();
     const int mid = f + (l - f) / 2;
     // __move_median_to_first(f, f + 1, mid, l - 1)
@@ -250,6 +250,7 @@ __device__ int partition_pivot(uint64_t* a, int f, int l, IT* Lp, IT* Rp) {
     }
     ssync<LDS>();
     const uint32_t pk = skey(pv);
+    if (pko) *pko = pk;
     // __unguarded_partition(f + 1, l, f): the stoppers of both scans, ranked
     int cl = 0, cr = 0;   // CH: chunks' loads in flight
     for (int base = f + 1; base < l; base += 64 * CH) {
@@ -434,9 +435,10 @@ __device__ void add_leaf(uint64_t* a, int* leaf, int& nleaf, int f, int l) {
 }
 
 // __introsort_loop over [0, n) of an LDS array with the given depth budget, then the
-// final insertion sort of its leaves
+// final insertion sort of its leaves.  B0 > 0: a right part whose pivot key is below B0 holds
+// only keys below B0 and is left unsorted (see mw_sort)
 template <int CAP>
-__device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds<CAP>& S) {
+__device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds<CAP>& S, uint32_t B0 = 0) {
     const int lane = lane_id();
     int* stk = S.stk;
     int ns = 0;
@@ -459,14 +461,17 @@ __device__ void introsort_lds(uint64_t* a, int n, int depth, SortLds<CAP>& S) {
                 break;
             }
             --d;
-            const int cut = partition_pivot<true>(a, f, l, S.lp, S.rp);
-            if (lane == 0) {
-                stk[3 * sp] = cut;
-                stk[3 * sp + 1] = l;
-                stk[3 * sp + 2] = d;
+            uint32_t pk;
+            const int cut = partition_pivot<true>(a, f, l, S.lp, S.rp, &pk);
+            if (pk >= B0) {
+                if (lane == 0) {
+                    stk[3 * sp] = cut;
+                    stk[3 * sp + 1] = l;
+                    stk[3 * sp + 2] = d;
+                }
+                lds_sync();
+                ++sp;
             }
-            lds_sync();
-            ++sp;
             l = cut;
         }
         if (!done && l - f > 1) {
@@ -584,7 +589,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair<CAP>
 // elements as the serial algorithm leaves them, and no stopper list goes to HBM.  The cut is
 // partition_pivot's: min(next left stopper, last swapped right stopper).
 template <int CAP>
-__device__ int partition_hoare(uint64_t* a, int f, int l, SortLds<CAP>& S) {
+__device__ int partition_hoare(uint64_t* a, int f, int l, SortLds<CAP>& S, uint32_t& pko) {
     constexpr int BT = CAP / 2, CH = 8;
     const int lane = lane_id();
     const int mid = f + (l - f) / 2;
@@ -600,6 +605,7 @@ __device__ int partition_hoare(uint64_t* a, int f, int l, SortLds<CAP>& S) {
     }
     mem_sync();
     const uint32_t pk = skey(pv);
+    pko = pk;
     uint64_t* LV = S.buf;
     uint64_t* RV = S.buf + BT;
     uint32_t* LP = reinterpret_cast<uint32_t*>(S.lp);   // lp | rp: 4 CAP bytes = 2 BT positions
@@ -707,8 +713,14 @@ __device__ __forceinline__ void q_unlock(int* lk) {
 __device__ __forceinline__ int q_get(int* v) { return __hip_atomic_load(v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void q_set(int* v, int x) { __hip_atomic_store(v, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
+// B0 > 0 (k_lsd_sort): only the order of the keys >= B0 is read (the seed scan stops at the
+// first key below B0: an undefined pixel), so a right part [cut, l) whose pivot key is below B0
+// — all of its keys are <= the pivot's — is not sorted further.  Every other range is
+// partitioned exactly as libstdc++ does, and the skipped ranges lie after every key >= B0, so
+// the keys >= B0 end in std::sort's permutation.  B0 = 0 sorts everything (the test hook).
 template <int CAP, int NW>
-__device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsMW<CAP, NW>& M) {
+__device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsMW<CAP, NW>& M,
+                                        uint32_t B0 = 0) {
     const int lane = lane_id(), w = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
         M.lock = 0;
@@ -773,7 +785,7 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
 #pragma unroll 4
                 for (int i = lane; i < m; i += 64) S.buf[i] = a[f + i];
                 lds_sync();
-                introsort_lds(S.buf, m, d, S);
+                introsort_lds(S.buf, m, d, S, B0);
                 for (int i = lane; i < m; i += 64) a[f + i] = S.buf[i];
                 mem_sync();
                 break;
@@ -785,8 +797,11 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
             }
             --d;
             // (partition_pivot ends with a fence: its swaps are visible to the wave that pops [cut, l))
-            const int cut = partition_hoare(a, f, l, S);
-            if (l - cut > 16) {
+            uint32_t pk;
+            const int cut = partition_hoare(a, f, l, S, pk);
+            if (pk < B0) {
+                // [cut, l): keys below B0 only, left unsorted
+            } else if (l - cut > 16) {
                 int pushed = 0;
                 if (lane == 0) {
                     q_lock(&M.lock);
@@ -947,7 +962,11 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o, const uint8_t* image
 __global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(LSD_SORT_WAVES))) k_lsd_sort(LsdDev o) {
     __shared__ SortLdsMW<LSD_SORT_CAP, LSD_SORT_WAVES> S;
     const size_t img = blockIdx.x;
-    mw_sort(o.keys + img * o.NP, o.NP, o.lpos + img * o.NP, o.rpos + img * o.NP, S);
+    // B0 as lsd_image computes it (the bins of k_lsd_keys)
+    const double mg = __longlong_as_double((long long)o.maxg[img]);
+    const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
+    const uint32_t B0 = (uint32_t)(int)(o.rho * bin_coef);
+    mw_sort(o.keys + img * o.NP, o.NP, o.lpos + img * o.NP, o.rpos + img * o.NP, S, B0);
 }
 
 // ---------------------------------------------------------------- the regions --

@@ -107,8 +107,9 @@ class ImagePipeline:
     LSD (lsd=True: the reference's LSDOptions, Config::lsdNFeatures = 300, min length
     0.025 * min(W, H)) and LBD.
 
-    Detection runs on its own context (its own stream) into `sets`
-    buffer sets in turn, through the stream-ordered detector calls (gfpl_*_async).  Every
+    Detection runs on two contexts of its own (two streams: ORB on one, LSD then LBD on the
+    other, so ORB of a batch overlaps its latency-bound LSD; the two join before `ready`) into
+    `sets` buffer sets in turn, through the stream-ordered detector calls (gfpl_*_async).  Every
     gfpl_frames it returns carries two events: `ready` (its detection is done) and
     `consumed` (recorded by the tracker call that reads it, gfpl_frames.ready / consumed),
     so a tracker call on another context waits for exactly that detection and the next
@@ -125,9 +126,11 @@ class ImagePipeline:
         # the detection stream is a torch stream (pooled by torch, never destroyed), so torch's
         # allocator may record the inputs' use on it (Tensor.record_stream)
         self._tstream = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+        self._ostream = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
         self.det = Context(cam, cfg, device=ctx.device, stream=self._tstream.cuda_stream)
+        self.det_orb = Context(cam, cfg, device=ctx.device, stream=self._ostream.cuda_stream)
         self.orb = ORBextractor(nfeatures, float(cfg.orb_scale_factor), int(cfg.orb_n_levels), 20, 7, W, H,
-                                max_images=batch, ctx=self.det)
+                                max_images=batch, ctx=self.det_orb)
         # the extractor writes the tracker's right pyramid (gfpl_frames.pyr_r): its levels must
         # be the camera's (gfpl_orb_extract checks it as well)
         geo = [(int(cam.lvl_cols[l]), int(cam.lvl_rows[l])) for l in range(int(cam.n_levels))]
@@ -158,23 +161,26 @@ class ImagePipeline:
                 "pyr_r": z(B * int(cam.pyr_bytes)),
                 "ts": torch.zeros(B, dtype=torch.float64, device=dev)})
         self.ready = [Event(self.det) for _ in range(sets)]
+        self.orb_done = [Event(self.det_orb) for _ in range(sets)]
         self.consumed = [Event(ctx) for _ in range(sets)]
         self.k = 0
         torch.cuda.synchronize(dev)   # the buffers' zero fills (default stream) before any detection
 
     def _begin(self, inputs):
         """next buffer set; the detection stream waits for the tracker's last read of it and for
-        the caller's stream (which produced the inputs)"""
+        the caller's stream (which produced the inputs); so does the ORB stream"""
         import torch
         s = self.k % self.sets
         self.k += 1
         self.consumed[s].wait(self.det)
+        self.consumed[s].wait(self.det_orb)
         ts = self._tstream
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(ts.device))
-        ts.wait_event(ev)
-        for t in inputs:
-            t.record_stream(ts)   # the caching allocator keeps them until the detection ran
+        for st in (ts, self._ostream):
+            st.wait_event(ev)
+            for t in inputs:
+                t.record_stream(st)   # the caching allocator keeps them until the detection ran
         return s, ts
 
     def detect(self, left, right, kl_left, n_kl_left, kl_right, n_kl_right, time_stamp):
@@ -212,10 +218,12 @@ class ImagePipeline:
         for side, img in ((0, left), (1, right)):
             pyr = b["pyr_l"] if side == 0 else b["pyr_r"]
             self.orb.extract_async(img, B, b["kps"][side], b["pdesc"][side], b["n_kp"][side], None, None, pyr, pb)
+        self.orb_done[s].record(self.det_orb)
         for side in range(2):
             self.lbd.compute_async(left if side == 0 else right, B, b["kl"][side], b["n_kl"][side], b["ldesc"][side])
         with torch.cuda.stream(ts):
             b["ts"].copy_(time_stamp)
+        self.orb_done[s].wait(self.det)
         self.ready[s].record(self.det)
         arrs = [b["n_kp"][0], b["n_kp"][1], b["kps"][0], b["kps"][1], b["pdesc"][0], b["pdesc"][1],
                 b["n_kl"][0], b["n_kl"][1], b["kl"][0], b["kl"][1], b["ldesc"][0], b["ldesc"][1], b["pyr_r"], b["ts"]]
@@ -232,14 +240,17 @@ class ImagePipeline:
             self.lsd.status()
 
     def synchronize(self):
+        self.det_orb.synchronize()
         self.det.synchronize()
 
     def close(self):
+        self.det_orb.synchronize()
         self.det.synchronize()
         self.orb.close()
         self.lbd.close()
         if self.lsd is not None:
             self.lsd.close()
-        for e in self.ready + self.consumed:
+        for e in self.ready + self.orb_done + self.consumed:
             e.close()
         self.det.close()
+        self.det_orb.close()
