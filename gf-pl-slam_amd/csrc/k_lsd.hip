@@ -1090,23 +1090,28 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
                 glob = true;
             }
             const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy);
-            const unsigned long long m = __ballot(av) >> (9 * k);
+            unsigned long long m = __ballot(av) >> (9 * k);
             if (!m) continue;
             const int b = 9 * k;
             const int prx = rl_i(rx, b), pry = rl_i(ry, b);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                if (!((m >> t) & 1ull)) continue;   // out of the image, used, or NOTDEF
-                const float at = rl_f(q.x, b + t);
-                // isAligned (lsd.cpp)
-                const double ad = (double)at * kDeg2Rad;
+            // isAligned (lsd.cpp) of every pending neighbour against the current reg_angle at
+            // once (lane b + t: neighbour t): the first aligned one is the next the serial
+            // loop adds, those before it failed against the same angle; the angle then
+            // changes and the neighbours after it are tested again (the used map of this
+            // point's neighbours does not change meanwhile: they are distinct pixels)
+            const double ad = (double)q.x * kDeg2Rad;
+            const bool mine = lane >= b && lane < b + 9;
+            while (m) {
                 double nt = reg_angle - ad;
                 if (nt < 0) nt = -nt;
                 if (nt > k32Pi) {
                     nt -= k2Pi;
                     if (nt < 0) nt = -nt;
                 }
-                if (!(nt <= prec)) continue;
+                const unsigned long long ma = (__ballot(mine && nt <= prec) >> b) & m;
+                if (!ma) break;
+                const int t = __ffsll((long long)ma) - 1;
+                m &= ~((2ull << t) - 1ull);
                 const int px = prx + t % 3 - 1, py = pry + t / 3 - 1;
                 const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
                 if (lane == 0) {
