@@ -109,6 +109,43 @@ __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, dou
 #define GFPL_POSE_RED_UNROLL 4
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
+// f64 a / b exactly as clang expands it for gfx950 (v_div_scale of the denominator, v_rcp and
+// two Newton steps, v_div_scale of the numerator, one correction, v_div_fmas, v_div_fixup),
+// with the reciprocal refinement of a denominator shared by the numerators divided by it: the
+// scaled denominator v_div_scale(b, b, a) can depend on a (a = 0, a tiny, |a / b| extreme), so
+// each division forms it and refines its own reciprocal unless its bits equal the shared one's —
+// every quotient is the bits of `a / b` (the refinement is a function of the scaled denominator)
+struct SharedDiv { double b, sb, r; };
+__device__ __forceinline__ double div_refine(double sb) {
+    double r = __builtin_amdgcn_rcp(sb);
+    double t = __builtin_fma(-sb, r, 1.0);
+    r = __builtin_fma(r, t, r);
+    t = __builtin_fma(-sb, r, 1.0);
+    return __builtin_fma(r, t, r);
+}
+__device__ __forceinline__ SharedDiv div_prep(double b, double a0) {
+    bool f;
+    const double sb = __builtin_amdgcn_div_scale(a0, b, false, &f);
+    return SharedDiv{b, sb, div_refine(sb)};
+}
+__device__ __forceinline__ double div_by(const SharedDiv& d, double a) {
+    bool f, vcc;
+    const double sb = __builtin_amdgcn_div_scale(a, d.b, false, &f);
+    double r = d.r;
+    if (__builtin_expect(__double_as_longlong(sb) != __double_as_longlong(d.sb), 0)) r = div_refine(sb);
+    const double sa = __builtin_amdgcn_div_scale(a, d.b, true, &vcc);
+    const double m = sa * r;
+    const double e = __builtin_fma(-sb, m, sa);
+    return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(e, r, m, vcc), d.b, a);
+}
+// projection (gfpl_device.hpp) with the two divisions by P[2] sharing the reciprocal
+__device__ __forceinline__ void projection_sd(const DevCam& c, const double* P, double* uv) {
+    const double nx = c.fx * P[0], ny = c.fy * P[1];
+    const SharedDiv dz = div_prep(P[2], nx);
+    uv[0] = c.cx + div_by(dz, nx);
+    uv[1] = c.cy + div_by(dz, ny);
+}
+
 // evaluate one point row (src/stereoFrameHandler.cpp:2130-2160) -> J[6], n, w;
 // in = X Y Z ox oy sigma2 (registers)
 __device__ __forceinline__ void eval_point(const DevCam& cam, double homog, const double* DT, const double* in,
@@ -116,14 +153,15 @@ __device__ __forceinline__ void eval_point(const DevCam& cam, double homog, cons
     const double Pp[3] = {in[0], in[1], in[2]};
     double Pc[3], uv[2];
     se3_apply(DT, Pp, Pc);
-    projection(cam, Pc, uv);
+    projection_sd(cam, Pc, uv);
     const double ex = uv[0] - in[3], ey = uv[1] - in[4];
     const double n = sqrt(ex * ex + ey * ey);
     double J[6];
     poseJac(cam, homog, Pc, ex, ey, J);
     const double m = ref_max(homog, n);
+    const SharedDiv dm = div_prep(m, J[0]);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) o[i] = J[i] / m;
+    for (int i = 0; i < 6; ++i) o[i] = div_by(dm, J[i]);
     o[6] = n;
     o[7] = 1.0 / (1.0 + (n * n) * in[5]);
 }
@@ -136,9 +174,9 @@ __device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const
     const double eP[3] = {in[3], in[4], in[5]};
     double sc[3], ec[3], su[2], eu[2];
     se3_apply(DT, sP, sc);
-    projection(cam, sc, su);
+    projection_sd(cam, sc, su);
     se3_apply(DT, eP, ec);
-    projection(cam, ec, eu);
+    projection_sd(cam, ec, eu);
     const double l0 = in[6], l1 = in[7], l2 = in[8];
     const double ds = (l0 * su[0] + l1 * su[1]) + l2;
     const double de = (l0 * eu[0] + l1 * eu[1]) + l2;
@@ -147,8 +185,12 @@ __device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const
     poseJac(cam, homog, sc, l0, l1, Js);
     poseJac(cam, homog, ec, l0, l1, Je);
     const double m = ref_max(homog, n);
+    double t[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) o[i] = (Js[i] * ds + Je[i] * de) / m;
+    for (int i = 0; i < 6; ++i) t[i] = Js[i] * ds + Je[i] * de;
+    const SharedDiv dm = div_prep(m, t[0]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] = div_by(dm, t[i]);
     o[6] = n;
     o[7] = 1.0 / (1.0 + (n * n) * in[9]);
 }
