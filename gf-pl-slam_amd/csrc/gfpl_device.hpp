@@ -696,6 +696,35 @@ GFPL_DEV void backProjection(const DevCam& c, double u, double v, double disp, d
     P[2] = bd * c.fx;
 }
 
+// f64 a / b exactly as clang expands it for gfx950 (v_div_scale of the denominator, v_rcp and
+// two Newton steps, v_div_scale of the numerator, one correction, v_div_fmas, v_div_fixup),
+// with the reciprocal refinement of a denominator shared by the numerators divided by it: the
+// scaled denominator v_div_scale(b, b, a) can depend on a (a = 0, a tiny, |a / b| extreme), so
+// each division forms it and refines its own reciprocal unless its bits equal the shared one's —
+// every quotient is the bits of `a / b` (the refinement is a function of the scaled denominator)
+struct SharedDiv { double b, sb, r; };
+GFPL_DEV double div_refine(double sb) {
+    double r = __builtin_amdgcn_rcp(sb);
+    double t = __builtin_fma(-sb, r, 1.0);
+    r = __builtin_fma(r, t, r);
+    t = __builtin_fma(-sb, r, 1.0);
+    return __builtin_fma(r, t, r);
+}
+GFPL_DEV SharedDiv div_prep(double b, double a0) {
+    bool f;
+    const double sb = __builtin_amdgcn_div_scale(a0, b, false, &f);
+    return SharedDiv{b, sb, div_refine(sb)};
+}
+GFPL_DEV double div_by(const SharedDiv& d, double a) {
+    bool f, vcc;
+    const double sb = __builtin_amdgcn_div_scale(a, d.b, false, &f);
+    double r = d.r;
+    if (__builtin_expect(__double_as_longlong(sb) != __double_as_longlong(d.sb), 0)) r = div_refine(sb);
+    const double sa = __builtin_amdgcn_div_scale(a, d.b, true, &vcc);
+    const double m = sa * r;
+    const double e = __builtin_fma(-sb, m, sa);
+    return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(e, r, m, vcc), d.b, a);
+}
 // Jacobian of a projected residual wrt the pose, weights (lx, ly)
 // (src/stereoFrameHandler.cpp:1383-1388, 1438-1443, 2150-2155, 2197-2202)
 GFPL_DEV void poseJac(const DevCam& c, double homog, const double* g, double lx, double ly, double* J) {

@@ -109,35 +109,6 @@ __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, dou
 #define GFPL_POSE_RED_UNROLL 4
 #define LS_K 10   // sX sY sZ eX eY eZ l0 l1 l2 sigma2
 
-// f64 a / b exactly as clang expands it for gfx950 (v_div_scale of the denominator, v_rcp and
-// two Newton steps, v_div_scale of the numerator, one correction, v_div_fmas, v_div_fixup),
-// with the reciprocal refinement of a denominator shared by the numerators divided by it: the
-// scaled denominator v_div_scale(b, b, a) can depend on a (a = 0, a tiny, |a / b| extreme), so
-// each division forms it and refines its own reciprocal unless its bits equal the shared one's —
-// every quotient is the bits of `a / b` (the refinement is a function of the scaled denominator)
-struct SharedDiv { double b, sb, r; };
-__device__ __forceinline__ double div_refine(double sb) {
-    double r = __builtin_amdgcn_rcp(sb);
-    double t = __builtin_fma(-sb, r, 1.0);
-    r = __builtin_fma(r, t, r);
-    t = __builtin_fma(-sb, r, 1.0);
-    return __builtin_fma(r, t, r);
-}
-__device__ __forceinline__ SharedDiv div_prep(double b, double a0) {
-    bool f;
-    const double sb = __builtin_amdgcn_div_scale(a0, b, false, &f);
-    return SharedDiv{b, sb, div_refine(sb)};
-}
-__device__ __forceinline__ double div_by(const SharedDiv& d, double a) {
-    bool f, vcc;
-    const double sb = __builtin_amdgcn_div_scale(a, d.b, false, &f);
-    double r = d.r;
-    if (__builtin_expect(__double_as_longlong(sb) != __double_as_longlong(d.sb), 0)) r = div_refine(sb);
-    const double sa = __builtin_amdgcn_div_scale(a, d.b, true, &vcc);
-    const double m = sa * r;
-    const double e = __builtin_fma(-sb, m, sa);
-    return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(e, r, m, vcc), d.b, a);
-}
 // projection (gfpl_device.hpp) with the two divisions by P[2] sharing the reciprocal
 __device__ __forceinline__ void projection_sd(const DevCam& c, const double* P, double* uv) {
     const double nx = c.fx * P[0], ny = c.fy * P[1];
