@@ -590,7 +590,7 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair<CAP>
 // partition_pivot's: min(next left stopper, last swapped right stopper).
 template <int CAP>
 __device__ int partition_hoare(uint64_t* a, int f, int l, SortLds<CAP>& S, uint32_t& pko) {
-    constexpr int BT = CAP / 2, CH = 8;
+    constexpr int BT = CAP / 2, CH = 16;
     const int lane = lane_id();
     const int mid = f + (l - f) / 2;
     const uint32_t ka = skey(a[f + 1]), kb = skey(a[mid]), kc = skey(a[l - 1]);
