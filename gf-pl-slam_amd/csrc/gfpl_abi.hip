@@ -25,6 +25,7 @@ struct gfpl_ctx {
     hipEvent_t ev[GFPL_NEV]{};
     float stage_ms[7]{};
     std::vector<gfpl_seqbatch*> sbs;   // live seqbatches: their match-list capacities bound gfpl_set_config
+    int n_detectors = 0;   // live ORB / LBD / LSD objects: they hold the context's stream (and ORB its camera)
 };
 
 struct gfpl_seqbatch {
@@ -56,12 +57,16 @@ struct gfpl_seqbatch {
 struct gfpl_event {
     int device = 0;
     hipEvent_t ev = nullptr;
+    int64_t records = 0;   // host-side count of records (gfpl_event_record, tracker `consumed` marks)
 };
 
 // for the other extern "C" objects built on a context (k_orb.hip)
 int gfpl_ctx_device(const gfpl_ctx* c) { return c->device; }
 void* gfpl_ctx_stream(const gfpl_ctx* c) { return (void*)c->stream; }
 const gfpl_camera* gfpl_ctx_camera(const gfpl_ctx* c) { return c->has_cam ? &c->cam : nullptr; }
+int64_t gfpl_event_records(const gfpl_event* e) { return e->records; }
+void gfpl_ctx_attach(gfpl_ctx* c) { ++c->n_detectors; }
+void gfpl_ctx_detach(gfpl_ctx* c) { --c->n_detectors; }
 
 
 namespace {
@@ -188,6 +193,9 @@ int check_in(gfpl_seqbatch* sb, const gfpl_frames* in) {
         return GFPL_E_INVALID;
     // the sub-pixel SAD reads pyramid rows as aligned dwords relative to each sequence's pyramid
     if (((uintptr_t)in->pyr_r & 3) != 0) return GFPL_E_INVALID;
+    // producer / consumer events must live on the context's device (as gfpl_event_wait checks)
+    if ((in->ready && in->ready->device != sb->ctx->device) || (in->consumed && in->consumed->device != sb->ctx->device))
+        return GFPL_E_INVALID;
     return GFPL_OK;
 }
 
@@ -204,7 +212,10 @@ int in_acquire(gfpl_seqbatch* sb, const gfpl_frames* in) {
     return -1;
 }
 int in_release(gfpl_seqbatch* sb, const gfpl_frames* in, int slot) {
-    if (in->consumed && hipEventRecord(in->consumed->ev, sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+    if (in->consumed) {
+        if (hipEventRecord(in->consumed->ev, sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+        ++in->consumed->records;
+    }
     if (slot < 0) return GFPL_OK;
     if (hipEventRecord(sb->ev_free[slot], sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
     sb->free_recorded[slot] = true;
@@ -262,6 +273,7 @@ int gfpl_create_async(int device, gfpl_ctx** out) {
 int gfpl_destroy(gfpl_ctx* c) {
     if (!c) return GFPL_E_INVALID;
     if (!c->sbs.empty()) return GFPL_E_STATE;   // its seqbatches use the context's stream and config
+    if (c->n_detectors != 0) return GFPL_E_STATE;   // so do its ORB / LBD / LSD objects
     for (int i = 0; i < GFPL_NEV; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->own_stream) {
@@ -291,9 +303,16 @@ int gfpl_event_destroy(gfpl_event* e) {
     return GFPL_OK;
 }
 
+int gfpl_event_record_count(const gfpl_event* e, int64_t* count) {
+    if (!e || !count) return GFPL_E_INVALID;
+    *count = e->records;
+    return GFPL_OK;
+}
+
 int gfpl_event_record(gfpl_event* e, gfpl_ctx* c) {
     if (!e || !c || e->device != c->device) return GFPL_E_INVALID;
     HIPCHK(hipEventRecord(e->ev, c->stream));
+    ++e->records;
     return GFPL_OK;
 }
 

@@ -53,6 +53,11 @@ hipError_t launch_kf_map_filter(const DevCam& cam, const double* T1, const doubl
 int gfpl_ctx_device(const gfpl_ctx* c);
 void* gfpl_ctx_stream(const gfpl_ctx* c);
 const gfpl_camera* gfpl_ctx_camera(const gfpl_ctx* c);   // NULL before gfpl_set_camera
+// a detector created on the context counts itself in until it is destroyed (gfpl_destroy refuses meanwhile)
+void gfpl_ctx_attach(gfpl_ctx* c);
+void gfpl_ctx_detach(gfpl_ctx* c);
+// how often the event was recorded (gfpl_event_record, or as a tracker call's gfpl_frames.consumed)
+int64_t gfpl_event_records(const gfpl_event* e);
 
 namespace gfpl {
 // Deferred error status of the stream-ordered detector calls (gfpl_*_async): the kernels

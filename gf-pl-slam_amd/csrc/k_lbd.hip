@@ -274,6 +274,7 @@ using namespace gfpl;
 struct gfpl_lbd {
     int device = 0;
     hipStream_t stream = nullptr;
+    gfpl_ctx* ctx = nullptr;   // counted in while this object lives
     AsyncStatus st;
     int max_images = 0;
     LbdDev d{};
@@ -335,6 +336,8 @@ extern "C" int gfpl_lbd_create(gfpl_ctx* ctx, int width, int height, int max_ima
     d.grad = (uint32_t*)p; p += b_g;
     d.err = (int*)p;
     if (o->st.init(d.err, o->stream) != hipSuccess) { o->st.destroy(); (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
+    o->ctx = ctx;
+    gfpl_ctx_attach(ctx);
     *out = o;
     return GFPL_OK;
 }
@@ -344,6 +347,7 @@ extern "C" int gfpl_lbd_destroy(gfpl_lbd* o) {
     (void)hipStreamSynchronize(o->stream);
     o->st.destroy();
     if (o->base) (void)hipFree(o->base);
+    gfpl_ctx_detach(o->ctx);
     delete o;
     return GFPL_OK;
 }

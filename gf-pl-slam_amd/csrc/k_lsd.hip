@@ -1519,6 +1519,7 @@ using namespace gfpl;
 struct gfpl_lsd {
     int device = 0;
     hipStream_t stream = nullptr;
+    gfpl_ctx* ctx = nullptr;   // counted in while this object lives
     AsyncStatus st;
     int max_images = 0;
     bool lds_used = false;
@@ -1601,6 +1602,8 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
         delete o;
         return GFPL_E_HIP;
     }
+    o->ctx = ctx;
+    gfpl_ctx_attach(ctx);
     *out = o;
     return GFPL_OK;
 }
@@ -1618,6 +1621,7 @@ extern "C" int gfpl_lsd_destroy(gfpl_lsd* o) {
     (void)hipStreamSynchronize(o->stream);
     o->st.destroy();
     if (o->base) (void)hipFree(o->base);
+    gfpl_ctx_detach(o->ctx);
     delete o;
     return GFPL_OK;
 }

@@ -1007,7 +1007,7 @@ using namespace gfpl;
 struct gfpl_orb {
     int device = 0;
     hipStream_t stream = nullptr;
-    const gfpl_ctx* ctx = nullptr;  // its camera checks the pyramid layout the tracker will read
+    gfpl_ctx* ctx = nullptr;  // its camera checks the pyramid layout the tracker will read
     AsyncStatus st;
     gfpl_orb_params prm{};
     int max_images = 0, kp_cap = 0;
@@ -1247,6 +1247,7 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
     }
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_orb_pattern), kOrbPattern, sizeof(kOrbPattern)) == hipSuccess;
     if (!ok || o->st.init(d.err, o->stream) != hipSuccess) { o->st.destroy(); (void)hipFree(o->base); delete o; return GFPL_E_HIP; }
+    gfpl_ctx_attach(ctx);
     *out = o;
     return GFPL_OK;
 }
@@ -1256,6 +1257,7 @@ extern "C" int gfpl_orb_destroy(gfpl_orb* o) {
     (void)hipStreamSynchronize(o->stream);
     o->st.destroy();
     if (o->base) (void)hipFree(o->base);
+    gfpl_ctx_detach(o->ctx);
     delete o;
     return GFPL_OK;
 }

@@ -223,6 +223,27 @@ class LsdParams(C.Structure):
         return cls(1, 1.0, 2.0, 22.5, 0.6, 1024, min_line_length * min(width, height), n_features)
 
 
+class DetectorParams(C.Structure):
+    """gfpl_detector_params: the ORB + LSD options StereoFrame's detection runs with
+    (src/stereoFrame.cpp:33-36, 1160-1172) and the raw LSD segment capacity."""
+    _fields_ = [("orb", OrbParams), ("lsd", LsdParams), ("seg_cap", C.c_int)]
+
+    @classmethod
+    def reference(cls, cam: "Camera", cfg: Optional["Config"] = None, nfeatures: Optional[int] = None):
+        p = cls()
+        check(hiplib().gfpl_detector_params_default(C.byref(cam), C.byref(cfg) if cfg is not None else None,
+                                                    C.byref(p)), "detector_params_default")
+        if nfeatures is not None:
+            p.orb.nfeatures = nfeatures
+        return p
+
+
+class DetectionsHost(C.Structure):
+    _fields_ = [("n_kp_l", C.c_int), ("n_kp_r", C.c_int), ("n_kl_l", C.c_int), ("n_kl_r", C.c_int),
+                ("kp_l", _vp), ("kp_r", _vp), ("pdesc_l", _vp), ("pdesc_r", _vp),
+                ("kl_l", _vp), ("kl_r", _vp), ("ldesc_l", _vp), ("ldesc_r", _vp)]
+
+
 class SynthParams(C.Structure):
     _fields_ = [("n_kp", C.c_int), ("n_kl", C.c_int), ("n_world_pts", C.c_int),
                 ("n_world_lines", C.c_int), ("dt", C.c_double), ("v_fwd", C.c_double),
@@ -278,6 +299,7 @@ def hiplib() -> C.CDLL:
             "gfpl_event_record": ([P, P], C.c_int),
             "gfpl_event_wait": ([P, P], C.c_int),
             "gfpl_event_synchronize": ([P], C.c_int),
+            "gfpl_event_record_count": ([P, P], C.c_int),
             "gfpl_orb_extract_async": ([P, P, C.c_int, P, P, P, P, P, P, C.c_int64], C.c_int),
             "gfpl_orb_status": ([P], C.c_int),
             "gfpl_lsd_detect_async": ([P, P, C.c_int, P, P, P], C.c_int),
@@ -340,6 +362,15 @@ def hiplib() -> C.CDLL:
             "gfpl_lbd_destroy": ([P], C.c_int),
             "gfpl_lbd_compute": ([P, P, C.c_int, P, P, P], C.c_int),
             "gfpl_lbd_gradients": ([P, P, P], C.c_int),
+            "gfpl_detector_params_default": ([P, P, P], C.c_int),
+            "gfpl_detector_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
+            "gfpl_detector_destroy": ([P], C.c_int),
+            "gfpl_detect_stereo_async": ([P, P, P, C.c_int, P, P], C.c_int),
+            "gfpl_detect_stereo_host": ([P, P, P, C.c_int, P, P], C.c_int),
+            "gfpl_detect_stereo": ([P, P, P, C.c_int, P, C.c_int, P], C.c_int),
+            "gfpl_detector_status": ([P], C.c_int),
+            "gfpl_detector_discard": ([P, P], C.c_int),
+            "gfpl_read_detections": ([P, P, C.c_int, P], C.c_int),
         }
         for n, (a, r) in sigs.items():
             try:
@@ -805,6 +836,13 @@ class Event:
     def synchronize(self):
         check(self.L.gfpl_event_synchronize(self.h), "gfpl_event_synchronize")
 
+    @property
+    def record_count(self) -> int:
+        """records so far (gfpl_event_record, or a tracker call's gfpl_frames.consumed mark)"""
+        n = C.c_int64(0)
+        check(self.L.gfpl_event_record_count(self.h, C.byref(n)), "gfpl_event_record_count")
+        return n.value
+
     def close(self):
         if getattr(self, "h", None):
             self.L.gfpl_event_destroy(self.h)
@@ -1253,6 +1291,81 @@ class BinaryDescriptor:
         if getattr(self, "_own", None):
             self.L.gfpl_destroy(self._own)
             self._own = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StereoDetector:
+    """gfpl_detector: StereoFrame's detection from a stereo pair of images on the device —
+    ORB of both images (the right pyramid kept for the sub-pixel refinement), LSD with the
+    lsdNFeatures cut and LBD of both (src/stereoFrame.cpp:148-172, 411-450, 1128-1227), for
+    up to `batch` stereo frames per call, on two streams of the detector's own.  detect()
+    returns the gfpl_frames view the tracker (StereoFrameHandler.initialize / insertStereoPair
+    / frameStep) reads with no copy, ordered by the view's ready / consumed events: at most
+    `sets` views may be outstanding (a tracker call reading a view, or discard(), frees it)."""
+
+    def __init__(self, ctx: Context, batch: int, kp_cap: int, kl_cap: int, params: Optional[DetectorParams] = None,
+                 sets: int = 2):
+        self.L = ctx.L
+        self.ctx, self.B, self.kp_cap, self.kl_cap = ctx, batch, kp_cap, kl_cap
+        self.params = params if params is not None else DetectorParams.reference(ctx.cam, ctx.cfg)
+        h = C.c_void_p()
+        check(self.L.gfpl_detector_create(ctx.h, C.byref(self.params), batch, kp_cap, kl_cap, sets, C.byref(h)),
+              "detector_create")
+        self.h = h
+
+    def detect(self, left, right, time_stamp, n: Optional[int] = None) -> Frames:
+        """left / right: device u8 [n][H][W] (torch), time_stamp: device f64 [n]; produced on
+        the context's stream.  Asynchronous (status() reports capacity errors)."""
+        n = self.B if n is None else n
+        fr = Frames()
+        check(self.L.gfpl_detect_stereo_async(self.h, _ptr(left), _ptr(right), n, _ptr(time_stamp), C.byref(fr)),
+              "detect_stereo_async")
+        fr._keep = [left, right, time_stamp]
+        return fr
+
+    def detect_host(self, left: np.ndarray, right: np.ndarray, time_stamp) -> Frames:
+        """HOST images [n][H][W] u8 (or one [H][W] image) and time stamps [n]."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        ts = np.ascontiguousarray(np.atleast_1d(time_stamp), np.float64)
+        n = 1 if left.ndim == 2 else left.shape[0]
+        if right.shape != left.shape or len(ts) != n:
+            raise ValueError("detect_host: left / right / time stamps disagree")
+        fr = Frames()
+        check(self.L.gfpl_detect_stereo_host(self.h, left.ctypes.data, right.ctypes.data, n, ts.ctypes.data,
+                                             C.byref(fr)), "detect_stereo_host")
+        return fr
+
+    def status(self) -> None:
+        check(self.L.gfpl_detector_status(self.h), "detector_status")
+
+    def discard(self, fr: Frames) -> None:
+        check(self.L.gfpl_detector_discard(self.h, C.byref(fr)), "detector_discard")
+
+    def read(self, fr: Frames, seq: int) -> dict:
+        """one sequence's detections of a view, on the host: kp_l / kp_r (KEYPOINT_DT),
+        pdesc_l / pdesc_r, kl_l / kl_r (KEYLINE_DT), ldesc_l / ldesc_r"""
+        out = {"kp_l": np.zeros(fr.kp_cap, KEYPOINT_DT), "kp_r": np.zeros(fr.kp_cap, KEYPOINT_DT),
+               "pdesc_l": np.zeros((fr.kp_cap, DESC), np.uint8), "pdesc_r": np.zeros((fr.kp_cap, DESC), np.uint8),
+               "kl_l": np.zeros(fr.kl_cap, KEYLINE_DT), "kl_r": np.zeros(fr.kl_cap, KEYLINE_DT),
+               "ldesc_l": np.zeros((fr.kl_cap, DESC), np.uint8), "ldesc_r": np.zeros((fr.kl_cap, DESC), np.uint8)}
+        d = DetectionsHost()
+        for k, a in out.items():
+            setattr(d, k, a.ctypes.data)
+        check(self.L.gfpl_read_detections(self.ctx.h, C.byref(fr), seq, C.byref(d)), "read_detections")
+        n = {"kp": (d.n_kp_l, d.n_kp_r), "pdesc": (d.n_kp_l, d.n_kp_r), "kl": (d.n_kl_l, d.n_kl_r),
+             "ldesc": (d.n_kl_l, d.n_kl_r)}
+        return {k: a[:n[k.split("_")[0]][0 if k.endswith("_l") else 1]].copy() for k, a in out.items()}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gfpl_detector_destroy(self.h)
+            self.h = None
 
     def __del__(self):
         try:

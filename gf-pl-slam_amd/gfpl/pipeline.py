@@ -114,8 +114,11 @@ class ImagePipeline:
     `consumed` (recorded by the tracker call that reads it, gfpl_frames.ready / consumed),
     so a tracker call on another context waits for exactly that detection and the next
     detection into the same set waits for exactly that read: detecting frame k + 1 while
-    frame k is tracked needs no host synchronisation.  Capacity / octave errors of the
-    asynchronous detectors are reported by status()."""
+    frame k is tracked needs no host synchronisation.  At most `sets` views may be
+    outstanding: detecting into a set whose last view no tracker call has read yet raises
+    (discard() releases a view that will not be tracked).  Capacity / octave errors of the
+    asynchronous detectors are reported by status(); device outputs are complete after
+    synchronize() (status() waits for the detectors' own status words only)."""
 
     def __init__(self, ctx: Context, cam, batch: int, kl_cap: int, nfeatures: int = 2000, lsd: bool = False,
                  cfg=None, sets: int = 2):
@@ -164,6 +167,7 @@ class ImagePipeline:
         self.orb_done = [Event(self.det_orb) for _ in range(sets)]
         self.consumed = [Event(ctx) for _ in range(sets)]
         self.k = 0
+        self._handed = [None] * sets   # consumed[s].record_count when set s's view was returned
         torch.cuda.synchronize(dev)   # the buffers' zero fills (default stream) before any detection
 
     def _begin(self, inputs):
@@ -171,6 +175,9 @@ class ImagePipeline:
         the caller's stream (which produced the inputs); so does the ORB stream"""
         import torch
         s = self.k % self.sets
+        if self._handed[s] is not None and self.consumed[s].record_count <= self._handed[s]:
+            raise RuntimeError(f"ImagePipeline: buffer set {s} still holds a view no tracker call has read "
+                               f"(at most {self.sets} detections may be outstanding; discard() releases one)")
         self.k += 1
         self.consumed[s].wait(self.det)
         self.consumed[s].wait(self.det_orb)
@@ -230,7 +237,16 @@ class ImagePipeline:
         fr = make_frames(B, self.kp_cap, self.kl_cap, arrs)
         fr.ready, fr.consumed = self.ready[s].h, self.consumed[s].h
         fr._events = (self.ready[s], self.consumed[s])
+        self._handed[s] = self.consumed[s].record_count
         return fr
+
+    def discard(self, fr):
+        """release a view no tracker call will read (its set may be detected into again)"""
+        for s in range(self.sets):
+            if fr.consumed == self.consumed[s].h.value:
+                self.consumed[s].record(self.det)
+                return
+        raise ValueError("discard: not a view of this pipeline")
 
     def status(self):
         """capacity / octave errors of the detections since the last status (waits for them)"""

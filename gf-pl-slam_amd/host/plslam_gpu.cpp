@@ -1,7 +1,15 @@
 // plslam_gpu.cpp — the per-frame loop of app/plslam_mod.cpp:318-515 over the
-// StVO host mirror, on synthetic stereo detections (gfpl_synth), GPU only.
+// StVO host mirror, GPU only: on a directory of rectified grey stereo images
+// (--images: detection on the GPU, the reference's insertStereoPair(img_l, img_r,
+// idx, ts) signature) or on synthetic stereo detections (gfpl_synth).
 //
 //   plslam_gpu [--camera vga|euroc|kitti|stress] [--frames N] [--seq S] [--out PREFIX] [--json]
+//              [--images DIR] [--orb-features N]
+//
+// --images DIR reads DIR/left/%06d.pgm and DIR/right/%06d.pgm (binary 8-bit PGM of the
+// camera's size; the reference's app reads its dataset through cv::imread) for frames
+// 0..N-1 (stopping at the first missing pair) and the time stamps from DIR/times.txt
+// (one per line; absent: 0.05 s per frame).
 //
 // Per frame: initialize (frame 0) or insertStereoPair -> optimizePose(prev_frame->DT)
 // -> numFrameLoss check -> needNewKF / currFrameIsKF -> updateFrame_ECCV18(T_base),
@@ -17,6 +25,7 @@
 // MapHandler::addKeyFrame's composition T_kf_w = prev_kf->T_kf_w * curr_kf->T_kf_w
 // (src/mapHandler.cpp:126-127) without the later BA refinements.  --json prints one
 // line per frame with the pose bits, for the parity test against the CPU oracle.
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <chrono>
@@ -98,9 +107,38 @@ static StereoFrame* make_frame(const gfpl_synth_params& sp, PinholeStereoCamera*
                            kls(lr, nlr), rows(ldl, nll), rows(ldr, nlr), std::move(pyr));
 }
 
+// binary PGM (P5, maxval 255): the pixels, or empty if the file is missing or malformed
+static std::vector<uint8_t> read_pgm(const std::string& path, int w, int h) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return {};
+    std::string magic;
+    int W = 0, H = 0, maxval = 0;
+    f >> magic;
+    auto skip = [&]() {   // whitespace and comments between header fields
+        while (f && (std::isspace(f.peek()) || f.peek() == '#')) {
+            if (f.peek() == '#') { std::string line; std::getline(f, line); }
+            else f.get();
+        }
+    };
+    skip(); f >> W; skip(); f >> H; skip(); f >> maxval;
+    if (magic != "P5" || maxval != 255 || !f) return {};
+    f.get();   // the single whitespace before the raster
+    if (W != w || H != h) throw std::runtime_error(path + ": image size differs from the camera's");
+    std::vector<uint8_t> px((size_t)w * h);
+    f.read(reinterpret_cast<char*>(px.data()), (std::streamsize)px.size());
+    if (!f) return {};
+    return px;
+}
+
+static std::string frame_name(const std::string& dir, const char* side, int k) {
+    char b[32];
+    std::snprintf(b, sizeof b, "%06d.pgm", k);
+    return dir + "/" + side + "/" + b;
+}
+
 static int run(int argc, char** argv) {
-    std::string camname = "vga", out;
-    int frames = 10, seq = 0;
+    std::string camname = "vga", out, images;
+    int frames = 10, seq = 0, orb_features = 0;
     bool json = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -113,6 +151,8 @@ static int run(int argc, char** argv) {
         else if (a == "--seq") seq = std::stoi(next());
         else if (a == "--out") out = next();
         else if (a == "--json") json = true;
+        else if (a == "--images") images = next();
+        else if (a == "--orb-features") orb_features = std::stoi(next());
         else { std::cerr << "unknown option " << a << "\n"; return 2; }
     }
     const CamDef* cd = nullptr;
@@ -123,7 +163,13 @@ static int run(int argc, char** argv) {
     gfpl_synth_params sp;
     gfpl_synth_default(&sp);
     if (camname == "kitti") { sp.dt = 0.1; sp.v_fwd = 8.0; sp.z_min = 4.0; sp.z_max = 40.0; }
-    const int kp_cap = 2048, kl_cap = 512;
+    const int kp_cap = images.empty() ? 2048 : 2320, kl_cap = images.empty() ? 512 : 320;
+    if (orb_features > 0) Config::orbNFeatures() = orb_features;
+    std::vector<double> times;
+    if (!images.empty()) {
+        std::ifstream ft(images + "/times.txt");
+        for (double t; ft >> t;) times.push_back(t);
+    }
 
     std::ofstream fAllFrameTrack, fLog;
     if (!out.empty()) {
@@ -140,7 +186,16 @@ static int run(int argc, char** argv) {
     Matrix4d T_kf_w = Matrix4d::Identity();   // the last keyframe's world pose (first KF: frame 0)
     int n_kf = 1;
     for (int k = 0; k < frames; ++k) {
-        StereoFrame* f = make_frame(sp, &cam, seq, k, kp_cap, kl_cap);
+        StereoFrame* f = nullptr;
+        if (images.empty()) {
+            f = make_frame(sp, &cam, seq, k, kp_cap, kl_cap);
+        } else {
+            const std::vector<uint8_t> L = read_pgm(frame_name(images, "left", k), cd->w, cd->h);
+            const std::vector<uint8_t> R = read_pgm(frame_name(images, "right", k), cd->w, cd->h);
+            if (L.empty() || R.empty()) break;
+            const double ts = k < (int)times.size() ? times[k] : 0.05 * k;
+            f = new StereoFrame(L.data(), R.data(), k, &cam, ts);   // = insertStereoPair(img_l, img_r, k, ts)
+        }
         if (k == 0) {
             StVO->initialize(f);
             keyframes.push_back({StVO->prev_frame->time_stamp, T_kf_w});

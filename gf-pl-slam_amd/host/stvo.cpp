@@ -2,6 +2,7 @@
 // every method forwards to libgfpl_hip.so and refreshes the host objects.
 #include "stvo.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <unordered_map>
@@ -64,6 +65,15 @@ StereoFrame::StereoFrame(const int& idx_, PinholeStereoCamera* cam_, const doubl
     if ((int64_t)pyramid_r.size() > cam->pyramidBytes())
         throw std::invalid_argument("StereoFrame: right pyramid larger than the camera's packed pyramid");
     pyramid_r.resize((size_t)cam->pyramidBytes(), 0);
+}
+
+StereoFrame::StereoFrame(const uint8_t* img_l_, const uint8_t* img_r_, const int& idx_, PinholeStereoCamera* cam_,
+                         const double& time_stamp_)
+    : time_stamp(time_stamp_), frame_idx(idx_), cam(cam_) {
+    if (!img_l_ || !img_r_) throw std::invalid_argument("StereoFrame: null image");
+    const size_t n = (size_t)cam->getWidth() * cam->getHeight();
+    gryImg_l.assign(img_l_, img_l_ + n);
+    gryImg_r.assign(img_r_, img_r_ + n);
 }
 
 StereoFrame::~StereoFrame() {
@@ -140,6 +150,7 @@ StereoFrameHandler::~StereoFrameHandler() {
     delete prev_frame;
     delete curr_frame;
     delete buf_;
+    if (det_) gfpl_detector_destroy(det_);
     if (sb_) gfpl_seqbatch_destroy(sb_);
     if (ctx_) gfpl_destroy(ctx_);
 }
@@ -155,7 +166,58 @@ void StereoFrameHandler::sync_config() {
     }
 }
 
+void StereoFrameHandler::detect(StereoFrame* f, gfpl_frames* dev) {
+    gfpl_detector_params p;
+    const gfpl_config c = Config::abi();
+    check(gfpl_detector_params_default(&cam->abi(), &c, &p), "gfpl_detector_params_default");
+    p.orb.nfeatures = Config::orbNFeatures();
+    p.lsd.n_features = Config::lsdNFeatures();
+    p.lsd.min_length = Config::minLineLength() * std::min(cam->getWidth(), cam->getHeight());
+    if (det_ && std::memcmp(&p, &det_prm_, sizeof p) != 0) {
+        check(gfpl_detector_destroy(det_), "gfpl_detector_destroy");
+        det_ = nullptr;
+    }
+    if (!det_) {
+        check(gfpl_detector_create(ctx_, &p, 1, kp_cap_, kl_cap_, 2, &det_), "gfpl_detector_create");
+        det_prm_ = p;
+    }
+    check(gfpl_detect_stereo(det_, f->gryImg_l.data(), f->gryImg_r.data(), 1, &f->time_stamp, 1, dev),
+          "gfpl_detect_stereo");
+}
+
+// points_l / points_r / pdesc_* / lines_* / ldesc_* as detectFeatures leaves them
+// (src/stereoFrame.cpp:1128-1227), before the stereo matching reorders pdesc_l / ldesc_l
+void StereoFrameHandler::pull_detections(StereoFrame* f, const gfpl_frames& dev) {
+    HostBuf& h = *buf_;
+    gfpl_detections_host d{};
+    d.kp_l = h.kp_l.data(); d.kp_r = h.kp_r.data(); d.kl_l = h.kl_l.data(); d.kl_r = h.kl_r.data();
+    d.pdesc_l = h.in_pdesc_l.data(); d.pdesc_r = h.in_pdesc_r.data();
+    d.ldesc_l = h.in_ldesc_l.data(); d.ldesc_r = h.in_ldesc_r.data();
+    check(gfpl_read_detections(ctx_, &dev, 0, &d), "gfpl_read_detections");
+    auto kps = [](const std::vector<gfpl_keypoint>& v, int n, std::vector<KeyPoint>& o) {
+        o.resize(n);
+        for (int i = 0; i < n; ++i) o[i] = {v[i].x, v[i].y, v[i].octave};
+    };
+    auto kls = [](const std::vector<gfpl_keyline>& v, int n, std::vector<KeyLine>& o) {
+        o.resize(n);
+        for (int i = 0; i < n; ++i) o[i] = {v[i].sx, v[i].sy, v[i].ex, v[i].ey, v[i].angle, v[i].octave};
+    };
+    auto rows = [](const std::vector<uint8_t>& v, int n, std::vector<Descriptor>& o) {
+        o.resize(n);
+        for (int i = 0; i < n; ++i) std::memcpy(o[i].data(), &v[32 * (size_t)i], 32);
+    };
+    kps(h.kp_l, d.n_kp_l, f->points_l); kps(h.kp_r, d.n_kp_r, f->points_r);
+    kls(h.kl_l, d.n_kl_l, f->lines_l); kls(h.kl_r, d.n_kl_r, f->lines_r);
+    rows(h.in_pdesc_l, d.n_kp_l, f->pdesc_l); rows(h.in_pdesc_r, d.n_kp_r, f->pdesc_r);
+    rows(h.in_ldesc_l, d.n_kl_l, f->ldesc_l); rows(h.in_ldesc_r, d.n_kl_r, f->ldesc_r);
+}
+
 void StereoFrameHandler::upload(StereoFrame* f, gfpl_frames* dev) {
+    if (f->hasImages()) {
+        detect(f, dev);
+        pull_detections(f, *dev);   // (the view stays valid: its buffer set is reused two detections later)
+        return;
+    }
     HostBuf& h = *buf_;
     const int nkl = (int)f->points_l.size(), nkr = (int)f->points_r.size();
     const int nll = (int)f->lines_l.size(), nlr = (int)f->lines_r.size();
@@ -323,6 +385,15 @@ void StereoFrameHandler::insertStereoPair(StereoFrame* frame) {
     lg.num_ln_stereo = (double)curr_frame->stereo_ls.size();
     lg.num_pt_cross = (double)matched_pt.size();
     lg.num_ln_cross = (double)matched_ls.size();
+}
+
+void StereoFrameHandler::initialize(const uint8_t* img_l, const uint8_t* img_r, const int idx, const double time_stamp) {
+    initialize(new StereoFrame(img_l, img_r, idx, cam, time_stamp));
+}
+
+void StereoFrameHandler::insertStereoPair(const uint8_t* img_l, const uint8_t* img_r, const int idx,
+                                          const double time_stamp) {
+    insertStereoPair(new StereoFrame(img_l, img_r, idx, cam, time_stamp));
 }
 
 void StereoFrameHandler::stereoMatching(StereoFrame* frame) {

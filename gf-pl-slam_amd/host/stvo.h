@@ -7,9 +7,13 @@
 // keeps the names, public members and call order a caller such as
 // app/plslam_mod.cpp:375-477, KeyFrame (src/keyFrame.cpp:26-58) or MapHandler
 // relies on, with these deliberate differences:
-//  * detection is out of scope: a StereoFrame is built from injected keypoints,
-//    keylines, descriptors and the right ORB pyramid (the reference's own
-//    simulator does the same through public members, src/simulate_line_cut.cpp:62-212);
+//  * a StereoFrame is built either from a grey stereo pair, as the reference's
+//    StereoFrame(img_l, img_r, idx, cam, ts) (detection then runs on the GPU,
+//    gfpl_detector: ORB, LSD, LBD), or from injected keypoints, keylines,
+//    descriptors and the right ORB pyramid (the reference's own simulator does the
+//    same through public members, src/simulate_line_cut.cpp:62-212);
+//  * images are raw 8-bit grey rows of the camera's width x height (cv::Mat
+//    CV_8UC1 data); colour conversion is the caller's;
 //  * Eigen / OpenCV are not available: Vector*/Matrix* are small row-major value
 //    types with the same element access (operator()), KeyPoint/KeyLine carry the
 //    fields the path reads;
@@ -104,6 +108,10 @@ public:
     static double& orbScaleFactor() { return getInstance().c.orb_scale_factor; }
     static int& orbNLevels() { return getInstance().c.orb_n_levels; }
     static double& lsdScale() { return getInstance().c.lsd_scale; }
+    // detection (src/config.cpp:107,134,143): used by the image-input calls
+    static int& orbNFeatures() { return getInstance().orb_nfeatures; }
+    static int& lsdNFeatures() { return getInstance().lsd_nfeatures; }
+    static double& minLineLength() { return getInstance().min_line_length; }
     static double& minEntropyRatio() { return getInstance().c.min_entropy_ratio; }
     static int& maxKFNumFrames() { return getInstance().c.max_kf_num_frames; }
     // the C-ABI view (bools folded in)
@@ -113,6 +121,8 @@ private:
     Config();
     gfpl_config c{};
     bool best_lr_matches = true, lr_in_parallel = true, use_line_conf_cut = true, max_vol_line_cut = true;
+    int orb_nfeatures = 1000, lsd_nfeatures = 300;
+    double min_line_length = 0.025;
 };
 
 // ---------------------------------------------------- PinholeStereoCamera --
@@ -192,11 +202,18 @@ struct TimeLog {
 };
 
 // ----------------------------------------------------------- StereoFrame --
-// include/stereoFrame.h:89-260.  Built from injected detections; after the
-// handler matched it, stereo_pt / stereo_ls and the reordered pdesc_l / ldesc_l
-// hold the stereo features exactly as extractStereoFeatures_ORBSLAM leaves them.
+// include/stereoFrame.h:89-260.  Built from a grey stereo pair (the handler
+// detects it on the GPU and fills points_* / lines_* / *desc_* as
+// detectFeatures does) or from injected detections; after the handler matched
+// it, stereo_pt / stereo_ls and the reordered pdesc_l / ldesc_l hold the stereo
+// features exactly as extractStereoFeatures_ORBSLAM leaves them.
 class StereoFrame {
 public:
+    // StereoFrame(img_l, img_r, idx, cam, time_stamp) (src/stereoFrame.cpp:46-60): the two
+    // grey images (cam width x height bytes each) are copied; detection runs when the
+    // handler takes the frame
+    StereoFrame(const uint8_t* img_l_, const uint8_t* img_r_, const int& idx_, PinholeStereoCamera* cam_,
+                const double& time_stamp_);
     StereoFrame(const int& idx_, PinholeStereoCamera* cam_, const double& time_stamp_,
                 std::vector<KeyPoint> points_l_, std::vector<KeyPoint> points_r_,
                 std::vector<Descriptor> pdesc_l_, std::vector<Descriptor> pdesc_r_,
@@ -224,7 +241,10 @@ public:
     std::vector<KeyPoint> points_l, points_r;
     std::vector<KeyLine> lines_l, lines_r;
     std::vector<Descriptor> pdesc_l, pdesc_r, ldesc_l, ldesc_r;
-    std::vector<uint8_t> pyramid_r;   // right ORB pyramid, levels packed (cam->pyramidBytes())
+    std::vector<uint8_t> pyramid_r;   // right ORB pyramid, levels packed (cam->pyramidBytes()); empty
+                                      // for an image frame (its pyramid stays on the device)
+    std::vector<uint8_t> gryImg_l, gryImg_r;   // image frames: the grey pair (else empty)
+    bool hasImages() const { return !gryImg_l.empty(); }
 
     PinholeStereoCamera* cam;
 
@@ -245,6 +265,10 @@ public:
     void initialize(StereoFrame* frame);
     // src/stereoFrameHandler.cpp:83-151 (takes ownership of the frame)
     void insertStereoPair(StereoFrame* frame);
+    // the reference's image signatures (include/stereoFrameHandler.h:48-53, called at
+    // app/plslam_mod.cpp:377,387): a StereoFrame of the grey pair, detected on the GPU
+    void initialize(const uint8_t* img_l, const uint8_t* img_r, const int idx, const double time_stamp);
+    void insertStereoPair(const uint8_t* img_l, const uint8_t* img_r, const int idx, const double time_stamp);
     // src/stereoFrameHandler.cpp:1939-2030; the app calls optimizePose(prev_frame->DT)
     void optimizePose(Matrix4d DT_ini);
     // src/stereoFrameHandler.cpp:864-922 (prev <- curr; logs T_base * old prev Tfw)
@@ -281,7 +305,9 @@ public:
 
 private:
     void sync_config();
-    void upload(StereoFrame* f, gfpl_frames* dev);
+    void upload(StereoFrame* f, gfpl_frames* dev);   // detects an image frame, uploads an injected one
+    void detect(StereoFrame* f, gfpl_frames* dev);
+    void pull_detections(StereoFrame* f, const gfpl_frames& dev);
     void pull(int which, StereoFrame* f, bool features, bool pose);
     void pull_track();
     void pull_kf();
@@ -289,6 +315,8 @@ private:
 
     gfpl_ctx* ctx_ = nullptr;
     gfpl_seqbatch* sb_ = nullptr;
+    gfpl_detector* det_ = nullptr;   // created at the first image frame (and when the detection config changes)
+    gfpl_detector_params det_prm_{};
     int kp_cap_, kl_cap_;
     gfpl_config cfg_{};
     struct HostBuf;   // gfpl_frame_host backing store

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GFPL_ABI_VERSION 3
+#define GFPL_ABI_VERSION 4
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
@@ -259,7 +259,11 @@ int  gfpl_event_destroy(gfpl_event* ev);
 int  gfpl_event_record(gfpl_event* ev, gfpl_ctx* ctx);
 int  gfpl_event_wait(gfpl_ctx* ctx, gfpl_event* ev);
 int  gfpl_event_synchronize(gfpl_event* ev);
-/* GFPL_E_STATE while seqbatches created on the context are still alive.       */
+/* how often the event was recorded so far (gfpl_event_record, or by a tracker call as a
+ * gfpl_frames.consumed event): a producer reusing buffers checks its views were read.  */
+int  gfpl_event_record_count(const gfpl_event* ev, int64_t* count);
+/* GFPL_E_STATE while seqbatches or ORB / LBD / LSD objects created on the context
+ * are still alive (they use its stream; ORB also reads its camera).           */
 int  gfpl_destroy(gfpl_ctx* ctx);
 int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
 /* max_point_match_num / max_line_match_num size the matched lists and the cut /
@@ -453,6 +457,65 @@ int  gfpl_lsd_status(gfpl_lsd* lsd);
  * each element, on DEVICE memory (n <= (width-1)(height-1)); the permutation the seed order
  * and the response sort use.  Synchronises.                                                 */
 int  gfpl_lsd_sort_desc(gfpl_lsd* lsd, uint64_t* a, int n);
+
+/* ------------------------------- stereo detection from images (§8(f)1-2) ---- */
+/* The detection half of StereoFrame(img_l, img_r, idx, cam, ts) as
+ * StereoFrameHandler::initialize / insertStereoPair(const Mat& img_l, const Mat& img_r,
+ * int idx, double ts) run it (include/stereoFrameHandler.h:48-53, src/stereoFrame.cpp:
+ * 148-172, 411-450, 1128-1227; called at app/plslam_mod.cpp:377,387): ORB of both images
+ * (the right one's pyramid kept for the sub-pixel refinement), LSD of both with the
+ * lsdNFeatures response cut, LBD of both — for B stereo frames, into device buffers a
+ * gfpl_frames view points at, so gfpl_initialize / gfpl_insert_stereo_pair / gfpl_frame_step
+ * read them without a copy.  The detector runs on two streams of its own; the view's
+ * `ready` event orders the tracker call after the detection and its `consumed` event
+ * (recorded by that tracker call) orders the next detection into the same buffer set
+ * (`sets` of them, used in turn) after the read.                                        */
+typedef struct gfpl_detector_params {
+    gfpl_orb_params orb;   /* Config::orbNFeatures / orbScaleFactor / orbNLevels, 20, 7     */
+    gfpl_lsd_params lsd;   /* the LSDOptions + lsdNFeatures + min line length              */
+    int seg_cap;           /* raw LSD segments per image (GFPL_E_CAPACITY beyond), 4096     */
+} gfpl_detector_params;
+typedef struct gfpl_detector gfpl_detector;
+/* the reference's Config defaults (src/config.cpp:107,134-152) for this camera; cfg NULL =
+ * gfpl_config_default.  (BASELINE cfg 2 runs orb.nfeatures = 2000.)                      */
+int  gfpl_detector_params_default(const gfpl_camera* cam, const gfpl_config* cfg, gfpl_detector_params* prm);
+/* On a context with a camera (GFPL_E_STATE otherwise); images are the camera's size, up
+ * to max_batch stereo frames per call; kp_cap / kl_cap rows per image (as the seqbatch's);
+ * sets 1..4 buffer sets.  The context cannot be destroyed while the detector lives.      */
+int  gfpl_detector_create(gfpl_ctx* ctx, const gfpl_detector_params* prm, int max_batch, int kp_cap,
+                          int kl_cap, int sets, gfpl_detector** out);
+int  gfpl_detector_destroy(gfpl_detector* det);
+/* Stream-ordered detection of n stereo frames: img_l / img_r DEVICE [n][H][W] u8 and
+ * time_stamp DEVICE [n], produced on the context's stream (the detection waits for it).
+ * *out is the view of the next buffer set (valid until that set is detected into again).
+ * GFPL_E_STATE when the set's previous view was never read by a tracker call (nor
+ * released with gfpl_detector_discard): at most `sets` views may be outstanding.       */
+int  gfpl_detect_stereo_async(gfpl_detector* det, const uint8_t* img_l, const uint8_t* img_r, int n,
+                              const double* time_stamp, gfpl_frames* out);
+/* The same from HOST images / time stamps (copied before it returns; the detection
+ * itself stays asynchronous).                                                            */
+int  gfpl_detect_stereo_host(gfpl_detector* det, const uint8_t* img_l, const uint8_t* img_r, int n,
+                             const double* time_stamp, gfpl_frames* out);
+/* capacity / octave errors of the detections since the last status (waits for them) */
+int  gfpl_detector_status(gfpl_detector* det);
+/* detect (host_pointers: the _host form) + status: returns after the detection finished */
+int  gfpl_detect_stereo(gfpl_detector* det, const uint8_t* img_l, const uint8_t* img_r, int n,
+                        const double* time_stamp, int host_pointers, gfpl_frames* out);
+/* release a view no tracker call will read (its set may then be detected into again) */
+int  gfpl_detector_discard(gfpl_detector* det, const gfpl_frames* view);
+
+/* Host copy of one sequence's detections of a DEVICE gfpl_frames view (the
+ * points_l / points_r / pdesc_* / lines_* / ldesc_* members of the reference's StereoFrame
+ * after detection).  Arrays are caller-allocated at the view's kp_cap / kl_cap (a NULL
+ * array is skipped); waits for the view's `ready` event.                               */
+typedef struct gfpl_detections_host {
+    int n_kp_l, n_kp_r, n_kl_l, n_kl_r;
+    gfpl_keypoint* kp_l;  gfpl_keypoint* kp_r;
+    uint8_t* pdesc_l;     uint8_t* pdesc_r;   /* [cap][32] */
+    gfpl_keyline* kl_l;   gfpl_keyline* kl_r;
+    uint8_t* ldesc_l;     uint8_t* ldesc_r;   /* [cap][32] */
+} gfpl_detections_host;
+int  gfpl_read_detections(gfpl_ctx* ctx, const gfpl_frames* view, int seq, gfpl_detections_host* out);
 
 /* ------------------------------------------------- keyframe consumers ---- */
 /* One keyframe's stereo features as KeyFrame::stereo_frame exposes them

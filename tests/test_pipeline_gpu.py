@@ -74,7 +74,8 @@ def test_images_to_poses_match_the_oracle_pipeline(disparity):
         fr = pipe.detect(left, right, to(kl[0]), torch.from_numpy(n[0]).to(dev), to(kl[1]),
                          torch.from_numpy(n[1]).to(dev), torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
         hfr, harr = _host_frames(cam, scenes, KP, KL, 0.05 * k)
-        pipe.status()   # waits for the detection stream; capacity errors raise
+        pipe.status()   # capacity errors raise
+        pipe.synchronize()   # every device output (the time stamps' copy included) is complete
         # the device detections are the oracle's, byte for byte (valid rows; the device
         # buffers keep stale rows past each count)
         d = [t.cpu().numpy() for t in fr._keep]
@@ -138,6 +139,7 @@ def test_images_to_poses_with_lsd_on_device():
         fr = pipe.detect_images(left, right, torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev))
         hfr, harr = _host_frames(cam, scenes, KP, KL, 0.05 * k)
         pipe.status()
+        pipe.synchronize()
         d = [t.cpu().numpy() for t in fr._keep]
         for side in range(2):
             nl_d = d[6 + side]
