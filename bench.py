@@ -75,6 +75,11 @@ WORKLOADS = {
     "cfg4": ("euroc", dict(z_min=2.0, z_max=12.0, respawn=16),
              "cfg4: EuRoC 752x480 rig on the MH_01..V1_03 ground-truth trajectories (rank mod 8), "
              "2000 ORB + 500 LBD, 10+10 GN iters"),
+    # cfg2 with 10% of the true observations displaced 3-8 px per frame: the pose optimisation's
+    # outlier branch (removeOutliers) and the MAD path run on a non-empty outlier set
+    "cfg2o": ("vga", dict(respawn=16, outlier_frac=0.1),
+              "cfg2o: cfg2 with 10% outlier observations (3-8 px displacements), 2000 ORB + 500 LBD per side, "
+              "10+10 GN iters"),
     # BASELINE configs[4]: stress, 8000 ORB + 2000 LBD per 1920x1080 frame, line cut on
     "cfg5": ("stress", dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=3200, z_max=12.0, respawn=16),
              "cfg5: stress 1920x1080 stereo (gazebo x3), 8000 ORB + 2000 LBD per side, good-line-cut on, "
@@ -634,7 +639,7 @@ def main():
     if sampler:
         sampler.initialize(h)
     step_s = []
-    stage_ms, stage_bytes, kern_ms, kern_bytes, counts = [], [], [], [], []
+    stage_ms, stage_bytes, kern_ms, kern_bytes, counts, cutc = [], [], [], [], [], []
     ctx.set_timing(True)
     for k in range(1, 1 + W + K):
         t0 = time.perf_counter()
@@ -654,6 +659,7 @@ def main():
             kern_ms.append(ctx.kernel_times())
             kern_bytes.append(h.last_step_kernel_bytes())
             counts.append(h.last_step_counts())
+            cutc.append(h.last_step_track_counts())
         if sampler:
             sampler.step(h, k)
         if rank == 0:   # progress (stderr): long runs under a watchdog keep writing
@@ -710,6 +716,10 @@ def main():
             except Exception as e:   # reported, never fatal to the contract line
                 det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}
         cmean = {n: round(float(np.mean([c[n] for c in counts])), 1) for n in gfpl.StereoFrameHandler.STEP_COUNTS}
+        # matched entries the pose optimisation flagged as outliers (removeOutliers); n_inliers
+        # above is the insert's (the list sizes), before optimize_pose
+        cmean["outliers_after_pose"] = round(float(np.mean([c["M_p"] + c["M_l"] for c in counts]) -
+                                                 np.mean([c["inliers_after_pose"] for c in cutc]) / B), 1)
         crange = {n: [round(float(min(c[n] for c in counts)), 1), round(float(max(c[n] for c in counts)), 1)]
                   for n in ("S_p", "S_l", "M_o", "M_p", "M_l")}
         out = {
@@ -746,6 +756,11 @@ def main():
                                            "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise "
                                            "vs the CPU oracle (oracle/)",
                                "first": sampler.msgs[:3] if sampler else []},
+            "cut_search": {"steps": int(sum(c["steps"] for c in cutc)),
+                           "exact_steps": int(sum(c["exact_steps"] for c in cutc)),
+                           "exact_frac": float(sum(c["exact_steps"] for c in cutc) / max(1, sum(c["steps"] for c in cutc))),
+                           "note": "greedy steps of the timed window; exact_steps: evaluated with the reference's own "
+                                   "arithmetic because a margin or the proven agreement bound failed (DESIGN.md §3)"},
             "host_fed": host_fed,
             "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES, sm)},
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},

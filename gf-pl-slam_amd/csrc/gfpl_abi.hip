@@ -1120,6 +1120,15 @@ int gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8) {
     return GFPL_OK;
 }
 
+int gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4) {
+    if (!sb || !counts4) return GFPL_E_INVALID;
+    int64_t v[STEP_REC];
+    int e = step_rec_sums(sb, v);
+    if (e) return e;
+    for (int s = 0; s < 4; ++s) counts4[s] = v[16 + s];
+    return GFPL_OK;
+}
+
 int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {
     if (!bytes) return GFPL_E_INVALID;
     int64_t v[7];

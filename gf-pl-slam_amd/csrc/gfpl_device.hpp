@@ -271,11 +271,58 @@ GFPL_DEV void mat4_vec(const double* M, const double* v, double* o) {
     for (int i = 0; i < 4; ++i) o[i] = t[i];
 }
 
-GFPL_DEV void se3_apply(const double* T, const double* P, double* o) {
+// ---- running error bounds (Wilkinson's running error analysis, used by the line cut's
+// certification).  An RB stands for a double the kernel computes from exact
+// inputs: m bounds |computed| and |exact| (the value of the same expression in real
+// arithmetic on the same inputs), e bounds |computed - exact|, lo (when known, else 0) bounds
+// min(|computed|, |exact|) from below — needed only for divisors.  The inputs of a range of
+// calls (a cut ratio c in [0, C]) enter with m = C, so the bounds hold for every c of the range.
+// The same templated code runs on double (the kernel's arithmetic) and on RB (its bounds), so
+// the bounds follow the kernel's expression trees exactly.  Every rounding costs u = 2^-53 of
+// the result's magnitude; the bound arithmetic itself is rounded, which the callers absorb in a
+// final relative slop factor.
+struct RB {
+    double m, e, lo;
+    GFPL_DEV RB() : m(0.0), e(0.0), lo(0.0) {}
+    GFPL_DEV RB(double x) : m(fabs(x)), e(0.0), lo(fabs(x)) {}
+    GFPL_DEV RB(double m_, double e_, double lo_) : m(m_), e(e_), lo(lo_) {}
+};
+constexpr double RB_U = 0x1p-53;
+GFPL_DEV RB operator+(const RB& a, const RB& b) {
+    const double m = a.m + b.m;
+    return RB(m * (1.0 + 4.0 * RB_U), a.e + b.e + RB_U * m, 0.0);
+}
+GFPL_DEV RB operator-(const RB& a, const RB& b) { return a + b; }
+GFPL_DEV RB operator-(const RB& a) { return a; }
+GFPL_DEV RB operator*(const RB& a, const RB& b) {
+    const double m = a.m * b.m;
+    return RB(m * (1.0 + 4.0 * RB_U), a.e * b.m + a.m * b.e + RB_U * m, a.lo * b.lo * (1.0 - 4.0 * RB_U));
+}
+GFPL_DEV RB operator/(const RB& a, const RB& b) {
+    if (!(b.lo > 0.0)) return RB(__builtin_inf(), __builtin_inf(), 0.0);
+    const double m = a.m / b.lo;
+    return RB(m * (1.0 + 4.0 * RB_U), a.e / b.lo + (a.m / b.lo) * (b.e / b.lo) + RB_U * m,
+              (a.lo / b.m) * (1.0 - 4.0 * RB_U));
+}
+// max is 1-Lipschitz: |max(h, x^) - max(h, x*)| <= |x^ - x*|
+GFPL_DEV RB ref_max(double h, const RB& x) {
+    const double ah = fabs(h);
+    return RB(ah > x.m ? ah : x.m, x.e, ah > x.lo ? ah : x.lo);
+}
+// a divisor's known lower bound (the exact value's, lo_exact), applied to the computed one
+GFPL_DEV void rb_floor(double&, double) {}
+GFPL_DEV void rb_floor(RB& z, double lo_exact) {
+    const double l = lo_exact - z.e;
+    if (l > z.lo) z.lo = l;
+}
+
+template <typename T, typename M>
+GFPL_DEV void se3_apply_t(const M* Tm, const T* P, T* o) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-        o[i] = ((T[i * 4 + 0] * P[0] + T[i * 4 + 1] * P[1]) + T[i * 4 + 2] * P[2]) + T[i * 4 + 3];
+        o[i] = ((T(Tm[i * 4 + 0]) * P[0] + T(Tm[i * 4 + 1]) * P[1]) + T(Tm[i * 4 + 2]) * P[2]) + T(Tm[i * 4 + 3]);
 }
+GFPL_DEV void se3_apply(const double* T, const double* P, double* o) { se3_apply_t<double, double>(T, P, o); }
 
 GFPL_DEV void skew3(const double* v, double* S) {
     S[0] = 0; S[1] = -v[2]; S[2] = v[1];
@@ -727,16 +774,20 @@ GFPL_DEV double div_by(const SharedDiv& d, double a) {
 }
 // Jacobian of a projected residual wrt the pose, weights (lx, ly)
 // (src/stereoFrameHandler.cpp:1383-1388, 1438-1443, 2150-2155, 2197-2202)
-GFPL_DEV void poseJac(const DevCam& c, double homog, const double* g, double lx, double ly, double* J) {
-    double gx = g[0], gy = g[1], gz = g[2];
-    double gz2 = gz * gz;
-    double fgz2 = c.fx / ref_max(homog, gz2);
+template <typename T>
+GFPL_DEV void poseJac_t(const DevCam& c, double homog, const T* g, T lx, T ly, T* J) {
+    T gx = g[0], gy = g[1], gz = g[2];
+    T gz2 = gz * gz;
+    T fgz2 = T(c.fx) / ref_max(homog, gz2);
     J[0] = (fgz2 * lx) * gz;
     J[1] = (fgz2 * ly) * gz;
     J[2] = (-fgz2) * ((gx * lx) + (gy * ly));
     J[3] = (-fgz2) * ((((gx * gy) * lx) + ((gy * gy) * ly)) + ((gz * gz) * ly));
     J[4] = fgz2 * ((((gx * gx) * lx) + ((gz * gz) * lx)) + ((gx * gy) * ly));
     J[5] = fgz2 * (((gx * gz) * ly) - ((gy * gz) * lx));
+}
+GFPL_DEV void poseJac(const DevCam& c, double homog, const double* g, double lx, double ly, double* J) {
+    poseJac_t<double>(c, homog, g, lx, ly, J);
 }
 
 // endpoint 3x3 covariance of the stereo line gate (src/stereoFrame.cpp:707-742)

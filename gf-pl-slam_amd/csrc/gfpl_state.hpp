@@ -72,10 +72,12 @@ struct DevTrack {
     int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
-#define STEP_REC 16   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
-                      // [8..15] counts N_o N_k M_o S_p' S_l' M_p M_l n_inliers (gfpl_last_step_counts)
-#define CUT_FAST 48   // doubles of per-line comparison polynomials (k_cut.hip, PD_*)
-#define CUT_REC 72    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (576 B)
+#define STEP_REC 20   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
+                      // [8..15] counts N_o N_k M_o S_p' S_l' M_p M_l n_inliers (gfpl_last_step_counts),
+                      // [16] line-cut search steps, [17] of them evaluated exactly (k_cut_search),
+                      // [18] n_inliers after optimize_pose (k_pose_finish), [19] 0
+#define CUT_FAST 56   // doubles of per-line comparison data (k_cut.hip, PD_*): polynomials, flags, error bounds
+#define CUT_REC 80    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (640 B)
 
 struct DevScratch {
     double* cut_rec;  // [B*mls_cap*CUT_REC] per matched line: P(t) coefficients of both cut endpoints, v'(t)

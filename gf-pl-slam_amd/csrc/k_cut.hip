@@ -22,25 +22,29 @@ struct LineCutData {
     double sP[3], eP[3], covS[9], covE[9], Jl[2];
 };
 
-// projected residual variance of one cut endpoint (src/stereoFrameHandler.cpp:1356-1369)
-__device__ __forceinline__ double endpointVar(const DevCam& cam, const double* DT_inv, const double* Jl,
-                                              const double* Pt, const double* cov) {
-    double Jdt[9];
+// projected residual variance of one cut endpoint (src/stereoFrameHandler.cpp:1356-1369).
+// Templated: T = double is the kernel's arithmetic, T = RB its running error bounds (the
+// point's depth then takes the lower bound zlo, see rb_floor).
+template <typename T>
+__device__ __forceinline__ T endpointVar_t(const DevCam& cam, const double* DT_inv, const T* Jl, const T* Pt,
+                                           const T* cov, double zlo) {
+    T Jdt[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) Jdt[i * 3 + j] = DT_inv[i * 4 + j];
-    double cur[3];
-    se3_apply(DT_inv, Pt, cur);
+        for (int j = 0; j < 3; ++j) Jdt[i * 3 + j] = T(DT_inv[i * 4 + j]);
+    T cur[3];
+    se3_apply_t<T, double>(DT_inv, Pt, cur);
+    rb_floor(cur[2], zlo);
     // getJacob3D_2D (src/stereoFrame.cpp:1394-1412)
-    const double f = cam.fx, pz = cur[2], pz_2 = pz * pz;
-    double Jp[9];
-    Jp[0] = f / pz; Jp[3] = 0.0; Jp[6] = 0.0;
-    Jp[1] = 0.0; Jp[4] = f / pz; Jp[7] = 0.0;
+    const T f = T(cam.fx), pz = cur[2], pz_2 = pz * pz;
+    T Jp[9];
+    Jp[0] = f / pz; Jp[3] = T(0.0); Jp[6] = T(0.0);
+    Jp[1] = T(0.0); Jp[4] = f / pz; Jp[7] = T(0.0);
     Jp[2] = ((-f) * cur[0]) / pz_2;
     Jp[5] = ((-f) * cur[1]) / pz_2;
-    Jp[8] = ((-f) * cam.b) / pz_2;
-    double T1[6], T2[6], T3[6], M[4];
+    Jp[8] = ((-f) * T(cam.b)) / pz_2;
+    T T1[6], T2[6], T3[6], M[4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -61,8 +65,8 @@ __device__ __forceinline__ double endpointVar(const DevCam& cam, const double* D
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             M[i * 2 + j] = (T3[i * 3 + 0] * Jp[j * 3 + 0] + T3[i * 3 + 1] * Jp[j * 3 + 1]) + T3[i * 3 + 2] * Jp[j * 3 + 2];
-    const double r0 = Jl[0] * M[0] + Jl[1] * M[2];
-    const double r1 = Jl[0] * M[1] + Jl[1] * M[3];
+    const T r0 = Jl[0] * M[0] + Jl[1] * M[2];
+    const T r1 = Jl[0] * M[1] + Jl[1] * M[3];
     return r0 * Jl[0] + r1 * Jl[1];
 }
 
@@ -72,20 +76,27 @@ __device__ __forceinline__ double endpointVar(const DevCam& cam, const double* D
 // Start endpoint: (sP, eP, covS, covE, c0); end endpoint: (eP, sP, covE, covS, c1).
 // The start terms depend on c0 only and the end terms on c1 only, which the
 // search exploits.
+template <typename T>
+__device__ __forceinline__ void cut_endpoint_t(const DevCam& cam, double homog, const double* DT_inv, const T* Jl,
+                                               const T* P0, const T* P1, const T* C0, const T* C1, T c, T* out7,
+                                               double zlo) {
+    T Pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Pt[k] = (T(1.0) - c) * P0[k] + c * P1[k];
+    const T a = (T(1.0) - c) * (T(1.0) - c), q = c * c;
+    T cov[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
+    out7[0] = endpointVar_t<T>(cam, DT_inv, Jl, Pt, cov, zlo);
+    T cur[3];
+    se3_apply_t<T, double>(DT_inv, Pt, cur);
+    rb_floor(cur[2], zlo);
+    poseJac_t<T>(cam, homog, cur, Jl[0], Jl[1], out7 + 1);
+}
 __device__ __forceinline__ void cut_endpoint(const DevCam& cam, double homog, const double* DT_inv, const double* Jl,
                                              const double* P0, const double* P1, const double* C0, const double* C1,
                                              double c, double* out7) {
-    double Pt[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Pt[k] = (1 - c) * P0[k] + c * P1[k];
-    const double a = (1 - c) * (1 - c), q = c * c;
-    double cov[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
-    out7[0] = endpointVar(cam, DT_inv, Jl, Pt, cov);
-    double cur[3];
-    se3_apply(DT_inv, Pt, cur);
-    poseJac(cam, homog, cur, Jl[0], Jl[1], out7 + 1);
+    cut_endpoint_t<double>(cam, homog, DT_inv, Jl, P0, P1, C0, C1, c, out7, 0.0);
 }
 
 // info = [Js Je] inv(diag(vs, ve)) [Js Je]^T, Eigen 2x2 inverse via invdet (ledger Q10)
@@ -153,26 +164,30 @@ __device__ __forceinline__ void load_line(const DevLines& L, size_t q, LineCutDa
 #define PD_VE 41     // v'_e(t) [5]
 #define PD_OK 46     // 1.0: gz^2 > 2 homog_th at both ends, one sign (fgz2 = fx / gz^2 on the segment)
 #define PD_NEXT 47   // list index of the line after this one (k_cut_search's prefetch)
-static_assert(CUT_FAST == 48, "per-line comparison data layout");
+#define PD_ERR 48    // k_cut_bounds: 14 floats (rounded up) packed in 7 doubles, per side (start, end):
+                     // eP[6] (|P(t) - P*(t)|, ours + the reference's endpoint Jacobian in P units) | ev
+                     // (|v'(t) - v'*(t)|), valid for every t of the range; +inf: no margined steps
+static_assert(CUT_FAST == 56, "per-line comparison data layout");
 
 // x^T A y, A symmetric packed (xx xy xz yy yz zz)
-__device__ __forceinline__ double sym3(const double* A, const double* x, const double* y) {
-    const double ax = (A[0] * y[0] + A[1] * y[1]) + A[2] * y[2];
-    const double ay = (A[1] * y[0] + A[3] * y[1]) + A[4] * y[2];
-    const double az = (A[2] * y[0] + A[4] * y[1]) + A[5] * y[2];
+template <typename T>
+__device__ __forceinline__ T sym3_t(const T* A, const T* x, const T* y) {
+    const T ax = (A[0] * y[0] + A[1] * y[1]) + A[2] * y[2];
+    const T ay = (A[1] * y[0] + A[3] * y[1]) + A[4] * y[2];
+    const T az = (A[2] * y[0] + A[4] * y[1]) + A[5] * y[2];
     return (x[0] * ax + x[1] * ay) + x[2] * az;
 }
 
 // coefficient k of P(t) for the blend g0 -> g1 (poseJac's six terms without fgz2)
-__device__ __forceinline__ void cut_poly_coeff(const double* g0, const double* g1, double lx, double ly, int k,
-                                               double* Pk) {
-    const double dx = g1[0] - g0[0], dy = g1[1] - g0[1], dz = g1[2] - g0[2];
+template <typename T>
+__device__ __forceinline__ void cut_poly_coeff_t(const T* g0, const T* g1, T lx, T ly, int k, T* Pk) {
+    const T dx = g1[0] - g0[0], dy = g1[1] - g0[1], dz = g1[2] - g0[2];
     // coefficient k of the product (a0 + t a1)(b0 + t b1)
-    auto prod = [&](double a0, double a1, double b0, double b1) {
+    auto prod = [&](T a0, T a1, T b0, T b1) -> T {
         return k == 0 ? a0 * b0 : (k == 1 ? a0 * b1 + a1 * b0 : a1 * b1);
     };
-    auto lin = [&](double a0, double a1) { return k == 0 ? a0 : (k == 1 ? a1 : 0.0); };
-    const double x0 = g0[0], y0 = g0[1], z0 = g0[2];
+    auto lin = [&](T a0, T a1) -> T { return k == 0 ? a0 : (k == 1 ? a1 : T(0.0)); };
+    const T x0 = g0[0], y0 = g0[1], z0 = g0[2];
     Pk[0] = lx * lin(z0, dz);
     Pk[1] = ly * lin(z0, dz);
     Pk[2] = -(lx * lin(x0, dx) + ly * lin(y0, dy));
@@ -181,44 +196,57 @@ __device__ __forceinline__ void cut_poly_coeff(const double* g0, const double* g
     Pk[5] = ly * prod(x0, dx, z0, dz) - lx * prod(y0, dy, z0, dz);
 }
 
-__device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutData& d, double homog, double* fd) {
-    double g[2][3];
-    se3_apply(Dl, d.sP, g[0]);
-    se3_apply(Dl, d.eP, g[1]);
-    double A[2][6];   // R covS R^T, R covE R^T
-    const double* Cs[2] = {d.covS, d.covE};
+// The comparison polynomials' coefficients of one line: P [side][k][6] (side 0: sP -> eP),
+// v' [side][5], and the transformed endpoints g [2][3]
+template <typename T>
+__device__ __forceinline__ void cut_poly_coef_t(const double* Dl, const T* sP, const T* eP, const T* covS,
+                                                const T* covE, const T* Jl, T* P, T* V, T* g) {
+    se3_apply_t<T, double>(Dl, sP, g);
+    se3_apply_t<T, double>(Dl, eP, g + 3);
+    T A[2][6];   // R covS R^T, R covE R^T
+    const T* Cs[2] = {covS, covE};
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
-        double T[9];   // R C
+        T Tm[9];   // R C
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                T[i * 3 + k] = (Dl[i * 4 + 0] * Cs[w][0 * 3 + k] + Dl[i * 4 + 1] * Cs[w][1 * 3 + k]) + Dl[i * 4 + 2] * Cs[w][2 * 3 + k];
+                Tm[i * 3 + k] = (T(Dl[i * 4 + 0]) * Cs[w][0 * 3 + k] + T(Dl[i * 4 + 1]) * Cs[w][1 * 3 + k]) +
+                                T(Dl[i * 4 + 2]) * Cs[w][2 * 3 + k];
         const int ii[6] = {0, 0, 0, 1, 1, 2}, jj[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
         for (int e = 0; e < 6; ++e)
-            A[w][e] = (T[ii[e] * 3 + 0] * Dl[jj[e] * 4 + 0] + T[ii[e] * 3 + 1] * Dl[jj[e] * 4 + 1]) +
-                      T[ii[e] * 3 + 2] * Dl[jj[e] * 4 + 2];
+            A[w][e] = (Tm[ii[e] * 3 + 0] * T(Dl[jj[e] * 4 + 0]) + Tm[ii[e] * 3 + 1] * T(Dl[jj[e] * 4 + 1])) +
+                      Tm[ii[e] * 3 + 2] * T(Dl[jj[e] * 4 + 2]);
     }
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
-        double* P = fd + (side ? PD_PE : PD_PS);
+        T* Ps = P + 18 * side;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) cut_poly_coeff(g[side], g[1 - side], d.Jl[0], d.Jl[1], k, P + 6 * k);
+        for (int k = 0; k < 3; ++k) cut_poly_coeff_t<T>(g + 3 * side, g + 3 * (1 - side), Jl[0], Jl[1], k, Ps + 6 * k);
         // v'(t) = (1-t)^2 Qa(t) + t^2 Qb(t), Q(t) = q0 + 2 t q1 + t^2 q2 for p(t) = P[0..2] = p0 + t p1
-        const double* p0 = P;
-        const double* p1 = P + 6;
-        const double a0 = sym3(A[side], p0, p0), a1 = sym3(A[side], p0, p1), a2 = sym3(A[side], p1, p1);
-        const double b0 = sym3(A[1 - side], p0, p0), b1 = sym3(A[1 - side], p0, p1), b2 = sym3(A[1 - side], p1, p1);
-        double* v = fd + (side ? PD_VE : PD_VS);
+        const T* p0 = Ps;
+        const T* p1 = Ps + 6;
+        const T a0 = sym3_t<T>(A[side], p0, p0), a1 = sym3_t<T>(A[side], p0, p1), a2 = sym3_t<T>(A[side], p1, p1);
+        const T b0 = sym3_t<T>(A[1 - side], p0, p0), b1 = sym3_t<T>(A[1 - side], p0, p1), b2 = sym3_t<T>(A[1 - side], p1, p1);
+        T* v = V + 5 * side;
         v[0] = a0;
-        v[1] = 2.0 * (a1 - a0);
-        v[2] = ((a2 - 4.0 * a1) + a0) + b0;
-        v[3] = 2.0 * ((a1 - a2) + b1);
+        v[1] = T(2.0) * (a1 - a0);
+        v[2] = ((a2 - T(4.0) * a1) + a0) + b0;
+        v[3] = T(2.0) * ((a1 - a2) + b1);
         v[4] = a2 + b2;
     }
-    const double z0 = g[0][2], z1 = g[1][2];
+}
+
+__device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutData& d, double homog, double* fd) {
+    double P[36], V[10], g[6];
+    cut_poly_coef_t<double>(Dl, d.sP, d.eP, d.covS, d.covE, d.Jl, P, V, g);
+#pragma unroll
+    for (int i = 0; i < 18; ++i) { fd[PD_PS + i] = P[i]; fd[PD_PE + i] = P[18 + i]; }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { fd[PD_VS + i] = V[i]; fd[PD_VE + i] = V[5 + i]; }
+    const double z0 = g[2], z1 = g[5];
     fd[PD_OK] = (((z0 > 0.0 && z1 > 0.0) || (z0 < 0.0 && z1 < 0.0)) && z0 * z0 > 2.0 * homog && z1 * z1 > 2.0 * homog)
                     ? 1.0 : 0.0;
 }
@@ -266,6 +294,8 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
 #pragma unroll
                 for (int i = 0; i < 21; ++i) rec_l[(size_t)m * CUT_REC + CUT_FAST + i] = info[i];   // k_cut_search subtracts it
                 double fd[CUT_FAST];
+#pragma unroll
+                for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
                 cut_poly_data(Dl, d, homog, fd);
                 fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
 #pragma unroll
@@ -293,6 +323,90 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         __syncthreads();
     }
     if (lane < 21) p.scr.cut_sum[24 * b + lane] = s;
+}
+
+// ---------------------------------------------------------------- bounds --
+// Per matched line, the error bounds of the margined comparisons' operands,
+// by running error analysis (RB) of the very expression trees the kernels evaluate, for every
+// ratio of the range c in [0, C], C = max(rng[1], 0) (rng inside [0, 1]; otherwise the line
+// gets +inf and is searched with exact steps):
+//  ours  — cut_poly_coef_t: |P_k(computed) - P_k*| per coefficient, summed over t^k, and v';
+//  ref   — cut_endpoint_t: the reference's endpoint Jacobian J and variance v as
+//          getPoseInfoOnLine computes them, |J^ - J*|, |v^ - v*|, moved to P units by the
+//          exact fgz2*(t) = fx / gz*(t)^2 >= fx / zmax^2 (J = fgz2 P, v = fgz2^2 v').
+// The depth gz* of the blended point lies between the transformed endpoints' (c in [0, 1]),
+// which bounds the divisors from below (zlo) and fgz2* from below (zmax).
+__device__ __forceinline__ float ceil_f32(double x) {
+    if (!(x >= 0.0)) return __builtin_inff();   // NaN / negative: no bound
+    float f = (float)x;
+    if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+__global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
+    const int b = blockIdx.y;
+    const int m = blockIdx.x * 64 + threadIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    if (m >= nls) return;
+    const DevLines& L = p.prev.ls;
+    const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+    double* rec = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const double C = fmax(rhi, 0.0), T = fmax(fabs(rlo), fabs(rhi));
+    float eb[14];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) eb[i] = __builtin_inff();
+    bool ok = rlo >= 0.0 && rhi <= 1.0 && rec[PD_OK] != 0.0 && p.cam.fx > 0.0;
+    RB sP[3], eP[3], cS[9], cE[9], Jl[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sP[k] = RB(L.sP[3 * q + k]); eP[k] = RB(L.eP[3 * q + k]); }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { cS[k] = RB(L.covS[9 * q + k]); cE[k] = RB(L.covE[9 * q + k]); }
+    Jl[0] = RB(L.le_obs[3 * q]);
+    Jl[1] = RB(L.le_obs[3 * q + 1]);
+    double eo[2][7];   // ours: eP[6], ev per side
+    double zlo = 0.0, zmax = 0.0;
+    if (ok) {
+        RB P[36], V[10], g[6];
+        cut_poly_coef_t<RB>(Dl, sP, eP, cS, cE, Jl, P, V, g);
+        double gd[6];
+        {
+            const double s3[3] = {L.sP[3 * q], L.sP[3 * q + 1], L.sP[3 * q + 2]};
+            const double e3[3] = {L.eP[3 * q], L.eP[3 * q + 1], L.eP[3 * q + 2]};
+            se3_apply(Dl, s3, gd);
+            se3_apply(Dl, e3, gd + 3);
+        }
+        zlo = fmin(fabs(gd[2]) - g[2].e, fabs(gd[5]) - g[5].e);
+        zmax = fmax(fabs(gd[2]) + g[2].e, fabs(gd[5]) + g[5].e);
+        ok = zlo > 0.0;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                eo[side][i] = (P[18 * side + i].e + T * (P[18 * side + 6 + i].e + T * P[18 * side + 12 + i].e));
+            const RB* v = V + 5 * side;
+            eo[side][6] = v[0].e + T * (v[1].e + T * (v[2].e + T * (v[3].e + T * v[4].e)));
+        }
+    }
+    if (ok) {
+        const double cam_fx = p.cam.fx;
+        const double s1 = zmax * zmax / cam_fx, s2 = s1 * s1;   // 1 / fgz2*_min, its square
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            RB o7[7];
+            cut_endpoint_t<RB>(p.cam, p.cfg.homog_th, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS,
+                               side ? cS : cE, RB(C, 0.0, 0.0), o7, zlo);
+            // 1% slop: the bound arithmetic's own rounding
+#pragma unroll
+            for (int i = 0; i < 6; ++i) eb[7 * side + i] = ceil_f32(1.01 * (eo[side][i] + o7[1 + i].e * s1));
+            eb[7 * side + 6] = ceil_f32(1.01 * (eo[side][6] + o7[0].e * s2));
+        }
+    }
+    float* out = reinterpret_cast<float*>(rec + PD_ERR);
+#pragma unroll
+    for (int i = 0; i < 14; ++i) out[i] = eb[i];
 }
 
 // ---------------------------------------------------------------- search --
@@ -348,7 +462,7 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
 #define CUT_SL 7         // exact endpoint slot (X): v, J[6]
 #define CUT_EP 43        // per-group exact endpoint block: 6 slots + 1 (odd stride)
 #define CUT_NX (CUT_FAST + 21)   // used part of a line record: comparison data | r = 0 info
-static_assert(CUT_REC * 8 == 576, "a record is 4.5 x 128 B: five 16-B loads per lane, the last by lanes 0-3");
+static_assert(CUT_REC * 8 == 640 && CUT_NX <= CUT_REC, "a record is 5 x 128 B: five 16-B loads per lane");
 
 // One reference-order cut endpoint (cut_endpoint) of line q: side 0 the start
 // endpoint blended sP -> eP, side 1 the end endpoint eP -> sP, at ratio t.
@@ -439,6 +553,11 @@ struct CutCmp {
     double cc[9];            // C(t0, t1): cc[3 i + k] multiplies t0^i t1^k
     double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2); line open only
     double bnd[3];           // the line's bound terms at |t| = T = max(|rlo|, |rhi|): P1, VsA, VeA
+    // the line's agreement bound: a step's neighbour value differs from the
+    // reference's metric by at most E = 1/v's (A1 + A2/v's) + 1/v'e (B1 + B2/v'e) + K0 (+ a
+    // per-step constant common to the step); the margins need E <= R0 = tau/8 - K0 and
+    // EV (1/v's + 1/v'e) <= 1/4.  Floats: R0 rounded down, the others up.
+    float eb[6];             // R0, A1, A2, B1, B2, EV
 };
 
 // d at (t0, t1), NaN when not healthy; bound_ok: the forward rounding-error bound of
@@ -448,15 +567,21 @@ struct CutCmp {
 // those of C, VsA those of v's (Horner with absolute coefficients at |t|).
 // with P1 = (Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2 given
 __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, double Ve, double C, double P1,
-                                              double VsA, double VeA, double tau, int& bound_ok) {
+                                              double VsA, double VeA, const float* eb, double tau, int& bound_ok) {
     const double D = __builtin_fma(Vs + Ns, Ve + Ne, -(C * C));
     const double den = Vs * Ve;
-    const double d = D * rcp_fast(den);
+    const double r = rcp_fast(den);
+    const double d = D * r;
     const double P2 = __builtin_fma(VsA, Ve, VeA * Vs);
     constexpr double u = 0x1p-53;
     const double Dd = D * den;
     const bool healthy = Vs > 0.0 && Ve > 0.0 && D > 0.0 && d < 1e300 && Dd < 1e300;
-    bound_ok = healthy && __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= (0.25 * tau - 4.0 * u) * Dd;
+    // agreement with the reference's metric (CutCmp::eb), in f32 with a 1e-4 allowance
+    const float iVs = (float)(Ve * r), iVe = (float)(Vs * r);
+    const float E = __builtin_fmaf(iVs, __builtin_fmaf(eb[2], iVs, eb[1]), iVe * __builtin_fmaf(eb[4], iVe, eb[3]));
+    const bool agree = E * 1.0001f <= eb[0] && eb[5] * (iVs + iVe) <= 0.25f;
+    bound_ok = healthy && agree &&
+               __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= (0.25 * tau - 4.0 * u) * Dd;
     return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
 // Bs, Be, VsA, VeA are Horner sums of non-negative terms in |t|, increasing in |t|: their values at
@@ -466,7 +591,7 @@ __device__ __forceinline__ double cut_dval(const CutCmp& c, double t0, double t1
     const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
     const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
                                    h2(c.cc[0], c.cc[3], c.cc[6], t0));
-    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], tau, bound_ok);
+    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tau, bound_ok);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -635,6 +760,87 @@ constexpr unsigned long long tri_pack(int want_row) {
     return v;
 }
 
+// Bound on entry e of |S (ours) - S (the reference's)| added by one finished line:
+// |P P^T / v' - P* P*^T / v'*| for both paths against the exact one, with |P - P*| <= e,
+// |v' - v'*| <= ev <= v'/4 (xs: v's, P_s[6], v'e, P_e[6] at the final ratios; te: e_s[6] ev_s
+// e_e[6] ev_e), + both assemblies' rounding, + the two sums' roundings (mid, nw: ours).
+__device__ __forceinline__ double cut_info_err(const double* xs, const double* te, int e, double mid, double nw) {
+    constexpr double u = 0x1p-53;
+    constexpr unsigned long long TR = tri_pack(1), TC = tri_pack(0);
+    const int ra = (int)((TR >> (3 * e)) & 7), cb = (int)((TC >> (3 * e)) & 7);
+    const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
+    const double evs = te[6], eve = te[13];
+    const bool vok = xs[0] > 0.0 && xs[7] > 0.0 && evs <= 0.25 * xs[0] && eve <= 0.25 * xs[7];
+    const double esa = te[ra], esb = te[cb], eea = te[7 + ra], eeb = te[7 + cb];
+    const double psa = fabs(xs[1 + ra]) + esa, psb = fabs(xs[1 + cb]) + esb;
+    const double pea = fabs(xs[8 + ra]) + eea, peb = fabs(xs[8 + cb]) + eeb;
+    const double ps2 = psa * psb * is, pe2 = pea * peb * ie;
+    const double d = (1.34 * (esa * psb + psa * esb)) * is + (1.78 * evs * is) * ps2 +
+                     (1.34 * (eea * peb + pea * eeb)) * ie + (1.78 * eve * ie) * pe2 + (14.0 * u) * (ps2 + pe2) +
+                     (2.02 * u) * (fabs(mid) + fabs(nw));
+    return vok ? d : __builtin_inf();
+}
+
+// The line's agreement bound, out of line (once per line).  Row i = j < 6, with
+// s_i = (S^-1)_ii (tg[57 + i]; x 1.002: the reference's S is within errS of ours, the solves'
+// rounding), S_ii, and the line's operand error bounds e (P units) / ev (v'), into wg[6 q + i]:
+//   q = 0 S_ii s_i, 1 sqrt(S_ii s_i), 2 s_i (|P_s,i|(T) + e_s,i)^2, 3 (end side), 4 e_s,i sqrt(s_i),
+//   5 e_e,i sqrt(s_i), 6 |log S_ii|, 7 sqrt(s_i) sum_k errS_ik sqrt(s_k)
+__device__ __attribute__((noinline)) void cut_bound_row(int j, double T, const double* fs, const double* sA,
+                                                        const double* tg, const float* eS, double* wg) {
+    const float* ef = reinterpret_cast<const float*>(fs + PD_ERR);
+    const double sg = 1.002 * tg[57 + j];
+    const double Sii = sA[tri(j, j)];
+    const double es = ef[j], ee = ef[7 + j];
+    const double ps = fabs(fs[PD_PS + j]) + T * (fabs(fs[PD_PS + 6 + j]) + T * fabs(fs[PD_PS + 12 + j])) + es;
+    const double pe = fabs(fs[PD_PE + j]) + T * (fabs(fs[PD_PE + 6 + j]) + T * fabs(fs[PD_PE + 12 + j])) + ee;
+    const double rs = sqrt(sg);
+    double row = 0.0;
+    for (int k = 0; k < 6; ++k) row = __builtin_fma((double)eS[j >= k ? tri(j, k) : tri(k, j)], sqrt(1.002 * tg[57 + k]), row);
+    const double kc = Sii * sg;
+    const int ex = __builtin_amdgcn_frexp_exp(Sii);
+    wg[j] = kc;
+    wg[6 + j] = sqrt(kc);
+    wg[12 + j] = sg * ps * ps;
+    wg[18 + j] = sg * pe * pe;
+    wg[24 + j] = es * rs;
+    wg[30 + j] = ee * rs;
+    wg[36 + j] = (Sii > 0.0 && Sii < 1e300) ? 0.6931471805599453 * (double)(abs(ex) + 1) : __builtin_inf();
+    wg[42 + j] = row * rs;
+}
+// ... combined (one lane): eb = R0, A1, A2, B1, B2, EV of CutCmp
+__device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, const double* cl, const double* fs,
+                                                         const double* wg, float* eb) {
+    const float* ef = reinterpret_cast<const float*>(fs + PD_ERR);
+    const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
+    double sum[8];
+    for (int q = 0; q < 8; ++q) {
+        double a = wg[6 * q];
+        for (int i = 1; i < 6; ++i) a = a + wg[6 * q + i];
+        sum[q] = a;
+    }
+    constexpr double u = 0x1p-53;
+    const double Kc = sum[0], xi = sum[1], Qs = sum[2], Qe = sum[3], Lam = sum[6];
+    const double epsS = sum[7] + (7.01 * u) * xi * xi;                                       // S difference + our factor
+    const double hs = sum[4] + (6.01 * u) * Bs * xi, he = sum[5] + (6.01 * u) * Be * xi;   // + the solves' rounding
+    const double evs = ef[6], eve = ef[13];
+    const double ck = 110.0 * u;   // the reference's assembly, LLT and logs, per unit of tr(A~^-1)
+    const double K0 = 1.002 * epsS + ck * Kc + (7.1 * u) * Lam;
+    const double bs = Bs + hs, be = Be + he;
+    const double A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs), A2 = 1.03 * 4.0 * bs * bs * evs;
+    const double B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be), B2 = 1.03 * 4.0 * be * be * eve;
+    double R0 = fmin(0.125 * tau, 1e-3) - 1.01 * K0;
+    if (!(epsS <= 1e-3 && Kc <= 1e8 && R0 > 0.0)) R0 = -1.0;
+    float r0f = (float)R0;
+    if ((double)r0f > R0) r0f = R0 > 0.0 ? __uint_as_float(__float_as_uint(r0f) - 1u) : -1.0f;
+    eb[0] = r0f;
+    eb[1] = ceil_f32(A1);
+    eb[2] = ceil_f32(A2);
+    eb[3] = ceil_f32(B1);
+    eb[4] = ceil_f32(B2);
+    eb[5] = ceil_f32(fmax(evs, eve));
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
@@ -647,9 +853,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
     //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
     //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
+    //   open: ... | diag(S^-1) [57..62]; the agreement bound's per-row partials over [0..48)
+    //   transition: the finished line's error bounds (+ evaluation) [0..14)
     __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];
-    __shared__ double dtl[CUT_G][13];           // DT_inv rows 0-2
     __shared__ CutCmp cmpl[CUT_G];              // comparison polynomials of the current line
+    // entrywise bound on |S (approximate, sumA) - S (the reference's)|, lower triangle
+    __shared__ float errS[CUT_G][21];
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -662,8 +871,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
     const double* rec_l = p.scr.cut_rec + (size_t)(live ? b : 0) * p.mls_cap * CUT_REC;
-    for (int i = j; i < 12; i += 8) dtl[g][i] = live && nls > 0 ? p.scr.cut_dtinv[16 * b + i] : 0.0;
-    const double* Dl = dtl[g];
+    const double* Dl = p.scr.cut_dtinv + 16 * (size_t)(live ? b : 0);   // DT_inv (exact steps only)
+    for (int e = j; e < 21; e += 8) errS[g][e] = 0.0f;   // line 0: S is the reference's
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     double* const xs = &tmp[g][CUT_EP];
@@ -707,6 +916,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
 #pragma unroll
             for (int i = 0; i < 6; ++i) wg[6 * j + i] = w[i];
+            // (S^-1)_jj = |L^-1 e_j|^2 for the agreement bound
+            double x[6], sg = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double uu = i == j ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < i; ++k) uu = __builtin_fma(-o[tri(i, k)], x[k], uu);
+                x[i] = uu * o[21 + i];
+                sg = __builtin_fma(x[i], x[i], sg);
+            }
+            tmp[g][57 + j] = sg;
         }
         wave_lds_sync();
 #pragma unroll
@@ -746,32 +966,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
         }
         wave_lds_sync();
-        // the line's bound terms at T (lane 7; see cut_dval)
+        // the line's bound terms at T (lane 7; see cut_dval), and lanes 0-5 the per-row terms of
+        // the agreement bound, row i = j: with s_i = (S^-1)_ii (x 1.002: the
+        // reference's S is within errS of ours, the solves' rounding), S_ii, and the line's
+        // operand error bounds e (P units) / ev (v'):
+        //   [0] S_ii s_i  [1] sqrt(S_ii s_i)  [2] s_i (|P_s,i|(T) + e_s,i)^2  [3] (end side)
+        //   [4] e_s,i sqrt(s_i)  [5] e_e,i sqrt(s_i)  [6] |log S_ii|  [7] sum_k errS_ik sqrt(s_i s_k)
+        // the line's bound terms at T (lane 7; see cut_dval), and the line's agreement bound
+        // (CutCmp::eb): per-row terms by lanes 0-5, combined by lane 7
+        const double T = fmax(fabs(rlo), fabs(rhi));
         if (j == 7) {
-            const double T = fmax(fabs(rlo), fabs(rhi));
             const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
             const double VsA = h4abs(cl + 10, T), VeA = h4abs(cl + 15, T);
             const double Bs2 = Bs * Bs, Be2 = Be * Be;
             cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
             cl[36] = VsA;
             cl[37] = VeA;
+        } else if (j < 6) {
+            cut_bound_row(j, T, fst[g], sumA[g], tmp[g], errS[g], wg);
         }
+        wave_lds_sync();
+        if (j == 7) cut_bound_line(T, tau, cl, fst[g], wg, cmpl[g].eb);
         wave_lds_sync();
         // the centre of the first step: d at (0, 0)
         const double vs0 = cl[10], ve0 = cl[15];
-        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], tau, c_ok);
+        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tau, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
-    // record (576 B) from HBM straight into LDS (global_load_lds, no registers); it is
+    // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
     size_t q_cur = 0, q_nx = 0;
     auto pf_issue = [&](int mm) {
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
         for (int k = 0; k < 5; ++k)
-            if (k < 4 || j < 4)
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
-                                                 (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
+                                             (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
     };
     if (m < nls) {
         q_cur = lb + mls[0];
@@ -788,6 +1018,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (nls > 1) pf_issue(1);
     }
     __syncthreads();
+    int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -816,6 +1047,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         if (!(tau > 0.0 && line_ok && c_ok && dc == dc)) ok = 0;
         const bool exact = act && (__ballot(!ok) & gmask) != 0;
+        n_steps += act ? 1 : 0;
+        n_exact += exact ? 1 : 0;
         double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
         int cnext = 1;
         if (__any(exact)) {
@@ -883,6 +1116,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
                     for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
                 }
+                // the error bounds of these operands (tmp[0..14): e_s[6] ev_s e_e[6] ev_e): the line's
+                // record bounds plus the Horner evaluation's; reference-order endpoints: none
+                constexpr double u = 0x1p-53;
+                const float* ef = reinterpret_cast<const float*>(&fst[g][PD_ERR]);
+                if (fst[g][PD_OK] != 0.0) {
+                    if (j < 6) {
+                        const double a0 = fabs(r0), a1 = fabs(r1);
+                        const double hs = fabs(fst[g][PD_PS + j]) + a0 * (fabs(fst[g][PD_PS + 6 + j]) + a0 * fabs(fst[g][PD_PS + 12 + j]));
+                        const double he = fabs(fst[g][PD_PE + j]) + a1 * (fabs(fst[g][PD_PE + 6 + j]) + a1 * fabs(fst[g][PD_PE + 12 + j]));
+                        tmp[g][j] = (double)ef[j] + (2.02 * u) * hs;
+                        tmp[g][7 + j] = (double)ef[7 + j] + (2.02 * u) * he;
+                    } else {
+                        const int o = j == 6 ? PD_VS : PD_VE, w = j == 6 ? 6 : 13;
+                        tmp[g][w] = (double)ef[w] + (4.04 * u) * h4abs(&fst[g][o], fabs(j == 6 ? r0 : r1));
+                    }
+                } else {
+                    tmp[g][j] = 0.0;
+                    if (j < 6) tmp[g][8 + j] = 0.0;
+                }
             }
             wave_lds_sync();   // the finished line's data is read before it is replaced
             if (pend) {
@@ -913,7 +1165,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 for (int kk = 0; kk < 3; ++kk) {
                     const int e = j + 8 * kk;
                     const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
-                    if (e < 21) sumA[g][e] = (sumA[g][e] + info[kk]) - nxl[x >> 4][16 * g + (x & 15)];
+                    if (e < 21) {
+                        const double mid = sumA[g][e] + info[kk];
+                        const double nw = mid - nxl[x >> 4][16 * g + (x & 15)];
+                        sumA[g][e] = nw;
+                        errS[g][e] = ceil_f32((double)errS[g][e] + 1.02 * cut_info_err(xs, tmp[g], e, mid, nw));
+                    }
                 }
             }
             wave_lds_sync();
@@ -925,6 +1182,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         } else if (pend) {
             ++wait;
         }
+    }
+    if (live && j == 0) {
+        p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
+        p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
     }
 }
 
@@ -981,6 +1242,7 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
 
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
     hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[0], s);
     hipLaunchKernelGGL(k_cut_search, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[1], s);

@@ -541,6 +541,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
 __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.B) return;
+    p.scr.bytes[(size_t)STEP_REC * b + 18] = p.tr.n_inliers[b];   // inliers after removeOutliers (step record)
     DevPose& CP = p.curr.pose;
     const DevPose& PP = p.prev.pose;
     const int ok = p.scr.pose_ok[b];

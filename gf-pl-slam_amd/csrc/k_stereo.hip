@@ -1117,6 +1117,9 @@ __global__ void k_step_bytes(KParams p) {
     // the counts the bytes are priced on (the bench's per-step means)
     rec[8] = No; rec[9] = Nk; rec[10] = Mo; rec[11] = Sp2; rec[12] = Sl2; rec[13] = Mp; rec[14] = Ml;
     rec[15] = p.tr.n_inliers[b];
+    if (!(p.cfg.use_line_conf_cut && Ml > 0)) rec[16] = rec[17] = 0;   // k_cut_search writes them otherwise
+    rec[18] = rec[15];   // until optimize_pose (k_pose_finish) records its inliers
+    rec[19] = 0;
     // insertStereoPair's last statement, numFrameSinceKeyframe++ (src/stereoFrameHandler.cpp:150):
     // this per-sequence kernel closes every gfpl_insert_stereo_pair
     p.tr.kf_nsince[b] = p.tr.kf_nsince[b] + 1;

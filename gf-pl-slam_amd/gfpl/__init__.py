@@ -250,7 +250,8 @@ class SynthParams(C.Structure):
                 ("yaw_rate", C.c_double), ("z_min", C.c_double), ("z_max", C.c_double),
                 ("px_noise", C.c_double), ("distractor_frac", C.c_double),
                 ("margin", C.c_int), ("seed", C.c_uint64),
-                ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp), ("respawn", C.c_int)]
+                ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp), ("respawn", C.c_int),
+                ("outlier_frac", C.c_double)]
 
 
 # ------------------------------------------------------------- libraries --
@@ -349,6 +350,7 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_bytes": ([P, P], C.c_int),
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_last_step_counts": ([P, P], C.c_int),
+            "gfpl_last_step_track_counts": ([P, P], C.c_int),
             "gfpl_lsd_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_lsd_destroy": ([P], C.c_int),
             "gfpl_lsd_detect": ([P, P, C.c_int, P, P, P], C.c_int),
@@ -997,6 +999,14 @@ class StereoFrameHandler:
         v = np.zeros(8, np.int64)
         check(self.L.gfpl_last_step_counts(self.h, v.ctypes.data), "last_step_counts")
         return {n: float(x) / self.B for n, x in zip(self.STEP_COUNTS, v)}
+
+    def last_step_track_counts(self) -> dict:
+        """The last step, summed over the batch (gfpl_last_step_track_counts): line-cut greedy
+        steps, those the certified search evaluated exactly, and the inliers
+        left after optimize_pose."""
+        v = np.zeros(4, np.int64)
+        check(self.L.gfpl_last_step_track_counts(self.h, v.ctypes.data), "last_step_track_counts")
+        return {"steps": int(v[0]), "exact_steps": int(v[1]), "inliers_after_pose": int(v[2])}
 
     def last_step_kernel_bytes(self) -> np.ndarray:
         v = np.zeros(4, np.int64)

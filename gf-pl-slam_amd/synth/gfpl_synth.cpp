@@ -289,11 +289,20 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
         const Landmark& lm = W.pts[o.lm];
         Rng ro(mix(mix(lm.key, (uint64_t)k), 7));
         gfpl_keypoint a, c;
-        a.x = (float)(o.ul + p->px_noise * ro.gauss());
-        a.y = (float)(o.vl + p->px_noise * ro.gauss());
+        // outliers: the observation (both images, and its stamped patch) moves by 3-8 px
+        double ox = 0.0, oy = 0.0;
+        if (p->outlier_frac > 0.0) {
+            Rng rq(mix(mix(lm.key, (uint64_t)k), 13));
+            if (rq.uni(0.0, 1.0) < p->outlier_frac) {
+                ox = rq.uni(3.0, 8.0) * ((rq.next() >> 63) ? -1.0 : 1.0);
+                oy = rq.uni(3.0, 8.0) * ((rq.next() >> 63) ? -1.0 : 1.0);
+            }
+        }
+        a.x = (float)(o.ul + ox + p->px_noise * ro.gauss());
+        a.y = (float)(o.vl + oy + p->px_noise * ro.gauss());
         a.octave = lm.octave;
-        c.x = (float)(o.ur + p->px_noise * ro.gauss());
-        c.y = (float)(o.vr + p->px_noise * ro.gauss());
+        c.x = (float)(o.ur + ox + p->px_noise * ro.gauss());
+        c.y = (float)(o.vr + oy + p->px_noise * ro.gauss());
         c.octave = lm.octave;
         std::array<uint8_t, 32> dl, dr;
         observe_code(ro, lm.code, dl.data());
@@ -304,8 +313,8 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
         float s = cam->inv_scale[o_];
         int cols = cam->lvl_cols[o_], rows = cam->lvl_rows[o_];
         uint8_t* img = pyr_r + cam->lvl_offset[o_];
-        int vv = (int)std::lround(o.vl * s);
-        int ul = (int)std::lround(o.ul * s), ur = (int)std::lround(o.ur * s);
+        int vv = (int)std::lround((o.vl + oy) * s);
+        int ul = (int)std::lround((o.ul + ox) * s), ur = (int)std::lround((o.ur + ox) * s);
         uint8_t patch[121];
         for (int q = 0; q < 121; ++q) patch[q] = (uint8_t)(ro.next() >> 56);
         for (int pass = 0; pass < 2; ++pass) {
@@ -364,6 +373,14 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
         if (!in_img(su, sv, cam, mm) || !in_img(eu, ev, cam, mm) ||
             !in_img(su - sd, sv, cam, mm) || !in_img(eu - ed, ev, cam, mm)) continue;
         Rng ro(mix(mix(sg.key, (uint64_t)k), 11));
+        if (p->outlier_frac > 0.0) {   // outliers: the segment moves by 3-8 px in both images
+            Rng rq(mix(mix(sg.key, (uint64_t)k), 17));
+            if (rq.uni(0.0, 1.0) < p->outlier_frac) {
+                const double ox = rq.uni(3.0, 8.0) * ((rq.next() >> 63) ? -1.0 : 1.0);
+                const double oy = rq.uni(3.0, 8.0) * ((rq.next() >> 63) ? -1.0 : 1.0);
+                su += ox; eu += ox; sv += oy; ev += oy;
+            }
+        }
         gfpl_keyline a, c;
         a.sx = (float)(su + p->px_noise * ro.gauss()); a.sy = (float)(sv + p->px_noise * ro.gauss());
         a.ex = (float)(eu + p->px_noise * ro.gauss()); a.ey = (float)(ev + p->px_noise * ro.gauss());

@@ -36,6 +36,9 @@ typedef struct gfpl_synth_params {
                                  drains as the camera moves); L > 0: each pool slot is
                                  re-sampled in the current frustum every L frames (per-slot
                                  phase), so the true-keypoint share is stationary          */
+    double   outlier_frac;    /* share of true observations displaced by 3-8 px (both images
+                                 alike, so stereo still matches) in a frame: the cross-frame
+                                 match of such an observation is a pose-optimisation outlier */
 } gfpl_synth_params;
 
 /* Default parameters for a camera (cfg 2 counts: 2000 ORB + 500 LBD). */

@@ -619,6 +619,11 @@ int  gfpl_last_step_stage_bytes(gfpl_seqbatch* sb, int64_t* bytes7);
  * S_p (stereo points of the new frame), S_l (its stereo lines), M_p (matched_pt), M_l
  * (matched_ls), n_inliers] of the last insert.  Synchronises.                   */
 int  gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8);
+/* More of the last step, summed over the batch: [line-cut greedy steps, steps the
+ * certified search evaluated with the reference's own arithmetic (the exact fallback,
+ * DESIGN.md §3), n_inliers after optimize_pose (removeOutliers; until it runs, the
+ * insert's list sizes), 0].  Synchronises.                                          */
+int  gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
  * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same
