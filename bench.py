@@ -97,6 +97,12 @@ def parse(argv=None):
     ap.add_argument("--no-detect", action="store_true", help="skip the ORB / LBD detection rates")
     ap.add_argument("--gen-threads", type=int, default=16,
                     help="host threads generating the input frames (capped by this rank's share of the cores)")
+    ap.add_argument("--distinct", type=int, default=0,
+                    help="distinct synthetic sequences per rank: 0 = all B unless generating them would take "
+                         "more than --gen-budget seconds on this rank's cores, then one chunk's worth, each "
+                         "uploaded to every chunk of the batch (B = whole batch, no replication)")
+    ap.add_argument("--gen-budget", type=float, default=60.0,
+                    help="host seconds of input generation per rank the auto --distinct allows")
     ap.add_argument("--chunk", type=int, default=0,
                     help="sequences per pinned host chunk of the input ring (0: B/8, at least 256)")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the pipelined host-fed (PCIe) measurement")
@@ -220,8 +226,9 @@ class ParitySampler:
     """Replays sampled sequences of the timed batch on the CPU oracle (the checker)
     and compares them with the GPU state after every step, bit for bit."""
 
-    def __init__(self, cam, cfg, sp, kp_cap, kl_cap, seq0, seqs, threads):
+    def __init__(self, cam, cfg, sp, kp_cap, kl_cap, seq0, seqs, threads, distinct=None):
         self.cam, self.sp, self.kp_cap, self.kl_cap, self.seq0 = cam, sp, kp_cap, kl_cap, seq0
+        self.distinct = distinct   # sequence b runs generator sequence seq0 + b % distinct
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle as O
@@ -254,7 +261,8 @@ class ParitySampler:
         """Frame k of every sampled sequence, generated again on the host (the generator is a
         pure function of (seed, sequence, frame), so these are the bytes the GPU step read)."""
         import gfpl
-        return [gfpl.HostFrames(self.cam, self.sp, 1, 1, self.kp_cap, self.kl_cap, seq0=self.seq0 + b, frame0=k,
+        return [gfpl.HostFrames(self.cam, self.sp, 1, 1, self.kp_cap, self.kl_cap,
+                                seq0=self.seq0 + (b % self.distinct if self.distinct else b), frame0=k,
                                 threads=1) for b in self.seqs]
 
     def initialize(self, h):
@@ -579,6 +587,22 @@ def main():
     ring = [gfpl.HostBatch(cam, sp, chunk, KP, KL, seq0=seq0, pinned=not dry) for _ in range(2)]
     pinned_bytes = 0 if dry else sum(r.nbytes() for r in ring)
     t_gen = 0.0
+    # input generation per rank: the generator costs ~1 ms per sequence-frame and core, the
+    # GPU step ~2 us per sequence-frame, so overlapping the two gains < 3%; when this rank's
+    # cores cannot generate all B sequences' frames within --gen-budget (8 ranks sharing one
+    # host's quota), one chunk of distinct sequences is generated per frame and uploaded into
+    # every chunk of the batch — every sequence is still tracked on the GPU from its own state
+    n_frames_gen = W + K + 1 + (0 if (world > 1 or args.no_host_fed or dry) else 2)
+    probe_n = min(chunk, 128)
+    t0 = time.perf_counter()
+    ring[1].fill(0, gen_threads, seq0=seq0, n=probe_n)
+    per_seq_frame = (time.perf_counter() - t0) / probe_n
+    gen_full_s = per_seq_frame * B * n_frames_gen
+    distinct = args.distinct if args.distinct > 0 else (B if gen_full_s <= args.gen_budget else chunk)
+    if distinct < B:
+        distinct = chunk   # one chunk of distinct sequences, replicated chunk-wise
+    gen_projected_s = per_seq_frame * distinct * n_frames_gen
+    replicate = distinct < B
 
     h = None if dry else gfpl.StereoFrameHandler(ctx, B, KP, KL)
 
@@ -587,12 +611,15 @@ def main():
         copy each chunk into staging buffer `slot` (gfpl_upload_frames_async); the next chunk
         is generated while the previous one is copied.  Returns the staged device view."""
         tick = []
+        if replicate:
+            ring[0].fill(k, gen_threads, seq0=seq0, n=chunk)
         for ci, s0 in enumerate(range(0, B, chunk)):
             n = min(chunk, B - s0)
-            hb = ring[ci % 2]
-            if ci >= 2 and h is not None:
+            hb = ring[0] if replicate else ring[ci % 2]
+            if ci >= 2 and h is not None and not replicate:
                 h.upload_wait(tick[ci - 2])   # the chunk's host buffer is free again
-            hb.fill(k, gen_threads, seq0=seq0 + s0, n=n)
+            if not replicate:
+                hb.fill(k, gen_threads, seq0=seq0 + s0, n=n)
             if h is not None:
                 tick.append(h.upload_async(hb.frames(n), s0, slot))
         if h is None:
@@ -601,7 +628,10 @@ def main():
         return h.staged_frames(slot)
 
     host_info = {"pinned_bytes_per_rank": int(pinned_bytes), "chunk_sequences": int(chunk),
-                 "gen_threads_per_rank": int(gen_threads), "cores_share_per_rank": int(share)}
+                 "gen_threads_per_rank": int(gen_threads), "cores_share_per_rank": int(share),
+                 "distinct_sequences_per_rank": int(distinct), "gen_ms_per_seq_frame": round(per_seq_frame * 1e3, 4),
+                 "gen_projected_s_per_rank": round(gen_projected_s, 1),
+                 "gen_all_distinct_s_per_rank": round(gen_full_s, 1)}
     if dry:
         t0 = time.perf_counter()
         stage_frame(0)
@@ -625,7 +655,8 @@ def main():
     sampler = None
     if args.parity_seqs > 0:
         n = min(args.parity_seqs, B)
-        sampler = ParitySampler(cam, cfg, sp, KP, KL, seq0, [int(x) for x in np.linspace(0, B - 1, n)], share)
+        sampler = ParitySampler(cam, cfg, sp, KP, KL, seq0, [int(x) for x in np.linspace(0, B - 1, n)], share,
+                                distinct=distinct if replicate else None)
 
     def sync_all():
         torch.cuda.synchronize(dev)
@@ -675,7 +706,8 @@ def main():
 
     host_fed = None
     if world == 1 and not args.no_host_fed:
-        host_fed = host_fed_rate(h, cam, sp, B, KP, KL, seq0, W + K + 1, gen_threads, per_in, dev)
+        host_fed = host_fed_rate(h, cam, sp, B, KP, KL, seq0, W + K + 1, gen_threads, per_in, dev,
+                                 distinct=distinct if replicate else B)
 
     if rank == 0:
         sm = np.mean(np.array(stage_ms, dtype=np.float64)[:, :6], axis=0)
@@ -736,7 +768,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (deterministic splitmix64 stereo detections + right ORB pyramid, gfpl_synth; "
                     "stationary scene: landmarks re-spawn in the frustum), generated per step on the host and "
-                    "uploaded to HBM before each timed step",
+                    "uploaded to HBM before each timed step" +
+                    (f"; {distinct} distinct generated sequences per rank, each uploaded to {B // distinct} of "
+                     f"the {B} tracked sequences (host generation budget)" if replicate else ""),
             "config": {"workload": desc, "sequences_per_gpu": B, "kp_per_side": int(sp.n_kp),
                        "kl_per_side": int(sp.n_kl), "gn_iters": "10+10",
                        "parallelism": f"sequences sharded 1/{world} per GPU",
@@ -776,7 +810,7 @@ def main():
         dist.destroy_process_group()
 
 
-def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, steps=8):
+def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, steps=8, distinct=None):
     """PCIe-inclusive rate of a host-fed pipeline (rank 0 at N=1, after the timed steps):
     two input frames (f0, f0 + 1) of all B sequences held in pinned host memory are uploaded
     with gfpl_upload_frames_async into the two staging buffers in turn — the copy of step
@@ -796,8 +830,13 @@ def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, ste
     if (avail is not None and avail < 2.6 * in_bytes) or free < 1.1 * in_bytes:
         return {"skipped": f"needs 2 x {in_bytes / 1e9:.1f} GB pinned host memory and a second staging buffer"}
     hb = [gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=True) for _ in range(2)]
+    D = distinct or B
     for i, x in enumerate(hb):
-        x.fill(f0 + i, gen_threads)
+        x.fill(f0 + i, gen_threads, n=D)
+        for s0 in range(D, B, D):   # replicated distinct sequences (see --distinct)
+            n = min(D, B - s0)
+            for a in x.arrays():
+                a[s0:s0 + n] = a[:n]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     h.upload_async(hb[0].frames(), 0, 1)

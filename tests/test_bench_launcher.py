@@ -50,6 +50,24 @@ def test_launcher_eight_ranks_fit_one_host():
     assert h["cores_share_per_rank"] == max(1, cores // 8) and h["gen_threads_per_rank"] <= h["cores_share_per_rank"]
 
 
+def test_eight_rank_generation_fits_its_budget():
+    """One rank's share of an 8-rank host (2 generator threads) at the headline batch (16384
+    sequences, 20 + 5 steps): generating every sequence's frames would take minutes, so the
+    rank generates one chunk of distinct sequences per frame and uploads it into every chunk
+    (stated in the line), and its projected generation time stays within the 60 s budget."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--batch", "16384",
+                        "--steps", "20", "--warmup", "5", "--no-cpu", "--gen-threads", "2"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    h = d["host"]
+    assert h["gen_threads_per_rank"] == 2
+    assert h["gen_all_distinct_s_per_rank"] > 60.0          # all 16384 would not fit
+    assert h["distinct_sequences_per_rank"] == h["chunk_sequences"] == 2048
+    assert h["gen_projected_s_per_rank"] <= 60.0
+    assert d["gen_s"] <= 0.2 * h["gen_projected_s_per_rank"] + 5.0   # the dry run generated one frame
+
+
 def test_cfg4_refuses_frames_past_the_trajectory():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "cfg4",
                         "--steps", "600", "--batch", "4", "--no-cpu"], capture_output=True, text=True, timeout=300,
