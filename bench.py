@@ -779,6 +779,11 @@ def main():
                          "unit": "GB/s", "frac": float(achieved / HBM_PEAK_GBS), "traffic": traffic,
                          "traffic_note": pmc_note,
                          "algorithmic_bytes_per_launch": float(k_bytes), "avg_launch_ms": float(k_ms),
+                         "occupancy": pmc.get("occupancy_waves_per_simd"),
+                         "occupancy_unit": "mean resident waves per SIMD (4 x SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8) "
+                                           "/ 1024 SIMDs, PMC over the same window)",
+                         "cycles": {k: pmc.get(k) for k in ("frac_wait_any", "frac_wait_inst", "frac_active",
+                                                             "cycle_closure")},
                          "window": f"the {K} timed steps (launches {W + 1}..{W + K} of each step kernel)"},
             "roofline_valu": roof_valu,
             "hbm_frac_step": float(step_bytes / (t_max / K) / 1e9 / HBM_PEAK_GBS),

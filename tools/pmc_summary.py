@@ -103,8 +103,15 @@ def summary(d, batch, workload, steps, warmup):
         if row.get("SQ_WAVE_CYCLES"):
             w = row["SQ_WAVE_CYCLES"]
             row["frac_wait_any"] = row.get("SQ_WAIT_ANY", 0) / w
-            row["frac_wait_inst"] = row.get("SQ_WAIT_INST_ANY", 0) / w
+            row["frac_wait_inst"] = row.get("SQ_WAIT_INST_ANY", 0) / w if "SQ_WAIT_INST_ANY" in row else None
             row["frac_active"] = row.get("SQ_ACTIVE_INST_ANY", 0) / w if "SQ_ACTIVE_INST_ANY" in row else None
+            # MI355X_MICROARCH.md §rocprofv3: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES
+            if row["frac_wait_inst"] is not None and row["frac_active"] is not None:
+                row["cycle_closure"] = row["frac_wait_any"] + row["frac_wait_inst"] + row["frac_active"]
+            # mean resident waves per SIMD: wave-cycles (quad-cycles x 4) over the kernel's cycles
+            # (GRBM_GUI_ACTIVE summed over the 8 XCDs) x 1024 SIMDs
+            if row.get("GRBM_GUI_ACTIVE"):
+                row["occupancy_waves_per_simd"] = 4.0 * w / (row["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
         out["kernels"][k] = row
     return out
 
@@ -132,7 +139,8 @@ def main():
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     keys = ["dispatches", "window", "hbm_bytes_per_launch", "valu_insts_per_wave", "lds_insts_per_wave", "SQ_WAVES",
-            "frac_wait_any", "frac_wait_inst", "frac_active", "SQ_LDS_BANK_CONFLICT"]
+            "frac_wait_any", "frac_wait_inst", "frac_active", "cycle_closure", "occupancy_waves_per_simd",
+            "SQ_LDS_BANK_CONFLICT"]
     for k, row in out["kernels"].items():
         print(k, {x: (round(row[x], 3) if isinstance(row.get(x), float) else row.get(x)) for x in keys if x in row})
     print("wrote", dst)

@@ -33,7 +33,8 @@ pmc() {   # name counters...
 }
 pmc fetch FETCH_SIZE && \
 pmc write WRITE_SIZE && \
-pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY || exit 1
+pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY && \
+pmc sq2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 B=$(python3 -c "import json,sys; print(json.loads([l for l in open('$OUT/pmc/fetch.log') if l.startswith('{')][-1])['config']['sequences_per_gpu'])") || exit 1
 python3 tools/pmc_summary.py $OUT/pmc $B $OUT/pmc_latest.json $WORKLOAD $STEPS $WARMUP > $OUT/pmc/summary.txt \
   && cp $OUT/pmc_latest.json profiles/pmc_latest.json || exit 1
