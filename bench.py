@@ -226,9 +226,9 @@ class ParitySampler:
     """Replays sampled sequences of the timed batch on the CPU oracle (the checker)
     and compares them with the GPU state after every step, bit for bit."""
 
-    def __init__(self, cam, cfg, sp, kp_cap, kl_cap, seq0, seqs, threads, distinct=None):
+    def __init__(self, cam, cfg, sp, kp_cap, kl_cap, seq0, seqs, threads, seq_of=None):
         self.cam, self.sp, self.kp_cap, self.kl_cap, self.seq0 = cam, sp, kp_cap, kl_cap, seq0
-        self.distinct = distinct   # sequence b runs generator sequence seq0 + b % distinct
+        self.seq_of = seq_of or (lambda b: b)   # tracked sequence b runs generator sequence seq0 + seq_of(b)
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle as O
@@ -262,7 +262,7 @@ class ParitySampler:
         pure function of (seed, sequence, frame), so these are the bytes the GPU step read)."""
         import gfpl
         return [gfpl.HostFrames(self.cam, self.sp, 1, 1, self.kp_cap, self.kl_cap,
-                                seq0=self.seq0 + (b % self.distinct if self.distinct else b), frame0=k,
+                                seq0=self.seq0 + self.seq_of(b), frame0=k,
                                 threads=1) for b in self.seqs]
 
     def initialize(self, h):
@@ -559,8 +559,14 @@ def main():
         keep += [T, t]   # the generator reads them through raw pointers
         synth_over = dict(synth_over, traj=T.ctypes.data, n_traj=len(t), traj_t=t.ctypes.data)
         desc = desc + f" [rank 0: {gfpl.EUROC_SEQS[0]}]"
-    sp = gfpl.synth_params(**synth_over)
+    # the right pyramid's levels 1.. are resized from level 0 (ComputePyramid): the host
+    # generates and uploads level 0 only (gfpl_upload_frames_l0_async builds the rest on the
+    # device); the oracle's frames (parity sampler, CPU baseline) carry the host-resized levels
+    sp = gfpl.synth_params(**synth_over, pyr_from_l0=1)
+    sp_up = gfpl.synth_params(**synth_over, pyr_from_l0=2)
     per_in = gfpl.input_bytes_per_frame(cam, KP, KL)
+    l0_bytes = int(cam.lvl_cols[0]) * int(cam.lvl_rows[0])
+    per_up = per_in - int(cam.pyr_bytes) + l0_bytes   # bytes per sequence-frame over PCIe
 
     if not dry:
         # device footprint per sequence: resident state + one staged input frame
@@ -584,7 +590,7 @@ def main():
     gen_threads = max(1, min(args.gen_threads, share))
     chunk = args.chunk or max(256, (B // 8 + 63) // 64 * 64)
     chunk = min(chunk, B)
-    ring = [gfpl.HostBatch(cam, sp, chunk, KP, KL, seq0=seq0, pinned=not dry) for _ in range(2)]
+    ring = [gfpl.HostBatch(cam, sp_up, chunk, KP, KL, seq0=seq0, pinned=not dry) for _ in range(2)]
     pinned_bytes = 0 if dry else sum(r.nbytes() for r in ring)
     t_gen = 0.0
     # input generation per rank: the generator costs ~1 ms per sequence-frame and core, the
@@ -598,9 +604,15 @@ def main():
     ring[1].fill(0, gen_threads, seq0=seq0, n=probe_n)
     per_seq_frame = (time.perf_counter() - t0) / probe_n
     gen_full_s = per_seq_frame * B * n_frames_gen
-    distinct = args.distinct if args.distinct > 0 else (B if gen_full_s <= args.gen_budget else chunk)
+    if args.distinct > 0:
+        distinct = min(args.distinct, B)
+    elif gen_full_s <= args.gen_budget:
+        distinct = B
+    else:   # the most distinct sequences (a multiple of 64, at most a chunk) the budget allows
+        distinct = int(args.gen_budget / (per_seq_frame * n_frames_gen)) // 64 * 64
+        distinct = max(64, min(chunk, distinct))
     if distinct < B:
-        distinct = chunk   # one chunk of distinct sequences, replicated chunk-wise
+        distinct = min(distinct, chunk)   # generated into one ring chunk, tiled, uploaded chunk-wise
     gen_projected_s = per_seq_frame * distinct * n_frames_gen
     replicate = distinct < B
 
@@ -612,7 +624,11 @@ def main():
         is generated while the previous one is copied.  Returns the staged device view."""
         tick = []
         if replicate:
-            ring[0].fill(k, gen_threads, seq0=seq0, n=chunk)
+            ring[0].fill(k, gen_threads, seq0=seq0, n=distinct)
+            for d0 in range(distinct, chunk, distinct):   # tile the distinct rows over the chunk
+                dn = min(distinct, chunk - d0)
+                for a in ring[0].arrays():
+                    a[d0:d0 + dn] = a[:dn]
         for ci, s0 in enumerate(range(0, B, chunk)):
             n = min(chunk, B - s0)
             hb = ring[0] if replicate else ring[ci % 2]
@@ -621,7 +637,7 @@ def main():
             if not replicate:
                 hb.fill(k, gen_threads, seq0=seq0 + s0, n=n)
             if h is not None:
-                tick.append(h.upload_async(hb.frames(n), s0, slot))
+                tick.append(h.upload_async(hb.frames(n), s0, slot, l0_stride=int(cam.pyr_bytes)))
         if h is None:
             return None
         h.upload_wait(tick[-1])
@@ -656,7 +672,7 @@ def main():
     if args.parity_seqs > 0:
         n = min(args.parity_seqs, B)
         sampler = ParitySampler(cam, cfg, sp, KP, KL, seq0, [int(x) for x in np.linspace(0, B - 1, n)], share,
-                                distinct=distinct if replicate else None)
+                                seq_of=(lambda b: (b % chunk) % distinct) if replicate else None)
 
     def sync_all():
         torch.cuda.synchronize(dev)
@@ -706,7 +722,7 @@ def main():
 
     host_fed = None
     if world == 1 and not args.no_host_fed:
-        host_fed = host_fed_rate(h, cam, sp, B, KP, KL, seq0, W + K + 1, gen_threads, per_in, dev,
+        host_fed = host_fed_rate(h, cam, sp_up, B, KP, KL, seq0, W + K + 1, gen_threads, per_up, dev,
                                  distinct=distinct if replicate else B)
 
     if rank == 0:
@@ -825,16 +841,17 @@ def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, ste
     and a second staging buffer in HBM; skipped (with the reason) when they do not fit."""
     import torch
     import gfpl
-    in_bytes = per_in * B
+    in_bytes = per_in * B                                    # over PCIe per step
+    row_bytes = gfpl.input_bytes_per_frame(cam, KP, KL) * B   # host rows (pyramid rows allocated whole)
     try:
         import psutil
         avail = psutil.virtual_memory().available
     except Exception:
         avail = None
     free, _ = torch.cuda.mem_get_info(dev)
-    if (avail is not None and avail < 2.6 * in_bytes) or free < 1.1 * in_bytes:
-        return {"skipped": f"needs 2 x {in_bytes / 1e9:.1f} GB pinned host memory and a second staging buffer"}
-    hb = [gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=True) for _ in range(2)]
+    if (avail is not None and avail < 2.6 * row_bytes) or free < 1.1 * row_bytes:
+        return {"skipped": f"needs 2 x {row_bytes / 1e9:.1f} GB pinned host memory and a second staging buffer"}
+    hb = [gfpl.HostBatch(cam, sp, B, KP, KL, seq0=seq0, pinned=True) for _ in range(2)]   # sp: level 0 only
     D = distinct or B
     for i, x in enumerate(hb):
         x.fill(f0 + i, gen_threads, n=D)
@@ -844,25 +861,27 @@ def host_fed_rate(h, cam, sp, B, KP, KL, seq0, f0, gen_threads, per_in, dev, ste
                 a[s0:s0 + n] = a[:n]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    h.upload_async(hb[0].frames(), 0, 1)
+    pb = int(cam.pyr_bytes)
+    h.upload_async(hb[0].frames(), 0, 1, l0_stride=pb)
     for j in range(steps):
         if j + 1 < steps:
-            h.upload_async(hb[(j + 1) % 2].frames(), 0, (j + 2) % 2)
+            h.upload_async(hb[(j + 1) % 2].frames(), 0, (j + 2) % 2, l0_stride=pb)
         h.frameStep(h.staged_frames((j + 1) % 2))
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     # the copy alone, for the upload rate
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    h.upload_wait(h.upload_async(hb[0].frames(), 0, 1))
+    h.upload_wait(h.upload_async(hb[0].frames(), 0, 1, l0_stride=pb))
     up = time.perf_counter() - t1
     del hb
     return {"value": B * steps / wall, "unit": "stereo frames/s", "steps": steps,
             "ms_per_step": wall / steps * 1e3, "upload_ms_per_step": up * 1e3, "upload_GBps": in_bytes / up / 1e9,
             "input_bytes_per_step": int(in_bytes),
-            "note": "frames f0, f0+1 of every sequence in pinned host memory, uploaded (gfpl_upload_frames_async, "
-                    "copy stream, two staging buffers) while the step on the other buffer runs; the frames "
-                    "alternate; generation / detection excluded"}
+            "note": "frames f0, f0+1 of every sequence in pinned host memory, uploaded (gfpl_upload_frames_l0_async: "
+                    "detections + level 0 of the right image; levels 1.. resized on the device, copy stream, two "
+                    "staging buffers) while the step on the other buffer runs; the frames alternate; generation / "
+                    "detection excluded"}
 
 
 if __name__ == "__main__":

@@ -52,6 +52,7 @@ struct gfpl_seqbatch {
     int64_t n_tickets = 0;
     int32_t* last_n_pt = nullptr;   // [B] list lengths before the last gfpl_update_frame
     int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
+    PyrBuild* pyrb = nullptr;       // levels 1.. of uploaded level-0 right images (gfpl_upload_frames_l0_async)
 };
 
 struct gfpl_event {
@@ -303,6 +304,14 @@ int gfpl_event_destroy(gfpl_event* e) {
     return GFPL_OK;
 }
 
+int gfpl_copy_to_host(gfpl_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c || (!dst && bytes) || (!src && bytes)) return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return GFPL_OK;
+}
+
 int gfpl_event_record_count(const gfpl_event* e, int64_t* count) {
     if (!e || !count) return GFPL_E_INVALID;
     *count = e->records;
@@ -417,6 +426,7 @@ int gfpl_seqbatch_destroy(gfpl_seqbatch* sb) {
     for (hipEvent_t e : sb->ev_ticket)
         if (e) (void)hipEventDestroy(e);
     if (sb->copy) (void)hipStreamDestroy(sb->copy);
+    pyrbuild_destroy(sb->pyrb);
     delete sb;
     return GFPL_OK;
 }
@@ -622,7 +632,33 @@ int stage_alloc(gfpl_seqbatch* sb, int slot) {
 
 extern "C" {
 
+namespace {
+// both upload forms; l0_stride > 0: host->pyr_r holds level-0 images l0_stride bytes apart and the
+// device builds levels 1.. (ORB resize) on the copy stream after the copy
+int upload_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t l0_stride, int64_t* ticket);
+}  // namespace
+
 int gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t* ticket) {
+    return upload_async(sb, host, s0, slot, 0, ticket);
+}
+
+int gfpl_upload_frames_l0_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t l0_stride,
+                                int64_t* ticket) {
+    if (!sb || !sb->ctx->has_cam) return GFPL_E_INVALID;
+    const gfpl_camera& cam = sb->ctx->cam;
+    if (l0_stride < (int64_t)cam.lvl_cols[0] * cam.lvl_rows[0]) return GFPL_E_INVALID;
+    if (!sb->pyrb) {
+        HIPCHK(hipSetDevice(sb->ctx->device));
+        const int e = pyrbuild_create(&cam, &sb->pyrb);
+        if (e) return e;
+    }
+    return upload_async(sb, host, s0, slot, l0_stride, ticket);
+}
+
+}  // extern "C"
+
+namespace {
+int upload_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t l0_stride, int64_t* ticket) {
     if (!sb || !host || (slot != 0 && slot != 1) || !sb->ctx->has_cam) return GFPL_E_INVALID;
     const int n = host->batch;
     if (n < 1 || s0 < 0 || s0 + n > sb->B || host->kp_cap != sb->kp_cap || host->kl_cap != sb->kl_cap)
@@ -644,7 +680,16 @@ int gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0,
     UP(pdesc_l, kp0 * 32, P * 32); UP(pdesc_r, kp0 * 32, P * 32);
     UP(n_kl_l, S, N); UP(n_kl_r, S, N); UP(kl_l, kl0, L); UP(kl_r, kl0, L);
     UP(ldesc_l, kl0 * 32, L * 32); UP(ldesc_r, kl0 * 32, L * 32);
-    UP(pyr_r, S * pyr, N * pyr); UP(time_stamp, S, N);
+    UP(time_stamp, S, N);
+    if (l0_stride > 0) {
+        const gfpl_camera& cam = sb->ctx->cam;
+        const size_t l0 = (size_t)cam.lvl_cols[0] * cam.lvl_rows[0];
+        uint8_t* dst = const_cast<uint8_t*>(d.pyr_r) + S * pyr;
+        HIPCHK(hipMemcpy2DAsync(dst, pyr, host->pyr_r, (size_t)l0_stride, l0, N, hipMemcpyHostToDevice, s));
+        HIPCHK(pyrbuild_run(sb->pyrb, dst, (long long)pyr, n, s));
+    } else {
+        UP(pyr_r, S * pyr, N * pyr);
+    }
 #undef UP
     HIPCHK(hipEventRecord(sb->ev_ready[slot], s));
     sb->ready_pending[slot] = true;
@@ -653,6 +698,9 @@ int gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0,
     if (ticket) *ticket = t;
     return GFPL_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int gfpl_upload_wait(gfpl_seqbatch* sb, int64_t ticket) {
     if (!sb || ticket < 0 || ticket >= sb->n_tickets) return GFPL_E_INVALID;

@@ -49,6 +49,15 @@ hipError_t launch_kf_map_filter(const DevCam& cam, const double* T1, const doubl
 
 }  // namespace gfpl
 
+namespace gfpl {
+// levels 1.. of packed pyramids (the camera's geometry) from their level 0, as ComputePyramid
+// resizes them (k_orb.hip: the ORB extractor's O1 tables and k_orb_resize)
+struct PyrBuild;
+int pyrbuild_create(const gfpl_camera* cam, PyrBuild** out);
+hipError_t pyrbuild_run(PyrBuild* pb, uint8_t* pyr, long long stride, int n, hipStream_t s);
+void pyrbuild_destroy(PyrBuild* pb);
+}  // namespace gfpl
+
 // context accessors for the other extern "C" objects built on a context (gfpl_abi.hip)
 int gfpl_ctx_device(const gfpl_ctx* c);
 void* gfpl_ctx_stream(const gfpl_ctx* c);

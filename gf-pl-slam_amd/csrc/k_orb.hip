@@ -1036,6 +1036,51 @@ inline int cv_round_f(float v) { return (int)std::nearbyintf(v); }
 inline int cv_round_d(double v) { return (int)std::nearbyint(v); }
 inline int16_t sat_short(float v) { return (int16_t)std::min(std::max(cv_round_f(v), -32768), 32767); }
 
+// O1 resize tables of levels 1.. of d's pyramid geometry (d.lv[l].w / h, d.nlevels): per level
+// the x offsets / weights and y offsets / weights, d.xmax, and k_orb_resize's LDS bytes
+void resize_tables(OrbDev& d, std::vector<int>& xofs_h, std::vector<int16_t>& alpha_h, std::vector<int>& yofs_h,
+                   std::vector<int16_t>& beta_h, long long* xoff, long long* yoff, int* resize_lds) {
+    for (int l = 1; l < d.nlevels; ++l) {
+        const OrbLevel& s = d.lv[l - 1];
+        const OrbLevel& t = d.lv[l];
+        const double scale_x = 1. / ((double)t.w / s.w), scale_y = 1. / ((double)t.h / s.h);
+        xoff[l] = (long long)xofs_h.size();
+        int xmax = t.w;
+        for (int dx = 0; dx < t.w; ++dx) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)std::floor(fx);
+            fx -= sx;
+            if (sx < 0) { fx = 0; sx = 0; }
+            if (sx + 1 >= s.w) {
+                xmax = std::min(xmax, dx);
+                if (sx >= s.w - 1) { fx = 0; sx = s.w - 1; }
+            }
+            xofs_h.push_back(sx);
+            alpha_h.push_back(sat_short((1.f - fx) * 2048));
+            alpha_h.push_back(sat_short(fx * 2048));
+        }
+        d.xmax[l] = xmax;
+        yoff[l] = (long long)yofs_h.size();
+        for (int dy = 0; dy < t.h; ++dy) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            const int sy = (int)std::floor(fy);
+            fy -= sy;
+            yofs_h.push_back(sy);
+            beta_h.push_back(sat_short((1.f - fy) * 2048));
+            beta_h.push_back(sat_short(fy * 2048));
+        }
+        // k_orb_resize's LDS: the most source rows a RESIZE_ROWS band reads + its output rows
+        int rows = 1;
+        for (int y0 = 0; y0 < t.h; y0 += RESIZE_ROWS) {
+            const int y1 = std::min(y0 + RESIZE_ROWS, t.h) - 1;
+            const int lo = std::min(std::max(yofs_h[yoff[l] + y0], 0), s.h - 1);
+            const int hi = std::min(std::max(yofs_h[yoff[l] + y1] + 1, 0), s.h - 1);
+            rows = std::max(rows, hi - lo + 1);
+        }
+        resize_lds[l] = 4 * (rows * ((s.w + 6) >> 2) + RESIZE_ROWS * ((t.w >> 2) + 2));
+    }
+}
+
 }  // namespace
 
 extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_orb_params* prm, int max_images,
@@ -1161,45 +1206,7 @@ extern "C" int gfpl_orb_create(gfpl_ctx* ctx, int width, int height, const gfpl_
     std::vector<int> xofs_h, yofs_h;
     std::vector<int16_t> alpha_h, beta_h;
     long long xoff[GFPL_MAX_LEVELS] = {}, yoff[GFPL_MAX_LEVELS] = {};
-    for (int l = 1; l < d.nlevels; ++l) {
-        const OrbLevel& s = d.lv[l - 1];
-        const OrbLevel& t = d.lv[l];
-        const double scale_x = 1. / ((double)t.w / s.w), scale_y = 1. / ((double)t.h / s.h);
-        xoff[l] = (long long)xofs_h.size();
-        int xmax = t.w;
-        for (int dx = 0; dx < t.w; ++dx) {
-            float fx = (float)((dx + 0.5) * scale_x - 0.5);
-            int sx = (int)std::floor(fx);
-            fx -= sx;
-            if (sx < 0) { fx = 0; sx = 0; }
-            if (sx + 1 >= s.w) {
-                xmax = std::min(xmax, dx);
-                if (sx >= s.w - 1) { fx = 0; sx = s.w - 1; }
-            }
-            xofs_h.push_back(sx);
-            alpha_h.push_back(sat_short((1.f - fx) * 2048));
-            alpha_h.push_back(sat_short(fx * 2048));
-        }
-        d.xmax[l] = xmax;
-        yoff[l] = (long long)yofs_h.size();
-        for (int dy = 0; dy < t.h; ++dy) {
-            float fy = (float)((dy + 0.5) * scale_y - 0.5);
-            const int sy = (int)std::floor(fy);
-            fy -= sy;
-            yofs_h.push_back(sy);
-            beta_h.push_back(sat_short((1.f - fy) * 2048));
-            beta_h.push_back(sat_short(fy * 2048));
-        }
-        // k_orb_resize's LDS: the most source rows a RESIZE_ROWS band reads + its output rows
-        int rows = 1;
-        for (int y0 = 0; y0 < t.h; y0 += RESIZE_ROWS) {
-            const int y1 = std::min(y0 + RESIZE_ROWS, t.h) - 1;
-            const int lo = std::min(std::max(yofs_h[yoff[l] + y0], 0), s.h - 1);
-            const int hi = std::min(std::max(yofs_h[yoff[l] + y1] + 1, 0), s.h - 1);
-            rows = std::max(rows, hi - lo + 1);
-        }
-        o->resize_lds[l] = 4 * (rows * ((s.w + 6) >> 2) + RESIZE_ROWS * ((t.w >> 2) + 2));
-    }
+    resize_tables(d, xofs_h, alpha_h, yofs_h, beta_h, xoff, yoff, o->resize_lds);
     int rz_max = 0;
     for (int l = 1; l < d.nlevels; ++l) rz_max = std::max(rz_max, o->resize_lds[l]);
     if (rz_max > 160 * 1024 - 64) { delete o; return GFPL_E_UNSUPPORTED; }
@@ -1261,6 +1268,77 @@ extern "C" int gfpl_orb_destroy(gfpl_orb* o) {
     delete o;
     return GFPL_OK;
 }
+
+// ---- pyramid builder (levels 1.. of packed right pyramids from their level 0; used by
+// gfpl_upload_frames_l0_async): the O1 tables of the camera's geometry, k_orb_resize per level
+namespace gfpl {
+struct PyrBuild {
+    OrbDev d{};
+    void* tables = nullptr;
+    int resize_lds[GFPL_MAX_LEVELS] = {};
+};
+int pyrbuild_create(const gfpl_camera* cam, PyrBuild** out) {
+    if (!cam || !out || cam->n_levels < 1 || cam->n_levels > GFPL_MAX_LEVELS) return GFPL_E_INVALID;
+    PyrBuild* pb = new PyrBuild();
+    OrbDev& d = pb->d;
+    d.W = cam->width;
+    d.H = cam->height;
+    d.nlevels = cam->n_levels;
+    for (int l = 0; l < d.nlevels; ++l) {
+        d.lv[l].w = cam->lvl_cols[l];
+        d.lv[l].h = cam->lvl_rows[l];
+        d.lv[l].off = cam->lvl_offset[l];
+    }
+    std::vector<int> xofs_h, yofs_h;
+    std::vector<int16_t> alpha_h, beta_h;
+    long long xoff[GFPL_MAX_LEVELS] = {}, yoff[GFPL_MAX_LEVELS] = {};
+    resize_tables(d, xofs_h, alpha_h, yofs_h, beta_h, xoff, yoff, pb->resize_lds);
+    int rz_max = 0;
+    for (int l = 1; l < d.nlevels; ++l) rz_max = std::max(rz_max, pb->resize_lds[l]);
+    if (rz_max > 160 * 1024 - 64) { delete pb; return GFPL_E_UNSUPPORTED; }
+    if (rz_max > 0 && hipFuncSetAttribute((const void*)k_orb_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          rz_max) != hipSuccess) { delete pb; return GFPL_E_HIP; }
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t bx = al(4 * xofs_h.size() + 4), ba = al(2 * alpha_h.size() + 4), by = al(4 * yofs_h.size() + 4),
+                 bb = al(2 * beta_h.size() + 4);
+    if (hipMalloc(&pb->tables, bx + ba + by + bb) != hipSuccess) { delete pb; return GFPL_E_HIP; }
+    char* q = (char*)pb->tables;
+    int* xo = (int*)q;
+    int16_t* ap = (int16_t*)(q + bx);
+    int* yo = (int*)(q + bx + ba);
+    int16_t* bp = (int16_t*)(q + bx + ba + by);
+    bool ok = true;
+    if (!xofs_h.empty()) {
+        ok = ok && hipMemcpy(xo, xofs_h.data(), 4 * xofs_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(ap, alpha_h.data(), 2 * alpha_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(yo, yofs_h.data(), 4 * yofs_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemcpy(bp, beta_h.data(), 2 * beta_h.size(), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (!ok) { (void)hipFree(pb->tables); delete pb; return GFPL_E_HIP; }
+    for (int l = 1; l < d.nlevels; ++l) {
+        d.xofs[l] = xo + xoff[l];
+        d.alpha[l] = ap + 2 * xoff[l];
+        d.yofs[l] = yo + yoff[l];
+        d.beta[l] = bp + 2 * yoff[l];
+    }
+    *out = pb;
+    return GFPL_OK;
+}
+hipError_t pyrbuild_run(PyrBuild* pb, uint8_t* pyr, long long stride, int n, hipStream_t s) {
+    OrbDev d = pb->d;
+    d.pyr = pyr;
+    d.pyr_stride = stride;
+    for (int l = 1; l < d.nlevels; ++l)
+        hipLaunchKernelGGL(k_orb_resize, dim3((d.lv[l].h + RESIZE_ROWS - 1) / RESIZE_ROWS, n), dim3(RESIZE_T),
+                           pb->resize_lds[l], s, d, l);
+    return hipGetLastError();
+}
+void pyrbuild_destroy(PyrBuild* pb) {
+    if (!pb) return;
+    if (pb->tables) (void)hipFree(pb->tables);
+    delete pb;
+}
+}  // namespace gfpl
 
 extern "C" int gfpl_orb_pyramid_bytes(const gfpl_orb* o, int64_t* bytes) {
     if (!o || !bytes) return GFPL_E_INVALID;

@@ -251,7 +251,7 @@ class SynthParams(C.Structure):
                 ("px_noise", C.c_double), ("distractor_frac", C.c_double),
                 ("margin", C.c_int), ("seed", C.c_uint64),
                 ("traj", _vp), ("n_traj", C.c_int), ("traj_t", _vp), ("respawn", C.c_int),
-                ("outlier_frac", C.c_double)]
+                ("outlier_frac", C.c_double), ("pyr_from_l0", C.c_int)]
 
 
 # ------------------------------------------------------------- libraries --
@@ -313,6 +313,7 @@ def hiplib() -> C.CDLL:
             "gfpl_get_camera": ([P, P], C.c_int),
             "gfpl_get_config": ([P, P], C.c_int),
             "gfpl_synchronize": ([P], C.c_int),
+            "gfpl_copy_to_host": ([P, P, P, C.c_size_t], C.c_int),
             "gfpl_seqbatch_create": ([P, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_seqbatch_destroy": ([P], C.c_int),
             "gfpl_seqbatch_bytes": ([P], C.c_int64),
@@ -325,6 +326,7 @@ def hiplib() -> C.CDLL:
             "gfpl_upload_frames": ([P, P, P], C.c_int),
             "gfpl_upload_frames_async": ([P, P, C.c_int, C.c_int, P], C.c_int),
             "gfpl_upload_wait": ([P, C.c_int64], C.c_int),
+            "gfpl_upload_frames_l0_async": ([P, P, C.c_int, C.c_int, C.c_int64, P], C.c_int),
             "gfpl_staged_frames": ([P, C.c_int, P], C.c_int),
             "gfpl_stereo_points": ([P, P], C.c_int),
             "gfpl_stereo_lines": ([P, P], C.c_int),
@@ -919,12 +921,18 @@ class StereoFrameHandler:
         dev._keep = [host]
         return dev
 
-    def upload_async(self, host: Frames, s0: int, slot: int) -> int:
+    def upload_async(self, host: Frames, s0: int, slot: int, l0_stride: int = 0) -> int:
         """gfpl_upload_frames_async: enqueue the copy of host.batch sequences of HOST frames
         into sequences [s0, s0 + host.batch) of staging buffer `slot` on the seqbatch's copy
-        stream; returns the ticket for upload_wait (host memory untouched until then)."""
+        stream; returns the ticket for upload_wait (host memory untouched until then).
+        l0_stride > 0 (gfpl_upload_frames_l0_async): only level 0 of each right pyramid is
+        copied (rows l0_stride bytes apart) and the device builds levels 1.. from it."""
         t = C.c_int64()
-        check(self.L.gfpl_upload_frames_async(self.h, C.byref(host), s0, slot, C.byref(t)), "upload_frames_async")
+        if l0_stride > 0:
+            check(self.L.gfpl_upload_frames_l0_async(self.h, C.byref(host), s0, slot, l0_stride, C.byref(t)),
+                  "upload_frames_l0_async")
+        else:
+            check(self.L.gfpl_upload_frames_async(self.h, C.byref(host), s0, slot, C.byref(t)), "upload_frames_async")
         return t.value
 
     def upload_wait(self, ticket: int):

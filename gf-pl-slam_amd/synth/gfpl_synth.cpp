@@ -167,6 +167,54 @@ void sample_segment(Rng& r, const gfpl_synth_params* p, const gfpl_camera* cam, 
     S.key = r.next();
 }
 
+// cv::resize(src, dst, Size(dw, dh), 0, 0, INTER_LINEAR) for 8UC1 (OpenCV's 11-bit fixed-point
+// resizeGeneric_: exact horizontal blend, vertical (s + 2^21) >> 22, rows clamped, the xofs border
+// rule), level by level as ComputePyramid builds the right pyramid; the same arithmetic as the
+// device's k_orb_resize (tests/test_synth.py pins it against the ORB oracle's restatement)
+inline int16_t sat_s16(float v) {
+    const int r = (int)std::nearbyintf(v);
+    return (int16_t)std::min(std::max(r, -32768), 32767);
+}
+void resize_linear_u8(const uint8_t* s, int sw, int sh, uint8_t* d, int dw, int dh) {
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    std::vector<int> xofs(dw), r0(dw), r1(dw);
+    std::vector<int16_t> alpha(2 * (size_t)dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        alpha[2 * dx] = sat_s16((1.f - fx) * 2048);
+        alpha[2 * dx + 1] = sat_s16(fx * 2048);
+    }
+    auto hrow = [&](int y, std::vector<int>& D) {
+        const uint8_t* S = s + (size_t)y * sw;
+        for (int dx = 0; dx < dw; ++dx) {
+            const int sx = xofs[dx];
+            D[dx] = dx < xmax ? S[sx] * alpha[2 * dx] + S[sx + 1] * alpha[2 * dx + 1] : S[sx] * 2048;
+        }
+    };
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = (int)std::floor(fy);
+        fy -= sy;
+        const int16_t b0 = sat_s16((1.f - fy) * 2048), b1 = sat_s16(fy * 2048);
+        auto clip = [&](int y) { return y >= 0 ? (y < sh ? y : sh - 1) : 0; };
+        hrow(clip(sy), r0);
+        hrow(clip(sy + 1), r1);
+        for (int dx = 0; dx < dw; ++dx) {
+            const int v = (r0[dx] * b0 + r1[dx] * b1 + (1 << 21)) >> 22;
+            d[(size_t)dy * dw + dx] = (uint8_t)std::min(std::max(v, 0), 255);
+        }
+    }
+}
+
 // The world seen at frame k.  respawn == 0: one pool sampled in the first camera's
 // frustum, fixed for the whole sequence (it drains as the camera moves on).
 // respawn == L > 0: every pool slot lives L frames and is re-sampled in the frustum of
@@ -263,8 +311,10 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
     const double m = p->margin;
     const double fx = cam->fx, fy = cam->fy, cx = cam->cx, cy = cam->cy, b = cam->b;
 
-    // ---- right pyramid noise
-    for (int64_t i = 0; i < cam->pyr_bytes; i += 8) {
+    // ---- right pyramid noise (level 0 only when the levels are resized from it)
+    const int64_t noise_bytes = p->pyr_from_l0 ? (int64_t)cam->lvl_cols[0] * cam->lvl_rows[0] : cam->pyr_bytes;
+    if (p->pyr_from_l0) std::memset(pyr_r + noise_bytes, 0, (size_t)(cam->pyr_bytes - noise_bytes));
+    for (int64_t i = 0; i < noise_bytes; i += 8) {
         uint64_t v = r.next();
         int64_t nb = std::min<int64_t>(8, cam->pyr_bytes - i);
         std::memcpy(pyr_r + i, &v, (size_t)nb);
@@ -317,6 +367,28 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
         int ul = (int)std::lround((o.ul + ox) * s), ur = (int)std::lround((o.ur + ox) * s);
         uint8_t patch[121];
         for (int q = 0; q < 121; ++q) patch[q] = (uint8_t)(ro.next() >> 56);
+        if (p->pyr_from_l0) {
+            // level 0: the patch magnified by the octave's scale S (nearest cell), so the
+            // resized level o shows it around the keypoint's level-o position
+            const double S = cam->scale[o_], iS = 1.0 / S;
+            const int W0 = cam->lvl_cols[0], H0 = cam->lvl_rows[0];
+            const double yc = o.vl + oy;
+            for (int pass = 0; pass < 2; ++pass) {
+                const double xc = (pass == 0 ? o.ul : o.ur) + ox;
+                const int x0 = std::max((int)std::floor(xc - 5.5 * S), 0), x1 = std::min((int)std::ceil(xc + 5.5 * S), W0 - 1);
+                const int y0 = std::max((int)std::floor(yc - 5.5 * S), 0), y1 = std::min((int)std::ceil(yc + 5.5 * S), H0 - 1);
+                int cxs[64];   // the patch column of each level-0 column (separable nearest cell)
+                const int nx = std::min(x1 - x0 + 1, 64);
+                for (int i = 0; i < nx; ++i)
+                    cxs[i] = 5 + std::min(std::max((int)std::lround((x0 + i - xc) * iS), -5), 5);
+                for (int yy = y0; yy <= y1; ++yy) {
+                    const uint8_t* prow = patch + 11 * (5 + std::min(std::max((int)std::lround((yy - yc) * iS), -5), 5));
+                    uint8_t* drow = pyr_r + (int64_t)yy * W0 + x0;
+                    for (int i = 0; i < nx; ++i) drow[i] = prow[cxs[i]];
+                }
+            }
+            continue;
+        }
         for (int pass = 0; pass < 2; ++pass) {
             int uc = pass == 0 ? ul : ur;
             for (int dy = -5; dy <= 5; ++dy)
@@ -327,6 +399,10 @@ extern "C" int gfpl_synth_frame_ex(const gfpl_synth_params* p, const gfpl_camera
                 }
         }
     }
+    if (p->pyr_from_l0 == 1)   // levels 1.. as ComputePyramid resizes them, each from the previous
+        for (int l = 1; l < cam->n_levels; ++l)
+            resize_linear_u8(pyr_r + cam->lvl_offset[l - 1], cam->lvl_cols[l - 1], cam->lvl_rows[l - 1],
+                             pyr_r + cam->lvl_offset[l], cam->lvl_cols[l], cam->lvl_rows[l]);
     auto distractor_kp = [&](Rng& rr) {
         gfpl_keypoint a;
         a.x = (float)rr.uni(m, cam->width - 1 - m);

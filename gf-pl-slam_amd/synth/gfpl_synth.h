@@ -39,6 +39,13 @@ typedef struct gfpl_synth_params {
     double   outlier_frac;    /* share of true observations displaced by 3-8 px (both images
                                  alike, so stereo still matches) in a frame: the cross-frame
                                  match of such an observation is a pose-optimisation outlier */
+    int      pyr_from_l0;     /* right pyramid: 0 = every level drawn and stamped on its own;
+                                 1 = level 0 drawn (each keypoint's patch stamped at level 0,
+                                 magnified by its octave's scale) and levels 1.. resized from it
+                                 as ORBextractor::ComputePyramid does (cv::resize INTER_LINEAR,
+                                 src/ORBextractor.cc:1107-1132; the device's k_orb_resize);
+                                 2 = level 0 only (the consumer builds the rest, e.g.
+                                 gfpl_upload_frames_l0_async)                                */
 } gfpl_synth_params;
 
 /* Default parameters for a camera (cfg 2 counts: 2000 ORB + 500 LBD). */

@@ -274,6 +274,9 @@ int  gfpl_set_config(gfpl_ctx* ctx, const gfpl_config* cfg);
 int  gfpl_get_camera(const gfpl_ctx* ctx, gfpl_camera* cam);
 int  gfpl_get_config(const gfpl_ctx* ctx, gfpl_config* cfg);
 int  gfpl_synchronize(gfpl_ctx* ctx);
+/* Copy `bytes` of DEVICE memory (e.g. a field of a gfpl_frames view) to HOST memory after the
+ * context's stream drained, for FFI callers without a HIP runtime of their own.  Synchronises. */
+int  gfpl_copy_to_host(gfpl_ctx* ctx, void* host_dst, const void* device_src, size_t bytes);
 
 /* B independent sequences (B StereoFrameHandler objects) resident in HBM.
  * kp_cap <= 8192 keypoints and kl_cap <= 2048 keylines per side (config 5:
@@ -313,6 +316,14 @@ int  gfpl_upload_frames(gfpl_seqbatch* sb, const gfpl_frames* host, gfpl_frames*
  * frame k in the other.  *ticket (nullable) names the copy for gfpl_upload_wait;
  * the host memory must stay unchanged until then.                              */
 int  gfpl_upload_frames_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot, int64_t* ticket);
+/* The same with only level 0 of each right pyramid on the host: host->pyr_r holds the
+ * level-0 images (lvl_cols[0] x lvl_rows[0] bytes) of the host->batch sequences, l0_stride
+ * bytes apart; after the copy the device builds levels 1.. of the staged pyramids as
+ * ORBextractor::ComputePyramid does (cv::resize INTER_LINEAR of the level above,
+ * src/ORBextractor.cc:1107-1132; the ORB extractor's k_orb_resize), on the copy stream —
+ * about half the bytes over PCIe at VGA.                                                   */
+int  gfpl_upload_frames_l0_async(gfpl_seqbatch* sb, const gfpl_frames* host, int s0, int slot,
+                                 int64_t l0_stride, int64_t* ticket);
 /* Block the host until the copy `ticket` (and every copy enqueued before it) is done. */
 int  gfpl_upload_wait(gfpl_seqbatch* sb, int64_t ticket);
 /* Device view (all B sequences) of staging buffer `slot` (GFPL_E_INVALID before its first upload). */

@@ -63,7 +63,8 @@ def test_eight_rank_generation_fits_its_budget():
     h = d["host"]
     assert h["gen_threads_per_rank"] == 2
     assert h["gen_all_distinct_s_per_rank"] > 60.0          # all 16384 would not fit
-    assert h["distinct_sequences_per_rank"] == h["chunk_sequences"] == 2048
+    assert h["chunk_sequences"] == 2048 and 64 <= h["distinct_sequences_per_rank"] <= 2048
+    assert h["distinct_sequences_per_rank"] % 64 == 0
     assert h["gen_projected_s_per_rank"] <= 60.0
     assert d["gen_s"] <= 0.2 * h["gen_projected_s_per_rank"] + 5.0   # the dry run generated one frame
 

@@ -325,24 +325,41 @@ def test_bench_workload_parity(wl):
     assert all(rep["pose_exact"])
 
 
-def test_async_double_buffered_upload_parity():
+@pytest.mark.parametrize("level0", [False, True])
+def test_async_double_buffered_upload_parity(level0):
     """gfpl_upload_frames_async: frames uploaded chunk by chunk from host memory into the two
     staging buffers on the copy stream, frame k + 1 copied while the step on frame k runs
-    (the staging events order them); poses and matched lists equal the oracle's."""
+    (the staging events order them); poses and matched lists equal the oracle's.  level0:
+    gfpl_upload_frames_l0_async copies only level 0 of each right pyramid (the host frames
+    hold level 0 alone, pyr_from_l0 = 2) and the device builds levels 1.. — byte-equal to the
+    host's ComputePyramid restatement (pyr_from_l0 = 1), which the oracle tracks on."""
     cfg = gfpl.default_config()
     cam = gfpl.make_camera("vga", cfg)
     B, F, KP, KL = 5, 5, 2048, 512
-    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=43, respawn=16), B, F, KP, KL)
+    H = gfpl.HostFrames(cam, gfpl.synth_params(seed=43, respawn=16, pyr_from_l0=1 if level0 else 0), B, F, KP, KL)
+    Hup = gfpl.HostFrames(cam, gfpl.synth_params(seed=43, respawn=16, pyr_from_l0=2), B, F, KP, KL) if level0 else H
     g = gfpl.StereoFrameHandler(gfpl.Context(cam, cfg), B, KP, KL)
     orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(B)]
 
     def upload(k, slot):
         # two chunks of 3 + 2 sequences
-        ts = [g.upload_async(gfpl.make_frames(n, KP, KL, [a[k, s0:s0 + n] for a in H.arrays()]), s0, slot)
+        ts = [g.upload_async(gfpl.make_frames(n, KP, KL, [a[k, s0:s0 + n] for a in Hup.arrays()]), s0, slot,
+                             l0_stride=int(cam.pyr_bytes) if level0 else 0)
               for s0, n in ((0, 3), (3, 2))]
         return ts[-1]
 
     g.upload_wait(upload(0, 0))
+    if level0:   # the device-built pyramids are the host restatement's, byte for byte
+        import torch
+        st = g.staged_frames(0)
+        pb = int(cam.pyr_bytes)
+        used = int(cam.lvl_offset[int(cam.n_levels) - 1]) + int(cam.lvl_cols[int(cam.n_levels) - 1]) * \
+            int(cam.lvl_rows[int(cam.n_levels) - 1])
+        buf = np.zeros(B * pb, np.uint8)
+        torch.cuda.synchronize()
+        assert gfpl.hiplib().gfpl_copy_to_host(g.ctx.h, buf.ctypes.data, st.pyr_r, B * pb) == 0
+        got = buf.reshape(B, pb)[:, :used]
+        assert (got == H.pyr_r[0][:, :used]).all()
     g.initialize(g.staged_frames(0))
     upload(1, 1)
     for k in range(1, F):

@@ -102,3 +102,44 @@ def test_trajectory_frames_are_not_wrapped():
         gfpl.HostFrames(cam, sp, 1, 5, 2048, 512)
     with pytest.raises(ValueError):
         gfpl.euroc_traj("mh_01", gfpl.EUROC_MAX_POSES + 1)
+
+
+def test_level0_pyramids_are_the_orb_resize_chain():
+    """pyr_from_l0 = 1: levels 1.. of the right pyramid are cv::resize INTER_LINEAR of the level
+    above (ComputePyramid, src/ORBextractor.cc:1107-1132) — byte-equal to the ORB oracle's
+    restatement, hence to the device's k_orb_resize (tests/test_orb_gpu.py); pyr_from_l0 = 2
+    writes level 0 only, byte-equal to mode 1's level 0, with the same detections."""
+    import oracle as O
+    for name in ("vga", "kitti", "euroc"):
+        cfg = gfpl.default_config()
+        cam = gfpl.make_camera(name, cfg)
+        W0, H0 = int(cam.lvl_cols[0]), int(cam.lvl_rows[0])
+        h1 = gfpl.HostFrames(cam, gfpl.synth_params(respawn=16, pyr_from_l0=1), 2, 2, 2048, 512)
+        h2 = gfpl.HostFrames(cam, gfpl.synth_params(respawn=16, pyr_from_l0=2), 2, 2, 2048, 512)
+        for f in range(2):
+            for b in range(2):
+                pyr = h1.pyr_r[f, b]
+                lv = lambda l: pyr[int(cam.lvl_offset[l]):int(cam.lvl_offset[l]) + int(cam.lvl_cols[l]) * int(cam.lvl_rows[l])] \
+                    .reshape(int(cam.lvl_rows[l]), int(cam.lvl_cols[l]))
+                for l in range(1, int(cam.n_levels)):
+                    want = O.orb_resize(np.ascontiguousarray(lv(l - 1)), int(cam.lvl_cols[l]), int(cam.lvl_rows[l]))
+                    assert (lv(l) == want).all(), (name, f, b, l)
+                assert (h2.pyr_r[f, b, :W0 * H0] == pyr[:W0 * H0]).all() and not h2.pyr_r[f, b, W0 * H0:].any()
+        for a1, a2 in zip(h1.arrays()[:12], h2.arrays()[:12]):
+            assert (a1 == a2).all()
+
+
+def test_level0_patches_survive_the_pyramid():
+    """The magnified level-0 stamps leave each true keypoint's patch at its octave level, so the
+    sub-pixel refinement (both windows from the right pyramid, ledger Q1) keeps most stereo points:
+    on the oracle, >= 85% of the per-level stamping's stereo points (VGA, 1800 true keypoints)."""
+    import oracle as O
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    n = {}
+    for mode in (0, 1):
+        h = gfpl.HostFrames(cam, gfpl.synth_params(respawn=16, pyr_from_l0=mode), 1, 1, 2048, 512)
+        o = O.OracleHandler(cam, cfg, 2048, 512)
+        o.initialize(h.frames(0), 0)
+        n[mode] = o.read_frame(gfpl.PREV).n_pt
+    assert n[1] >= 0.85 * n[0] and n[1] > 1200, n
