@@ -94,6 +94,16 @@ def test_bench_config_parity():
     _check(rep)
 
 
+def test_outlier_workload_parity():
+    """cfg2o: 10% of the true observations displaced 3-8 px per frame (synth outlier_frac), so
+    removeOutliers (src/stereoFrameHandler.cpp:2058-2116) flags more than the MAD tail and the
+    stage-2 restart sees a changed list; pyramids resized from level 0 (pyr_from_l0 = 1)."""
+    rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
+                        n_seq=3, n_frames=5, kp_cap=2048, kl_cap=512,
+                        synth_over=dict(respawn=16, outlier_frac=0.1, pyr_from_l0=1), seed=17)
+    _check(rep)
+
+
 def test_kitti_camera_parity():
     rep = _run_sequence("kitti", dict(max_iters=10, max_iters_ref=10), n_seq=2, n_frames=4, kp_cap=2048,
                         kl_cap=512, synth_over=dict(dt=0.1, v_fwd=8.0, z_min=4.0, z_max=40.0), seed=3)
