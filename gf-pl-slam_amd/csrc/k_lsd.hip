@@ -5,7 +5,8 @@
 // images resident in HBM, the arithmetic pinned as the CPU oracle's ledger S1-S7
 // (oracle/gfpl_lsd_oracle.cpp).  Kernels, one launch each for the whole batch:
 //  k_lsd_grad      per pixel (lsd.cpp ll_angle, S1): the 2x2 gradient, NOTDEF test, fastAtan2
-//                  angle (degrees, float), cos / sin of float(angle) (S3), the image's max norm
+//                  angle (degrees, float), cos / sin of float(angle) (S3), the image's max norm,
+//                  a compact index per defined pixel
 //  k_lsd_keys      per pixel: the 64-bit sort element (norm bin << 32 | y << 16 | x), row-major
 //  k_lsd_sort      one wave per image: libstdc++ std::sort's permutation (S2).  Introsort's
 //                  Hoare partition is restated in parallel: the k-th left stopper swaps with
@@ -19,7 +20,8 @@
 //                  order-dependent angle update runs lane-uniform over them), region2rect /
 //                  get_theta (list-ordered sums from lane values), refine and
 //                  reduce_region_radius (its swap-with-last removal as a parallel hole/filler
-//                  pairing); the used map is an LDS bitmap when it fits
+//                  pairing); the used map is an LDS bitmap over the image's defined pixels
+//                  (compact indices from k_lsd_grad) when they are at most a quarter of it
 //  k_lsd_keylines  one wave per image: checkLineExtremes, the min-length filter (order-
 //                  preserving), KeyLine angle / response, and the response std::sort + resize
 #include <hip/hip_runtime.h>
@@ -37,7 +39,7 @@ namespace gfpl {
 #define LSD_RING 256               // region list entries mirrored in LDS
 #define LSD_SMALL 64               // ranges up to this size: one lane runs libstdc++'s serial loop
                                    // (32 / 48 / 64 / 96: 22.2k / 23.5k / 23.7k / 23.1k images/s)
-#define LSD_USED_LDS_MAX (64 * 1024)   // bytes of LDS bitmap (W*H <= 524288 px)
+#define LSD_CID_MAX 491520         // compact used-map bits at most (60 KB of LDS + the ring)
 
 struct LsdDev {
     int W, H, NP;                  // NP = (W-1)(H-1) sorted pixels
@@ -55,7 +57,12 @@ struct LsdDev {
     int* rpos;                     // [n][NP]
     uint32_t* reg;                 // [n][W*H] region list
     uint32_t* tmp;                 // [n][W*H] region scratch
-    uint8_t* used_g;               // [n][W*H] used map when the bitmap does not fit LDS
+    uint32_t* cid;                 // [n][W*H] a defined pixel's index among the image's defined
+                                   // pixels (k_lsd_grad; any injective order): its used bit
+    int* ndef;                     // [n] defined pixels of the image
+    int cid_cap;                   // compact used-map bits (LDS): images with more defined
+                                   // pixels grow with the HBM byte map
+    uint8_t* used_g;               // [n][W*H] used map of the images above cid_cap
     float4* segs;                  // [n][seg_cap]
     int* nseg;                     // [n]
     float* kl_tmp;                 // [n][seg_cap][6]  filtered keylines (sx sy ex ey angle response)
@@ -831,11 +838,13 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
 #define LSD_GRAD_ROWS 64   // rows per workgroup (16 passes of 4): one max-norm atomic per 4096 px
 __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* images) {
     __shared__ unsigned long long wmaxv[4];
+    __shared__ int wcnt[4], wbase;
     const int img = blockIdx.z;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int W = o.W, H = o.H;
     const uint8_t* I = images + (size_t)img * W * H;
     unsigned long long b = 0;   // bits of the max norm of defined pixels (norm >= 0 orders like its bits)
+    uint32_t dmask = 0;         // pass r / 4 defined
     for (int r = 0; r < LSD_GRAD_ROWS; r += 4) {
         const int y = blockIdx.y * LSD_GRAD_ROWS + r + (threadIdx.x >> 6);
         if (x >= W || y >= H) continue;
@@ -858,18 +867,41 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
         }
         o.px[p] = make_float4(a, cs.x, cs.y, __uint_as_float(g));
         o.ang[p] = a;
-        if (a >= 0.0f) o.scs[p] = make_float2(cs.z, cs.w);
+        if (a >= 0.0f) {
+            o.scs[p] = make_float2(cs.z, cs.w);
+            dmask |= 1u << (r >> 2);
+        }
     }
     for (int off = 32; off; off >>= 1) {
         const unsigned long long t = __shfl_xor(b, off);
         b = t > b ? t : b;
     }
-    if ((threadIdx.x & 63) == 0) wmaxv[threadIdx.x >> 6] = b;
+    // compact indices of the defined pixels: the workgroup's count by a wave scan + one atomic
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int c = __popc(dmask);
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(c, off);
+        if (lane >= off) c += t;
+    }
+    if (lane == 63) wcnt[wv] = c;
+    if (lane == 0) wmaxv[wv] = b;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long m = wmaxv[0];
         for (int w = 1; w < 4; ++w) m = wmaxv[w] > m ? wmaxv[w] : m;
         if (m) atomicMax(&o.maxg[img], m);
+        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        wbase = tot ? atomicAdd(&o.ndef[img], tot) : 0;
+    }
+    __syncthreads();
+    if (dmask) {
+        int k = wbase + c - __popc(dmask);
+        for (int w = 0; w < wv; ++w) k += wcnt[w];
+        for (int r = 0; r < LSD_GRAD_ROWS; r += 4) {
+            if (!((dmask >> (r >> 2)) & 1u)) continue;
+            const int y = blockIdx.y * LSD_GRAD_ROWS + r + wv;
+            o.cid[(size_t)img * W * H + (size_t)y * W + x] = (uint32_t)k++;
+        }
     }
 }
 
@@ -972,25 +1004,26 @@ __global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_wav
 // ---------------------------------------------------------------- the regions --
 namespace {
 
+// The used map of one image: LU — an LDS bitmap over the image's defined pixels, indexed by
+// their compact index c (only defined pixels are ever used: seeds and aligned neighbours), so
+// a VGA image needs ~3 KB instead of a 38 KB bitmap over every pixel; !LU — an HBM byte map
+// by pixel (images with more than cid_cap defined pixels)
 template <bool LU>
 struct Used {
     uint32_t* bits;   // LDS bitmap (LU)
     uint8_t* g;       // global byte map (!LU)
     int W;
-    __device__ __forceinline__ bool get(int x, int y) const {
-        const int p = y * W + x;
-        if (LU) return (bits[p >> 5] >> (p & 31)) & 1u;
-        return g[p] != 0;
+    __device__ __forceinline__ bool get(int x, int y, uint32_t c) const {
+        if (LU) return (bits[c >> 5] >> (c & 31)) & 1u;
+        return g[y * W + x] != 0;
     }
-    __device__ __forceinline__ void set1(int x, int y) const {   // one lane
-        const int p = y * W + x;
-        if (LU) atomicOr(&bits[p >> 5], 1u << (p & 31));
-        else g[p] = 1;
+    __device__ __forceinline__ void set1(int x, int y, uint32_t c) const {   // one lane
+        if (LU) atomicOr(&bits[c >> 5], 1u << (c & 31));
+        else g[y * W + x] = 1;
     }
-    __device__ __forceinline__ void clr(int x, int y) const {    // any lanes
-        const int p = y * W + x;
-        if (LU) atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
-        else g[p] = 0;
+    __device__ __forceinline__ void clr(int x, int y, uint32_t c) const {    // any lanes
+        if (LU) atomicAnd(&bits[c >> 5], ~(1u << (c & 31)));
+        else g[y * W + x] = 0;
     }
     __device__ __forceinline__ void sync() const {
         if (LU) lds_sync();
@@ -1002,6 +1035,7 @@ struct Rect { double x1, y1, x2, y2, width; };
 
 struct Img {
     const float4* px;
+    const uint32_t* cid;
     uint32_t* reg;
     uint32_t* tmp;
     uint32_t* ring;   // LDS
@@ -1022,10 +1056,11 @@ __device__ __forceinline__ double modgrad(const Img& I, int x, int y) {
 // has_pre: lanes 0-24 of `pre` hold the records of the seed's 5x5 neighbourhood (lane
 // 5 (dy + 2) + dx + 2) and lane 25 of `pcs` its seed (cos, sin): the first two batches (the
 // seed and the pixels it adds) need no HBM round trip.  (seed_deg: the seed's angle record)
+// (scid: the seed's compact index; pre_c: lanes 0-24's compact indices with `pre`)
 template <bool LU>
-__device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, float seed_deg, double prec,
-                           double& reg_angle, bool& in_hbm, bool has_pre = false, float4 pre = float4{},
-                           float2 pcs = float2{}) {
+__device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, uint32_t scid, float seed_deg,
+                           double prec, double& reg_angle, bool& in_hbm, bool has_pre = false,
+                           float4 pre = float4{}, float2 pcs = float2{}, uint32_t pre_c = 0) {
     const int lane = lane_id();
     int n = 0;
     reg_angle = (double)seed_deg * kDeg2Rad;
@@ -1042,7 +1077,7 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
     lds_u32* ring = (lds_u32*)(uintptr_t)(uint32_t)(uintptr_t)I.ring;
     if (lane == 0) {
         ring[0] = s;
-        U.set1(sx, sy);
+        U.set1(sx, sy, scid);
     }
     n = 1;
     bool glob = false;   // (uniform) new points go to the HBM list too
@@ -1075,21 +1110,30 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
             ok = xx >= 0 && yy >= 0 && xx < I.W && yy < I.H;
         }
         float4 q = make_float4(-1.0f, 0.f, 0.f, 0.f);
+        uint32_t cq = 0;
         bool inwin = false;
         if (has_pre) {   // (uniform)
             const int ox = xx - sx + 2, oy = yy - sy + 2;
             inwin = ok && ox >= 0 && ox < 5 && oy >= 0 && oy < 5;
             const int src = inwin ? 5 * oy + ox : 0;
             const float4 w = make_float4(__shfl(pre.x, src), __shfl(pre.y, src), __shfl(pre.z, src), __shfl(pre.w, src));
-            if (inwin) q = w;
+            const uint32_t wc = LU ? (uint32_t)__shfl((int)pre_c, src) : 0u;
+            if (inwin) {
+                q = w;
+                cq = wc;
+            }
         }
-        if (ok && !inwin) q = I.px[yy * I.W + xx];
+        if (ok && !inwin) {
+            q = I.px[yy * I.W + xx];
+            if (LU) cq = I.cid[yy * I.W + xx];
+        }
+        if (!(q.x >= 0.0f)) cq = 0;   // (an undefined pixel has no index)
         for (int k = 0; k < nb; ++k) {
             if (!glob && n > LSD_RING - 16) {   // <= 9 points join per step: the ring has not wrapped
                 for (int e = lane; e < n; e += 64) I.reg[e] = ring[e];
                 glob = true;
             }
-            const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy);
+            const bool av = g == k && ok && q.x >= 0.0f && !U.get(xx, yy, cq);
             unsigned long long m = __ballot(av) >> (9 * k);
             if (!m) continue;
             const int b = 9 * k;
@@ -1114,8 +1158,9 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, floa
                 m &= ~((2ull << t) - 1ull);
                 const int px = prx + t % 3 - 1, py = pry + t / 3 - 1;
                 const uint32_t e = ((uint32_t)py << 16) | (uint32_t)px;
+                const uint32_t pc = LU ? (uint32_t)rl_i((int)cq, b + t) : 0u;
                 if (lane == 0) {
-                    U.set1(px, py);
+                    U.set1(px, py, pc);
                     if (glob) I.reg[n] = e;
                     ring[n & (LSD_RING - 1)] = e;
                 }
@@ -1239,7 +1284,10 @@ __device__ bool reduce_region_radius(const Img& I, const Used<LU>& U, int& n, do
                 const uint32_t r = I.reg[i];
                 const double px = (double)(int)(r & 0xffff), py = (double)(int)(r >> 16);
                 far = (px - xc) * (px - xc) + (py - yc) * (py - yc) > rad_sq;
-                if (far) U.clr((int)(r & 0xffff), (int)(r >> 16));
+                if (far) {
+                    const int x = (int)(r & 0xffff), y = (int)(r >> 16);
+                    U.clr(x, y, LU ? I.cid[y * I.W + x] : 0u);
+                }
             }
             nk += __popcll(__ballot(i < n && !far));
         }
@@ -1303,7 +1351,7 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
         if (i < n) {
             const uint32_t r = I.reg[i];
             const int x = (int)(r & 0xffff), y = (int)(r >> 16);
-            U.clr(x, y);
+            U.clr(x, y, LU ? I.cid[y * I.W + x] : 0u);
             in = sqrt(((double)x - xc) * ((double)x - xc) + ((double)y - yc) * ((double)y - yc)) < rec.width;
             if (in) ad = angle_diff_signed((double)I.px[y * I.W + x].x * kDeg2Rad, ang_c);
         }
@@ -1321,7 +1369,8 @@ __device__ bool refine(const Img& I, const Used<LU>& U, int& n, double reg_angle
     const double mean_angle = sum / (double)cnt;
     const double tau = 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / (double)cnt + mean_angle * mean_angle);
     bool in_hbm;
-    n = region_grow<LU>(I, U, sx, sy, I.px[sy * I.W + sx].x, tau, reg_angle, in_hbm);
+    n = region_grow<LU>(I, U, sx, sy, LU ? I.cid[sy * I.W + sx] : 0u, I.px[sy * I.W + sx].x, tau, reg_angle,
+                        in_hbm);
     ring_to_hbm(I, n, in_hbm);
     mem_sync();   // the region list (HBM) is read by every lane next
     if (n < 2) return false;
@@ -1335,10 +1384,11 @@ template <bool LU>
 __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ring) {
     const int lane = lane_id();
     const size_t off = (size_t)img * o.W * o.H;
-    Img I{o.px + off, o.reg + off, o.tmp + off, ring, o.W, o.H};
+    Img I{o.px + off, o.cid + off, o.reg + off, o.tmp + off, ring, o.W, o.H};
     Used<LU> U{bits, o.used_g + off, o.W};
+    const uint32_t* cidp = o.cid + off;
     if (LU) {
-        const int nw = (o.W * o.H + 31) >> 5;
+        const int nw = (o.ndef[img] + 31) >> 5;
         for (int i = lane; i < nw; i += 64) bits[i] = 0;
         lds_sync();
     } else {
@@ -1351,6 +1401,7 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
     // software pipeline: chunk c+2's keys and chunk c+1's angles load while chunk c is processed
     uint64_t e1 = lane < o.NP ? keys[lane] : 0;
     float a1 = lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+    uint32_t c1 = (LU && lane < o.NP) ? cidp[(int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff)] : 0u;
     // (a candidate's angle record comes with the scan: a region's first round trip is its
     // seed's neighbourhood)
     uint64_t e2 = 64 + lane < o.NP ? keys[64 + lane] : 0;
@@ -1366,22 +1417,25 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
         int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0x7fff);
         const bool iso = (e >> 31) & 1u;   // (k_lsd_keys)
         const float a0 = a1;
+        const uint32_t c0 = a0 >= 0.0f ? c1 : 0u;   // (an undefined pixel has no index)
         e1 = e2;
         a1 = base + 64 + lane < o.NP ? pxf[4 * ((int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff))] : -1.0f;
+        if (LU) c1 = base + 64 + lane < o.NP ? cidp[(int)((e1 >> 16) & 0x7fff) * o.W + (int)(e1 & 0xffff)] : 0u;
         e2 = base + 128 + lane < o.NP ? keys[base + 128 + lane] : 0;
         bool cand = a0 >= 0.0f;
         int pre_j = -1;   // the candidate whose 5x5 records and seed (cos, sin) `pre` holds
         float4 pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
         float2 pcs = make_float2(0.f, 0.f);
+        uint32_t pre_c = 0;
         for (;;) {
-            const unsigned long long m = __ballot(cand && !U.get(px, py));
+            const unsigned long long m = __ballot(cand && !U.get(px, py, c0));
             if (!m) break;
             // isolated seeds ahead of the next one that grows become used, in one step
             const unsigned long long mg = m & __ballot(!iso);
             const unsigned long long mi = mg ? m & ((mg & (0ull - mg)) - 1ull) : m;
             if (mi) {
                 if ((mi >> lane) & 1ull) {
-                    U.set1(px, py);
+                    U.set1(px, py, c0);
                     cand = false;
                 }
                 U.sync();
@@ -1395,18 +1449,23 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
             const bool has_pre = pre_j == j;
             const float4 cur = pre;
             const float2 cur_cs = pcs;
+            const uint32_t cur_c = pre_c;
             const unsigned long long m2 = mg & ~((2ull << j) - 1ull);
             pre_j = m2 ? __ffsll((long long)m2) - 1 : -1;
             pre = make_float4(-1.0f, 0.f, 0.f, 0.f);
             if (pre_j >= 0) {   // (separate registers: no wait for one load before the other)
                 const int cx = rl_i(px, pre_j), cy = rl_i(py, pre_j);
                 const int xx = cx + lane % 5 - 2, yy = cy + lane / 5 - 2;
-                if (lane < 25 && xx >= 0 && yy >= 0 && xx < o.W && yy < o.H) pre = I.px[yy * o.W + xx];
+                if (lane < 25 && xx >= 0 && yy >= 0 && xx < o.W && yy < o.H) {
+                    pre = I.px[yy * o.W + xx];
+                    if (LU) pre_c = cidp[yy * o.W + xx];
+                }
                 if (lane == 25) pcs = o.scs[off + (size_t)cy * o.W + cx];
             }
             double reg_angle;
             bool in_hbm;
-            int n = region_grow<LU>(I, U, sx, sy, rl_f(a0, j), o.prec, reg_angle, in_hbm, has_pre, cur, cur_cs);
+            int n = region_grow<LU>(I, U, sx, sy, LU ? (uint32_t)rl_i((int)c0, j) : 0u, rl_f(a0, j), o.prec, reg_angle,
+                                    in_hbm, has_pre, cur, cur_cs, cur_c);
             if (n < o.min_reg_size) continue;
             ring_to_hbm(I, n, in_hbm);
             mem_sync();   // the region list (HBM) is read by every lane next
@@ -1429,12 +1488,17 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
 
 }  // namespace
 
+// one wave per image, both launched over the batch: the compact LDS bitmap (cid_cap bits
+// after the ring) for the images with at most cid_cap defined pixels, the HBM byte map for the
+// others (separate kernels: one holding both paths took 184 VGPRs and a private segment)
 __global__ void __launch_bounds__(64) k_lsd_grow_lds(LsdDev o) {
     extern __shared__ uint32_t lds[];
+    if (o.ndef[blockIdx.x] > o.cid_cap) return;
     lsd_image<true>(o, blockIdx.x, lds + LSD_RING, lds);
 }
 __global__ void __launch_bounds__(64) k_lsd_grow_glb(LsdDev o) {
     __shared__ uint32_t ring[LSD_RING];
+    if (o.ndef[blockIdx.x] <= o.cid_cap) return;
     lsd_image<false>(o, blockIdx.x, nullptr, ring);
 }
 
@@ -1522,7 +1586,6 @@ struct gfpl_lsd {
     gfpl_ctx* ctx = nullptr;   // counted in while this object lives
     AsyncStatus st;
     int max_images = 0;
-    bool lds_used = false;
     size_t lds_bytes = 0;
     LsdDev d{};
     void* base = nullptr;
@@ -1559,14 +1622,16 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
         d.min_reg_size = (int)(size_t)(-log_nt / std::log10(p));
     }
     const size_t px = (size_t)width * height, M = (size_t)max_images, NP = (size_t)d.NP, SC = (size_t)seg_cap;
-    o->lds_used = (px + 31) / 32 * 4 <= LSD_USED_LDS_MAX;
-    o->lds_bytes = (px + 31) / 32 * 4 + 4 * LSD_RING;
+    // the compact used map covers a quarter of the pixels defined (VGA: 9.6 KB; the scenes
+    // measured define 5-8%), so 15 images share a CU's LDS instead of 4 with a full-image bitmap
+    d.cid_cap = (int)std::min<size_t>(((px + 3) / 4 + 31) & ~(size_t)31, LSD_CID_MAX);
+    o->lds_bytes = (size_t)d.cid_cap / 8 + 4 * LSD_RING;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t b_tab = al(16 * 1021 * 1021), b_px = al(16 * M * px), b_scs = al(8 * M * px), b_ang = al(4 * M * px), b_max = al(8 * M),
                  b_keys = al(8 * M * NP), b_pos = al(4 * M * NP), b_reg = al(4 * M * px),
-                 b_used = o->lds_used ? 0 : al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
+                 b_used = al(M * px), b_segs = al(16 * M * SC), b_nseg = al(4 * M),
                  b_klt = al(24 * M * SC), b_rk = al(8 * M * SC), b_rl = al(4 * M * SC);
-    const size_t total = b_tab + b_px + b_scs + b_ang + b_max + b_keys + 2 * b_pos + 2 * b_reg + b_used + b_segs + b_nseg +
+    const size_t total = b_tab + b_px + b_scs + b_ang + b_max + b_keys + 2 * b_pos + 3 * b_reg + b_used + b_segs + 2 * b_nseg +
                          b_klt + b_rk + 2 * b_rl + 256;
     if (hipMalloc(&o->base, total) != hipSuccess) { delete o; return GFPL_E_HIP; }
     char* p = (char*)o->base;
@@ -1580,16 +1645,17 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     d.rpos = (int*)p; p += b_pos;
     d.reg = (uint32_t*)p; p += b_reg;
     d.tmp = (uint32_t*)p; p += b_reg;
-    d.used_g = b_used ? (uint8_t*)p : nullptr; p += b_used;
+    d.cid = (uint32_t*)p; p += b_reg;
+    d.used_g = (uint8_t*)p; p += b_used;
     d.segs = (float4*)p; p += b_segs;
     d.nseg = (int*)p; p += b_nseg;
+    d.ndef = (int*)p; p += b_nseg;
     d.kl_tmp = (float*)p; p += b_klt;
     d.rkeys = (uint64_t*)p; p += b_rk;
     d.rl = (int*)p; p += b_rl;
     d.rr = (int*)p; p += b_rl;
     d.err = (int*)p;
-    if (o->lds_used &&
-        hipFuncSetAttribute((const void*)k_lsd_grow_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_lsd_grow_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)o->lds_bytes) != hipSuccess) {
         (void)hipFree(o->base);
         delete o;
@@ -1632,15 +1698,15 @@ extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, 
     if (hipSetDevice(o->device) != hipSuccess) return GFPL_E_HIP;
     const LsdDev& d = o->d;
     hipStream_t s = o->stream;
-    if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess) return GFPL_E_HIP;
+    if (hipMemsetAsync(d.maxg, 0, 8 * (size_t)n, s) != hipSuccess ||
+        hipMemsetAsync(d.ndef, 0, 4 * (size_t)n, s) != hipSuccess)
+        return GFPL_E_HIP;
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.W - 1 + 63) / 64, (d.H - 1 + 3) / 4, n), dim3(256), 0, s, d, images);
     hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
-    if (o->lds_used)
-        hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
-    else
-        hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
     hipLaunchKernelGGL(k_lsd_keylines, dim3(n), dim3(64), 0, s, d, keylines, n_kl, response);
     if (hipGetLastError() != hipSuccess) return GFPL_E_HIP;
     return o->st.enqueue(s) == hipSuccess ? GFPL_OK : GFPL_E_HIP;

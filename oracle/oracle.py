@@ -347,6 +347,18 @@ def lsd_constants(width: int, height: int, params=None):
     return pr.value, rho.value, mrs.value
 
 
+def lsd_defined_count(image: np.ndarray, params=None) -> int:
+    """Pixels with a defined level-line angle (ledger S1: norm = sqrt((gx^2 + gy^2) / 4) > rho,
+    the last row and column NOTDEF)."""
+    im = np.asarray(image, np.int64)
+    h, w = im.shape
+    _, rho, _ = lsd_constants(w, h, params)
+    da = im[1:, 1:] - im[:-1, :-1]
+    bc = im[:-1, 1:] - im[1:, :-1]
+    gx, gy = da + bc, da - bc
+    return int((np.sqrt((gx * gx + gy * gy) / 4.0) > rho).sum())
+
+
 def atan2(y: float, x: float) -> float:
     return lib().gfplo_atan2(y, x)
 

@@ -61,11 +61,25 @@ def test_lsd_parity_cameras(cam):
     _check(np.stack([left, right, gfpl.synth_image(5, 0, w, h)]))
 
 
-def test_lsd_parity_global_used_map():
-    """1280 x 720: the used map does not fit the LDS bitmap (global byte map path)."""
+def test_lsd_parity_large_image():
+    """1280 x 720: a 28.8 KB compact used map (a quarter of the pixels)."""
     w, h = 1280, 720
     left, _, _, _ = P.synth_stereo_steps(4, 0, w, h)
     _check(np.stack([left]), kl_cap=600)
+
+
+def test_lsd_parity_mixed_used_maps():
+    """One batch whose noise images define more than a quarter of their pixels (HBM byte map,
+    k_lsd_grow_glb) between scene images (compact LDS bitmap, k_lsd_grow_lds)."""
+    w, h = 320, 240
+    rng = np.random.default_rng(11)
+    noise = rng.integers(0, 256, (h, w)).astype(np.uint8)
+    blocks = np.clip(noise.astype(np.int32) // 4 + np.kron(rng.integers(0, 4, (h // 40, w // 40)) * 60,
+                                                           np.ones((40, 40), np.int32)), 0, 255).astype(np.uint8)
+    left, right, _, _ = P.synth_stereo_steps(4, 0, w, h)
+    ndef = [O.lsd_defined_count(im) for im in (noise, blocks, left)]
+    assert ndef[0] > w * h // 4 and ndef[1] > w * h // 4 and ndef[2] < w * h // 4, ndef
+    _check(np.stack([left, noise, right, blocks]), gfpl.LsdParams.reference(w, h, n_features=0), kl_cap=4096)
 
 
 def test_lsd_keep_all_and_small_budget():
