@@ -109,6 +109,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
+    ap.add_argument("--b1-steps", type=int, default=40, help="timed steps of the B = 1 latency leg")
     ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only (gloo): launcher, broadcast, sharding, input generation and reductions; "
@@ -345,6 +347,65 @@ def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, 
             "host": cores_info}
 
 
+def latency_b1(ctx, cam, cfg, sp, kp_cap, kl_cap, seq, warmup, steps):
+    """Per-frame latency of ONE sequence (B = 1, rank 0 at N = 1, after the timed batch; not
+    part of `value`): the same workload's sequence `seq` stepped alone — wall clock per
+    frameStep bracketed by device syncs (inputs resident in HBM, uploaded before), HIP-event
+    stage / kernel times of every timed step — beside the CPU oracle's single-thread time per
+    frame on the same frames of the same sequence (the reference runs one sequence on one
+    core: app/plslam_mod.cpp:387-411)."""
+    import torch
+    import gfpl
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n_fr = warmup + steps + 1
+    H = gfpl.HostFrames(cam, sp, 1, n_fr, kp_cap, kl_cap, seq0=seq, threads=1)
+    h = gfpl.StereoFrameHandler(ctx, 1, kp_cap, kl_cap)
+
+    def staged(k):
+        h.upload_wait(h.upload_async(H.frames(k), 0, k % 2))
+        return h.staged_frames(k % 2)
+    h.initialize(staged(0))
+    wall, st, kt = [], [], []
+    for k in range(1, n_fr):
+        dv = staged(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h.frameStep(dv)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if k > warmup:
+            wall.append(t1 - t0)
+            st.append(ctx.stage_times())
+            kt.append(ctx.kernel_times())
+    h.close()
+    o = O.OracleHandler(cam, cfg, kp_cap, kl_cap)
+    o.initialize(H.frames(0), 0)
+    cpu = []
+    for k in range(1, n_fr):
+        t0 = time.perf_counter()
+        o.insertStereoPair(H.frames(k), 0)
+        o.optimizePose()
+        o.updateFrame()
+        if k > warmup:
+            cpu.append(time.perf_counter() - t0)
+    sm = np.mean(np.array(st, dtype=np.float64)[:, :6], axis=0)
+    km = np.mean(np.array(kt, dtype=np.float64), axis=0)
+    lat = 1e3 * float(np.mean(wall))
+    cpu_ms = 1e3 * float(np.mean(cpu))
+    return {"latency_b1_ms": lat, "latency_b1_p50_ms": 1e3 * float(np.median(wall)),
+            "latency_b1_max_ms": 1e3 * float(np.max(wall)),
+            "stage_ms_b1": {n: round(float(v), 4) for n, v in zip(STAGES, sm)},
+            "kernel_ms_b1": {n: round(float(v), 4) for n, v in
+                             zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
+            "b1_slowest_stage": STAGES[int(np.argmax(sm))],
+            "stage_sum_b1_ms": float(np.sum(sm)),
+            "cpu_1thread_ms_per_frame": cpu_ms,
+            "gpu_b1_vs_one_core": cpu_ms / lat,
+            "sample": f"sequence {seq}, frames {warmup + 1}..{n_fr - 1} ({steps} steps) after {warmup} warm-up steps; "
+                      f"CPU: oracle/ C++ on one host thread, the same frames"}
+
+
 # ----------------------------------------------------------------------- main --
 def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     """SURVEY §8(f)1-2 on the bench camera, measured after the timed tracking steps (not part of
@@ -402,32 +463,34 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
                   "parity_vs_oracle_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
     lbd.close()
     # LSD (gfpl_lsd_detect, the reference's LSDOptions, 300 keylines kept): its per-image chain
-    # (sort + region growing) is latency-bound, so it is measured at 4 images per CU
-    n_lsd = 1024
+    # (sort + region growing) is latency-bound; measured at 2048 images per call (the left and
+    # right images of images_to_poses_lsd's 1024-frame step) and at 1024
     from gfpl.pipeline import synth_stereo_steps
+    n_max = 2048
     li = np.stack([synth_stereo_steps(i // 2, 0, W, H)[i % 2] for i in range(8)]
-                  + [imgs[i % n_img] for i in range(n_lsd - 8)])
+                  + [imgs[i % n_img] for i in range(n_max - 8)])
     d_li = torch.from_numpy(li).to(dev)
-    lsd = gfpl.LSDDetector(W, H, max_images=n_lsd, kl_cap=320)
-    d_kl = torch.zeros(n_lsd * 320 * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
-    d_n = torch.zeros(n_lsd, dtype=torch.int32, device=dev)
-    lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
-    t = []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+    lsd = gfpl.LSDDetector(W, H, max_images=n_max, kl_cap=320)
+    d_kl = torch.zeros(n_max * 320 * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
+    d_n = torch.zeros(n_max, dtype=torch.int32, device=dev)
+    for n_lsd, key in ((2048, "lsd"), (1024, "lsd_1024")):
         lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
-        t.append(time.perf_counter() - t0)
-    kl_all = d_kl.cpu().numpy().view(gfpl.KEYLINE_DT).reshape(n_lsd, 320)
-    cnt = d_n.cpu().numpy()
-    par = True
-    for i in (0, 1, 8):
-        rk, _, _ = O.lsd_detect(li[i])
-        par = par and int(cnt[i]) == len(rk) and kl_all[i, :cnt[i]].tobytes() == rk.tobytes()
-    out["lsd"] = {"images_per_s": n_lsd / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
-                  "images_per_call": n_lsd, "keylines_per_image": float(cnt.mean()),
-                  "parity_vs_oracle_images_0_1_8": bool(par),
-                  "data": "8 staircase stereo images + gfpl_synth_image textures"}
+        t = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
+            t.append(time.perf_counter() - t0)
+        kl_all = d_kl.cpu().numpy().view(gfpl.KEYLINE_DT).reshape(n_max, 320)
+        cnt = d_n.cpu().numpy()[:n_lsd]
+        par = True
+        for i in (0, 1, 8):
+            rk, _, _ = O.lsd_detect(li[i])
+            par = par and int(cnt[i]) == len(rk) and kl_all[i, :cnt[i]].tobytes() == rk.tobytes()
+        out[key] = {"images_per_s": n_lsd / float(np.mean(t)), "ms_per_call": 1e3 * float(np.mean(t)),
+                    "images_per_call": n_lsd, "keylines_per_image": float(cnt.mean()),
+                    "parity_vs_oracle_images_0_1_8": bool(par),
+                    "data": "8 staircase stereo images + gfpl_synth_image textures"}
     lsd.close()
     # with detection on the GPU a host-fed pipeline uploads the two grey images of a stereo
     # frame instead of the pyramid + features: the PCIe ceiling derived from the measured rate
@@ -750,6 +813,12 @@ def main():
                          "unit": "G wave-VALU-instructions/s", "frac": gips / VALU_PEAK_GIPS,
                          "valu_insts_per_launch": pmc["SQ_INSTS_VALU"], "waves_per_launch": pmc.get("SQ_WAVES"),
                          "source": os.path.relpath(args.pmc, ROOT)}
+        b1 = None
+        if world == 1 and not args.no_b1:
+            try:
+                b1 = latency_b1(ctx, cam, cfg, sp, KP, KL, seq0, W, args.b1_steps)
+            except Exception as e:   # reported, never fatal to the contract line
+                b1 = {"error": f"{type(e).__name__}: {e}"}
         cpu = None
         if world == 1 and not args.no_cpu:
             nt = args.cpu_threads or cores
@@ -821,6 +890,8 @@ def main():
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
             "stage_bytes_per_step": {n: int(v) for n, v in zip(STAGES, sb)},
             "cpu_baseline": cpu,
+            "latency_b1_ms": b1.get("latency_b1_ms") if b1 else None,
+            "latency_b1": b1,
             "detection": det,
             "host": host_info,
             "gen_s": round(t_gen, 2),

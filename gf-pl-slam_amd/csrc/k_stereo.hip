@@ -209,6 +209,13 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #ifndef GFPL_SP_WAVES
 #define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
+// a wave-uniform float pinned to a scalar register (the compiler folds a plain readfirstlane of
+// a uniform value and keeps it in a VGPR)
+__device__ __forceinline__ float sgpr_f32(float v) {
+    float r;
+    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v));
+    return r;
+}
 #define SP_CHUNK 32       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
 #define SP_MINR_PAD 32    // minr bins span [-PAD, H + PAD) (k_stereo_points, SEG): every band is shorter
 
@@ -400,8 +407,10 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         return (int)rowlo[o * NBIN + min(max(row - misc[22 + o] + SP_MINR_PAD, 0), NBIN - 1)];
     };
     const float minD = 0;
-    const float maxD = (float)p.cam.fx;
-    const float mbf = (float)(p.cam.fx * p.cam.b);
+    // uniform constants kept in scalar registers (held as VGPRs, maxD was the kernel's one
+    // spill at its 80-register budget)
+    const float maxD = sgpr_f32((float)p.cam.fx);
+    const float mbf = sgpr_f32((float)(p.cam.fx * p.cam.b));
     // per left keypoint: band search + Hamming (src/stereoFrame.cpp:502-545).  A match
     // leaves (bestDist, bestIdxR) in pairs[iL] and iL in order[t] for the sub-pixel pass;
     // order[t] / pairs[iL] are private to the thread that owns slot t.
