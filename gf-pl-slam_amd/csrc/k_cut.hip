@@ -559,15 +559,33 @@ struct CutCmp {
     // EV (1/v's + 1/v'e) <= 1/4.  Floats: R0 rounded down, the others up.
     float eb[6];             // R0, A1, A2, B1, B2, EV
 };
+// The step's operands (CutCmp without bs / be), held in registers from one reload to the next:
+// they are reloaded after a line transition or an exact round and dead inside those blocks, so
+// the per-step loop reads no LDS (before: 18 ds_read2_b64 per step) and the transition / exact
+// code keeps its register budget.
+struct CutReg {
+    double ns[5], ne[5], vs[5], ve[5], cc[9], bnd[3];
+    float eb[6];
+};
+__device__ __forceinline__ void cut_reg_load(const CutCmp& c, CutReg& r) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { r.ns[i] = c.ns[i]; r.ne[i] = c.ne[i]; r.vs[i] = c.vs[i]; r.ve[i] = c.ve[i]; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.cc[i] = c.cc[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r.bnd[i] = c.bnd[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.eb[i] = c.eb[i];
+}
 
 // d at (t0, t1), NaN when not healthy; bound_ok: the forward rounding-error bound of
-// d (relative, unit roundoff u, first order) is at most tau / 4:
+// d (relative, unit roundoff u, first order) is at most tau / 4 (tq = tau / 4 - 4u):
 //   40u [(Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2] / D + 16u (VsA / v's + VeA / v'e) + 4u,
 // where Bs^2 bounds the absolute terms of Ns and of the Gram entries behind it, Bs Be
 // those of C, VsA those of v's (Horner with absolute coefficients at |t|).
 // with P1 = (Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2 given
 __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, double Ve, double C, double P1,
-                                              double VsA, double VeA, const float* eb, double tau, int& bound_ok) {
+                                              double VsA, double VeA, const float* eb, double tq, int& bound_ok) {
     const double D = __builtin_fma(Vs + Ns, Ve + Ne, -(C * C));
     const double den = Vs * Ve;
     const double r = rcp_fast(den);
@@ -581,17 +599,17 @@ __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, 
     const float E = __builtin_fmaf(iVs, __builtin_fmaf(eb[2], iVs, eb[1]), iVe * __builtin_fmaf(eb[4], iVe, eb[3]));
     const bool agree = E * 1.0001f <= eb[0] && eb[5] * (iVs + iVe) <= 0.25f;
     bound_ok = healthy && agree &&
-               __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= (0.25 * tau - 4.0 * u) * Dd;
+               __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= tq * Dd;
     return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
 }
 // Bs, Be, VsA, VeA are Horner sums of non-negative terms in |t|, increasing in |t|: their values at
 // T = max(|rlo|, |rhi|) bound them for every valid neighbour (|t0|, |t1| <= T), so the line's P1,
 // VsA, VeA (cmp.bnd, formed when it opens) replace the four per-neighbour evaluations
-__device__ __forceinline__ double cut_dval(const CutCmp& c, double t0, double t1, double tau, int& bound_ok) {
+__device__ __forceinline__ double cut_dval(const CutReg& c, double t0, double t1, double tq, int& bound_ok) {
     const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
     const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
                                    h2(c.cc[0], c.cc[3], c.cc[6], t0));
-    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tau, bound_ok);
+    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tq, bound_ok);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -867,6 +885,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     const double tau = p.cfg.cut_certify;
+    const double tq = sgpr_f64(0.25 * tau - 4.0 * 0x1p-53);   // d's bound budget (cut_dcore_p1)
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
@@ -880,7 +899,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     double* const gm = &tmp[g][36];
     // neighbour j of this lane
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
-    const unsigned long long gmask = 0xFFull << (8 * g);
     constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
     // group state (identical in the 8 lanes of a group)
     int m = 0;
@@ -990,7 +1008,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         wave_lds_sync();
         // the centre of the first step: d at (0, 0)
         const double vs0 = cl[10], ve0 = cl[15];
-        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tau, c_ok);
+        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
@@ -1018,6 +1036,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (nls > 1) pf_issue(1);
     }
     __syncthreads();
+    CutReg cr;
+    cut_reg_load(cmpl[g], cr);
     int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
@@ -1029,10 +1049,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (t1 < rlo || t1 > rhi) valid = 0;
         int bok;
         double dj;
-        {
-            const CutCmp cmp = cmpl[g];
-            dj = cut_dval(cmp, t0, t1, tau, bok);
-        }
+        dj = cut_dval(cr, t0, t1, tq, bok);
         double top;
         int best = group_first_max(dj, valid, j, dc, top);
         // every comparison the decision rests on must clear the margin, every d its
@@ -1046,7 +1063,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (valid && !(dc - dj > tau * dc)) ok = 0;
         }
         if (!(tau > 0.0 && line_ok && c_ok && dc == dc)) ok = 0;
-        const bool exact = act && (__ballot(!ok) & gmask) != 0;
+        const bool exact = act && ((__ballot(!ok) >> (8 * g)) & 0xFFull) != 0;   // (the group's 8 bits)
         n_steps += act ? 1 : 0;
         n_exact += exact ? 1 : 0;
         double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
@@ -1062,6 +1079,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const double sd = __shfl(dj, src);
             const int sb = __shfl(bok, src);
             if (exact) { dnext = sd; cnext = sb; }
+            cut_reg_load(cmpl[g], cr);   // (unchanged; reloaded so that it is dead across the call)
         }
         int finalize = 0;
         if (act) {
@@ -1179,6 +1197,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
+            cut_reg_load(cmpl[g], cr);   // the opened lines' operands (the others' unchanged)
         } else if (pend) {
             ++wait;
         }

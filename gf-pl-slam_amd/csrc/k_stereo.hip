@@ -209,13 +209,6 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #ifndef GFPL_SP_WAVES
 #define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
-// a wave-uniform float pinned to a scalar register (the compiler folds a plain readfirstlane of
-// a uniform value and keeps it in a VGPR)
-__device__ __forceinline__ float sgpr_f32(float v) {
-    float r;
-    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v));
-    return r;
-}
 #define SP_CHUNK 32       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
 #define SP_MINR_PAD 32    // minr bins span [-PAD, H + PAD) (k_stereo_points, SEG): every band is shorter
 
