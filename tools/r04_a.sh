@@ -10,3 +10,4 @@ grep -E "^(FAILED|ERROR)" $O/pytest_gpu.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 240 python bench.py --steps 20 --warmup 5 --no-detect > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['stage_ms'], d['kernel_ms'], d['cut_search'], d['parity_sampled']['mismatches'], d['host_fed'], d['counts_per_seq_step'])"
+bash tools/ab_bench.sh $O/ab 10 build/base default
