@@ -34,8 +34,8 @@
 
 namespace gfpl {
 
-// ranges up to CAP elements are sorted in LDS: CAP 2048 (34 KB, 4 images per CU) for batches up to
-// 4 images per CU, CAP 1024 (19 KB, 8 images per CU) above
+// ranges up to CAP elements are sorted in LDS: CAP 1024 (36.5 KB per two-wave workgroup, 4 images
+// per CU) for batches up to 4 images per CU, CAP 512 (24 KB, 6 per CU) above (k_lsd_sort<CAP>)
 #define LSD_RING 256               // region list entries mirrored in LDS
 #define LSD_SMALL 64               // ranges up to this size: one lane runs libstdc++'s serial loop
                                    // (32 / 48 / 64 / 96: 22.2k / 23.5k / 23.7k / 23.1k images/s)
@@ -991,8 +991,12 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o, const uint8_t* image
         ((uint64_t)(uint32_t)bin << 32) | (iso << 31) | ((uint32_t)y << 16) | (uint32_t)x;
 }
 
+// CAP: LSD_SORT_CAP (36.5 KB per workgroup, four images per CU) for batches up to four images per
+// CU; half of it (24 KB, six per CU) for larger batches, whose images would otherwise run in two
+// rounds of four per CU (the ranges between the capacities partition in HBM instead of LDS)
+template <int CAP>
 __global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(LSD_SORT_WAVES))) k_lsd_sort(LsdDev o) {
-    __shared__ SortLdsMW<LSD_SORT_CAP, LSD_SORT_WAVES> S;
+    __shared__ SortLdsMW<CAP, LSD_SORT_WAVES> S;
     const size_t img = blockIdx.x;
     // B0 as lsd_image computes it (the bins of k_lsd_keys)
     const double mg = __longlong_as_double((long long)o.maxg[img]);
@@ -1586,6 +1590,7 @@ struct gfpl_lsd {
     gfpl_ctx* ctx = nullptr;   // counted in while this object lives
     AsyncStatus st;
     int max_images = 0;
+    int n_cu = 256;            // compute units of the device (the sort's capacity choice)
     size_t lds_bytes = 0;
     LsdDev d{};
     void* base = nullptr;
@@ -1603,6 +1608,10 @@ extern "C" int gfpl_lsd_create(gfpl_ctx* ctx, const gfpl_lsd_params* prm, int wi
     o->device = dev;
     o->stream = (hipStream_t)gfpl_ctx_stream(ctx);
     o->max_images = max_images;
+    {
+        int cu = 0;
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cu > 0) o->n_cu = cu;
+    }
     LsdDev& d = o->d;
     d.W = width;
     d.H = height;
@@ -1704,7 +1713,10 @@ extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, 
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.W - 1 + 63) / 64, (d.H - 1 + 3) / 4, n), dim3(256), 0, s, d, images);
-    hipLaunchKernelGGL(k_lsd_sort, dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
+    if (n <= 4 * o->n_cu)
+        hipLaunchKernelGGL((k_lsd_sort<LSD_SORT_CAP>), dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
+    else
+        hipLaunchKernelGGL((k_lsd_sort<LSD_SORT_CAP / 2>), dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
     hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
     hipLaunchKernelGGL(k_lsd_keylines, dim3(n), dim3(64), 0, s, d, keylines, n_kl, response);

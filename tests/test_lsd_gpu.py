@@ -168,7 +168,7 @@ def test_lsd_parity_dense_scenes():
 
 
 def test_lsd_parity_large_batch_small_lds_sort():
-    """More than 4 images per CU: the sort runs with the 1024-element LDS capacity (8 per CU)."""
+    """More than 4 images per CU: the sort runs with the 512-element LDS capacity (k_lsd_sort<512>)."""
     w, h = 96, 72
     n = 1100
     imgs = np.stack([_dense_image(1000 + i, w, h) if i % 50 == 0 else gfpl.synth_image(i, 0, w, h)
