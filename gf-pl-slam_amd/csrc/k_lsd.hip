@@ -1104,7 +1104,7 @@ __device__ int region_grow(const Img& I, const Used<LU>& U, int sx, int sy, uint
                 r = n - idx > LSD_RING ? I.reg[idx] : (uint32_t)ring[idx & (LSD_RING - 1)];
             }
         } else if (g < nb) {
-            r = ring[(i + g) & (LSD_RING - 1)];
+            r = i == 0 ? s : (uint32_t)ring[(i + g) & (LSD_RING - 1)];   // (the first batch is the seed)
         }
         if (g < nb) {
             rx = (int)(r & 0xffff);
