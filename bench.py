@@ -883,6 +883,8 @@ def main():
             "cut_search": {"steps": int(sum(c["steps"] for c in cutc)),
                            "exact_steps": int(sum(c["exact_steps"] for c in cutc)),
                            "exact_frac": float(sum(c["exact_steps"] for c in cutc) / max(1, sum(c["steps"] for c in cutc))),
+                           "lines_unbounded_frac": float(sum(c["lines_unbounded"] for c in cutc) /
+                                                         max(1.0, B * float(sum(c["M_l"] for c in counts)))),
                            "note": "greedy steps of the timed window; exact_steps: evaluated with the reference's own "
                                    "arithmetic because a margin or the proven agreement bound failed (DESIGN.md §3)"},
             "host_fed": host_fed,

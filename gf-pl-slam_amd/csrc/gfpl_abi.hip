@@ -183,6 +183,9 @@ KParams params(gfpl_seqbatch* sb, const gfpl_frames* in) {
     // seqbatch lives, so these clamps never change a result (defence in depth)
     p.cfg.max_point_match_num = std::min(p.cfg.max_point_match_num, sb->mpt_cap);
     p.cfg.max_line_match_num = std::min(p.cfg.max_line_match_num, sb->mls_cap);
+    p.sp_maxD = (float)p.cam.fx;
+    p.sp_mbf = (float)(p.cam.fx * p.cam.b);
+    p.cut_tq = 0.25 * p.cfg.cut_certify - 4.0 * 0x1p-53;
     return p;
 }
 
@@ -1175,6 +1178,15 @@ int gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4) {
     if (e) return e;
     for (int s = 0; s < 4; ++s) counts4[s] = v[16 + s];
     return GFPL_OK;
+}
+
+int gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines) {
+    if (!sb || !out || b < 0 || b >= sb->B || n_lines < 0 || n_lines > sb->mls_cap) return GFPL_E_INVALID;
+    if (hipSetDevice(sb->ctx->device) != hipSuccess) return GFPL_E_HIP;
+    if (hipStreamSynchronize(sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+    const size_t n = (size_t)n_lines * CUT_REC;
+    return hipMemcpy(out, sb->scr.cut_rec + (size_t)b * sb->mls_cap * CUT_REC, n * sizeof(double),
+                     hipMemcpyDeviceToHost) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
 }
 
 int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {

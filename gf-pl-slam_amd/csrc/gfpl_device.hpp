@@ -421,21 +421,6 @@ GFPL_DEV double logdet6_lower(double* a /* 21, destroyed */) {
 template <typename T>
 GFPL_DEV void swap_v(T& a, T& b) { T t = a; a = b; b = t; }
 
-// Wave-uniform values pinned to scalar registers (the compiler folds a plain readfirstlane of a
-// uniform value and may keep it in a VGPR, which it then spills under pressure).  Call where
-// every lane of the wave is active (kernel scope).
-__device__ __forceinline__ float sgpr_f32(float v) {
-    float r;
-    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(v));
-    return r;
-}
-__device__ __forceinline__ double sgpr_f64(double v) {
-    int lo, hi;
-    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(lo) : "v"(__double2loint(v)));
-    asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(hi) : "v"(__double2hiint(v)));
-    return __hiloint2double(hi, lo);
-}
-
 // LDLT solve, Eigen 3.3 semantics (see oracle ldlt_solve6).  ONE LANE only (k_pose's lane 0):
 // each pivot index is made wave-uniform (readfirstlane), so a pivot swap is one scalar branch
 // to the block of moves for that index instead of selects over every candidate index.

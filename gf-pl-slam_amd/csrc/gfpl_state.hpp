@@ -75,7 +75,8 @@ struct DevTrack {
 #define STEP_REC 20   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
                       // [8..15] counts N_o N_k M_o S_p' S_l' M_p M_l n_inliers (gfpl_last_step_counts),
                       // [16] line-cut search steps, [17] of them evaluated exactly (k_cut_search),
-                      // [18] n_inliers after optimize_pose (k_pose_finish), [19] 0
+                      // [18] n_inliers after optimize_pose (k_pose_finish), [19] lines whose agreement bound
+                      // was unusable (k_cut_search: R0 <= 0 or a term not finite; their steps are exact)
 #define CUT_FAST 56   // doubles of per-line comparison data (k_cut.hip, PD_*): polynomials, flags, error bounds
 #define CUT_REC 80    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (640 B)
 
@@ -108,6 +109,11 @@ struct KParams {
     gfpl_frames in;       // device pointers of the current input batch
     int B, kp_cap, kl_cap, mpt_cap, mls_cap;
     const double* dt_ini; // [B*16] explicit GN initial guesses (optimizePose(DT_ini)); null: prev.DT
+    // derived constants, formed on the host so the kernels read them as scalars (kernel
+    // arguments live in SGPRs; the same values formed on the device sit in VGPRs, which the
+    // register allocator spills under pressure)
+    float sp_maxD, sp_mbf;   // k_stereo_points: (float)fx, (float)(fx * b)
+    double cut_tq;           // k_cut_search: cut_certify / 4 - 4u, the budget of d's rounding bound
 };
 
 }  // namespace gfpl

@@ -462,7 +462,9 @@ __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
 #define CUT_SL 7         // exact endpoint slot (X): v, J[6]
 #define CUT_EP 43        // per-group exact endpoint block: 6 slots + 1 (odd stride)
 #define CUT_NX (CUT_FAST + 21)   // used part of a line record: comparison data | r = 0 info
-static_assert(CUT_REC * 8 == 640 && CUT_NX <= CUT_REC, "a record is 5 x 128 B: five 16-B loads per lane");
+static_assert(CUT_REC * 8 == 640 && CUT_NX + 3 <= CUT_REC, "a record is 5 x 128 B: five 16-B loads per lane");
+// record slots CUT_NX .. CUT_NX + 2: the line's agreement bound as k_cut_search formed it (6 floats,
+// CutCmp::eb; diagnostics, gfpl_debug_cut_records)
 
 // One reference-order cut endpoint (cut_endpoint) of line q: side 0 the start
 // endpoint blended sP -> eP, side 1 the end endpoint eP -> sP, at ratio t.
@@ -597,7 +599,12 @@ __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, 
     // agreement with the reference's metric (CutCmp::eb), in f32 with a 1e-4 allowance
     const float iVs = (float)(Ve * r), iVe = (float)(Vs * r);
     const float E = __builtin_fmaf(iVs, __builtin_fmaf(eb[2], iVs, eb[1]), iVe * __builtin_fmaf(eb[4], iVe, eb[3]));
+#ifdef GFPL_CUT_DBG_AGREE_OFF
+    const bool agree = true;   // (diagnostic build only: the agreement test disabled)
+    (void)E;
+#else
     const bool agree = E * 1.0001f <= eb[0] && eb[5] * (iVs + iVe) <= 0.25f;
+#endif
     bound_ok = healthy && agree &&
                __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= tq * Dd;
     return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
@@ -885,7 +892,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     const double tau = p.cfg.cut_certify;
-    const double tq = sgpr_f64(0.25 * tau - 4.0 * 0x1p-53);   // d's bound budget (cut_dcore_p1)
+    const double tq = p.cut_tq;   // d's bound budget tau / 4 - 4u (cut_dcore_p1; a kernel argument: SGPRs)
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)(live ? b : 0) * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
@@ -910,6 +917,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     int wait = 0;        // iterations spent waiting for that transition
     double dc = 0.0;     // d of the centre
     int c_ok = 0;        // its error bound is within tau / 4
+    int n_unb = 0;       // lines opened without a usable agreement bound
     // A line opens (its data in fst, S in registers): every lane factors S (identical
     // values), lane k < 6 solves W_k = L^-1 P_k (side k / 3, power k % 3), lane j forms
     // Gram entries j, j + 8, j + 16, and every lane reads the 21 back into its
@@ -1006,6 +1014,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         wave_lds_sync();
         if (j == 7) cut_bound_line(T, tau, cl, fst[g], wg, cmpl[g].eb);
         wave_lds_sync();
+        {   // the line's bound, kept in its record (slots CUT_NX.., diagnostics) and counted if unusable
+            const float* e6 = cmpl[g].eb;
+            bool usable = e6[0] > 0.0f;
+#pragma unroll
+            for (int i = 1; i < 6; ++i) usable = usable && e6[i] < __builtin_inff();
+            n_unb += usable ? 0 : 1;
+            if (j < 6 && live) reinterpret_cast<float*>(const_cast<double*>(rec_l) + (size_t)m * CUT_REC + CUT_NX)[j] = e6[j];
+        }
         // the centre of the first step: d at (0, 0)
         const double vs0 = cl[10], ve0 = cl[15];
         dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
@@ -1205,6 +1221,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (live && j == 0) {
         p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
         p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
+        p.scr.bytes[(size_t)STEP_REC * b + 19] = n_unb;
     }
 }
 

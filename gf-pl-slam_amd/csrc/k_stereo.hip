@@ -400,10 +400,10 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         return (int)rowlo[o * NBIN + min(max(row - misc[22 + o] + SP_MINR_PAD, 0), NBIN - 1)];
     };
     const float minD = 0;
-    // uniform constants kept in scalar registers (held as VGPRs, maxD was the kernel's one
-    // spill at its 80-register budget)
-    const float maxD = sgpr_f32((float)p.cam.fx);
-    const float mbf = sgpr_f32((float)(p.cam.fx * p.cam.b));
+    // (float)fx and (float)(fx b) from the kernel arguments (scalar registers): formed here they
+    // sat in VGPRs, and maxD was the kernel's one spill at its 80-register budget
+    const float maxD = p.sp_maxD;
+    const float mbf = p.sp_mbf;
     // per left keypoint: band search + Hamming (src/stereoFrame.cpp:502-545).  A match
     // leaves (bestDist, bestIdxR) in pairs[iL] and iL in order[t] for the sub-pixel pass;
     // order[t] / pairs[iL] are private to the thread that owns slot t.
@@ -1121,7 +1121,7 @@ __global__ void k_step_bytes(KParams p) {
     rec[15] = p.tr.n_inliers[b];
     if (!(p.cfg.use_line_conf_cut && Ml > 0)) rec[16] = rec[17] = 0;   // k_cut_search writes them otherwise
     rec[18] = rec[15];   // until optimize_pose (k_pose_finish) records its inliers
-    rec[19] = 0;
+    if (!(p.cfg.use_line_conf_cut && Ml > 0)) rec[19] = 0;   // k_cut_search writes it otherwise
     // insertStereoPair's last statement, numFrameSinceKeyframe++ (src/stereoFrameHandler.cpp:150):
     // this per-sequence kernel closes every gfpl_insert_stereo_pair
     p.tr.kf_nsince[b] = p.tr.kf_nsince[b] + 1;

@@ -353,6 +353,7 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_last_step_counts": ([P, P], C.c_int),
             "gfpl_last_step_track_counts": ([P, P], C.c_int),
+            "gfpl_debug_cut_records": ([P, C.c_int, P, C.c_int], C.c_int),
             "gfpl_lsd_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_lsd_destroy": ([P], C.c_int),
             "gfpl_lsd_detect": ([P, P, C.c_int, P, P, P], C.c_int),
@@ -1014,7 +1015,14 @@ class StereoFrameHandler:
         left after optimize_pose."""
         v = np.zeros(4, np.int64)
         check(self.L.gfpl_last_step_track_counts(self.h, v.ctypes.data), "last_step_track_counts")
-        return {"steps": int(v[0]), "exact_steps": int(v[1]), "inliers_after_pose": int(v[2])}
+        return {"steps": int(v[0]), "exact_steps": int(v[1]), "inliers_after_pose": int(v[2]),
+                "lines_unbounded": int(v[3])}
+
+    def debug_cut_records(self, b: int, n_lines: int) -> np.ndarray:
+        """gfpl_debug_cut_records: sequence b's line-cut records [n_lines][80] (float64)."""
+        out = np.zeros((n_lines, 80), np.float64)
+        check(self.L.gfpl_debug_cut_records(self.h, b, out.ctypes.data, n_lines), "debug_cut_records")
+        return out
 
     def last_step_kernel_bytes(self) -> np.ndarray:
         v = np.zeros(4, np.int64)

@@ -633,8 +633,13 @@ int  gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8);
 /* More of the last step, summed over the batch: [line-cut greedy steps, steps the
  * certified search evaluated with the reference's own arithmetic (the exact fallback,
  * DESIGN.md §3), n_inliers after optimize_pose (removeOutliers; until it runs, the
- * insert's list sizes), 0].  Synchronises.                                          */
+ * insert's list sizes), searched lines whose agreement bound was unusable —
+ * every step of such a line is exact].  Synchronises.                                */
 int  gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4);
+/* Diagnostics: the line-cut records of sequence b's first n_lines matched lines of the last
+ * insert (80 doubles each: comparison data, bounds, r = 0 info, the agreement bound as
+ * k_cut_search formed it — DESIGN.md §3; layout in k_cut.hip).  Synchronises.      */
+int  gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
  * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same
