@@ -47,7 +47,6 @@ def main():
         print(json.dumps({"frame": k, **tc, "M_l_mean": cnt["M_l"],
                           "exact_frac": tc["exact_steps"] / max(1, tc["steps"])}), flush=True)
     # records of the cut of the last insert: slot 77-79 = eb (6 floats); PD_VS 36, PD_VE 41
-    ml = int(h.read_last_track(0).get("n_matched_ls", a.lines)) if hasattr(h, "read_last_track") else a.lines
     n = min(a.lines, KL)
     rec = h.debug_cut_records(0, n)
     eb = rec[:, 77:80].copy().view(np.float32).reshape(n, 6)
