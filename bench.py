@@ -110,6 +110,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
+    ap.add_argument("--cut-certify", type=float, default=None,
+                    help="gfpl_config.cut_certify (the certified line-cut margin; default: the library's)")
     ap.add_argument("--b1-steps", type=int, default=40, help="timed steps of the B = 1 latency leg")
     ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -603,6 +605,8 @@ def main():
 
     cam_name, synth_over, desc = WORKLOADS[args.workload]
     cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
+    if args.cut_certify is not None:
+        cfg.cut_certify = args.cut_certify
     cam = gfpl.make_camera(cam_name, cfg)
     if world > 1:
         # RCCL broadcast of the camera + config block; every rank

@@ -191,4 +191,4 @@ def test_host_mirror_from_images_matches_the_oracle_chain(tmp_path):
         f = t.split(" ")
         n_kp_l = len(O.orb_extract(imgs[k][0], nfeatures=NFEAT, kp_cap=KP)["kps"])
         assert int(f[11]) == n_kp_l and int(f[12]) == len(O.lsd_detect(imgs[k][0])[0]), (k, f[11:13])
-    assert lines[-1]["matched_pt"] > 30 and lines[-1]["matched_ls"] > 5, lines[-1]
+    assert lines[-1]["matched_pt"] > 20 and lines[-1]["matched_ls"] > 5, lines[-1]   # (tracking, not lost)

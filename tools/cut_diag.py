@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--lines", type=int, default=24)
     ap.add_argument("--workload", default="cfg2")
+    ap.add_argument("--certify", default="", help="comma-separated cut_certify values to sweep (counts only)")
     a = ap.parse_args()
     import torch
     import gfpl
@@ -31,6 +32,31 @@ def main():
     cam = gfpl.make_camera(cam_name, cfg)
     sp = gfpl.synth_params(**synth_over, pyr_from_l0=1)
     KP, KL = 2048, 512
+    if a.certify:
+        H = gfpl.HostFrames(cam, sp, a.batch, a.frames + 1, KP, KL, seq0=0, threads=8)
+        for tau in [float(x) for x in a.certify.split(",")]:
+            c2 = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0,
+                                     cut_certify=tau)
+            ctx = gfpl.Context(cam, c2)
+            h = gfpl.StereoFrameHandler(ctx, a.batch, KP, KL)
+
+            def up(k):
+                h.upload_wait(h.upload_async(H.frames(k), 0, k % 2))
+                return h.staged_frames(k % 2)
+            h.initialize(up(0))
+            tot = {"steps": 0, "exact_steps": 0, "lines_unbounded": 0}
+            ml = 0.0
+            for k in range(1, a.frames + 1):
+                h.frameStep(up(k))
+                tc = h.last_step_track_counts()
+                for n in tot:
+                    tot[n] += tc[n]
+                ml += h.last_step_counts()["M_l"] * a.batch
+            print(json.dumps({"cut_certify": tau, **tot, "exact_frac": tot["exact_steps"] / max(1, tot["steps"]),
+                              "lines_unbounded_frac": tot["lines_unbounded"] / max(1.0, ml)}), flush=True)
+            h.close()
+            ctx.close()
+        return
     ctx = gfpl.Context(cam, cfg)
     h = gfpl.StereoFrameHandler(ctx, a.batch, KP, KL)
     H = gfpl.HostFrames(cam, sp, a.batch, a.frames + 1, KP, KL, seq0=0, threads=8)
