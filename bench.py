@@ -112,6 +112,8 @@ def parse(argv=None):
     ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
     ap.add_argument("--cut-certify", type=float, default=None,
                     help="gfpl_config.cut_certify (the certified line-cut margin; default: the library's)")
+    ap.add_argument("--cut-proof", action="store_true",
+                    help="gfpl_config.cut_proof = 1: margined line-cut decisions only under the proven bound")
     ap.add_argument("--b1-steps", type=int, default=40, help="timed steps of the B = 1 latency leg")
     ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -607,6 +609,8 @@ def main():
     cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     if args.cut_certify is not None:
         cfg.cut_certify = args.cut_certify
+    if args.cut_proof:
+        cfg.cut_proof = 1
     cam = gfpl.make_camera(cam_name, cfg)
     if world > 1:
         # RCCL broadcast of the camera + config block; every rank
@@ -884,7 +888,8 @@ def main():
                                            "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise "
                                            "vs the CPU oracle (oracle/)",
                                "first": sampler.msgs[:3] if sampler else []},
-            "cut_search": {"steps": int(sum(c["steps"] for c in cutc)),
+            "cut_search": {"mode": "proven" if cfg.cut_proof else "measured", "cut_certify": float(cfg.cut_certify),
+                           "steps": int(sum(c["steps"] for c in cutc)),
                            "exact_steps": int(sum(c["exact_steps"] for c in cutc)),
                            "exact_frac": float(sum(c["exact_steps"] for c in cutc) / max(1, sum(c["steps"] for c in cutc))),
                            "lines_unbounded_frac": float(sum(c["lines_unbounded"] for c in cutc) /

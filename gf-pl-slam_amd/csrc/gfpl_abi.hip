@@ -232,6 +232,7 @@ int cfg_supported(const gfpl_config& c) {
     if (c.max_line_match_num < 1 || c.max_line_match_num > GFPL_MAX_MATCHED_LS) return GFPL_E_INVALID;
     // the certified cut search needs a margin far above its ~1e-13 error
     if (!(c.cut_certify == 0.0 || (c.cut_certify >= 1e-10 && c.cut_certify < 1.0))) return GFPL_E_INVALID;
+    if (c.cut_proof != 0 && c.cut_proof != 1) return GFPL_E_INVALID;
     return GFPL_OK;
 }
 

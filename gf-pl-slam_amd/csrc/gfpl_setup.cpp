@@ -44,6 +44,7 @@ extern "C" int gfpl_config_default(gfpl_config* c) {
     c->min_entropy_ratio = 0.90;
     c->max_kf_num_frames = 50;
     c->cut_certify = 1e-9;
+    c->cut_proof = 0;
     return GFPL_OK;
 }
 

@@ -586,6 +586,7 @@ __device__ __forceinline__ void cut_reg_load(const CutCmp& c, CutReg& r) {
 // where Bs^2 bounds the absolute terms of Ns and of the Gram entries behind it, Bs Be
 // those of C, VsA those of v's (Horner with absolute coefficients at |t|).
 // with P1 = (Bs^2 + VsA)(Be^2 + VeA) + Bs^2 Be^2 given
+template <bool PROOF>
 __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, double Ve, double C, double P1,
                                               double VsA, double VeA, const float* eb, double tq, int& bound_ok) {
     const double D = __builtin_fma(Vs + Ns, Ve + Ne, -(C * C));
@@ -599,12 +600,11 @@ __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, 
     // agreement with the reference's metric (CutCmp::eb), in f32 with a 1e-4 allowance
     const float iVs = (float)(Ve * r), iVe = (float)(Vs * r);
     const float E = __builtin_fmaf(iVs, __builtin_fmaf(eb[2], iVs, eb[1]), iVe * __builtin_fmaf(eb[4], iVe, eb[3]));
-#ifdef GFPL_CUT_DBG_AGREE_OFF
-    const bool agree = true;   // (diagnostic build only: the agreement test disabled)
+// PROOF: the margins also need the proven agreement bound (cut_proof = 1); measured mode
+    // (cut_proof = 0) rests on the measured agreement
+    bool agree = true;
+    if (PROOF) agree = E * 1.0001f <= eb[0] && eb[5] * (iVs + iVe) <= 0.25f;
     (void)E;
-#else
-    const bool agree = E * 1.0001f <= eb[0] && eb[5] * (iVs + iVe) <= 0.25f;
-#endif
     bound_ok = healthy && agree &&
                __builtin_fma((40.0 * u) * P1, den, ((16.0 * u) * P2) * D) <= tq * Dd;
     return healthy ? d : __longlong_as_double(0x7ff8000000000000ll);
@@ -612,11 +612,12 @@ __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, 
 // Bs, Be, VsA, VeA are Horner sums of non-negative terms in |t|, increasing in |t|: their values at
 // T = max(|rlo|, |rhi|) bound them for every valid neighbour (|t0|, |t1| <= T), so the line's P1,
 // VsA, VeA (cmp.bnd, formed when it opens) replace the four per-neighbour evaluations
+template <bool PROOF>
 __device__ __forceinline__ double cut_dval(const CutReg& c, double t0, double t1, double tq, int& bound_ok) {
     const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
     const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
                                    h2(c.cc[0], c.cc[3], c.cc[6], t0));
-    return cut_dcore_p1(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tq, bound_ok);
+    return cut_dcore_p1<PROOF>(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tq, bound_ok);
 }
 
 // The reference's evaluation of one step (X): neighbour j's metric logdet(info_j + S)
@@ -866,6 +867,7 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
     eb[5] = ceil_f32(fmax(evs, eve));
 }
 
+template <bool PROOF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
@@ -944,6 +946,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             for (int i = 0; i < 6; ++i) wg[6 * j + i] = w[i];
             // (S^-1)_jj = |L^-1 e_j|^2 for the agreement bound
             double x[6], sg = 0.0;
+            if (PROOF) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 double uu = i == j ? 1.0 : 0.0;
@@ -953,6 +956,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 sg = __builtin_fma(x[i], x[i], sg);
             }
             tmp[g][57 + j] = sg;
+            }
         }
         wave_lds_sync();
 #pragma unroll
@@ -1008,13 +1012,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
             cl[36] = VsA;
             cl[37] = VeA;
-        } else if (j < 6) {
+        } else if (PROOF && j < 6) {
             cut_bound_row(j, T, fst[g], sumA[g], tmp[g], errS[g], wg);
         }
         wave_lds_sync();
-        if (j == 7) cut_bound_line(T, tau, cl, fst[g], wg, cmpl[g].eb);
+        if (PROOF && j == 7) cut_bound_line(T, tau, cl, fst[g], wg, cmpl[g].eb);
         wave_lds_sync();
-        {   // the line's bound, kept in its record (slots CUT_NX.., diagnostics) and counted if unusable
+        if (PROOF) {   // the line's bound, kept in its record (slots CUT_NX.., diagnostics) and counted if unusable
             const float* e6 = cmpl[g].eb;
             bool usable = e6[0] > 0.0f;
 #pragma unroll
@@ -1024,7 +1028,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         // the centre of the first step: d at (0, 0)
         const double vs0 = cl[10], ve0 = cl[15];
-        dc = cut_dcore_p1(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
+        dc = cut_dcore_p1<PROOF>(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
@@ -1065,7 +1069,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (t1 < rlo || t1 > rhi) valid = 0;
         int bok;
         double dj;
-        dj = cut_dval(cr, t0, t1, tq, bok);
+#ifdef GFPL_CUT_LDS_OPERANDS
+        cut_reg_load(cmpl[g], cr);   // (A/B build: the operands re-read from LDS every step)
+#endif
+        dj = cut_dval<PROOF>(cr, t0, t1, tq, bok);
         double top;
         int best = group_first_max(dj, valid, j, dc, top);
         // every comparison the decision rests on must clear the margin, every d its
@@ -1154,7 +1161,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 // record bounds plus the Horner evaluation's; reference-order endpoints: none
                 constexpr double u = 0x1p-53;
                 const float* ef = reinterpret_cast<const float*>(&fst[g][PD_ERR]);
-                if (fst[g][PD_OK] != 0.0) {
+                if (!PROOF) {
+                } else if (fst[g][PD_OK] != 0.0) {
                     if (j < 6) {
                         const double a0 = fabs(r0), a1 = fabs(r1);
                         const double hs = fabs(fst[g][PD_PS + j]) + a0 * (fabs(fst[g][PD_PS + 6 + j]) + a0 * fabs(fst[g][PD_PS + 12 + j]));
@@ -1203,7 +1211,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                         const double mid = sumA[g][e] + info[kk];
                         const double nw = mid - nxl[x >> 4][16 * g + (x & 15)];
                         sumA[g][e] = nw;
-                        errS[g][e] = ceil_f32((double)errS[g][e] + 1.02 * cut_info_err(xs, tmp[g], e, mid, nw));
+                        if (PROOF) errS[g][e] = ceil_f32((double)errS[g][e] + 1.02 * cut_info_err(xs, tmp[g], e, mid, nw));
                     }
                 }
             }
@@ -1278,9 +1286,13 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
 
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
     hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
-    hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+    // proven mode: the per-line operand error bounds the agreement bound starts from
+    if (p.cfg.cut_proof) hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[0], s);
-    hipLaunchKernelGGL(k_cut_search, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+    if (p.cfg.cut_proof)
+        hipLaunchKernelGGL(k_cut_search<true>, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_cut_search<false>, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[1], s);
     hipLaunchKernelGGL(k_cut_finish, dim3(p.B), dim3(64), 0, s, p);
     return hipGetLastError();

@@ -69,7 +69,7 @@ class Config(C.Structure):
                 ("lsd_scale", C.c_double), ("cut_step", C.c_double),
                 ("cut_rng", C.c_double * 2), ("proj_gate_px", C.c_double),
                 ("min_entropy_ratio", C.c_double), ("max_kf_num_frames", C.c_int),
-                ("cut_certify", C.c_double)]
+                ("cut_certify", C.c_double), ("cut_proof", C.c_int)]
 
 
 KEYPOINT_DT = np.dtype([("x", "<f4"), ("y", "<f4"), ("octave", "<i4")])

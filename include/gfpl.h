@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GFPL_ABI_VERSION 4
+#define GFPL_ABI_VERSION 5
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
@@ -117,6 +117,11 @@ typedef struct gfpl_config {
     double cut_certify;          /* (new) 1e-9: relative margin of the certified line-cut
                                     search; 0 = every neighbour evaluated with
                                     the reference's LLT; nonzero values below 1e-10 are rejected */
+    int    cut_proof;            /* (new) 0: a margined decision also rests on the measured
+                                    agreement of the comparison operands with the reference's
+                                    (DESIGN.md §3); 1: only on the proven per-step agreement
+                                    bound — a step it does not cover takes the reference's
+                                    evaluation.  Default 0. */
 } gfpl_config;
 
 /* cv::KeyPoint subset used by the path */
