@@ -561,10 +561,7 @@ struct CutCmp {
     // EV (1/v's + 1/v'e) <= 1/4.  Floats: R0 rounded down, the others up.
     float eb[6];             // R0, A1, A2, B1, B2, EV
 };
-// The step's operands (CutCmp without bs / be), held in registers from one reload to the next:
-// they are reloaded after a line transition or an exact round and dead inside those blocks, so
-// the per-step loop reads no LDS (before: 18 ds_read2_b64 per step) and the transition / exact
-// code keeps its register budget.
+// The step's operands (CutCmp without bs / be), read from LDS each step.
 struct CutReg {
     double ns[5], ne[5], vs[5], ve[5], cc[9], bnd[3];
     float eb[6];
@@ -1056,8 +1053,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (nls > 1) pf_issue(1);
     }
     __syncthreads();
-    CutReg cr;
-    cut_reg_load(cmpl[g], cr);
     int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
@@ -1069,9 +1064,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (t1 < rlo || t1 > rhi) valid = 0;
         int bok;
         double dj;
-#ifdef GFPL_CUT_LDS_OPERANDS
-        cut_reg_load(cmpl[g], cr);   // (A/B build: the operands re-read from LDS every step)
-#endif
+        CutReg cr;
+        cut_reg_load(cmpl[g], cr);   // the line's operands from LDS, every step (a register-resident
+                                     // copy reloaded only after transitions / exact rounds measured
+                                     // 7.00 vs 6.70 ms: its spills around those blocks cost more)
         dj = cut_dval<PROOF>(cr, t0, t1, tq, bok);
         double top;
         int best = group_first_max(dj, valid, j, dc, top);
@@ -1102,7 +1098,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const double sd = __shfl(dj, src);
             const int sb = __shfl(bok, src);
             if (exact) { dnext = sd; cnext = sb; }
-            cut_reg_load(cmpl[g], cr);   // (unchanged; reloaded so that it is dead across the call)
         }
         int finalize = 0;
         if (act) {
@@ -1221,7 +1216,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
-            cut_reg_load(cmpl[g], cr);   // the opened lines' operands (the others' unchanged)
         } else if (pend) {
             ++wait;
         }
