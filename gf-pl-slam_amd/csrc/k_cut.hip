@@ -76,7 +76,7 @@ __device__ __forceinline__ T endpointVar_t(const DevCam& cam, const double* DT_i
 // Start endpoint: (sP, eP, covS, covE, c0); end endpoint: (eP, sP, covE, covS, c1).
 // The start terms depend on c0 only and the end terms on c1 only, which the
 // search exploits.
-template <typename T>
+template <typename T, bool VAR = true>
 __device__ __forceinline__ void cut_endpoint_t(const DevCam& cam, double homog, const double* DT_inv, const T* Jl,
                                                const T* P0, const T* P1, const T* C0, const T* C1, T c, T* out7,
                                                double zlo) {
@@ -87,7 +87,7 @@ __device__ __forceinline__ void cut_endpoint_t(const DevCam& cam, double homog, 
     T cov[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
-    out7[0] = endpointVar_t<T>(cam, DT_inv, Jl, Pt, cov, zlo);
+    if (VAR) out7[0] = endpointVar_t<T>(cam, DT_inv, Jl, Pt, cov, zlo);
     T cur[3];
     se3_apply_t<T, double>(DT_inv, Pt, cur);
     rb_floor(cur[2], zlo);
@@ -330,10 +330,13 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
 // by running error analysis (RB) of the very expression trees the kernels evaluate, for every
 // ratio of the range c in [0, C], C = max(rng[1], 0) (rng inside [0, 1]; otherwise the line
 // gets +inf and is searched with exact steps):
-//  ours  — cut_poly_coef_t: |P_k(computed) - P_k*| per coefficient, summed over t^k, and v';
-//  ref   — cut_endpoint_t: the reference's endpoint Jacobian J and variance v as
-//          getPoseInfoOnLine computes them, |J^ - J*|, |v^ - v*|, moved to P units by the
-//          exact fgz2*(t) = fx / gz*(t)^2 >= fx / zmax^2 (J = fgz2 P, v = fgz2^2 v').
+//  ours  — cut_poly_coef_t: |P_k(computed) - P_k*| per coefficient, summed over t^k;
+//  ref   — cut_endpoint_t: the reference's endpoint Jacobian J as getPoseInfoOnLine computes
+//          it, |J^ - J*|, moved to P units by the exact fgz2*(t) = fx / gz*(t)^2 >= fx / zmax^2
+//          (J = fgz2 P).  No variance bound: the proven search takes the reference's own
+//          variances (its v'-table, k_cut_search<true>), where a bound over the range would be
+//          ~1e-9 relative — the reference's v = l^T Jp (R C R^T) Jp^T l cancels the depth
+//          variance along the viewing ray (~1e7 x the result in the synthetic workload).
 // The depth gz* of the blended point lies between the transformed endpoints' (c in [0, 1]),
 // which bounds the divisors from below (zlo) and fgz2* from below (zmax).
 __device__ __forceinline__ float ceil_f32(double x) {
@@ -396,12 +399,15 @@ __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             RB o7[7];
-            cut_endpoint_t<RB>(p.cam, p.cfg.homog_th, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS,
+            cut_endpoint_t<RB, false>(p.cam, p.cfg.homog_th, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS,
                                side ? cS : cE, RB(C, 0.0, 0.0), o7, zlo);
             // 1% slop: the bound arithmetic's own rounding
 #pragma unroll
             for (int i = 0; i < 6; ++i) eb[7 * side + i] = ceil_f32(1.01 * (eo[side][i] + o7[1 + i].e * s1));
-            eb[7 * side + 6] = ceil_f32(1.01 * (eo[side][6] + o7[0].e * s2));
+            // v': the proven search evaluates with the reference's own endpoint variances (its
+            // v'-table), whose only difference from the exact scaled value is the scaling's rounding
+            (void)s2;
+            eb[7 * side + 6] = 0.0f;
         }
     }
     float* out = reinterpret_cast<float*>(rec + PD_ERR);
@@ -609,9 +615,13 @@ __device__ __forceinline__ double cut_dcore_p1(double Ns, double Vs, double Ne, 
 // Bs, Be, VsA, VeA are Horner sums of non-negative terms in |t|, increasing in |t|: their values at
 // T = max(|rlo|, |rhi|) bound them for every valid neighbour (|t0|, |t1| <= T), so the line's P1,
 // VsA, VeA (cmp.bnd, formed when it opens) replace the four per-neighbour evaluations
+// (PROOF: v's, v'e are the reference's own endpoint variances at t0, t1, scaled — vs_t, ve_t —
+// instead of the quartics)
 template <bool PROOF>
-__device__ __forceinline__ double cut_dval(const CutReg& c, double t0, double t1, double tq, int& bound_ok) {
-    const double Ns = h4(c.ns, t0), Vs = h4(c.vs, t0), Ne = h4(c.ne, t1), Ve = h4(c.ve, t1);
+__device__ __forceinline__ double cut_dval(const CutReg& c, double t0, double t1, double tq, int& bound_ok,
+                                           double vs_t = 0.0, double ve_t = 0.0) {
+    const double Ns = h4(c.ns, t0), Ne = h4(c.ne, t1);
+    const double Vs = PROOF ? vs_t : h4(c.vs, t0), Ve = PROOF ? ve_t : h4(c.ve, t1);
     const double C = __builtin_fma(t1, __builtin_fma(t1, h2(c.cc[2], c.cc[5], c.cc[8], t0), h2(c.cc[1], c.cc[4], c.cc[7], t0)),
                                    h2(c.cc[0], c.cc[3], c.cc[6], t0));
     return cut_dcore_p1<PROOF>(Ns, Vs, Ne, Ve, C, c.bnd[0], c.bnd[1], c.bnd[2], c.eb, tq, bound_ok);

@@ -1378,6 +1378,7 @@ struct gfplo_handler {
                 }
                 last_step = this_step;
                 if (hit) {
+                    if (cand[0] < L.cut[0] || cand[1] < L.cut[1]) g_cut_stats[7]++;   // a ratio moved back
                     L.cut[0] = cand[0]; L.cut[1] = cand[1];
                     std::memcpy(L.invCov, cand_info, sizeof cand_info);
                     metric_back = metric_init;
@@ -1885,7 +1886,8 @@ int gfplo_inverse_se3(const double* T, double* out) { inverse_se3(T, out); retur
 
 /* line-cut work counters since the last call (analysis of the search shape):
  * lines, steps, valid evaluations, bit-distinct evaluations per line,
- * lines that never moved, setup logdets not implied by the previous line */
+ * lines that never moved, setup logdets not implied by the previous line, (7) moves that
+ * decrease a ratio */
 extern "C" void gfplo_cut_stats(int64_t* out8) {
     for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
 }

@@ -28,7 +28,7 @@ fi
 pmc() {   # name counters...
   local name=$1; shift
   timeout -k 10 500 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/pmc/$name -o $name -f csv -- \
-      python3 bench.py --no-cpu --parity-seqs 0 --no-detect --no-host-fed $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
+      python3 bench.py --no-cpu --parity-seqs 0 --no-detect --no-host-fed --no-b1 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
     || { echo "pmc $name failed"; tail -5 $OUT/pmc/$name.log; return 1; }
 }
 pmc fetch FETCH_SIZE && \
@@ -40,7 +40,7 @@ python3 tools/pmc_summary.py $OUT/pmc $B $OUT/pmc_latest.json $WORKLOAD $STEPS $
   && cp $OUT/pmc_latest.json profiles/pmc_latest.json || exit 1
 timeout -k 10 900 python3 bench.py $BENCH_ARGS > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py --no-cpu --parity-seqs 0 $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 \
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof -f csv -- python3 bench.py --no-cpu --parity-seqs 0 --no-b1 $BENCH_ARGS > $OUT/bench_rocprof.log 2>&1 \
   || { echo "rocprof failed"; tail -5 $OUT/bench_rocprof.log; exit 1; }
 tail -1 $OUT/bench_rocprof.log
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/bench_kernel_stats.csv \;
