@@ -404,10 +404,21 @@ __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
             // 1% slop: the bound arithmetic's own rounding
 #pragma unroll
             for (int i = 0; i < 6; ++i) eb[7 * side + i] = ceil_f32(1.01 * (eo[side][i] + o7[1 + i].e * s1));
-            // v': the proven search evaluates with the reference's own endpoint variances (its
-            // v'-table), whose only difference from the exact scaled value is the scaling's rounding
+            // v': the proven search evaluates with the reference's own endpoint variances scaled by
+            // fgz2 = fx / gz^2 of the blended point (its v'-table): slot 6 is gz's relative error
+            // bound over the range (the blend and DT_inv's rounding), which the scaling carries x 4
             (void)s2;
-            eb[7 * side + 6] = 0.0f;
+            {
+                const RB c(C, 0.0, 0.0);
+                const RB* Q0 = side ? eP : sP;
+                const RB* Q1 = side ? sP : eP;
+                RB Pt[3], cur[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) Pt[k] = (RB(1.0) - c) * Q0[k] + c * Q1[k];
+                se3_apply_t<RB, double>(Dl, Pt, cur);
+                rb_floor(cur[2], zlo);
+                eb[7 * side + 6] = cur[2].lo > 0.0 ? ceil_f32(1.01 * cur[2].e / cur[2].lo) : __builtin_inff();
+            }
         }
     }
     float* out = reinterpret_cast<float*>(rec + PD_ERR);
@@ -652,6 +663,32 @@ __device__ __attribute__((noinline)) double cut_exact_step(const double* sj, con
     return vj;
 }
 
+// Proven mode: v'_ref(c) = v / fgz2^2 with v the reference's endpoint variance at ratio c (the
+// expression tree of cut_endpoint_t<double>, hence its bits) and fgz2 = fx / max(homog, gz^2) of
+// the blended point (poseJac's); P(t) of the comparison polynomials is J / fgz2, so the pair
+// (P, v'_ref) carries the reference's info J J^T / v up to the scaling's rounding
+#define CUT_KS 22   // ratio keys per side: the bit patterns the search's ratios take (k_cut_search<true>)
+__device__ __forceinline__ double ref_vprime(const DevCam& cam, double homog, const double* Dl, const DevLines& L,
+                                             size_t q, int side, double c) {
+    const double* P0 = side ? L.eP + 3 * q : L.sP + 3 * q;
+    const double* P1 = side ? L.sP + 3 * q : L.eP + 3 * q;
+    const double* C0 = side ? L.covE + 9 * q : L.covS + 9 * q;
+    const double* C1 = side ? L.covS + 9 * q : L.covE + 9 * q;
+    const double Jl[2] = {L.le_obs[3 * q], L.le_obs[3 * q + 1]};
+    double Pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Pt[k] = (1.0 - c) * P0[k] + c * P1[k];
+    const double a = (1.0 - c) * (1.0 - c), qq = c * c;
+    double cov[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + qq * C1[i];
+    const double v = endpointVar_t<double>(cam, Dl, Jl, Pt, cov, 0.0);
+    double cur[3];
+    se3_apply(Dl, Pt, cur);
+    const double f = cam.fx / ref_max(homog, cur[2] * cur[2]);
+    return v / (f * f);
+}
+
 // Group-of-8 exchange on the DPP crossbar (no LDS): xor 1, xor 2 (quad_perm) and
 // the half-row mirror (lane i <-> 7 - i) pair every lane of a group in 3 steps.
 template <int CTRL>
@@ -793,34 +830,13 @@ constexpr unsigned long long tri_pack(int want_row) {
     return v;
 }
 
-// Bound on entry e of |S (ours) - S (the reference's)| added by one finished line:
-// |P P^T / v' - P* P*^T / v'*| for both paths against the exact one, with |P - P*| <= e,
-// |v' - v'*| <= ev <= v'/4 (xs: v's, P_s[6], v'e, P_e[6] at the final ratios; te: e_s[6] ev_s
-// e_e[6] ev_e), + both assemblies' rounding, + the two sums' roundings (mid, nw: ours).
-__device__ __forceinline__ double cut_info_err(const double* xs, const double* te, int e, double mid, double nw) {
-    constexpr double u = 0x1p-53;
-    constexpr unsigned long long TR = tri_pack(1), TC = tri_pack(0);
-    const int ra = (int)((TR >> (3 * e)) & 7), cb = (int)((TC >> (3 * e)) & 7);
-    const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
-    const double evs = te[6], eve = te[13];
-    const bool vok = xs[0] > 0.0 && xs[7] > 0.0 && evs <= 0.25 * xs[0] && eve <= 0.25 * xs[7];
-    const double esa = te[ra], esb = te[cb], eea = te[7 + ra], eeb = te[7 + cb];
-    const double psa = fabs(xs[1 + ra]) + esa, psb = fabs(xs[1 + cb]) + esb;
-    const double pea = fabs(xs[8 + ra]) + eea, peb = fabs(xs[8 + cb]) + eeb;
-    const double ps2 = psa * psb * is, pe2 = pea * peb * ie;
-    const double d = (1.34 * (esa * psb + psa * esb)) * is + (1.78 * evs * is) * ps2 +
-                     (1.34 * (eea * peb + pea * eeb)) * ie + (1.78 * eve * ie) * pe2 + (14.0 * u) * (ps2 + pe2) +
-                     (2.02 * u) * (fabs(mid) + fabs(nw));
-    return vok ? d : __builtin_inf();
-}
-
 // The line's agreement bound, out of line (once per line).  Row i = j < 6, with
-// s_i = (S^-1)_ii (tg[57 + i]; x 1.002: the reference's S is within errS of ours, the solves'
+// s_i = (S^-1)_ii (tg[57 + i]; x 1.002: the solves'
 // rounding), S_ii, and the line's operand error bounds e (P units) / ev (v'), into wg[6 q + i]:
 //   q = 0 S_ii s_i, 1 sqrt(S_ii s_i), 2 s_i (|P_s,i|(T) + e_s,i)^2, 3 (end side), 4 e_s,i sqrt(s_i),
-//   5 e_e,i sqrt(s_i), 6 |log S_ii|, 7 sqrt(s_i) sum_k errS_ik sqrt(s_k)
+//   5 e_e,i sqrt(s_i), 6 |log S_ii|, 7 0 (S is the reference's own in proven mode)
 __device__ __attribute__((noinline)) void cut_bound_row(int j, double T, const double* fs, const double* sA,
-                                                        const double* tg, const float* eS, double* wg) {
+                                                        const double* tg, double* wg) {
     const float* ef = reinterpret_cast<const float*>(fs + PD_ERR);
     const double sg = 1.002 * tg[57 + j];
     const double Sii = sA[tri(j, j)];
@@ -829,7 +845,7 @@ __device__ __attribute__((noinline)) void cut_bound_row(int j, double T, const d
     const double pe = fabs(fs[PD_PE + j]) + T * (fabs(fs[PD_PE + 6 + j]) + T * fabs(fs[PD_PE + 12 + j])) + ee;
     const double rs = sqrt(sg);
     double row = 0.0;
-    for (int k = 0; k < 6; ++k) row = __builtin_fma((double)eS[j >= k ? tri(j, k) : tri(k, j)], sqrt(1.002 * tg[57 + k]), row);
+    // (S is the reference's own, bit for bit, in proven mode: the entrywise difference term is 0)
     const double kc = Sii * sg;
     const int ex = __builtin_amdgcn_frexp_exp(Sii);
     wg[j] = kc;
@@ -856,12 +872,16 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
     const double Kc = sum[0], xi = sum[1], Qs = sum[2], Qe = sum[3], Lam = sum[6];
     const double epsS = sum[7] + (7.01 * u) * xi * xi;                                       // S difference + our factor
     const double hs = sum[4] + (6.01 * u) * Bs * xi, he = sum[5] + (6.01 * u) * Be * xi;   // + the solves' rounding
-    const double evs = ef[6], eve = ef[13];
+    // v': the reference's own variance scaled by our fgz2 (the line's v'-table), relative error
+    // <= 4 x the blended depth's (ef[6] / ef[13], k_cut_bounds) + the scaling's roundings
+    const double rvs = 4.1 * (double)ef[6] + 12.0 * u, rve = 4.1 * (double)ef[13] + 12.0 * u;
     const double ck = 110.0 * u;   // the reference's assembly, LLT and logs, per unit of tr(A~^-1)
     const double K0 = 1.002 * epsS + ck * Kc + (7.1 * u) * Lam;
     const double bs = Bs + hs, be = Be + he;
-    const double A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs), A2 = 1.03 * 4.0 * bs * bs * evs;
-    const double B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be), B2 = 1.03 * 4.0 * be * be * eve;
+    // |Delta(1/v')| (B + eta)^2 <= rv (B + eta)^2 / v' (v' within rv <= 1/4 of its value): the
+    // rank-one term's v part joins A1 / B1
+    const double A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs + 4.0 * rvs * bs * bs), A2 = 0.0;
+    const double B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be + 4.0 * rve * be * be), B2 = 0.0;
     double R0 = fmin(0.125 * tau, 1e-3) - 1.01 * K0;
     if (!(epsS <= 1e-3 && Kc <= 1e8 && R0 > 0.0)) R0 = -1.0;
     float r0f = (float)R0;
@@ -871,7 +891,7 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
     eb[2] = ceil_f32(A2);
     eb[3] = ceil_f32(B1);
     eb[4] = ceil_f32(B2);
-    eb[5] = ceil_f32(fmax(evs, eve));
+    eb[5] = (rvs <= 0.25 && rve <= 0.25) ? 0.0f : __builtin_inff();   // the per-step |ev| <= v'/4 test
 }
 
 template <bool PROOF>
@@ -891,8 +911,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     //   transition: the finished line's error bounds (+ evaluation) [0..14)
     __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];
     __shared__ CutCmp cmpl[CUT_G];              // comparison polynomials of the current line
-    // entrywise bound on |S (approximate, sumA) - S (the reference's)|, lower triangle
-    __shared__ float errS[CUT_G][21];
+    // proven mode: the line's v'_ref at every ratio key (side * CUT_KS + slot), the keys (the bit
+    // patterns 0, s, 2s, ... as r + s accumulates them, and k s - s where it differs from
+    // (k - 1) s) and their +s / -s links (-1: no key; such a ratio is evaluated exactly)
+    __shared__ double vtab[PROOF ? CUT_G : 1][PROOF ? 2 * CUT_KS : 1];
+    __shared__ double ckey[PROOF ? CUT_KS : 1];
+    __shared__ int cnxt[PROOF ? CUT_KS : 1], cprv[PROOF ? CUT_KS : 1], ckn[1];
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -907,7 +931,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int32_t* mls = p.tr.matched_ls + (size_t)(live ? b : 0) * p.mls_cap;
     const double* rec_l = p.scr.cut_rec + (size_t)(live ? b : 0) * p.mls_cap * CUT_REC;
     const double* Dl = p.scr.cut_dtinv + 16 * (size_t)(live ? b : 0);   // DT_inv (exact steps only)
-    for (int e = j; e < 21; e += 8) errS[g][e] = 0.0f;   // line 0: S is the reference's
     const double st = p.cfg.cut_step;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     double* const xs = &tmp[g][CUT_EP];
@@ -916,6 +939,32 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // neighbour j of this lane
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
+    if (PROOF) {   // the ratio keys and their links (lane 0, once)
+        if (lane == 0) {
+            auto bits = [](double x) { return __double_as_longlong(x); };
+            int n = 0;
+            for (double t = 0.0; n < CUT_KS && t <= rhi; t = t + st) ckey[n++] = t;
+            const int ns = n;
+            for (int i = 1; i < ns && n < CUT_KS; ++i) {
+                const double e = ckey[i] - st;
+                bool have = false;
+                for (int k2 = 0; k2 < n; ++k2) have = have || bits(ckey[k2]) == bits(e);
+                if (!have && e >= rlo) ckey[n++] = e;
+            }
+            for (int i = 0; i < n; ++i) {
+                const double up = ckey[i] + st, dn = ckey[i] - st;
+                int a = -1, c = -1;
+                for (int k2 = 0; k2 < n; ++k2) {
+                    if (bits(ckey[k2]) == bits(up)) a = k2;
+                    if (bits(ckey[k2]) == bits(dn)) c = k2;
+                }
+                cnxt[i] = a;
+                cprv[i] = c;
+            }
+            ckn[0] = n;
+        }
+        __syncthreads();
+    }
     // group state (identical in the 8 lanes of a group)
     int m = 0;
     int m_sync = 0;      // sumE holds the exact invCov_sum before line m_sync
@@ -927,11 +976,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     double dc = 0.0;     // d of the centre
     int c_ok = 0;        // its error bound is within tau / 4
     int n_unb = 0;       // lines opened without a usable agreement bound
+    // proven mode: the key slots of r0 / r1 and of their +s / -s neighbours (-1: none)
+    int i0 = 0, i1 = 0, n0s = -1, p0s = -1, n1s = -1, p1s = -1;
+    size_t q_cur = 0, q_nx = 0;   // the current / next line (global index)
     // A line opens (its data in fst, S in registers): every lane factors S (identical
     // values), lane k < 6 solves W_k = L^-1 P_k (side k / 3, power k % 3), lane j forms
     // Gram entries j, j + 8, j + 16, and every lane reads the 21 back into its
     // comparison polynomials.  Margins need the factor healthy and PD_OK.
     auto open_line = [&]() {
+        if (PROOF) {   // the line's v'_ref at every key, both sides (ref_vprime), and r = (0, 0)'s slots
+            const int nk = ckn[0];
+            for (int idx = j; idx < 2 * nk; idx += 8) {
+                const int side = idx >= nk ? 1 : 0, slot = idx - side * nk;
+                vtab[g][side * CUT_KS + slot] = ref_vprime(cam, homog, Dl, L, q_cur, side, ckey[slot]);
+            }
+            i0 = 0;
+            i1 = 0;
+            n0s = n1s = cnxt[0];
+            p0s = p1s = cprv[0];
+        }
         double o[28];
         {
             double S[21];
@@ -1005,10 +1068,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         wave_lds_sync();
         // the line's bound terms at T (lane 7; see cut_dval), and lanes 0-5 the per-row terms of
         // the agreement bound, row i = j: with s_i = (S^-1)_ii (x 1.002: the
-        // reference's S is within errS of ours, the solves' rounding), S_ii, and the line's
+        // solves' rounding), S_ii, and the line's
         // operand error bounds e (P units) / ev (v'):
         //   [0] S_ii s_i  [1] sqrt(S_ii s_i)  [2] s_i (|P_s,i|(T) + e_s,i)^2  [3] (end side)
-        //   [4] e_s,i sqrt(s_i)  [5] e_e,i sqrt(s_i)  [6] |log S_ii|  [7] sum_k errS_ik sqrt(s_i s_k)
+        //   [4] e_s,i sqrt(s_i)  [5] e_e,i sqrt(s_i)  [6] |log S_ii|  [7] 0
         // the line's bound terms at T (lane 7; see cut_dval), and the line's agreement bound
         // (CutCmp::eb): per-row terms by lanes 0-5, combined by lane 7
         const double T = fmax(fabs(rlo), fabs(rhi));
@@ -1020,7 +1083,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             cl[36] = VsA;
             cl[37] = VeA;
         } else if (PROOF && j < 6) {
-            cut_bound_row(j, T, fst[g], sumA[g], tmp[g], errS[g], wg);
+            cut_bound_row(j, T, fst[g], sumA[g], tmp[g], wg);
         }
         wave_lds_sync();
         if (PROOF && j == 7) cut_bound_line(T, tau, cl, fst[g], wg, cmpl[g].eb);
@@ -1034,13 +1097,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (j < 6 && live) reinterpret_cast<float*>(const_cast<double*>(rec_l) + (size_t)m * CUT_REC + CUT_NX)[j] = e6[j];
         }
         // the centre of the first step: d at (0, 0)
-        const double vs0 = cl[10], ve0 = cl[15];
+        const double vs0 = PROOF ? vtab[g][0] : cl[10], ve0 = PROOF ? vtab[g][CUT_KS] : cl[15];
         dc = cut_dcore_p1<PROOF>(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
-    size_t q_cur = 0, q_nx = 0;
     auto pf_issue = [&](int mm) {
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
@@ -1078,7 +1140,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         cut_reg_load(cmpl[g], cr);   // the line's operands from LDS, every step (a register-resident
                                      // copy reloaded only after transitions / exact rounds measured
                                      // 7.00 vs 6.70 ms: its spills around those blocks cost more)
-        dj = cut_dval<PROOF>(cr, t0, t1, tq, bok);
+        double vst = 0.0, vet = 0.0;
+        if (PROOF) {   // the reference's v' at t0 / t1 from the line's key table (no key: NaN, exact)
+            const int s0 = nb0 > 0.0 ? n0s : (nb0 < 0.0 ? p0s : i0);
+            const int s1 = nb1 > 0.0 ? n1s : (nb1 < 0.0 ? p1s : i1);
+            vst = s0 >= 0 ? vtab[g][s0] : __longlong_as_double(0x7ff8000000000000ll);
+            vet = s1 >= 0 ? vtab[g][CUT_KS + s1] : __longlong_as_double(0x7ff8000000000000ll);
+        }
+        dj = cut_dval<PROOF>(cr, t0, t1, tq, bok, vst, vet);
         double top;
         int best = group_first_max(dj, valid, j, dc, top);
         // every comparison the decision rests on must clear the margin, every d its
@@ -1113,6 +1182,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (act) {
             first = 0;
             if (best >= 0) {
+                if (PROOF) {   // the new ratios' key slots (r + s, r - s, r: the table's links)
+                    const double a0 = nb_step(best, 0, st), a1 = nb_step(best, 1, st);
+                    i0 = i0 < 0 ? -1 : (a0 > 0.0 ? n0s : (a0 < 0.0 ? p0s : i0));
+                    i1 = i1 < 0 ? -1 : (a1 > 0.0 ? n1s : (a1 < 0.0 ? p1s : i1));
+                    n0s = i0 >= 0 ? cnxt[i0] : -1;
+                    p0s = i0 >= 0 ? cprv[i0] : -1;
+                    n1s = i1 >= 0 ? cnxt[i1] : -1;
+                    p1s = i1 >= 0 ? cprv[i1] : -1;
+                }
                 r0 = r0 + nb_step(best, 0, st);
                 r1 = r1 + nb_step(best, 1, st);
                 dc = dnext;
@@ -1146,7 +1224,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 // with PD_OK = 0 (the segment leaves the polynomial form's domain, rare)
                 // lanes 0 / 1 write the reference-order endpoints (v, J) instead, J Js^T / v
                 // being the same matrix as P P^T / v'
-                if (fst[g][PD_OK] != 0.0) {
+                if (!PROOF && fst[g][PD_OK] != 0.0) {   // (proven mode: the reference's endpoints, below)
                     if (j < 6) {
                         xs[1 + j] = h2(fst[g][PD_PS + j], fst[g][PD_PS + 6 + j], fst[g][PD_PS + 12 + j], r0);
                         xs[8 + j] = h2(fst[g][PD_PE + j], fst[g][PD_PE + 6 + j], fst[g][PD_PE + 12 + j], r1);
@@ -1162,36 +1240,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
                     for (int i = 0; i < 7; ++i) xs[7 * j + i] = o7[i];
                 }
-                // the error bounds of these operands (tmp[0..14): e_s[6] ev_s e_e[6] ev_e): the line's
-                // record bounds plus the Horner evaluation's; reference-order endpoints: none
-                constexpr double u = 0x1p-53;
-                const float* ef = reinterpret_cast<const float*>(&fst[g][PD_ERR]);
-                if (!PROOF) {
-                } else if (fst[g][PD_OK] != 0.0) {
-                    if (j < 6) {
-                        const double a0 = fabs(r0), a1 = fabs(r1);
-                        const double hs = fabs(fst[g][PD_PS + j]) + a0 * (fabs(fst[g][PD_PS + 6 + j]) + a0 * fabs(fst[g][PD_PS + 12 + j]));
-                        const double he = fabs(fst[g][PD_PE + j]) + a1 * (fabs(fst[g][PD_PE + 6 + j]) + a1 * fabs(fst[g][PD_PE + 12 + j]));
-                        tmp[g][j] = (double)ef[j] + (2.02 * u) * hs;
-                        tmp[g][7 + j] = (double)ef[7 + j] + (2.02 * u) * he;
-                    } else {
-                        const int o = j == 6 ? PD_VS : PD_VE, w = j == 6 ? 6 : 13;
-                        tmp[g][w] = (double)ef[w] + (4.04 * u) * h4abs(&fst[g][o], fabs(j == 6 ? r0 : r1));
-                    }
-                } else {
-                    tmp[g][j] = 0.0;
-                    if (j < 6) tmp[g][8 + j] = 0.0;
-                }
             }
             wave_lds_sync();   // the finished line's data is read before it is replaced
             if (pend) {
-                // lane j: entries j, j + 8, j + 16 of info = Ps Ps^T / v's + Pe Pe^T / v'e
+                // lane j: entries j, j + 8, j + 16 of info = Ps Ps^T / v's + Pe Pe^T / v'e; proven
+                // mode: the reference's own assembly of its endpoints (cut_assemble's expressions,
+                // entry by entry), so sumA / sumE stay the reference's invCov_sum bit for bit
                 const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
+                const double invdet = 1.0 / (xs[0] * xs[7] - 0.0 * 0.0);
+                const double i00 = xs[7] * invdet, i10 = -0.0 * invdet, i01 = -0.0 * invdet, i11 = xs[0] * invdet;
 #pragma unroll
                 for (int kk = 0; kk < 3; ++kk) {
                     const int e = min(j + 8 * kk, 20);   // entries past 20 are computed and dropped
                     const int ra = (int)((TRI_ROW >> (3 * e)) & 7), cb = (int)((TRI_COL >> (3 * e)) & 7);
-                    info[kk] = __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
+                    if (PROOF) {
+                        const double T0 = xs[1 + ra] * i00 + xs[8 + ra] * i10, T1 = xs[1 + ra] * i01 + xs[8 + ra] * i11;
+                        info[kk] = T0 * xs[1 + cb] + T1 * xs[8 + cb];
+                    } else {
+                        info[kk] = __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
+                    }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1205,6 +1272,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (pend) {
                 q_cur = q_nx;
                 q_nx = lb + (size_t)(int)fst[g][PD_NEXT];
+                if (PROOF) m_sync = m;   // sumE was brought up to line m above
                 first = 1;
                 r0 = 0.0;
                 r1 = 0.0;
@@ -1216,7 +1284,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                         const double mid = sumA[g][e] + info[kk];
                         const double nw = mid - nxl[x >> 4][16 * g + (x & 15)];
                         sumA[g][e] = nw;
-                        if (PROOF) errS[g][e] = ceil_f32((double)errS[g][e] + 1.02 * cut_info_err(xs, tmp[g], e, mid, nw));
+                        if (PROOF) sumE[g][e] = mid;   // the exact invCov_sum, kept current (m_sync = m)
                     }
                 }
             }

@@ -94,6 +94,14 @@ def test_bench_config_parity():
     _check(rep)
 
 
+def test_proven_cut_parity():
+    """Proven-mode line cut (gfpl_config.cut_proof = 1) against the oracle: the v'-table of the
+    reference's own endpoint variances, the exact running invCov_sum and the per-step bound."""
+    rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0, cut_proof=1),
+                        n_seq=3, n_frames=5, kp_cap=2048, kl_cap=512, seed=9)
+    _check(rep)
+
+
 def test_outlier_workload_parity():
     """cfg2o: 10% of the true observations displaced 3-8 px per frame (synth outlier_frac), so
     removeOutliers (src/stereoFrameHandler.cpp:2058-2116) flags more than the MAD tail and the
@@ -407,21 +415,28 @@ def test_cut_certify_margin_validated():
 
 
 def test_line_cut_certified_matches_exact_at_scale():
-    """512 sequences x 3 frames on the GPU twice — certified search and exact steps
-    only — cut ratios, invCovPose of every matched line and the poses bit-identical."""
+    """512 sequences x 3 frames on the GPU three times — the margined search in measured mode,
+    in proven mode (gfpl_config.cut_proof: a margined decision only under the proven per-step
+    agreement bound) and exact steps only — cut ratios, invCovPose of every
+    matched line and the poses bit-identical; proven mode certifies most steps."""
     n, F, KP, KL = 512, 3, 2048, 512
     base = dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     cam = gfpl.make_camera("vga", gfpl.default_config(**base))
     H = gfpl.HostFrames(cam, gfpl.synth_params(seed=21), n, F, KP, KL)
     D = gfpl.DeviceFrames(H)
     out = []
-    for margin in (1e-9, 0.0):
-        ctx = gfpl.Context(cam, gfpl.default_config(cut_certify=margin, **base))
+    proven = {"steps": 0, "exact_steps": 0, "lines_unbounded": 0}
+    for margin, proof in ((1e-9, 0), (1e-9, 1), (0.0, 0)):
+        ctx = gfpl.Context(cam, gfpl.default_config(cut_certify=margin, cut_proof=proof, **base))
         h = gfpl.StereoFrameHandler(ctx, n, KP, KL)
         h.initialize(D.frames(0))
         res = []
         for k in range(1, F):
             h.insertStereoPair(D.frames(k))
+            if proof:
+                tc = h.last_step_track_counts()
+                for key in proven:
+                    proven[key] += tc[key]
             h.optimizePose()
             for b in range(n):
                 tr = h.read_track(b)
@@ -431,14 +446,17 @@ def test_line_cut_certified_matches_exact_at_scale():
                             h.read_frame(gfpl.CURR, b).get("Tfw")))
             h.updateFrame()
         out.append(res)
-    n_lines = 0
-    for (ma, ca, ia, ta), (mb, cb, ib, tb) in zip(*out):
-        assert np.array_equal(ma, mb)
-        assert np.array_equal(ca.view(np.uint64), cb.view(np.uint64))
-        assert np.array_equal(ia.view(np.uint64), ib.view(np.uint64))
-        assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64))
-        n_lines += len(ma)
-    assert n_lines > 100 * n
+    for other in (out[1], out[2]):
+        n_lines = 0
+        for (ma, ca, ia, ta), (mb, cb, ib, tb) in zip(out[0], other):
+            assert np.array_equal(ma, mb)
+            assert np.array_equal(ca.view(np.uint64), cb.view(np.uint64))
+            assert np.array_equal(ia.view(np.uint64), ib.view(np.uint64))
+            assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64))
+            n_lines += len(ma)
+        assert n_lines > 100 * n
+    print("proven mode:", proven)
+    assert proven["steps"] > 0 and proven["exact_steps"] < 0.05 * proven["steps"], proven
 
 
 # ---- keyframe decision: needNewKF / currFrameIsKF
