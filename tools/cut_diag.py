@@ -23,12 +23,13 @@ def main():
     ap.add_argument("--lines", type=int, default=24)
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--certify", default="", help="comma-separated cut_certify values to sweep (counts only)")
+    ap.add_argument("--proof", type=int, default=1, help="gfpl_config.cut_proof")
     a = ap.parse_args()
     import torch
     import gfpl
     import bench
     cam_name, synth_over, _ = bench.WORKLOADS[a.workload]
-    cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
+    cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0, cut_proof=a.proof)
     cam = gfpl.make_camera(cam_name, cfg)
     sp = gfpl.synth_params(**synth_over, pyr_from_l0=1)
     KP, KL = 2048, 512
@@ -36,7 +37,7 @@ def main():
         H = gfpl.HostFrames(cam, sp, a.batch, a.frames + 1, KP, KL, seq0=0, threads=8)
         for tau in [float(x) for x in a.certify.split(",")]:
             c2 = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0,
-                                     cut_certify=tau)
+                                     cut_certify=tau, cut_proof=a.proof)
             ctx = gfpl.Context(cam, c2)
             h = gfpl.StereoFrameHandler(ctx, a.batch, KP, KL)
 
