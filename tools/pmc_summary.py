@@ -97,6 +97,9 @@ def summary(d, batch, workload, steps, warmup):
         row["window"] = used
         if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
             row["hbm_bytes_per_launch"] = (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024.0
+            # FETCH_SIZE as counted for dword-aligned gathers (tools/probe/fetch_calib.hip,
+            # profiles/r04_fcal: 0.95 known bytes per counted byte, against 2.00 for 16-B streams)
+            row["hbm_bytes_per_launch_gather_cal"] = (row["FETCH_SIZE"] / 0.95 + row["WRITE_SIZE"]) * 1024.0
         if row.get("SQ_WAVES"):
             row["valu_insts_per_wave"] = row.get("SQ_INSTS_VALU", 0) / row["SQ_WAVES"]
             row["lds_insts_per_wave"] = row.get("SQ_INSTS_LDS", 0) / row["SQ_WAVES"]
@@ -138,7 +141,7 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    keys = ["dispatches", "window", "hbm_bytes_per_launch", "valu_insts_per_wave", "lds_insts_per_wave", "SQ_WAVES",
+    keys = ["dispatches", "window", "hbm_bytes_per_launch", "hbm_bytes_per_launch_gather_cal", "valu_insts_per_wave", "lds_insts_per_wave", "SQ_WAVES",
             "frac_wait_any", "frac_wait_inst", "frac_active", "cycle_closure", "occupancy_waves_per_simd",
             "SQ_LDS_BANK_CONFLICT"]
     for k, row in out["kernels"].items():
