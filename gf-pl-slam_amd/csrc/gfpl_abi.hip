@@ -140,6 +140,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.n_subpix = c.take<int32_t>(B);
     sb->scr.cut_sum = c.take<double>(B * 24);
     sb->scr.cut_dtinv = c.take<double>(B * 16);
+    sb->scr.cut_vtab = c.take<double>(B * sb->mls_cap * 2 * CUT_KS);
     sb->scr.pose_DT = c.take<double>(B * 16);
     sb->scr.pose_H = c.take<double>(B * 36);
     sb->scr.pose_err = c.take<double>(B);
@@ -186,6 +187,29 @@ KParams params(gfpl_seqbatch* sb, const gfpl_frames* in) {
     p.sp_maxD = (float)p.cam.fx;
     p.sp_mbf = (float)(p.cam.fx * p.cam.b);
     p.cut_tq = 0.25 * p.cfg.cut_certify - 4.0 * 0x1p-53;
+    {   // the proven line cut's ratio keys (same IEEE additions as the search's r + s)
+        const double s = p.cfg.cut_step, lo = p.cfg.cut_rng[0], hi = p.cfg.cut_rng[1];
+        auto same = [](double x, double y) { return std::memcmp(&x, &y, sizeof x) == 0; };
+        int n = 0;
+        for (double t = 0.0; n < CUT_KS && t <= hi && s > 0.0; t = t + s) p.cut_keys[n++] = t;
+        const int ns = n;
+        for (int i = 1; i < ns && n < CUT_KS; ++i) {
+            const double e = p.cut_keys[i] - s;
+            bool have = false;
+            for (int k = 0; k < n; ++k) have = have || same(p.cut_keys[k], e);
+            if (!have && e >= lo) p.cut_keys[n++] = e;
+        }
+        for (int i = 0; i < n; ++i) {
+            int up = -1, dn = -1;
+            for (int k = 0; k < n; ++k) {
+                if (same(p.cut_keys[k], p.cut_keys[i] + s)) up = k;
+                if (same(p.cut_keys[k], p.cut_keys[i] - s)) dn = k;
+            }
+            p.cut_knxt[i] = (int8_t)up;
+            p.cut_kprv[i] = (int8_t)dn;
+        }
+        p.cut_nkeys = n;
+    }
     return p;
 }
 

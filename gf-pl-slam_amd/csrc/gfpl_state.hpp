@@ -77,6 +77,7 @@ struct DevTrack {
                       // [16] line-cut search steps, [17] of them evaluated exactly (k_cut_search),
                       // [18] n_inliers after optimize_pose (k_pose_finish), [19] lines whose agreement bound
                       // was unusable (k_cut_search: R0 <= 0 or a term not finite; their steps are exact)
+#define CUT_KS 22     // proven line cut: ratio keys per side (KParams::cut_keys)
 #define CUT_FAST 56   // doubles of per-line comparison data (k_cut.hip, PD_*): polynomials, flags, error bounds
 #define CUT_REC 80    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (640 B)
 
@@ -89,6 +90,8 @@ struct DevScratch {
     int32_t* n_subpix; // [B] left keypoints that reached the sub-pixel SAD (M_o)
     double* cut_sum;   // [B*24] invCov_sum (lower triangle) after the r=0 pass
     double* cut_dtinv; // [B*16] DT_inv of the line cut
+    double* cut_vtab;  // [B*mls_cap*2*CUT_KS] proven line cut: the reference's scaled endpoint variance
+                       // per matched line, side and ratio key (k_cut_vtab)
     double* pose_DT;   // [B*16] GN result before the final bookkeeping
     double* pose_H;    // [B*36] last evaluated H
     double* pose_err;  // [B]
@@ -114,6 +117,12 @@ struct KParams {
     // register allocator spills under pressure)
     float sp_maxD, sp_mbf;   // k_stereo_points: (float)fx, (float)(fx * b)
     double cut_tq;           // k_cut_search: cut_certify / 4 - 4u, the budget of d's rounding bound
+    // proven line cut: the ratio keys — the bit patterns the greedy search's ratios take: 0, s, 2s, ...
+    // as r + s accumulates them (<= rng[1]) and k s - s where its bits differ from (k - 1) s — with
+    // their +s / -s links (-1: no key)
+    double cut_keys[CUT_KS];
+    int cut_nkeys;
+    int8_t cut_knxt[CUT_KS], cut_kprv[CUT_KS];
 };
 
 }  // namespace gfpl

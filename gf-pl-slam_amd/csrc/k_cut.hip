@@ -345,6 +345,51 @@ __device__ __forceinline__ float ceil_f32(double x) {
     if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
     return f;
 }
+// Proven mode: v'_ref(c) = v / fgz2^2 with v the reference's endpoint variance at ratio c (the
+// expression tree of cut_endpoint_t<double>, hence its bits) and fgz2 = fx / max(homog, gz^2) of
+// the blended point (poseJac's); P(t) of the comparison polynomials is J / fgz2, so the pair
+// (P, v'_ref) carries the reference's info J J^T / v up to the scaling's rounding
+__device__ __forceinline__ double ref_vprime(const DevCam& cam, double homog, const double* Dl, const DevLines& L,
+                                             size_t q, int side, double c) {
+    const double* P0 = side ? L.eP + 3 * q : L.sP + 3 * q;
+    const double* P1 = side ? L.sP + 3 * q : L.eP + 3 * q;
+    const double* C0 = side ? L.covE + 9 * q : L.covS + 9 * q;
+    const double* C1 = side ? L.covS + 9 * q : L.covE + 9 * q;
+    const double Jl[2] = {L.le_obs[3 * q], L.le_obs[3 * q + 1]};
+    double Pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Pt[k] = (1.0 - c) * P0[k] + c * P1[k];
+    const double a = (1.0 - c) * (1.0 - c), qq = c * c;
+    double cov[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + qq * C1[i];
+    const double v = endpointVar_t<double>(cam, Dl, Jl, Pt, cov, 0.0);
+    double cur[3];
+    se3_apply(Dl, Pt, cur);
+    const double f = cam.fx / ref_max(homog, cur[2] * cur[2]);
+    return v / (f * f);
+}
+
+// Proven line cut: per matched line, side and ratio key, the reference's endpoint variance scaled
+// by its fgz2 (ref_vprime), into cut_vtab — one thread per (line, side, key), consecutive threads
+// on one line (its inputs are one broadcast load)
+__global__ void __launch_bounds__(256) k_cut_vtab(KParams p) {
+    const int b = blockIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    const int nk = p.cut_nkeys;
+    if (nls == 0 || nk == 0) return;
+    const DevLines& L = p.prev.ls;
+    const double* Dl = p.scr.cut_dtinv + 16 * (size_t)b;
+    const int per = 2 * nk;
+    for (int idx = threadIdx.x; idx < nls * per; idx += 256) {
+        const int m = idx / per, r = idx - m * per;
+        const int side = r >= nk ? 1 : 0, slot = r - side * nk;
+        const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+        p.scr.cut_vtab[((size_t)b * p.mls_cap + m) * (2 * CUT_KS) + side * CUT_KS + slot] =
+            ref_vprime(p.cam, p.cfg.homog_th, Dl, L, q, side, p.cut_keys[slot]);
+    }
+}
+
 __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
     const int b = blockIdx.y;
     const int m = blockIdx.x * 64 + threadIdx.x;
@@ -663,31 +708,6 @@ __device__ __attribute__((noinline)) double cut_exact_step(const double* sj, con
     return vj;
 }
 
-// Proven mode: v'_ref(c) = v / fgz2^2 with v the reference's endpoint variance at ratio c (the
-// expression tree of cut_endpoint_t<double>, hence its bits) and fgz2 = fx / max(homog, gz^2) of
-// the blended point (poseJac's); P(t) of the comparison polynomials is J / fgz2, so the pair
-// (P, v'_ref) carries the reference's info J J^T / v up to the scaling's rounding
-#define CUT_KS 22   // ratio keys per side: the bit patterns the search's ratios take (k_cut_search<true>)
-__device__ __forceinline__ double ref_vprime(const DevCam& cam, double homog, const double* Dl, const DevLines& L,
-                                             size_t q, int side, double c) {
-    const double* P0 = side ? L.eP + 3 * q : L.sP + 3 * q;
-    const double* P1 = side ? L.sP + 3 * q : L.eP + 3 * q;
-    const double* C0 = side ? L.covE + 9 * q : L.covS + 9 * q;
-    const double* C1 = side ? L.covS + 9 * q : L.covE + 9 * q;
-    const double Jl[2] = {L.le_obs[3 * q], L.le_obs[3 * q + 1]};
-    double Pt[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Pt[k] = (1.0 - c) * P0[k] + c * P1[k];
-    const double a = (1.0 - c) * (1.0 - c), qq = c * c;
-    double cov[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + qq * C1[i];
-    const double v = endpointVar_t<double>(cam, Dl, Jl, Pt, cov, 0.0);
-    double cur[3];
-    se3_apply(Dl, Pt, cur);
-    const double f = cam.fx / ref_max(homog, cur[2] * cur[2]);
-    return v / (f * f);
-}
 
 // Group-of-8 exchange on the DPP crossbar (no LDS): xor 1, xor 2 (quad_perm) and
 // the half-row mirror (lane i <-> 7 - i) pair every lane of a group in 3 steps.
@@ -911,12 +931,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     //   transition: the finished line's error bounds (+ evaluation) [0..14)
     __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];
     __shared__ CutCmp cmpl[CUT_G];              // comparison polynomials of the current line
-    // proven mode: the line's v'_ref at every ratio key (side * CUT_KS + slot), the keys (the bit
-    // patterns 0, s, 2s, ... as r + s accumulates them, and k s - s where it differs from
-    // (k - 1) s) and their +s / -s links (-1: no key; such a ratio is evaluated exactly)
+    // proven mode: the line's v'_ref at every ratio key (side * CUT_KS + slot; k_cut_vtab) and the
+    // keys' +s / -s links (KParams::cut_keys; -1: no key — such a ratio is evaluated exactly)
     __shared__ double vtab[PROOF ? CUT_G : 1][PROOF ? 2 * CUT_KS : 1];
-    __shared__ double ckey[PROOF ? CUT_KS : 1];
-    __shared__ int cnxt[PROOF ? CUT_KS : 1], cprv[PROOF ? CUT_KS : 1], ckn[1];
+    __shared__ int cnxt[PROOF ? CUT_KS : 1], cprv[PROOF ? CUT_KS : 1];
     const int lane = threadIdx.x;
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
@@ -939,29 +957,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // neighbour j of this lane
     const double nb0 = nb_step(j, 0, st), nb1 = nb_step(j, 1, st);
     constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
-    if (PROOF) {   // the ratio keys and their links (lane 0, once)
-        if (lane == 0) {
-            auto bits = [](double x) { return __double_as_longlong(x); };
-            int n = 0;
-            for (double t = 0.0; n < CUT_KS && t <= rhi; t = t + st) ckey[n++] = t;
-            const int ns = n;
-            for (int i = 1; i < ns && n < CUT_KS; ++i) {
-                const double e = ckey[i] - st;
-                bool have = false;
-                for (int k2 = 0; k2 < n; ++k2) have = have || bits(ckey[k2]) == bits(e);
-                if (!have && e >= rlo) ckey[n++] = e;
-            }
-            for (int i = 0; i < n; ++i) {
-                const double up = ckey[i] + st, dn = ckey[i] - st;
-                int a = -1, c = -1;
-                for (int k2 = 0; k2 < n; ++k2) {
-                    if (bits(ckey[k2]) == bits(up)) a = k2;
-                    if (bits(ckey[k2]) == bits(dn)) c = k2;
-                }
-                cnxt[i] = a;
-                cprv[i] = c;
-            }
-            ckn[0] = n;
+    if (PROOF) {   // the ratio keys and their links (host-formed, KParams)
+        if (lane < CUT_KS) {
+            cnxt[lane] = p.cut_knxt[lane];
+            cprv[lane] = p.cut_kprv[lane];
         }
         __syncthreads();
     }
@@ -984,12 +983,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // Gram entries j, j + 8, j + 16, and every lane reads the 21 back into its
     // comparison polynomials.  Margins need the factor healthy and PD_OK.
     auto open_line = [&]() {
-        if (PROOF) {   // the line's v'_ref at every key, both sides (ref_vprime), and r = (0, 0)'s slots
-            const int nk = ckn[0];
-            for (int idx = j; idx < 2 * nk; idx += 8) {
-                const int side = idx >= nk ? 1 : 0, slot = idx - side * nk;
-                vtab[g][side * CUT_KS + slot] = ref_vprime(cam, homog, Dl, L, q_cur, side, ckey[slot]);
-            }
+        if (PROOF) {   // the line's v'_ref at every key, both sides (k_cut_vtab), and r = (0, 0)'s slots
+            const double* vt = p.scr.cut_vtab + ((size_t)(live ? b : 0) * p.mls_cap + m) * (2 * CUT_KS);
+            for (int idx = j; idx < 2 * CUT_KS; idx += 8) vtab[g][idx] = vt[idx];
             i0 = 0;
             i1 = 0;
             n0s = n1s = cnxt[0];
@@ -1359,7 +1355,10 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
     hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
     // proven mode: the per-line operand error bounds the agreement bound starts from
-    if (p.cfg.cut_proof) hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+    if (p.cfg.cut_proof) {
+        hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);
+    }
     if (marks) (void)hipEventRecord(marks[0], s);
     if (p.cfg.cut_proof)
         hipLaunchKernelGGL(k_cut_search<true>, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
