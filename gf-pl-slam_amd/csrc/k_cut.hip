@@ -923,7 +923,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double fst[CUT_G][CUT_FAST + 1]; // comparison data of the current line
     // next-line records, written by LDS-DMA: 16-B piece k of group g's record lands at
     // nxl[k][16 g + ...] (the DMA writes base + 16 * lane)
-    __shared__ __attribute__((aligned(16))) double nxl[5][128];
+    // (proven mode: no prefetch buffer — its v'-tables take the LDS, and 5 KB more would cost the
+    // eighth wave of a CU; the record is read from HBM when the line opens)
+    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? 1 : 5][128];
     // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
     //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
     //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
@@ -1100,6 +1102,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
     auto pf_issue = [&](int mm) {
+        if (PROOF) return;
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
         for (int k = 0; k < 5; ++k)
@@ -1257,11 +1260,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (PROOF) {
 #pragma unroll
-                for (int k = 0; k < CUT_FAST / 8; ++k) {
-                    const int e = j + 8 * k;
-                    fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
+                    for (int k = 0; k < CUT_FAST / 8; ++k) fst[g][j + 8 * k] = rec_l[(size_t)m * CUT_REC + j + 8 * k];
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int k = 0; k < CUT_FAST / 8; ++k) {
+                        const int e = j + 8 * k;
+                        fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
+                    }
                 }
             }
             wave_lds_sync();
@@ -1278,7 +1286,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
                     if (e < 21) {
                         const double mid = sumA[g][e] + info[kk];
-                        const double nw = mid - nxl[x >> 4][16 * g + (x & 15)];
+                        const double nw = mid - (PROOF ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
                         sumA[g][e] = nw;
                         if (PROOF) sumE[g][e] = mid;   // the exact invCov_sum, kept current (m_sync = m)
                     }
