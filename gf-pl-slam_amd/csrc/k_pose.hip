@@ -171,6 +171,8 @@ struct PoseCtx {
     const double* lin;   // [LS_K][mls_cap]
     size_t mpt_cap, mls_cap;
     const uint8_t* act;  // LDS [npt + nls] list-position inlier flags
+    uint16_t* idxp;      // LDS [mpt_cap] the active points' list positions, in list order
+    uint16_t* idxl;      // LDS [mls_cap] the active lines'
     int npt, nls;
 };
 
@@ -189,9 +191,31 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     else if (e < 27) { ia = e - 21; ib = 6; }
     else { ia = 6; ib = 6; }
     const double* buf = list == 0 ? cp : cl;
-    const int nch = (max(X.npt, X.nls) + 63) >> 6;
     const uint8_t* actp = X.act;
     const uint8_t* actl = X.act + X.npt;
+    // the active entries, compacted in list order (an inactive entry is a zero row, and adding
+    // +0.0 to a sum that started at +0.0 never changes it: skipping them leaves H bit-identical);
+    // after removeOutliers about a third of the entries are inactive
+    int np_act = 0, nl_act = 0;
+    {
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        for (int b0 = 0; b0 < X.npt; b0 += 64) {
+            const int f = b0 + lane;
+            const bool a = f < X.npt && actp[f];
+            const unsigned long long m = __ballot(a);
+            if (a) X.idxp[np_act + __popcll(m & lt)] = (uint16_t)f;
+            np_act += __popcll(m);
+        }
+        for (int b0 = 0; b0 < X.nls; b0 += 64) {
+            const int f = b0 + lane;
+            const bool a = f < X.nls && actl[f];
+            const unsigned long long m = __ballot(a);
+            if (a) X.idxl[nl_act + __popcll(m & lt)] = (uint16_t)f;
+            nl_act += __popcll(m);
+        }
+        __syncthreads();
+    }
+    const int nch = (max(np_act, nl_act) + 63) >> 6;
     for (int it = 0; it < max_iters; ++it) {
         // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
         // holding 16 doubles in registers across the chunk loop
@@ -202,7 +226,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
         double pv[PT_K], lv[LS_K];
         auto load_chunk = [&](int c) {
             const int f = (c << 6) + lane;
-            const int fp = min(f, max(X.npt - 1, 0)), fl = min(f, max(X.nls - 1, 0));
+            const int fp = f < np_act ? (int)X.idxp[f] : 0, fl = f < nl_act ? (int)X.idxl[f] : 0;
 #pragma unroll
             for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
 #pragma unroll
@@ -212,14 +236,14 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
         for (int c = 0; c < nch; ++c) {
             const int f = (c << 6) + lane;
             double o[8];
-            if (f < X.npt && actp[f]) eval_point(cam, homog, DT, pv, o);
+            if (f < np_act) eval_point(cam, homog, DT, pv, o);
             else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cp[i * CH_STRIDE + lane] = o[i];
-            if (f < X.nls && actl[f]) eval_line(cam, homog, DT, lv, o);
+            if (f < nl_act) eval_line(cam, homog, DT, lv, o);
             else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = 0.0;
@@ -366,7 +390,8 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8
+// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8 (16-B padded) |
+// idx[mpt_cap + mls_cap] u16 (the active points' / lines' list positions, gauss_newton)
 #ifndef GFPL_POSE_WAVES
 #define GFPL_POSE_WAVES 2
 #endif
@@ -382,6 +407,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     double* cl = cp + 8 * CH_STRIDE;
     double* buf = cp;   // MAD sort buffer: never live together with the GN chunk rows
     uint8_t* act = (uint8_t*)(cp + region);
+    uint16_t* idxa = (uint16_t*)(act + ((p.mpt_cap + p.mls_cap + 15) & ~15));   // compacted active positions
     const DevPose& PP = p.prev.pose;
     const DevPoints& P = p.prev.pt;
     const DevLines& L = p.prev.ls;
@@ -393,6 +419,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     double* pin = p.scr.pose_in + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
     double* lin = pin + PT_K * p.mpt_cap;
     X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
+    X.idxp = idxa; X.idxl = idxa + p.mpt_cap;
     if (lane < 16) {   // Q2: the app passes prev_frame->DT (app/plslam_mod.cpp:408)
         S.DTini[lane] = p.dt_ini ? p.dt_ini[16 * b + lane] : PP.DT[16 * b + lane];
         S.DT[lane] = S.DTini[lane];
@@ -683,7 +710,7 @@ hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
     const size_t region = (size_t)std::max(16 * CH_STRIDE, NP2);
-    const size_t lds = region * 8 + (p.mpt_cap + p.mls_cap) + 16;
+    const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 2 * (size_t)(p.mpt_cap + p.mls_cap) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
