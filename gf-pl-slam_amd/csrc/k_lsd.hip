@@ -5,8 +5,7 @@
 // images resident in HBM, the arithmetic pinned as the CPU oracle's ledger S1-S7
 // (oracle/gfpl_lsd_oracle.cpp).  Kernels, one launch each for the whole batch:
 //  k_lsd_grad      per pixel (lsd.cpp ll_angle, S1): the 2x2 gradient, NOTDEF test, fastAtan2
-//                  angle (degrees, float), cos / sin of float(angle) (S3), the image's max norm,
-//                  a compact index per defined pixel
+//                  angle (degrees, float), cos / sin of float(angle) (S3), the image's max norm
 //  k_lsd_keys      per pixel: the 64-bit sort element (norm bin << 32 | y << 16 | x), row-major
 //  k_lsd_sort      one wave per image: libstdc++ std::sort's permutation (S2).  Introsort's
 //                  Hoare partition is restated in parallel: the k-th left stopper swaps with
@@ -57,9 +56,9 @@ struct LsdDev {
     int* rpos;                     // [n][NP]
     uint32_t* reg;                 // [n][W*H] region list
     uint32_t* tmp;                 // [n][W*H] region scratch
-    uint32_t* cid;                 // [n][W*H] a defined pixel's index among the image's defined
-                                   // pixels (k_lsd_grad; any injective order): its used bit
-    int* ndef;                     // [n] defined pixels of the image
+    uint32_t* cid;                 // [n][W*H] a defined pixel's position in the sorted keys (k_lsd_sort):
+                                   // its bit in the compact used map
+    int* ndef;                     // [n] the sorted keys with a bin >= B0 (every defined pixel; k_lsd_sort)
     int cid_cap;                   // compact used-map bits (LDS): images with more defined
                                    // pixels grow with the HBM byte map
     uint8_t* used_g;               // [n][W*H] used map of the images above cid_cap
@@ -838,13 +837,11 @@ __device__ __forceinline__ void mw_sort(uint64_t* a, int n, int* Lp, int* Rp, So
 #define LSD_GRAD_ROWS 64   // rows per workgroup (16 passes of 4): one max-norm atomic per 4096 px
 __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* images) {
     __shared__ unsigned long long wmaxv[4];
-    __shared__ int wcnt[4], wbase;
     const int img = blockIdx.z;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int W = o.W, H = o.H;
     const uint8_t* I = images + (size_t)img * W * H;
     unsigned long long b = 0;   // bits of the max norm of defined pixels (norm >= 0 orders like its bits)
-    uint32_t dmask = 0;         // pass r / 4 defined
     for (int r = 0; r < LSD_GRAD_ROWS; r += 4) {
         const int y = blockIdx.y * LSD_GRAD_ROWS + r + (threadIdx.x >> 6);
         if (x >= W || y >= H) continue;
@@ -867,41 +864,18 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdDev o, const uint8_t* image
         }
         o.px[p] = make_float4(a, cs.x, cs.y, __uint_as_float(g));
         o.ang[p] = a;
-        if (a >= 0.0f) {
-            o.scs[p] = make_float2(cs.z, cs.w);
-            dmask |= 1u << (r >> 2);
-        }
+        if (a >= 0.0f) o.scs[p] = make_float2(cs.z, cs.w);
     }
     for (int off = 32; off; off >>= 1) {
         const unsigned long long t = __shfl_xor(b, off);
         b = t > b ? t : b;
     }
-    // compact indices of the defined pixels: the workgroup's count by a wave scan + one atomic
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int c = __popc(dmask);
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(c, off);
-        if (lane >= off) c += t;
-    }
-    if (lane == 63) wcnt[wv] = c;
-    if (lane == 0) wmaxv[wv] = b;
+    if ((threadIdx.x & 63) == 0) wmaxv[threadIdx.x >> 6] = b;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long m = wmaxv[0];
         for (int w = 1; w < 4; ++w) m = wmaxv[w] > m ? wmaxv[w] : m;
         if (m) atomicMax(&o.maxg[img], m);
-        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        wbase = tot ? atomicAdd(&o.ndef[img], tot) : 0;
-    }
-    __syncthreads();
-    if (dmask) {
-        int k = wbase + c - __popc(dmask);
-        for (int w = 0; w < wv; ++w) k += wcnt[w];
-        for (int r = 0; r < LSD_GRAD_ROWS; r += 4) {
-            if (!((dmask >> (r >> 2)) & 1u)) continue;
-            const int y = blockIdx.y * LSD_GRAD_ROWS + r + wv;
-            o.cid[(size_t)img * W * H + (size_t)y * W + x] = (uint32_t)k++;
-        }
     }
 }
 
@@ -1003,6 +977,28 @@ __global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_wav
     const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
     const uint32_t B0 = (uint32_t)(int)(o.rho * bin_coef);
     mw_sort(o.keys + img * o.NP, o.NP, o.lpos + img * o.NP, o.rpos + img * o.NP, S, B0);
+    // the compact indices of the used map (k_lsd_grow_lds): a pixel's position in the sorted
+    // prefix of keys >= B0 — every defined pixel is there (norm > rho gives a bin >= B0), the
+    // sort leaves that prefix first and in order, and everything after it is below B0
+    __shared__ int pfx;
+    __syncthreads();
+    const uint64_t* a = o.keys + img * o.NP;
+    if (threadIdx.x == 0) {
+        int lo = 0, hi = o.NP;   // the first position with a bin below B0
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((uint32_t)(a[mid] >> 32) >= B0) lo = mid + 1;
+            else hi = mid;
+        }
+        pfx = lo;
+        o.ndef[img] = lo;
+    }
+    __syncthreads();
+    uint32_t* cid = o.cid + img * (size_t)o.W * o.H;
+    for (int i = threadIdx.x; i < pfx; i += blockDim.x) {
+        const uint64_t e = a[i];
+        cid[(int)((e >> 16) & 0x7fff) * o.W + (int)(e & 0xffff)] = (uint32_t)i;
+    }
 }
 
 // ---------------------------------------------------------------- the regions --
