@@ -503,7 +503,7 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     return out
 
 
-def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False):
+def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False):
     """Images in HBM to poses on one device (gfpl.pipeline), measured after the
     timed tracking steps (not part of `value`): per step ORB on both images of B stereo frames,
     LBD (and LSD when lsd) on the pipeline's detection stream, one StereoFrameHandler step on
@@ -524,6 +524,8 @@ def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False):
     frames = []
     for k in range(2 + 2 * steps):
         sc = [synth_stereo_steps(b, k, W, H) for b in range(B)]
+        if progress:
+            print(f"[pipeline_rate] frame {k} of {2 + 2 * steps} generated", file=sys.stderr, flush=True)
         kl = [np.zeros((B, KL), gfpl.KEYLINE_DT) for _ in range(2)]
         n = [np.zeros(B, np.int32) for _ in range(2)]
         for b, x in enumerate(sc):

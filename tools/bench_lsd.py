@@ -27,6 +27,8 @@ def images(W, H, n):
             out.append(l if (i // 2) % 2 == 0 else r)
         else:
             out.append(gfpl.synth_image(i, i % 5, W, H))
+        if i % 1024 == 1023:
+            print(f"[bench_lsd] {i + 1} of {n} images generated", file=sys.stderr, flush=True)
     return np.stack(out)
 
 

@@ -24,7 +24,7 @@ def main():
     out = {}
     for lsd in ((a.lsd == 1,) if a.lsd < 2 else (False, True)):
         out["images_to_poses_lsd" if lsd else "images_to_poses"] = bench.pipeline_rate(cam, cfg, B=a.batch,
-                                                                                       steps=a.steps, lsd=lsd)
+                                                                                       steps=a.steps, lsd=lsd, progress=True)
     print(json.dumps(out))
 
 
