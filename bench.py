@@ -110,6 +110,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
+    ap.add_argument("--dump-records", default=None,
+                    help="save every sequence's record of the last timed step (gfpl_debug_step_records, .npy) "
+                         "and the instrumented builds' clocks (gfpl_debug_clocks, *_clk.npy)")
     ap.add_argument("--cut-certify", type=float, default=None,
                     help="gfpl_config.cut_certify (the certified line-cut margin; default: the library's)")
     ap.add_argument("--cut-proof", action="store_true",
@@ -467,17 +470,18 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
                   "parity_vs_oracle_image0": bool((d_desc.cpu().numpy().reshape(n_img, n_lines, 32)[0] == ref).all())}
     lbd.close()
     # LSD (gfpl_lsd_detect, the reference's LSDOptions, 300 keylines kept): its per-image chain
-    # (sort + region growing) is latency-bound; measured at 2048 images per call (the left and
-    # right images of images_to_poses_lsd's 1024-frame step) and at 1024
+    # (sort + region growing, one workgroup per image) is latency-bound and needs images in
+    # flight: measured at 3072 images per call (the left and right images of
+    # images_to_poses_lsd's 1536-frame step; 4096 measured 60.9k, profiles/r04_n), 2048 and 1024
     from gfpl.pipeline import synth_stereo_steps
-    n_max = 2048
+    n_max = 3072
     li = np.stack([synth_stereo_steps(i // 2, 0, W, H)[i % 2] for i in range(8)]
                   + [imgs[i % n_img] for i in range(n_max - 8)])
     d_li = torch.from_numpy(li).to(dev)
     lsd = gfpl.LSDDetector(W, H, max_images=n_max, kl_cap=320)
     d_kl = torch.zeros(n_max * 320 * gfpl.KEYLINE_DT.itemsize, dtype=torch.uint8, device=dev)
     d_n = torch.zeros(n_max, dtype=torch.int32, device=dev)
-    for n_lsd, key in ((2048, "lsd"), (1024, "lsd_1024")):
+    for n_lsd, key in ((3072, "lsd"), (2048, "lsd_2048"), (1024, "lsd_1024")):
         lsd.detect_batch(d_li, n_lsd, d_kl, d_n)
         t = []
         for _ in range(3):
@@ -785,6 +789,12 @@ def main():
         if rank == 0:   # progress (stderr): long runs under a watchdog keep writing
             print(f"[bench] step {k}/{W + K}: {1e3 * (ts1 - ts0):.2f} ms", file=sys.stderr, flush=True)
     elapsed = float(np.sum(step_s))
+    if args.dump_records and rank == 0:
+        np.save(args.dump_records, h.debug_step_records())
+        try:
+            np.save(args.dump_records.replace(".npy", "") + "_clk.npy", h.debug_clocks())
+        except AttributeError:   # a library from before gfpl_debug_clocks
+            pass
     lost = sum(h.read_track(b)["num_frame_loss"] > 0 for b in range(0, B, max(1, B // 16)))
     par = [sampler.frames, sampler.mismatch_frames] if sampler else [0, 0]
     if world > 1:
@@ -839,7 +849,7 @@ def main():
             det = detection_rates(cam, up_Bps)
             try:
                 det["images_to_poses"] = pipeline_rate(cam, cfg)
-                det["images_to_poses_lsd"] = pipeline_rate(cam, cfg, lsd=True)
+                det["images_to_poses_lsd"] = pipeline_rate(cam, cfg, B=1536, lsd=True)
             except Exception as e:   # reported, never fatal to the contract line
                 det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}
         cmean = {n: round(float(np.mean([c[n] for c in counts])), 1) for n in gfpl.StereoFrameHandler.STEP_COUNTS}

@@ -146,8 +146,10 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_err = c.take<double>(B);
     sb->scr.pose_ok = c.take<int32_t>(B);
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
+    sb->scr.pose_idx = c.take<uint32_t>(B * (size_t)std::max(sb->mpt_cap, sb->mls_cap));
     sb->scr.pose_dtini = c.take<double>(B * 16);
     sb->scr.cross_tinv = c.take<double>(B * 16);
+    sb->scr.dbg = c.take<int64_t>(B * 8);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);
@@ -1212,6 +1214,22 @@ int gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines) {
     const size_t n = (size_t)n_lines * CUT_REC;
     return hipMemcpy(out, sb->scr.cut_rec + (size_t)b * sb->mls_cap * CUT_REC, n * sizeof(double),
                      hipMemcpyDeviceToHost) == hipSuccess ? GFPL_OK : GFPL_E_HIP;
+}
+
+int gfpl_debug_step_records(gfpl_seqbatch* sb, int64_t* out) {
+    if (!sb || !out) return GFPL_E_INVALID;
+    if (hipSetDevice(sb->ctx->device) != hipSuccess) return GFPL_E_HIP;
+    if (hipStreamSynchronize(sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+    return hipMemcpy(out, sb->scr.bytes, (size_t)sb->B * STEP_REC * sizeof(int64_t), hipMemcpyDeviceToHost) == hipSuccess
+               ? GFPL_OK : GFPL_E_HIP;
+}
+
+int gfpl_debug_clocks(gfpl_seqbatch* sb, int64_t* out) {
+    if (!sb || !out) return GFPL_E_INVALID;
+    if (hipSetDevice(sb->ctx->device) != hipSuccess) return GFPL_E_HIP;
+    if (hipStreamSynchronize(sb->ctx->stream) != hipSuccess) return GFPL_E_HIP;
+    return hipMemcpy(out, sb->scr.dbg, (size_t)sb->B * 8 * sizeof(int64_t), hipMemcpyDeviceToHost) == hipSuccess
+               ? GFPL_OK : GFPL_E_HIP;
 }
 
 int gfpl_last_step_bytes(gfpl_seqbatch* sb, int64_t* bytes) {

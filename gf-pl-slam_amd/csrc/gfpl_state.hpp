@@ -97,9 +97,12 @@ struct DevScratch {
     double* pose_err;  // [B]
     int32_t* pose_ok;  // [B] 1: stage-2 result usable
     double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
+    uint32_t* pose_idx; // [B*max(mpt_cap, mls_cap)] the active entries' list positions in list order
+                        // (k_pose: points in the low, lines in the high 16 bits)
     double* pose_dtini; // [B*16] staging of gfpl_optimize_pose_ini's DT_ini
     int32_t* kf_mask;  // [B] staging of gfpl_curr_frame_is_kf's mask
     double* cross_tinv; // [B*16] inverse of the predicted curr.Tfw (k_predict_pose -> k_cross_points)
+    int64_t* dbg;       // [B*8] diagnostic clocks (only builds with -DGFPL_SP_CLOCK write them)
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

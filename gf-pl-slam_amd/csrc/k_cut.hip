@@ -943,6 +943,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double vtab[PROOF ? CUT_G : 1][PROOF ? 2 * CUT_KS : 1];
     __shared__ int cnxt[PROOF ? CUT_KS : 1], cprv[PROOF ? CUT_KS : 1];
     const int lane = threadIdx.x;
+#ifdef GFPL_CUT_CLOCK
+    const uint64_t t_beg = wall_clock64();   // (diagnostic build: the wave's duration in record slot 19)
+#endif
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
     const bool live = b < p.B;
@@ -1310,6 +1313,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
         p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
         p.scr.bytes[(size_t)STEP_REC * b + 19] = n_unb;
+#ifdef GFPL_CUT_CLOCK
+        p.scr.bytes[(size_t)STEP_REC * b + 19] = (int64_t)(wall_clock64() - t_beg);
+#endif
     }
 }
 

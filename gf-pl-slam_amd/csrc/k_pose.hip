@@ -25,10 +25,8 @@ namespace gfpl {
 struct PoseLDS {
     double DT[16];
     double DTini[16];
-    double H[36];
-    double part[64];
-    double inc[6];    // the GN increment (lane 0's LDLT solve)
-    double X[48];     // se3_update_wave scratch: expmap | s, V | inverse
+    double H[36];     // (the reduction partials, the increment and se3_update_wave's scratch live
+                      // in the chunk region, dead between chunk loops: 944 B less per wave)
     int brk;
     int upd;          // apply inc to DT (the error test did not stop the loop)
     int ninl;
@@ -171,8 +169,8 @@ struct PoseCtx {
     const double* lin;   // [LS_K][mls_cap]
     size_t mpt_cap, mls_cap;
     const uint8_t* act;  // LDS [npt + nls] list-position inlier flags
-    uint16_t* idxp;      // LDS [mpt_cap] the active points' list positions, in list order
-    uint16_t* idxl;      // LDS [mls_cap] the active lines'
+    uint32_t* idx;       // HBM [max(mpt_cap, mls_cap)] the active points' (low 16 bits) and lines'
+                         // (high 16 bits) list positions, in list order
     int npt, nls;
 };
 
@@ -203,19 +201,26 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             const int f = b0 + lane;
             const bool a = f < X.npt && actp[f];
             const unsigned long long m = __ballot(a);
-            if (a) X.idxp[np_act + __popcll(m & lt)] = (uint16_t)f;
+            if (a) reinterpret_cast<uint16_t*>(X.idx + np_act + __popcll(m & lt))[0] = (uint16_t)f;
             np_act += __popcll(m);
         }
         for (int b0 = 0; b0 < X.nls; b0 += 64) {
             const int f = b0 + lane;
             const bool a = f < X.nls && actl[f];
             const unsigned long long m = __ballot(a);
-            if (a) X.idxl[nl_act + __popcll(m & lt)] = (uint16_t)f;
+            if (a) reinterpret_cast<uint16_t*>(X.idx + nl_act + __popcll(m & lt))[1] = (uint16_t)f;
             nl_act += __popcll(m);
         }
         __syncthreads();
     }
-    const int nch = (max(np_act, nl_act) + 63) >> 6;
+    const int ntot = max(np_act, nl_act), nch = (ntot + 63) >> 6;
+    // a chunk's list positions are loaded one chunk ahead of its inputs (the inputs' loads
+    // depend on them); chunk 0's are reloaded per iteration (kept in a register across the
+    // iterations and the se3_update_wave call, they cost 45 VGPR spills at 128 registers)
+    auto load_idx = [&](int c) { const int f = (c << 6) + lane; return f < ntot ? X.idx[f] : 0u; };
+    double* part = cp;        // [64] the 28 + 28 reduction partials
+    double* incs = cp + 64;   // [6] the increment
+    double* xs = cp + 72;     // [48] se3_update_wave scratch
     for (int it = 0; it < max_iters; ++it) {
         // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
         // holding 16 doubles in registers across the chunk loop
@@ -224,15 +229,16 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
         // raw inputs of chunk c + 1 are loaded into registers while chunk c is
         // reduced, so the SoA scratch latency hides behind the LDS reduction
         double pv[PT_K], lv[LS_K];
-        auto load_chunk = [&](int c) {
+        auto load_chunk = [&](int c, uint32_t ix) {
             const int f = (c << 6) + lane;
-            const int fp = f < np_act ? (int)X.idxp[f] : 0, fl = f < nl_act ? (int)X.idxl[f] : 0;
+            const int fp = f < np_act ? (int)(ix & 0xFFFFu) : 0, fl = f < nl_act ? (int)(ix >> 16) : 0;
 #pragma unroll
             for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
 #pragma unroll
             for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
         };
-        load_chunk(0);
+        load_chunk(0, load_idx(0));
+        uint32_t ix = load_idx(1);
         for (int c = 0; c < nch; ++c) {
             const int f = (c << 6) + lane;
             double o[8];
@@ -250,7 +256,10 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
-            if (c + 1 < nch) load_chunk(c + 1);
+            if (c + 1 < nch) {
+                load_chunk(c + 1, ix);
+                ix = load_idx(c + 2);
+            }
             __syncthreads();
             const double* A = buf + ia * CH_STRIDE;
             const double* Bv = buf + ib * CH_STRIDE;
@@ -266,20 +275,20 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             }
             __syncthreads();
         }
-        S.part[lane] = s;
+        part[lane] = s;
         __syncthreads();
         // H = H_p + H_l, one element per lane (the symmetric pair gets the same sum)
         if (lane < 36) {
             const int r = lane / 6, c = lane - 6 * (lane / 6);
             const int t = r >= c ? tri(r, c) : tri(c, r);
-            S.H[lane] = S.part[t] + S.part[28 + t];
+            S.H[lane] = part[t] + part[28 + t];
         }
         __syncthreads();
         if (lane == 0) {
             double H[36], g[6];
             for (int i = 0; i < 36; ++i) H[i] = S.H[i];
-            for (int i = 0; i < 6; ++i) g[i] = S.part[21 + i] + S.part[28 + 21 + i];
-            double ee = S.part[27] + S.part[28 + 27];
+            for (int i = 0; i < 6; ++i) g[i] = part[21 + i] + part[28 + 21 + i];
+            double ee = part[27] + part[28 + 27];
             ee = ee / (double)(S.cnt[1] + S.cnt[0]);
             S.err = ee;
             int brk = 0, upd = 0;
@@ -288,7 +297,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             } else {
                 double inc[6];
                 ldlt_solve6_one_lane(H, g, inc);
-                for (int i = 0; i < 6; ++i) S.inc[i] = inc[i];
+                for (int i = 0; i < 6; ++i) incs[i] = inc[i];
                 upd = 1;
                 const double nrm = sqrt(((((inc[0] * inc[0] + inc[1] * inc[1]) + inc[2] * inc[2]) + inc[3] * inc[3]) +
                                          inc[4] * inc[4]) + inc[5] * inc[5]);
@@ -299,7 +308,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             S.upd = upd;
         }
         __syncthreads();
-        if (S.upd) se3_update_wave(S.inc, S.DT, S.X);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
+        if (S.upd) se3_update_wave(incs, S.DT, xs);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
         if (S.brk) break;
     }
 }
@@ -390,10 +399,11 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8 (16-B padded) |
-// idx[mpt_cap + mls_cap] u16 (the active points' / lines' list positions, gauss_newton)
+// dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8 (16-B padded):
+// 9.3 KB + 576 B static at the default caps (500 / 300), so 16 waves fit a CU's 160 KB (4 per
+// SIMD, as the 122 VGPRs allow); the compacted positions gauss_newton walks live in HBM
 #ifndef GFPL_POSE_WAVES
-#define GFPL_POSE_WAVES 2
+#define GFPL_POSE_WAVES 4
 #endif
 __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -407,7 +417,6 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     double* cl = cp + 8 * CH_STRIDE;
     double* buf = cp;   // MAD sort buffer: never live together with the GN chunk rows
     uint8_t* act = (uint8_t*)(cp + region);
-    uint16_t* idxa = (uint16_t*)(act + ((p.mpt_cap + p.mls_cap + 15) & ~15));   // compacted active positions
     const DevPose& PP = p.prev.pose;
     const DevPoints& P = p.prev.pt;
     const DevLines& L = p.prev.ls;
@@ -419,7 +428,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     double* pin = p.scr.pose_in + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
     double* lin = pin + PT_K * p.mpt_cap;
     X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
-    X.idxp = idxa; X.idxl = idxa + p.mpt_cap;
+    X.idx = p.scr.pose_idx + (size_t)b * (size_t)max(p.mpt_cap, p.mls_cap);
     if (lane < 16) {   // Q2: the app passes prev_frame->DT (app/plslam_mod.cpp:408)
         S.DTini[lane] = p.dt_ini ? p.dt_ini[16 * b + lane] : PP.DT[16 * b + lane];
         S.DT[lane] = S.DTini[lane];
@@ -710,7 +719,7 @@ hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
     const size_t region = (size_t)std::max(16 * CH_STRIDE, NP2);
-    const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 2 * (size_t)(p.mpt_cap + p.mls_cap) + 16;
+    const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 16;
     hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);

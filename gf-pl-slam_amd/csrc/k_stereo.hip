@@ -231,6 +231,12 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // half the entries of the single sorted list); keypoints whose octave is outside the
 // pyramid form one extra segment, searched by bisection when it is not empty.  The
 // candidates, hence the lexicographic (dist, iR) minimum, are the same either way.
+// diagnostic build (-DGFPL_SP_CLOCK): the phase boundaries' wall clock per sequence (scr.dbg)
+#ifdef GFPL_SP_CLOCK
+#define SP_CLK(k) do { if (threadIdx.x == 0) p.scr.dbg[8 * (size_t)blockIdx.x + (k)] = (int64_t)wall_clock64(); } while (0)
+#else
+#define SP_CLK(k) do { } while (0)
+#endif
 template <int BLOCK, bool SEG>
 __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams p, int KP2) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -254,6 +260,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     // band scan is over (LDS, no scattered 4-B global stores)
     float* depth = recx;
     const int tid = threadIdx.x;
+    SP_CLK(0);
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
     const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
     const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
@@ -395,6 +402,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     __syncthreads();
     }
+    SP_CLK(1);
     // SEG: first candidate of segment o for a row: the first bin with minr >= row - D_o
     auto seg_start = [&](int o, int row) {
         return (int)rowlo[o * NBIN + min(max(row - misc[22 + o] + SP_MINR_PAD, 0), NBIN - 1)];
@@ -534,6 +542,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     }
     __syncthreads();
+    SP_CLK(2);
     // SEG: the SAD jobs counting-sorted by the tile of their window — (level, 8-row band,
     // 64-px column strip), coarser on large images so the tiles fit 4096 bins — so the 16 quads
     // of a wave read overlapping window rows (one cache line serves several lanes) instead of
@@ -589,6 +598,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         for (int r = 0; r < RMAX; ++r)
             if (jb[r] != 0xFFFFFFFFu) sj[(int)off[jr[r] & 0xFFFFu] + (int)(jr[r] >> 16)] = jb[r];
         __syncthreads();
+        SP_CLK(3);
         jobs = sj;
     }
     // sub-pixel refinement + disparity gate (src/stereoFrame.cpp:547-583), one DPP quad
@@ -637,6 +647,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         }
     }
     __syncthreads();
+    SP_CLK(4);
     // sort(vDistIdx) (src/stereoFrame.cpp:585): the (dist, iL) keys ascending
     uint32_t* keys = pairs;
     if (SEG) {
@@ -761,6 +772,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         p.curr.pose.time_stamp[b] = p.in.time_stamp[b];
         p.scr.n_subpix[b] = misc[2];
     }
+    SP_CLK(5);
 }
 
 // ------------------------------------------------------- stereo lines --

@@ -354,6 +354,8 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_counts": ([P, P], C.c_int),
             "gfpl_last_step_track_counts": ([P, P], C.c_int),
             "gfpl_debug_cut_records": ([P, C.c_int, P, C.c_int], C.c_int),
+            "gfpl_debug_step_records": ([P, P], C.c_int),
+            "gfpl_debug_clocks": ([P, P], C.c_int),
             "gfpl_lsd_create": ([P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)], C.c_int),
             "gfpl_lsd_destroy": ([P], C.c_int),
             "gfpl_lsd_detect": ([P, P, C.c_int, P, P, P], C.c_int),
@@ -1022,6 +1024,18 @@ class StereoFrameHandler:
         """gfpl_debug_cut_records: sequence b's line-cut records [n_lines][80] (float64)."""
         out = np.zeros((n_lines, 80), np.float64)
         check(self.L.gfpl_debug_cut_records(self.h, b, out.ctypes.data, n_lines), "debug_cut_records")
+        return out
+
+    def debug_step_records(self) -> np.ndarray:
+        """gfpl_debug_step_records: every sequence's record of the last step [B][20] (int64)."""
+        out = np.zeros((self.B, 20), np.int64)
+        check(self.L.gfpl_debug_step_records(self.h, out.ctypes.data), "debug_step_records")
+        return out
+
+    def debug_clocks(self) -> np.ndarray:
+        """gfpl_debug_clocks: the instrumented builds' per-sequence clocks [B][8] (int64)."""
+        out = np.zeros((self.B, 8), np.int64)
+        check(self.L.gfpl_debug_clocks(self.h, out.ctypes.data), "debug_clocks")
         return out
 
     def last_step_kernel_bytes(self) -> np.ndarray:

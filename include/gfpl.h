@@ -645,6 +645,13 @@ int  gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4);
  * insert (80 doubles each: comparison data, bounds, r = 0 info, the agreement bound as
  * k_cut_search formed it — DESIGN.md §3; layout in k_cut.hip).  Synchronises.      */
 int  gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines);
+/* Every sequence's record of the last step: B x 20 int64 — stage bytes [0..7], the counts of
+ * gfpl_last_step_counts [8..15], line-cut steps / exact steps [16..17], inliers after the pose
+ * [18], lines without a usable bound [19] (layout: STEP_REC in gfpl_state.hpp).  Synchronises. */
+int  gfpl_debug_step_records(gfpl_seqbatch* sb, int64_t* out);
+/* B x 8 int64 of diagnostic clocks (100 MHz wall clock) that instrumented builds of the library
+ * write (e.g. -DGFPL_SP_CLOCK: k_stereo_points' phase boundaries); zeros otherwise. Synchronises. */
+int  gfpl_debug_clocks(gfpl_seqbatch* sb, int64_t* out);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
  * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same

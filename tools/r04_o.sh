@@ -9,3 +9,15 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu --ti
   || { grep -E "passed|failed|Error" $O/pytest.log | tail -5; exit 1; }
 grep -E "passed|failed" $O/pytest.log | tail -1
 bash tools/ab_bench.sh $O 20 default build/ab_prev default
+# line-cut search balance (wave durations, -DGFPL_CUT_CLOCK build)
+export GFPL_LIB_DIR=$(realpath build/ab_clock)
+timeout -k 10 300 python bench.py --steps 3 --warmup 2 --no-cpu --no-detect --no-host-fed --no-b1 --parity-seqs 2 \
+    --dump-records $O/records.npy > $O/bench_clock.log 2>&1 || { tail -5 $O/bench_clock.log; exit 1; }
+unset GFPL_LIB_DIR
+python tools/cut_balance.py $O/records.npy | tee $O/balance.json
+# k_stereo_points phase split (-DGFPL_SP_CLOCK build)
+export GFPL_LIB_DIR=$(realpath build/ab_spclk)
+timeout -k 10 300 python bench.py --steps 3 --warmup 2 --no-cpu --no-detect --no-host-fed --no-b1 --parity-seqs 2 \
+    --dump-records $O/records_sp.npy > $O/bench_spclk.log 2>&1 || { tail -5 $O/bench_spclk.log; exit 1; }
+unset GFPL_LIB_DIR
+python tools/sp_phases.py $O/records_sp_clk.npy | tee $O/sp_phases.json
