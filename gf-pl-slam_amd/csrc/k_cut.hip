@@ -919,6 +919,27 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
     eb[5] = (rvs <= 0.25 && rve <= 0.25) ? 0.0f : __builtin_inff();   // the per-step |ev| <= v'/4 test
 }
 
+// Issue priority by progress.  A SIMD holds two search waves with the same work (B = 16384: 300
+// lines per sequence, the greedy steps per wave within 2%), and the arbiter prefers the older of two
+// ready waves: measured per wave (-DGFPL_CUT_CLOCK, profiles/r04_o), the first wave of every SIMD
+// took 4.9 ms and the second 5.6 ms, which then ran its last part alone.  The priority falls by one
+// level per quarter of the wave's lines, so a wave that is ahead yields to one that is behind.
+#ifndef GFPL_CUT_FAIR
+#define GFPL_CUT_FAIR 1
+#endif
+__device__ __forceinline__ void cut_progress_prio(int done, int total) {
+    done += __shfl_xor(done, 8);
+    done += __shfl_xor(done, 16);
+    done += __shfl_xor(done, 32);
+    total += __shfl_xor(total, 8);
+    total += __shfl_xor(total, 16);
+    total += __shfl_xor(total, 32);
+    const int q = __builtin_amdgcn_readfirstlane(total > 0 ? (4 * done) / total : 4);
+    if (q <= 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 template <bool PROOF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
@@ -1133,6 +1154,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
+    if (GFPL_CUT_FAIR) cut_progress_prio(0, j == 0 ? nls : 0);
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -1305,6 +1327,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
+            if (GFPL_CUT_FAIR) cut_progress_prio(j == 0 ? m : 0, j == 0 ? nls : 0);
         } else if (pend) {
             ++wait;
         }
