@@ -150,6 +150,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_dtini = c.take<double>(B * 16);
     sb->scr.cross_tinv = c.take<double>(B * 16);
     sb->scr.dbg = c.take<int64_t>(B * 8);
+    sb->scr.cut_prog = c.take<int32_t>((size_t)1 << 17);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);

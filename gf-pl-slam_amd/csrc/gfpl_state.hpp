@@ -103,6 +103,7 @@ struct DevScratch {
     int32_t* kf_mask;  // [B] staging of gfpl_curr_frame_is_kf's mask
     double* cross_tinv; // [B*16] inverse of the predicted curr.Tfw (k_predict_pose -> k_cross_points)
     int64_t* dbg;       // [B*8] diagnostic clocks (only builds with -DGFPL_SP_CLOCK write them)
+    int32_t* cut_prog;  // [1 << 17] k_cut_search: lines done per (XCC, SE, SH, CU, SIMD, wave slot)
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

@@ -298,8 +298,14 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
                 cut_poly_data(Dl, d, homog, fd);
                 fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
+#ifndef GFPL_PREP_PROBE   // (timing probe: without the comparison-data stores; the search then runs exact)
 #pragma unroll
                 for (int i = 0; i < CUT_FAST; ++i) rec_l[(size_t)m * CUT_REC + i] = fd[i];
+#else
+                rec_l[(size_t)m * CUT_REC + PD_OK] = 0.0;   // (every step exact: the index field stays valid)
+                rec_l[(size_t)m * CUT_REC + PD_NEXT] = fd[PD_NEXT];
+                if (fd[0] == 12345.678) rec_l[(size_t)m * CUT_REC] = fd[1];
+#endif
             } else {
                 const size_t q = pbase + mpt[m];
                 double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
@@ -920,25 +926,39 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
 }
 
 // Issue priority by progress.  A SIMD holds two search waves with the same work (B = 16384: 300
-// lines per sequence, the greedy steps per wave within 2%), and the arbiter prefers the older of two
-// ready waves: measured per wave (-DGFPL_CUT_CLOCK, profiles/r04_o), the first wave of every SIMD
-// took 4.9 ms and the second 5.6 ms, which then ran its last part alone.  The priority falls by one
-// level per quarter of the wave's lines, so a wave that is ahead yields to one that is behind.
+// lines per sequence, the greedy steps per wave within 2%), yet measured per wave
+// (-DGFPL_CUT_CLOCK, profiles/r04_o, r04_r) the one in wave slot 0 finished in 5.2 ms and the one in
+// slot 1 in 5.6 ms (up to 6.3), which then ran its end alone.  GFPL_CUT_FAIR 1: the priority falls
+// one level per quarter of the wave's lines; 2: the two waves of a SIMD publish their progress (lines
+// done) in HBM at every line transition and the one ahead of its partner yields (priority 0 vs 2).
 #ifndef GFPL_CUT_FAIR
-#define GFPL_CUT_FAIR 1
+#define GFPL_CUT_FAIR 2
 #endif
+__device__ __forceinline__ int wave_sum8(int v) {   // sum over the wave's 8 groups of lane 8g's value
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return __builtin_amdgcn_readfirstlane(v);
+}
 __device__ __forceinline__ void cut_progress_prio(int done, int total) {
-    done += __shfl_xor(done, 8);
-    done += __shfl_xor(done, 16);
-    done += __shfl_xor(done, 32);
-    total += __shfl_xor(total, 8);
-    total += __shfl_xor(total, 16);
-    total += __shfl_xor(total, 32);
-    const int q = __builtin_amdgcn_readfirstlane(total > 0 ? (4 * done) / total : 4);
+    done = wave_sum8(done);
+    total = wave_sum8(total);
+    const int q = total > 0 ? (4 * done) / total : 4;
     if (q <= 0) __builtin_amdgcn_s_setprio(3);
     else if (q == 1) __builtin_amdgcn_s_setprio(2);
     else if (q == 2) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
+}
+// the wave's progress slot and its SIMD partner's (slot ^ 1) in scr.cut_prog: one entry per
+// (XCC, SE, SH, CU, SIMD, wave slot) from the HW_ID / XCC_ID registers
+struct CutProg { int* own; int* partner; };
+__device__ __forceinline__ CutProg cut_prog_slots(int* base) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+    const unsigned simd = ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) * 4u +
+                          ((hw >> 4) & 3u);
+    const unsigned slot = hw & 15u;
+    return CutProg{base + simd * 16u + slot, base + simd * 16u + (slot ^ 1u)};
 }
 template <bool PROOF>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
@@ -1154,7 +1174,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
-    if (GFPL_CUT_FAIR) cut_progress_prio(0, j == 0 ? nls : 0);
+#if GFPL_CUT_FAIR == 1
+    cut_progress_prio(0, j == 0 ? nls : 0);
+#elif GFPL_CUT_FAIR == 2
+    const CutProg prog = cut_prog_slots(p.scr.cut_prog);
+    if (lane == 0) __hip_atomic_store(prog.own, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int partner_done = 0;   // the partner's lines done as read at the previous transition
+    __builtin_amdgcn_s_setprio(2);
+#endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -1327,7 +1354,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
-            if (GFPL_CUT_FAIR) cut_progress_prio(j == 0 ? m : 0, j == 0 ? nls : 0);
+#if GFPL_CUT_FAIR == 1
+            cut_progress_prio(j == 0 ? m : 0, j == 0 ? nls : 0);
+#elif GFPL_CUT_FAIR == 2
+            {
+                const int done = wave_sum8(j == 0 ? m : 0);
+                if (done > __builtin_amdgcn_readfirstlane(partner_done)) __builtin_amdgcn_s_setprio(0);
+                else __builtin_amdgcn_s_setprio(2);
+                if (lane == 0) __hip_atomic_store(prog.own, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                partner_done = __hip_atomic_load(prog.partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used next time
+            }
+#endif
         } else if (pend) {
             ++wait;
         }
@@ -1337,7 +1374,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
         p.scr.bytes[(size_t)STEP_REC * b + 19] = n_unb;
 #ifdef GFPL_CUT_CLOCK
-        p.scr.bytes[(size_t)STEP_REC * b + 19] = (int64_t)(wall_clock64() - t_beg);
+        const uint64_t t_end = wall_clock64();
+        p.scr.bytes[(size_t)STEP_REC * b + 19] = (int64_t)(t_end - t_beg);
+        p.scr.dbg[8 * (size_t)b + 0] = (int64_t)t_beg;
+        p.scr.dbg[8 * (size_t)b + 1] = (int64_t)t_end;
+        p.scr.dbg[8 * (size_t)b + 2] = (int64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+        p.scr.dbg[8 * (size_t)b + 3] = (int64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
 #endif
     }
 }

@@ -10,6 +10,8 @@
 // One workgroup owns one sequence's frame: the band search, the (dist,iL) sort,
 // the median gate and the order-preserving compaction are all block-local, so a
 // frame never crosses workgroups and B sequences fill the 256 CUs.
+#include <type_traits>
+
 #include "gfpl_kernels.hpp"
 #include "gfpl_knn.hpp"
 
@@ -466,39 +468,48 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                 int j = need ? seg_start(o, row) : 0;
                 const int jend = need ? (int)rowlo[o * NBIN + row + 1 + SP_MINR_PAD] : 0;
                 bool more = j < jend;
-                while (__any(more)) {
-                    int c0 = more ? j : 0x7FFFFFFF;
-#pragma unroll
-                    for (int sh = 1; sh < 64; sh <<= 1) c0 = min(c0, __shfl_xor(c0, sh));
-                    {
-                        const int je = c0 + (lane >> 1);
-                        if (je < Nr && (rkey[je] >> 28) == (uint32_t)o) {
-                            const int iR = (int)(rkey[je] & 0xFFFFu);
-                            wst[lane] = *reinterpret_cast<const u32x4*>(DR + (size_t)iR * 32 + 16 * (lane & 1));   // entry lane >> 1, half lane & 1
+                // segment o < nlev holds only octave-o keypoints, and a lane walks it only when o is
+                // within levelL +- 1: the octave test is the out-of-range segment's alone
+                auto walk = [&](auto oseg) {
+                    while (__any(more)) {
+                        // the chunk starts at the smallest pending j, which is the first pending
+                        // lane's: lanes are in row order and the band bounds grow with the row, so
+                        // the pending lanes' j never decrease with the lane index
+                        const int c0 = __builtin_amdgcn_readlane(j, __builtin_ctzll(__ballot(more)));
+                        {
+                            const int je = c0 + (lane >> 1);
+                            if (je < Nr && (rkey[je] >> 28) == (uint32_t)o) {
+                                const int iR = (int)(rkey[je] & 0xFFFFu);
+                                wst[lane] = *reinterpret_cast<const u32x4*>(DR + (size_t)iR * 32 + 16 * (lane & 1));   // entry lane >> 1, half lane & 1
+                            }
                         }
+                        wave_lds_sync();
+                        const int jl = min(c0 + SP_CHUNK, jend);
+                        for (; j < jl; ++j) {
+                            // every LDS read of the entry issued together: one round trip per candidate
+                            const uint32_t k = rkey[j];
+                            const uint32_t m = recm[j];
+                            const float uR = recx[j];
+                            const u32x4 a = wst[2 * (j - c0)], c = wst[2 * (j - c0) + 1];
+                            const int minr = (int)((k >> 16) & 0xFFFu) - 1024;
+                            const int iR = (int)(k & 0xFFFFu);
+                            const uint32_t dr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+                            const uint32_t key = ((uint32_t)hamming8<1>(dl, dr) << 16) | (uint32_t)iR;
+                            // the tests as one mask and the minimum as a select: no branch around the distance
+                            bool pass = (minr + (int)(m >> 8) >= row) & (uR >= minU) & (uR <= maxU);   // maxr >= row
+                            if (!decltype(oseg)::value) {
+                                int octR = (int)(int8_t)(uint8_t)(m & 0xFFu);
+                                if (octR == -128) octR = KR[iR].octave;
+                                pass = pass & (octR >= levelL - 1) & (octR <= levelL + 1);
+                            }
+                            best = min(best, pass ? key : 0xFFFFFFFFu);
+                        }
+                        more = j < jend;
+                        wave_lds_sync();   // the chunk is read before the next one overwrites it
                     }
-                    wave_lds_sync();
-                    const int jl = min(c0 + SP_CHUNK, jend);
-                    for (; j < jl; ++j) {
-                        // every LDS read of the entry issued together: one round trip per candidate
-                        const uint32_t k = rkey[j];
-                        const uint32_t m = recm[j];
-                        const float uR = recx[j];
-                        const u32x4 a = wst[2 * (j - c0)], c = wst[2 * (j - c0) + 1];
-                        const int minr = (int)((k >> 16) & 0xFFFu) - 1024;
-                        const int iR = (int)(k & 0xFFFFu);
-                        int octR = (int)(int8_t)(uint8_t)(m & 0xFFu);
-                        if (octR == -128) octR = KR[iR].octave;
-                        const uint32_t dr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-                        const uint32_t key = ((uint32_t)hamming8<1>(dl, dr) << 16) | (uint32_t)iR;
-                        // the tests as one mask and the minimum as a select: no branch around the distance
-                        const bool pass = (minr + (int)(m >> 8) >= row) &   // maxr >= row
-                                          (octR >= levelL - 1) & (octR <= levelL + 1) & (uR >= minU) & (uR <= maxU);
-                        best = min(best, pass ? key : 0xFFFFFFFFu);
-                    }
-                    more = j < jend;
-                    wave_lds_sync();   // the chunk is read before the next one overwrites it
-                }
+                };
+                if (o < nlev) walk(std::true_type{});
+                else walk(std::false_type{});
             }
             const int bestDist = (int)(best >> 16), bestIdxR = (int)(best & 0xFFFFu);
             if (t < N) finish_kp(t, iL, kpL, bestDist, bestIdxR);
