@@ -291,8 +291,13 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 LineCutData d;
                 load_line(L, lb + mls[m], d);
                 poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
+                // the record is written 16 B per lane and store (lanes write 64 different records, so
+                // every store instruction touches 64 cache lines: 8-B stores took a third of the
+                // kernel, profiles/r04_s/bench_prepprobe.log); the pad double after the info is zeroed
+                double2* rq = reinterpret_cast<double2*>(rec_l + (size_t)m * CUT_REC);
 #pragma unroll
-                for (int i = 0; i < 21; ++i) rec_l[(size_t)m * CUT_REC + CUT_FAST + i] = info[i];   // k_cut_search subtracts it
+                for (int i = 0; i < 10; ++i) rq[CUT_FAST / 2 + i] = make_double2(info[2 * i], info[2 * i + 1]);   // k_cut_search subtracts it
+                rq[CUT_FAST / 2 + 10] = make_double2(info[20], 0.0);
                 double fd[CUT_FAST];
 #pragma unroll
                 for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
@@ -300,7 +305,7 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
 #ifndef GFPL_PREP_PROBE   // (timing probe: without the comparison-data stores; the search then runs exact)
 #pragma unroll
-                for (int i = 0; i < CUT_FAST; ++i) rec_l[(size_t)m * CUT_REC + i] = fd[i];
+                for (int i = 0; i < CUT_FAST / 2; ++i) rq[i] = make_double2(fd[2 * i], fd[2 * i + 1]);
 #else
                 rec_l[(size_t)m * CUT_REC + PD_OK] = 0.0;   // (every step exact: the index field stays valid)
                 rec_l[(size_t)m * CUT_REC + PD_NEXT] = fd[PD_NEXT];

@@ -175,8 +175,23 @@ struct PoseCtx {
 };
 
 // gaussNewtonOptimization (:2032-2056): DT updated in place in S, H = last evaluated
+// (experiment, -DGFPL_POSE_FAIR) issue priority by progress: 3 in the first half of the first GN run,
+// down to 0 in the second half of the second, so the waves dispatched last are not starved by the
+// older ones at the end of the grid
+__device__ __forceinline__ void pose_prio(int stage, int it, int n) {
+#ifdef GFPL_POSE_FAIR
+    const int q = 2 * stage + (2 * it >= n ? 1 : 0);
+    if (q <= 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)stage; (void)it; (void)n;
+#endif
+}
+
 __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl,
-                             int max_iters) {
+                             int max_iters, int stage) {
     const int lane = threadIdx.x;
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
@@ -222,6 +237,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     double* incs = cp + 64;   // [6] the increment
     double* xs = cp + 72;     // [48] se3_update_wave scratch
     for (int it = 0; it < max_iters; ++it) {
+        pose_prio(stage, it, max_iters);
         // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
         // holding 16 doubles in registers across the chunk loop
         const double* DT = S.DT;
@@ -463,7 +479,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     int ok = 0;        // 1: stage-2 DT usable
     double err = 0.0;  // err of the last GN run (reference: uninitialised when no GN runs, pinned 0)
     if (S.ninl > p.cfg.min_features) {
-        gauss_newton(p, X, S, cp, cl, p.cfg.max_iters);
+        gauss_newton(p, X, S, cp, cl, p.cfg.max_iters, 0);
         err = S.err;
         double DTs[16];
         for (int i = 0; i < 16; ++i) DTs[i] = S.DT[i];
@@ -557,7 +573,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
             if (S.ninl > p.cfg.min_features) {
                 if (lane < 16) S.DT[lane] = S.DTini[lane];   // Q3: stage 2 restarts from DT_ini
                 __syncthreads();
-                gauss_newton(p, X, S, cp, cl, p.cfg.max_iters_ref);
+                gauss_newton(p, X, S, cp, cl, p.cfg.max_iters_ref, 1);
                 err = S.err;
                 ok = 1;
             }
