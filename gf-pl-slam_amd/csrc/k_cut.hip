@@ -252,6 +252,9 @@ __device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutDat
 }
 
 // ------------------------------------------------------------------ prep --
+#ifndef GFPL_PREP_STAGE
+#define GFPL_PREP_STAGE 1
+#endif
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
@@ -286,27 +289,26 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         const int m = ((lines ? c : c - nl_ch) << 6) + lane;
         const int cnt = min(64, (lines ? nls : npt) - (((lines ? c : c - nl_ch)) << 6));
         double info[21];
+        double fd[CUT_FAST];   // (lines) the record's comparison data
         if (lane < cnt) {
             if (lines) {
                 LineCutData d;
                 load_line(L, lb + mls[m], d);
                 poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
-                // the record is written 16 B per lane and store (lanes write 64 different records, so
-                // every store instruction touches 64 cache lines: 8-B stores took a third of the
-                // kernel, profiles/r04_s/bench_prepprobe.log); the pad double after the info is zeroed
-                double2* rq = reinterpret_cast<double2*>(rec_l + (size_t)m * CUT_REC);
-#pragma unroll
-                for (int i = 0; i < 10; ++i) rq[CUT_FAST / 2 + i] = make_double2(info[2 * i], info[2 * i + 1]);   // k_cut_search subtracts it
-                rq[CUT_FAST / 2 + 10] = make_double2(info[20], 0.0);
-                double fd[CUT_FAST];
 #pragma unroll
                 for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
                 cut_poly_data(Dl, d, homog, fd);
                 fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
-#ifndef GFPL_PREP_PROBE   // (timing probe: without the comparison-data stores; the search then runs exact)
+#if !GFPL_PREP_STAGE && !defined(GFPL_PREP_PROBE)
+                // the record written 16 B per lane and store
+                double2* rq = reinterpret_cast<double2*>(rec_l + (size_t)m * CUT_REC);
+#pragma unroll
+                for (int i = 0; i < 10; ++i) rq[CUT_FAST / 2 + i] = make_double2(info[2 * i], info[2 * i + 1]);   // k_cut_search subtracts it
+                rq[CUT_FAST / 2 + 10] = make_double2(info[20], 0.0);
 #pragma unroll
                 for (int i = 0; i < CUT_FAST / 2; ++i) rq[i] = make_double2(fd[2 * i], fd[2 * i + 1]);
-#else
+#endif
+#ifdef GFPL_PREP_PROBE   // (timing probe: without the comparison-data stores; the search then runs exact)
                 rec_l[(size_t)m * CUT_REC + PD_OK] = 0.0;   // (every step exact: the index field stays valid)
                 rec_l[(size_t)m * CUT_REC + PD_NEXT] = fd[PD_NEXT];
                 if (fd[0] == 12345.678) rec_l[(size_t)m * CUT_REC] = fd[1];
@@ -325,6 +327,39 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
 #pragma unroll
                     for (int j = 0; j <= i; ++j) info[tri(i, j)] = J[i] * J[j];
             }
+        }
+#if GFPL_PREP_STAGE && !defined(GFPL_PREP_PROBE)
+        if (lines) {   // (wave-uniform)
+            // The chunk's records (comparison data | r = 0 info | pad) leave in five slices of 16
+            // doubles staged through the chunk buffer (idle until the sums): a store instruction then
+            // writes 8 whole 128-B lines of 8 records instead of 16 B of each of 64 records — stored
+            // straight from the lanes, the records took a third of the kernel
+            // (profiles/r04_s/bench_prepprobe.log)
+            double* stg = &chunk[0][0];   // [64][17] (odd row stride: the lanes' rows spread over the banks)
+            const int pl = lane >> 3, pp = lane & 7;
+            double* rc = rec_l + (size_t)(c << 6) * CUT_REC;
+#pragma unroll
+            for (int sl = 0; sl < CUT_REC / 16; ++sl) {
+                if (lane < cnt) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const int x = 16 * sl + k;
+                        stg[lane * 17 + k] = x < CUT_FAST ? fd[x] : (x < CUT_FAST + 21 ? info[x - CUT_FAST] : 0.0);
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int g8 = 0; g8 < 8; ++g8) {
+                    const int ln = 8 * g8 + pl;
+                    if (ln < cnt)
+                        reinterpret_cast<double2*>(rc + (size_t)ln * CUT_REC + 16 * sl)[pp] =
+                            make_double2(stg[ln * 17 + 2 * pp], stg[ln * 17 + 2 * pp + 1]);
+                }
+                __syncthreads();
+            }
+        }
+#endif
+        if (lane < cnt) {
 #pragma unroll
             for (int i = 0; i < 21; ++i) chunk[i][lane] = info[i];
         }
