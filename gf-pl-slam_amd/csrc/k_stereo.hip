@@ -234,6 +234,16 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // pyramid form one extra segment, searched by bisection when it is not empty.  The
 // candidates, hence the lexicographic (dist, iR) minimum, are the same either way.
 // diagnostic build (-DGFPL_SP_CLOCK): the phase boundaries' wall clock per sequence (scr.dbg)
+// Issue priority by phase (setup 3, band scan 2, sub-pixel SAD 1, emission 0): of two ready waves the
+// arbiter favours the older, so without it the workgroups dispatched last trail at the end of the grid
+#ifndef GFPL_SP_PRIO
+#define GFPL_SP_PRIO 1
+#endif
+#if GFPL_SP_PRIO
+#define SP_PRIO(k) __builtin_amdgcn_s_setprio(k)
+#else
+#define SP_PRIO(k) do { } while (0)
+#endif
 #ifdef GFPL_SP_CLOCK
 #define SP_CLK(k) do { if (threadIdx.x == 0) p.scr.dbg[8 * (size_t)blockIdx.x + (k)] = (int64_t)wall_clock64(); } while (0)
 #else
@@ -263,6 +273,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     float* depth = recx;
     const int tid = threadIdx.x;
     SP_CLK(0);
+    SP_PRIO(3);
     const int N = min(p.in.n_kp_l[b], cap), Nr = min(p.in.n_kp_r[b], cap);
     const gfpl_keypoint* KL = p.in.kp_l + (size_t)b * cap;
     const gfpl_keypoint* KR = p.in.kp_r + (size_t)b * cap;
@@ -405,6 +416,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     __syncthreads();
     }
     SP_CLK(1);
+    SP_PRIO(2);
     // SEG: first candidate of segment o for a row: the first bin with minr >= row - D_o
     auto seg_start = [&](int o, int row) {
         return (int)rowlo[o * NBIN + min(max(row - misc[22 + o] + SP_MINR_PAD, 0), NBIN - 1)];
@@ -554,6 +566,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     __syncthreads();
     SP_CLK(2);
+    SP_PRIO(1);
     // SEG: the SAD jobs counting-sorted by the tile of their window — (level, 8-row band,
     // 64-px column strip), coarser on large images so the tiles fit 4096 bins — so the 16 quads
     // of a wave read overlapping window rows (one cache line serves several lanes) instead of
@@ -659,6 +672,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     }
     __syncthreads();
     SP_CLK(4);
+    SP_PRIO(0);
     // sort(vDistIdx) (src/stereoFrame.cpp:585): the (dist, iL) keys ascending
     uint32_t* keys = pairs;
     if (SEG) {
