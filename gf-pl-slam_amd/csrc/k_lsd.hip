@@ -38,6 +38,9 @@ namespace gfpl {
 #define LSD_RING 256               // region list entries mirrored in LDS
 #define LSD_SMALL 64               // ranges up to this size: one lane runs libstdc++'s serial loop
                                    // (32 / 48 / 64 / 96: 22.2k / 23.5k / 23.7k / 23.1k images/s)
+#ifndef GFPL_LSD_PRIO
+#define GFPL_LSD_PRIO 1
+#endif
 #define LSD_CID_MAX 491520         // compact used-map bits at most (60 KB of LDS + the ring)
 
 struct LsdDev {
@@ -1411,7 +1414,19 @@ __device__ void lsd_image(const LsdDev& o, int img, uint32_t* bits, uint32_t* ri
     const double mg = __longlong_as_double((long long)o.maxg[img]);
     const double bin_coef = (mg > 0) ? (double)(o.n_bins - 1) / mg : 0;
     const uint32_t B0 = (uint32_t)(int)(o.rho * bin_coef);
+#if GFPL_LSD_PRIO
+    const int nscan = max(1, o.ndef[img]);   // the seeds scanned: every defined pixel
+#endif
     for (int base = 0; base < o.NP; base += 64) {
+#if GFPL_LSD_PRIO
+        {   // issue priority by progress through the seeds (3 .. 0): the waves of a SIMD keep pace
+            const int q = (4 * base) / nscan;
+            if (q <= 0) __builtin_amdgcn_s_setprio(3);
+            else if (q == 1) __builtin_amdgcn_s_setprio(2);
+            else if (q == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         const uint64_t e = e1;
         if ((uint32_t)(__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32))) < B0) break;
         int px = (int)(e & 0xffff), py = (int)((e >> 16) & 0x7fff);
