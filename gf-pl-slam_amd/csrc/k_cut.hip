@@ -255,9 +255,6 @@ __device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutDat
 #ifndef GFPL_PREP_STAGE
 #define GFPL_PREP_STAGE 1
 #endif
-#ifndef GFPL_PREP_PRIO
-#define GFPL_PREP_PRIO 1
-#endif
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
@@ -288,16 +285,6 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     double s = 0.0;
     const int nl_ch = (nls + 63) >> 6, np_ch = (npt + 63) >> 6;
     for (int c = 0; c < nl_ch + np_ch; ++c) {
-#if GFPL_PREP_PRIO
-        {   // issue priority by progress (3 .. 0 over the chunks): the waves dispatched last are not
-            // starved by the older ones at the end of the grid
-            const int q = (4 * c) / (nl_ch + np_ch);
-            if (q == 0) __builtin_amdgcn_s_setprio(3);
-            else if (q == 1) __builtin_amdgcn_s_setprio(2);
-            else if (q == 2) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
         const bool lines = c < nl_ch;
         const int m = ((lines ? c : c - nl_ch) << 6) + lane;
         const int cnt = min(64, (lines ? nls : npt) - (((lines ? c : c - nl_ch)) << 6));
@@ -1442,9 +1429,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #ifndef GFPL_FIN_WAVES
 #define GFPL_FIN_WAVES 1
 #endif
-#ifndef GFPL_FIN_STAGE
-#define GFPL_FIN_STAGE 1
-#endif
 __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -1453,12 +1437,6 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)b * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
-#if GFPL_FIN_STAGE
-    // a line's invCovPose (36 doubles, 288 B) leaves in three 96-B slices staged through LDS: six
-    // lanes per line, ten lines per store instruction instead of 16 B of each of 64 lines
-    // (k_cut_prep's records: 1.66 -> 1.11 ms the same way)
-    __shared__ double stg[64][13];
-#endif
     double Dl[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
@@ -1474,37 +1452,13 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
             r0 = L.cut[2 * q];
             r1 = L.cut[2 * q + 1];
             poseInfoOnLine<true>(cam, p.cfg.homog_th, Dl, d, r0, r1, info);
-#if !GFPL_FIN_STAGE
             // 16-B stores: a line's 36 doubles are contiguous and 288-B aligned (carve: 256-B field base)
+            // (staged through LDS like k_cut_prep's records they measured 1.01 vs 0.82 ms: the lines of
+            // a chunk are scattered over the frame, so the slices do not merge; profiles/r04_u)
             double2* iv = reinterpret_cast<double2*>(L.invcov + 36 * q);
 #pragma unroll
             for (int i = 0; i < 18; ++i) iv[i] = make_double2(info[2 * i], info[2 * i + 1]);
-#endif
         }
-#if GFPL_FIN_STAGE
-        {
-            const int cnt = min(64, nls - m0);
-            const int ln0 = (int)threadIdx.x / 6, pc = (int)threadIdx.x - 6 * ln0;   // lanes 60-63 idle
-#pragma unroll
-            for (int sl = 0; sl < 3; ++sl) {
-                if (live) {
-#pragma unroll
-                    for (int k = 0; k < 12; ++k) stg[threadIdx.x][k] = info[12 * sl + k];
-                }
-                __syncthreads();
-#pragma unroll
-                for (int g = 0; g < 7; ++g) {
-                    const int ln = 10 * g + ln0;
-                    if (ln0 < 10 && ln < cnt) {
-                        const size_t qq = lb + mls[m0 + ln];
-                        reinterpret_cast<double2*>(L.invcov + 36 * qq + 12 * sl)[pc] =
-                            make_double2(stg[ln][2 * pc], stg[ln][2 * pc + 1]);
-                    }
-                }
-                __syncthreads();
-            }
-        }
-#endif
         if (live && !(fabs(r0) < 0.0001 && fabs(r1) < 0.0001)) {
             double sP[3] = {d.sP[0], d.sP[1], d.sP[2]}, eP[3] = {d.eP[0], d.eP[1], d.eP[2]};
             if (fabs(r0) > 0.0001) {
