@@ -240,7 +240,7 @@ def test_pose_only_noise_free_parity():
 
 def test_stress_config_parity():
     """BASELINE configs[4]: 1920x1080 stereo, 8000 ORB + 2000 LBD per side, line cut on."""
-    rep = _run_sequence("stress", {}, n_seq=2, n_frames=5, kp_cap=8192, kl_cap=2048,
+    rep = _run_sequence("stress", {}, n_seq=3, n_frames=8, kp_cap=8192, kl_cap=2048,
                         synth_over=dict(n_kp=8000, n_kl=2000, n_world_pts=10400, n_world_lines=2800,
                                         z_max=12.0), seed=19)
     _check(rep)
