@@ -220,6 +220,9 @@ __device__ int hist_rank_c(const int* h, int r) {
 #ifndef GFPL_CL_WAVES
 #define GFPL_CL_WAVES 1
 #endif
+#ifndef GFPL_CL_PRIO
+#define GFPL_CL_PRIO 1
+#endif
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -243,6 +246,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         const size_t pb = (size_t)b * cap;
         const uint8_t* DP = P.desc + pb * 32;
         const uint8_t* DC = Cc.desc + pb * 32;
+#if GFPL_CL_PRIO
+        __builtin_amdgcn_s_setprio(3);   // issue priority by phase: the last-dispatched workgroups keep up
+#endif
         knn_stage_soa(tb, cap, DC, Sc);
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = -1;   // 21 keys (atomicMin)
@@ -252,6 +258,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         // 21 (curr queries against prev trains, best index only) from the same distance tiles
         knn2_mfma<1, true, true>(tb, cap, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112, lut, (uint32_t*)i21);
         __syncthreads();
+#if GFPL_CL_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
         for (int i = tid; i < Sl; i += blockDim.x) {
             const uint32_t k0 = (uint32_t)i12[i], k1 = (uint32_t)d112[i];
             const int d0 = (int)(k0 >> 16), d1 = (int)(k1 >> 16);

@@ -801,6 +801,14 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
 }
 
 // ------------------------------------------------------- stereo lines --
+#ifndef GFPL_SL_PRIO
+#define GFPL_SL_PRIO 1
+#endif
+#if GFPL_SL_PRIO
+#define SL_PRIO(k) __builtin_amdgcn_s_setprio(k)
+#else
+#define SL_PRIO(k) do { } while (0)
+#endif
 struct LineOut {
     double spl[2], epl[2], sdisp, edisp, sP[3], eP[3], le[3], angle;
     int level;
@@ -926,6 +934,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     }
     const uint8_t* DLg = p.in.ldesc_l + (size_t)b * cap * 32;
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
+    SL_PRIO(3);   // issue priority by phase (as k_stereo_points: the last-dispatched workgroups keep up)
     knn_stage_soa(tb, cap, DRg, NR);
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = -1;   // R->L keys (atomicMin)
@@ -935,6 +944,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     // (only its best index is used) from the same distance tiles (RL)
     knn2_mfma<CELL, true, true>(tb, cap, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1, lut, (uint32_t*)rl_i);
     __syncthreads();
+    SL_PRIO(1);
     for (int i = tid; i < NL; i += blockDim.x) {
         const uint32_t k0 = (uint32_t)lr_i[i], k1 = (uint32_t)lr_d1[i];
         const int d0 = (int)(k0 >> 16), d1 = (int)(k1 >> 16);
