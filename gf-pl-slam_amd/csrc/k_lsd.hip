@@ -588,9 +588,6 @@ __device__ void wave_sort(uint64_t* a, int n, int* Lp, int* Rp, SortLdsPair<CAP>
 #ifndef LSD_SORT_CAP
 #define LSD_SORT_CAP 1024    // 2 waves x ~17 KB + the queue: four images' workgroups per CU
 #endif
-#ifndef LSD_SORT_T3
-#define LSD_SORT_T3 1000000  // batches above T3 images per CU sort with CAP / 4 (experiment; off)
-#endif
 #define LSD_QCAP 192         // shared queue entries (a full queue spills to the wave's own stack)
 // __unguarded_partition_pivot(a + f, a + l) of a range in HBM by one wave, as Hoare's two scans
 // in rounds of up to BT stopper pairs: the left scan gathers the next BT left stoppers (key <=
@@ -974,8 +971,8 @@ __global__ void __launch_bounds__(256) k_lsd_keys(LsdDev o, const uint8_t* image
 // CAP: LSD_SORT_CAP (36.5 KB per workgroup, four images per CU) for batches up to four images per
 // CU; half of it (24 KB, six per CU) for larger batches, whose images would otherwise run in two
 // rounds of four per CU (the ranges between the capacities partition in HBM instead of LDS)
-template <int CAP, int WPE = LSD_SORT_WAVES>
-__global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(WPE))) k_lsd_sort(LsdDev o) {
+template <int CAP>
+__global__ void __launch_bounds__(64 * LSD_SORT_WAVES) __attribute__((amdgpu_waves_per_eu(LSD_SORT_WAVES))) k_lsd_sort(LsdDev o) {
     __shared__ SortLdsMW<CAP, LSD_SORT_WAVES> S;
     const size_t img = blockIdx.x;
     // B0 as lsd_image computes it (the bins of k_lsd_keys)
@@ -1727,12 +1724,13 @@ extern "C" int gfpl_lsd_detect_async(gfpl_lsd* o, const uint8_t* images, int n, 
     hipLaunchKernelGGL(k_lsd_grad, dim3((d.W + 63) / 64, (d.H + LSD_GRAD_ROWS - 1) / LSD_GRAD_ROWS, n), dim3(256), 0, s,
                        d, images);
     hipLaunchKernelGGL(k_lsd_keys, dim3((d.W - 1 + 63) / 64, (d.H - 1 + 3) / 4, n), dim3(256), 0, s, d, images);
+    // (a third tier, CAP / 4 at 128 VGPRs so eight images share a CU, measured 56.9k vs 64.8k
+    // images/s at 3072: its 12 VGPR spills and the smaller LDS ranges cost more than the
+    // residency gained; profiles/r04_y)
     if (n <= 4 * o->n_cu)
         hipLaunchKernelGGL((k_lsd_sort<LSD_SORT_CAP>), dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
-    else if (n <= LSD_SORT_T3 * o->n_cu)
+    else
         hipLaunchKernelGGL((k_lsd_sort<LSD_SORT_CAP / 2>), dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
-    else   // (CAP / 4, 18 KB: eight images per CU at 128 VGPRs)
-        hipLaunchKernelGGL((k_lsd_sort<LSD_SORT_CAP / 4, 4>), dim3(n), dim3(64 * LSD_SORT_WAVES), 0, s, d);
     hipLaunchKernelGGL(k_lsd_grow_glb, dim3(n), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_lsd_grow_lds, dim3(n), dim3(64), o->lds_bytes, s, d);
     hipLaunchKernelGGL(k_lsd_keylines, dim3(n), dim3(64), 0, s, d, keylines, n_kl, response);
