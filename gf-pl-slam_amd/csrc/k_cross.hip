@@ -58,6 +58,9 @@ __global__ void __launch_bounds__(64) k_predict_pose(KParams p) {
 #ifndef GFPL_CP_WAVES
 #define GFPL_CP_WAVES 8   // 2 workgroups / CU (84-B spill; 3.2 -> 2.6 ms measured)
 #endif
+#ifndef GFPL_CP_PRIO
+#define GFPL_CP_PRIO 1    // issue priority by phase (projection 3, matching 1)
+#endif
 __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p, CrossGrid G) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
@@ -86,6 +89,9 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
         const DevPoints& Cc = p.curr.pt;
         const size_t pb = (size_t)b * cap;
         double* proj = p.scr.proj + pb * 2;   // exact projections (L2-resident)
+#if GFPL_CP_PRIO
+        __builtin_amdgcn_s_setprio(3);
+#endif
         // 1. projectPrev3DPoint (src/stereoFrame.cpp:1550-1570) + bucket histogram
         for (int q = tid; q < Sp; q += blockDim.x) {
             double v[4] = {P.P[3 * (pb + q)], P.P[3 * (pb + q) + 1], P.P[3 * (pb + q) + 2], 1.0};
@@ -133,6 +139,9 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
         const float radius = (float)p.cfg.point_match_radius;
         const int cap_m = p.cfg.max_point_match_num;
         const uint8_t* PD = P.desc + pb * 32;
+#if GFPL_CP_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
         int off = 0;
         for (int c0 = 0; c0 < Sc; c0 += blockDim.x) {
             const int t = c0 + tid;

@@ -7,4 +7,4 @@ mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 \
   || { grep -E "passed|failed|Error" $O/pytest.log | tail -5; exit 1; }
 grep -E "passed|failed" $O/pytest.log | tail -1
-bash tools/ab_bench.sh $O 20 default build/ab_noslcl default build/ab_noslcl
+bash tools/ab_bench.sh $O 20 default build/ab_noslcl build/ab_nocp default build/ab_noslcl build/ab_nocp
