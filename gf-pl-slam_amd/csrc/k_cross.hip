@@ -58,9 +58,6 @@ __global__ void __launch_bounds__(64) k_predict_pose(KParams p) {
 #ifndef GFPL_CP_WAVES
 #define GFPL_CP_WAVES 8   // 2 workgroups / CU (84-B spill; 3.2 -> 2.6 ms measured)
 #endif
-#ifndef GFPL_CP_PRIO
-#define GFPL_CP_PRIO 1    // issue priority by phase (projection 3, matching 1)
-#endif
 __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p, CrossGrid G) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
@@ -89,9 +86,6 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
         const DevPoints& Cc = p.curr.pt;
         const size_t pb = (size_t)b * cap;
         double* proj = p.scr.proj + pb * 2;   // exact projections (L2-resident)
-#if GFPL_CP_PRIO
-        __builtin_amdgcn_s_setprio(3);
-#endif
         // 1. projectPrev3DPoint (src/stereoFrame.cpp:1550-1570) + bucket histogram
         for (int q = tid; q < Sp; q += blockDim.x) {
             double v[4] = {P.P[3 * (pb + q)], P.P[3 * (pb + q) + 1], P.P[3 * (pb + q) + 2], 1.0};
@@ -139,9 +133,6 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
         const float radius = (float)p.cfg.point_match_radius;
         const int cap_m = p.cfg.max_point_match_num;
         const uint8_t* PD = P.desc + pb * 32;
-#if GFPL_CP_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
         int off = 0;
         for (int c0 = 0; c0 < Sc; c0 += blockDim.x) {
             const int t = c0 + tid;
@@ -229,9 +220,6 @@ __device__ int hist_rank_c(const int* h, int r) {
 #ifndef GFPL_CL_WAVES
 #define GFPL_CL_WAVES 1
 #endif
-#ifndef GFPL_CL_PRIO
-#define GFPL_CL_PRIO 1
-#endif
 template <int BLOCK>
 __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -255,9 +243,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         const size_t pb = (size_t)b * cap;
         const uint8_t* DP = P.desc + pb * 32;
         const uint8_t* DC = Cc.desc + pb * 32;
-#if GFPL_CL_PRIO
-        __builtin_amdgcn_s_setprio(3);   // issue priority by phase: the last-dispatched workgroups keep up
-#endif
         knn_stage_soa(tb, cap, DC, Sc);
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = -1;   // 21 keys (atomicMin)
@@ -267,9 +252,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         // 21 (curr queries against prev trains, best index only) from the same distance tiles
         knn2_mfma<1, true, true>(tb, cap, Sc, DP, Sl, (uint32_t*)i12, (uint32_t*)d112, lut, (uint32_t*)i21);
         __syncthreads();
-#if GFPL_CL_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
         for (int i = tid; i < Sl; i += blockDim.x) {
             const uint32_t k0 = (uint32_t)i12[i], k1 = (uint32_t)d112[i];
             const int d0 = (int)(k0 >> 16), d1 = (int)(k1 >> 16);
