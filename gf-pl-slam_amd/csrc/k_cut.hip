@@ -983,6 +983,12 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
 #ifndef GFPL_CUT_FAIR
 #define GFPL_CUT_FAIR 2
 #endif
+// proven mode: 16-B pieces per lane of the next line's record prefetched into LDS (3: its first
+// 48 doubles, 3 KB per wave — with the v'-tables a fourth piece passes the 20 KB that keeps 8
+// waves per CU; 1: none, the record is read from HBM when the line opens)
+#ifndef CUT_PF_PROOF
+#define CUT_PF_PROOF 3
+#endif
 __device__ __forceinline__ int wave_sum8(int v) {   // sum over the wave's 8 groups of lane 8g's value
     v += __shfl_xor(v, 8);
     v += __shfl_xor(v, 16);
@@ -1020,7 +1026,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // nxl[k][16 g + ...] (the DMA writes base + 16 * lane)
     // (proven mode: no prefetch buffer — its v'-tables take the LDS, and 5 KB more would cost the
     // eighth wave of a CU; the record is read from HBM when the line opens)
-    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? 1 : 5][128];
+    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? CUT_PF_PROOF : 5][128];
     // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
     //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
     //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
@@ -1200,10 +1206,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
     auto pf_issue = [&](int mm) {
-        if (PROOF) return;
+        if (PROOF && CUT_PF_PROOF < 2) return;
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
+        for (int k = 0; k < (PROOF ? CUT_PF_PROOF : 5); ++k)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
                                              (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
     };
@@ -1365,7 +1371,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
-                if (PROOF) {
+                if (PROOF && CUT_PF_PROOF < 2) {
 #pragma unroll
                     for (int k = 0; k < CUT_FAST / 8; ++k) fst[g][j + 8 * k] = rec_l[(size_t)m * CUT_REC + j + 8 * k];
                 } else {
@@ -1373,7 +1379,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
                     for (int k = 0; k < CUT_FAST / 8; ++k) {
                         const int e = j + 8 * k;
-                        fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
+                        // (proven mode: the entries past the prefetched pieces from HBM)
+                        fst[g][e] = (PROOF && e >= 16 * CUT_PF_PROOF) ? rec_l[(size_t)m * CUT_REC + e]
+                                                                       : nxl[e >> 4][16 * g + (e & 15)];
                     }
                 }
             }
@@ -1391,7 +1399,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
                     if (e < 21) {
                         const double mid = sumA[g][e] + info[kk];
-                        const double nw = mid - (PROOF ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
+                        const double nw = mid - ((PROOF && (CUT_PF_PROOF < 2 || x >= 16 * CUT_PF_PROOF))
+                                                 ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
                         sumA[g][e] = nw;
                         if (PROOF) sumE[g][e] = mid;   // the exact invCov_sum, kept current (m_sync = m)
                     }
