@@ -348,21 +348,13 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                     }
                 }
                 __syncthreads();
-                // four LDS reads in flight before their stores (a guarded read per store
-                // serialised 40 LDS round trips per chunk); rows past cnt are read, not stored
+                // (reading four slices ahead of their stores measured the same: profiles/r04_aa)
 #pragma unroll
-                for (int g4 = 0; g4 < 8; g4 += 4) {
-                    double2 v[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ln = 8 * (g4 + u) + pl;
-                        v[u] = make_double2(stg[ln * 17 + 2 * pp], stg[ln * 17 + 2 * pp + 1]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ln = 8 * (g4 + u) + pl;
-                        if (ln < cnt) reinterpret_cast<double2*>(rc + (size_t)ln * CUT_REC + 16 * sl)[pp] = v[u];
-                    }
+                for (int g8 = 0; g8 < 8; ++g8) {
+                    const int ln = 8 * g8 + pl;
+                    if (ln < cnt)
+                        reinterpret_cast<double2*>(rc + (size_t)ln * CUT_REC + 16 * sl)[pp] =
+                            make_double2(stg[ln * 17 + 2 * pp], stg[ln * 17 + 2 * pp + 1]);
                 }
                 __syncthreads();
             }
