@@ -975,11 +975,12 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
 #ifndef GFPL_CUT_FAIR
 #define GFPL_CUT_FAIR 2
 #endif
-// proven mode: 16-B pieces per lane of the next line's record prefetched into LDS (3: its first
-// 48 doubles, 3 KB per wave — with the v'-tables a fourth piece passes the 20 KB that keeps 8
-// waves per CU; 1: none, the record is read from HBM when the line opens)
+// proven mode: 16-B pieces per lane of the next line's record prefetched into LDS (1: none, the
+// record is read from HBM when the line opens; 3: its first 48 doubles, 3 KB per wave — with the
+// v'-tables a fourth piece passes the 20 KB that keeps 8 waves per CU — measured 10.32 vs 10.25 ms,
+// profiles/r04_ab: the proven transitions are bound by their exact endpoint work, not this read)
 #ifndef CUT_PF_PROOF
-#define CUT_PF_PROOF 3
+#define CUT_PF_PROOF 1
 #endif
 __device__ __forceinline__ int wave_sum8(int v) {   // sum over the wave's 8 groups of lane 8g's value
     v += __shfl_xor(v, 8);
