@@ -298,17 +298,24 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         __syncthreads();
         constexpr int RMAX = 2048 / BLOCK;   // kp_cap <= 2048 on this layout
         uint32_t rk[RMAX], rbr[RMAX], lbr[RMAX];
+        float rx[RMAX];      // the record fields, kept from this pass (no second read of KR)
+        uint32_t rm[RMAX];
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) {
             const int i = tid + r * BLOCK;
             rk[r] = 0xFFFFFFFFu;
             rbr[r] = 0u;
             lbr[r] = 0u;
+            rx[r] = 0.0f;
+            rm[r] = 0u;
             if (i < Nr) {
                 const gfpl_keypoint kp = KR[i];
                 const float rr = 2.0f * p.cam.scale[clamp_level(kp.octave, nlev)];
                 const int maxr = (int)ceilf(kp.y + rr);
                 const int minr = (int)floorf(kp.y - rr);
+                const int oc = (kp.octave >= -127 && kp.octave <= 127) ? kp.octave : -128;
+                rx[r] = kp.x;
+                rm[r] = ((uint32_t)(maxr - minr) << 8) | ((uint32_t)oc & 0xFFu);
                 const int seg = (kp.octave >= 0 && kp.octave < nlev) ? kp.octave : nlev;
                 // rows are < 2048 (GFPL_MAX_IMAGE_DIM): the key keeps minr clamped to [-1024, 3071]
                 const int mc = min(max(minr, -1024), 3071);
@@ -332,22 +339,20 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         // exclusive scans of both histograms in place (u16 offsets), block-wide
         uint16_t* offr = rowlo;
         uint16_t* offl = reinterpret_cast<uint16_t*>(hl);
-        {
-            const int per = (nbr + BLOCK - 1) / BLOCK, b0 = min(tid * per, nbr), b1 = min(b0 + per, nbr);
-            int sum = 0;
-            for (int x = b0; x < b1; ++x) sum += offr[x];
+        {   // one block scan for both: the right sums in the low, the left in the high 16 bits
+            // (each total is at most kp_cap <= 2048, so the halves never carry into each other)
+            const int pr = (nbr + BLOCK - 1) / BLOCK, r0 = min(tid * pr, nbr), r1 = min(r0 + pr, nbr);
+            const int pq = (nbl + BLOCK - 1) / BLOCK, l0 = min(tid * pq, nbl), l1 = min(l0 + pq, nbl);
+            int sr = 0, sl = 0;
+            for (int x = r0; x < r1; ++x) sr += offr[x];
+            for (int x = l0; x < l1; ++x) sl += offl[x];
             int tot;
-            int run = block_exclusive_scan<BLOCK>(sum, misc + 4, &tot);
-            for (int x = b0; x < b1; ++x) { const int c = offr[x]; offr[x] = (uint16_t)run; run += c; }
-            if (tid == 0) offr[nbr] = (uint16_t)tot;
-        }
-        {
-            const int per = (nbl + BLOCK - 1) / BLOCK, b0 = min(tid * per, nbl), b1 = min(b0 + per, nbl);
-            int sum = 0;
-            for (int x = b0; x < b1; ++x) sum += offl[x];
-            int tot;
-            int run = block_exclusive_scan<BLOCK>(sum, misc + 4, &tot);
-            for (int x = b0; x < b1; ++x) { const int c = offl[x]; offl[x] = (uint16_t)run; run += c; }
+            const int run2 = block_exclusive_scan<BLOCK>(sr | (sl << 16), misc + 4, &tot);
+            int run = run2 & 0xFFFF;
+            for (int x = r0; x < r1; ++x) { const int c = offr[x]; offr[x] = (uint16_t)run; run += c; }
+            run = run2 >> 16;
+            for (int x = l0; x < l1; ++x) { const int c = offl[x]; offl[x] = (uint16_t)run; run += c; }
+            if (tid == 0) offr[nbr] = (uint16_t)(tot & 0xFFFF);
         }
         __syncthreads();
         // scatter: keys with their x, band height maxr - minr and octave (int8; -128 = out
@@ -357,13 +362,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             const int i = tid + r * BLOCK;
             if (i < Nr) {
                 const int j = (int)offr[rbr[r] & 0xFFFFu] + (int)(rbr[r] >> 16);
-                const gfpl_keypoint kp = KR[i];
-                const float rr = 2.0f * p.cam.scale[clamp_level(kp.octave, nlev)];
-                const int band = (int)ceilf(kp.y + rr) - (int)floorf(kp.y - rr);
-                const int oc = (kp.octave >= -127 && kp.octave <= 127) ? kp.octave : -128;
                 rkey[j] = rk[r];
-                recx[j] = kp.x;
-                recm[j] = (uint16_t)(((uint32_t)band << 8) | ((uint32_t)oc & 0xFFu));
+                recx[j] = rx[r];
+                recm[j] = (uint16_t)rm[r];
             }
             if (i < N) order[(int)offl[lbr[r] & 0xFFFFu] + (int)(lbr[r] >> 16)] = (uint32_t)i;
         }
