@@ -829,17 +829,20 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
     L.cut = cut;
     // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at their final
     //    ratios), eight lines per round: lane j computes the reference-order info of line
-    //    m_sync + j at its final ratios (stored by lane 0 at the line's finalisation; read
-    //    past the L1), lanes 0-6 add them into sumE in list order, seven entries per pass
+    //    m_sync + j at its final ratios (stored by lane 0 of the same wave at the line's
+    //    finalisation), lanes 0-6 add them into sumE in list order, seven entries per pass.
+    //    Writer and readers are one wave, so a workgroup-scope fence orders them: the device-scope
+    //    __threadfence this used wrote back the XCD's L2 (buffer_wbl2) at every round of eight
+    //    lines, and the waves with an exact step ran 0.1-0.7 ms longer (profiles/r04_s records)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     while (__any(exact && m_sync < m)) {
         const bool fl = exact && m_sync < m;
         const int nl = fl ? min(8, m - m_sync) : 0;
-        __threadfence();
         double info[21];
         if (j < nl) {
             const size_t qf = lb + mls[m_sync + j];
-            const double c0 = __hip_atomic_load(&L.cut[2 * qf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double c1 = __hip_atomic_load(&L.cut[2 * qf + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double c0 = __hip_atomic_load(&L.cut[2 * qf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const double c1 = __hip_atomic_load(&L.cut[2 * qf + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             double s7[7], e7[7];
             exact_endpoint(cam, homog, Dl, L, qf, 0, c0, s7);
             exact_endpoint(cam, homog, Dl, L, qf, 1, c1, e7);
