@@ -810,13 +810,21 @@ struct CutX {
     int best;     // the reference's decision for groups that took the exact step (else unchanged)
     int m_sync;   // sumE now holds the exact invCov_sum before line m_sync (= m for those groups)
 };
+template <typename T>
+__device__ __forceinline__ T* rl_ptr(T* p, int l) {   // lane l's pointer, wave-uniform
+    const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
 __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid, int first, int m, int m_sync, double r0,
                                                           double r1, size_t q_cur, size_t lb, int best,
                                                           const int32_t* mls, const double* rec_l, double* sP, double* eP,
                                                           double* covS, double* covE, double* le_obs, double* cut,
-                                                          double* sumE, double* tmp, const double* Dl, double fx, double cb,
-                                                          double homog, double st) {
+                                                          double* sumE, double* tmp, double* tmpw, const double* Dl,
+                                                          double fx, double cb, double homog, double st) {
     const int j = threadIdx.x & 7;
+    const int lane = threadIdx.x & 63;
     DevCam cam{};
     cam.fx = fx;
     cam.b = cb;
@@ -828,43 +836,64 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
     L.le_obs = le_obs;
     L.cut = cut;
     // 1. the exact invCov_sum is brought up to line m (lines m_sync .. m-1 at their final
-    //    ratios), eight lines per round: lane j computes the reference-order info of line
-    //    m_sync + j at its final ratios (stored by lane 0 of the same wave at the line's
-    //    finalisation), lanes 0-6 add them into sumE in list order, seven entries per pass.
-    //    Writer and readers are one wave, so a workgroup-scope fence orders them: the device-scope
-    //    __threadfence this used wrote back the XCD's L2 (buffer_wbl2) at every round of eight
-    //    lines, and the waves with an exact step ran 0.1-0.7 ms longer (profiles/r04_s records)
+    //    ratios, stored by lane 0 of the group at each line's finalisation).  The whole wave
+    //    serves one group at a time: lane l computes the reference-order info of line
+    //    m_sync + l (64 lines per round; eight per round with the group's own lanes made an
+    //    exact step cost ~130 us, profiles/r04_ad records), the infos and the lines' r = 0
+    //    infos go through the wave's X scratch (idle outside exact rounds and line opens), and
+    //    the group's lanes 0-3 add them into sumE in list order, four entries per pass.
+    //    Writer and readers are one wave, so a workgroup-scope fence orders them (the
+    //    device-scope __threadfence used before wrote back the XCD's L2 every round).
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    while (__any(exact && m_sync < m)) {
-        const bool fl = exact && m_sync < m;
-        const int nl = fl ? min(8, m - m_sync) : 0;
-        double info[21];
-        if (j < nl) {
-            const size_t qf = lb + mls[m_sync + j];
-            const double c0 = __hip_atomic_load(&L.cut[2 * qf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const double c1 = __hip_atomic_load(&L.cut[2 * qf + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            double s7[7], e7[7];
-            exact_endpoint(cam, homog, Dl, L, qf, 0, c0, s7);
-            exact_endpoint(cam, homog, Dl, L, qf, 1, c1, e7);
-            cut_assemble<false>(s7, e7, info);
-        }
+    {
+        unsigned long long need = __ballot(j == 0 && exact && m_sync < m);
+        while (need) {   // (wave-uniform)
+            const int gl = __ffsll((long long)need) - 1;   // lane 8 G of the group served
+            need &= need - 1;
+            const int ms = __builtin_amdgcn_readlane(m_sync, gl), me = __builtin_amdgcn_readlane(m, gl);
+            const size_t lbG = (size_t)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)lb, gl) |
+                               ((size_t)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(lb >> 32), gl) << 32);
+            const int32_t* mlsG = rl_ptr(mls, gl);
+            const double* recG = rl_ptr(rec_l, gl);
+            const double* DlG = rl_ptr(Dl, gl);
+            double* sumEG = rl_ptr(sumE, gl);
+            const bool mine = (lane >> 3) == (gl >> 3);
+            for (int s0 = ms; s0 < me; s0 += 64) {
+                const int nl = min(64, me - s0);
+                double info[21];
+                if (lane < nl) {
+                    const size_t qf = lbG + mlsG[s0 + lane];
+                    const double c0 = __hip_atomic_load(&L.cut[2 * qf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const double c1 = __hip_atomic_load(&L.cut[2 * qf + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    double s7[7], e7[7];
+                    exact_endpoint(cam, homog, DlG, L, qf, 0, c0, s7);
+                    exact_endpoint(cam, homog, DlG, L, qf, 1, c1, e7);
+                    cut_assemble<false>(s7, e7, info);
+                }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            if (j < nl) {
+                for (int c = 0; c < 6; ++c) {
+                    if (lane < nl) {
 #pragma unroll
-                for (int i = 0; i < 7; ++i) tmp[7 * j + i] = info[7 * c + i];
+                        for (int i = 0; i < 4; ++i) {
+                            const int e = 4 * c + i;
+                            if (e < 21) {
+                                tmpw[4 * lane + i] = info[e];
+                                tmpw[256 + 4 * lane + i] = recG[(size_t)(s0 + lane) * CUT_REC + CUT_FAST + e];
+                            }
+                        }
+                    }
+                    wave_lds_sync();
+                    if (mine && j < 4 && 4 * c + j < 21) {
+                        const int e = 4 * c + j;
+                        double Se = sumEG[e];
+                        for (int l = 0; l < nl; ++l) Se = (Se - tmpw[256 + 4 * l + j]) + tmpw[4 * l + j];
+                        sumEG[e] = Se;
+                    }
+                    wave_lds_sync();
+                }
             }
-            wave_lds_sync();
-            if (fl && j < 7) {
-                const int e = 7 * c + j;
-                double Se = sumE[e];
-                for (int l = 0; l < nl; ++l)
-                    Se = (Se - rec_l[(size_t)(m_sync + l) * CUT_REC + CUT_FAST + e]) + tmp[7 * l + j];
-                sumE[e] = Se;
-            }
-            wave_lds_sync();
+            if (mine) m_sync = me;
         }
-        m_sync += nl;
     }
     // 2. exact endpoints of this step's six slots (lanes 0-2: start endpoint at
     //    r0 + {-s, 0, +s}, lanes 3-5: end endpoint), exact S of line m
@@ -1029,6 +1058,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     //   open: ... | diag(S^-1) [57..62]; the agreement bound's per-row partials over [0..48)
     //   transition: the finished line's error bounds (+ evaluation) [0..14)
     __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];
+    static_assert(CUT_G * (CUT_EP + 25 + 1) >= 512, "the exact-sum flush stages 64 x (4 + 4) doubles in tmp");
     __shared__ CutCmp cmpl[CUT_G];              // comparison polynomials of the current line
     // proven mode: the line's v'_ref at every ratio key (side * CUT_KS + slot; k_cut_vtab) and the
     // keys' +s / -s links (KParams::cut_keys; -1: no key — such a ratio is evaluated exactly)
@@ -1275,7 +1305,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (__any(exact)) {
             // ---- X: the reference's evaluation of this step for the groups that need it
             const CutX xr = cut_exact_round(exact, valid, first, m, m_sync, r0, r1, q_cur, lb, best, mls, rec_l, L.sP, L.eP,
-                                            L.covS, L.covE, L.le_obs, L.cut, sumE[g], tmp[g], Dl, cam.fx, cam.b, homog, st);
+                                            L.covS, L.covE, L.le_obs, L.cut, sumE[g], tmp[g], &tmp[0][0], Dl, cam.fx, cam.b,
+                                            homog, st);
             best = xr.best;
             m_sync = xr.m_sync;
             // the next centre's d and bound come from the lane that evaluated it
