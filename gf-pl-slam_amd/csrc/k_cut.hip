@@ -810,6 +810,9 @@ struct CutX {
     int best;     // the reference's decision for groups that took the exact step (else unchanged)
     int m_sync;   // sumE now holds the exact invCov_sum before line m_sync (= m for those groups)
 };
+#ifndef GFPL_FLUSH8
+#define GFPL_FLUSH8 1
+#endif
 template <typename T>
 __device__ __forceinline__ T* rl_ptr(T* p, int l) {   // lane l's pointer, wave-uniform
     const unsigned long long v = reinterpret_cast<unsigned long long>(p);
@@ -870,6 +873,27 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
                     exact_endpoint(cam, homog, DlG, L, qf, 1, c1, e7);
                     cut_assemble<false>(s7, e7, info);
                 }
+#if GFPL_FLUSH8
+                // eight entries per pass (the lines' infos in the X scratch, their r = 0 infos read
+                // from HBM in the chain)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (lane < nl) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+                            if (8 * c + i < 21) tmpw[8 * lane + i] = info[8 * c + i];
+                    }
+                    wave_lds_sync();
+                    if (mine && 8 * c + j < 21) {
+                        const int e = 8 * c + j;
+                        double Se = sumEG[e];
+                        const double* rr = recG + (size_t)s0 * CUT_REC + CUT_FAST + e;
+                        for (int l = 0; l < nl; ++l) Se = (Se - rr[(size_t)l * CUT_REC]) + tmpw[8 * l + j];
+                        sumEG[e] = Se;
+                    }
+                    wave_lds_sync();
+                }
+#else
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
                     if (lane < nl) {
@@ -891,6 +915,7 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
                     }
                     wave_lds_sync();
                 }
+#endif
             }
             if (mine) m_sync = me;
         }
