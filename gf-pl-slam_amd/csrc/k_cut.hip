@@ -810,9 +810,6 @@ struct CutX {
     int best;     // the reference's decision for groups that took the exact step (else unchanged)
     int m_sync;   // sumE now holds the exact invCov_sum before line m_sync (= m for those groups)
 };
-#ifndef GFPL_FLUSH8
-#define GFPL_FLUSH8 1
-#endif
 template <typename T>
 __device__ __forceinline__ T* rl_ptr(T* p, int l) {   // lane l's pointer, wave-uniform
     const unsigned long long v = reinterpret_cast<unsigned long long>(p);
@@ -844,7 +841,9 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
     //    m_sync + l (64 lines per round; eight per round with the group's own lanes made an
     //    exact step cost ~130 us, profiles/r04_ad records), the infos and the lines' r = 0
     //    infos go through the wave's X scratch (idle outside exact rounds and line opens), and
-    //    the group's lanes 0-3 add them into sumE in list order, four entries per pass.
+    //    the group's lanes 0-3 add them into sumE in list order, four entries per pass (eight
+    //    per pass with the r = 0 infos read from HBM in the chain measured slower, 5.68 vs 5.57 ms;
+    //    profiles/r04_af).
     //    Writer and readers are one wave, so a workgroup-scope fence orders them (the
     //    device-scope __threadfence used before wrote back the XCD's L2 every round).
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -873,27 +872,6 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
                     exact_endpoint(cam, homog, DlG, L, qf, 1, c1, e7);
                     cut_assemble<false>(s7, e7, info);
                 }
-#if GFPL_FLUSH8
-                // eight entries per pass (the lines' infos in the X scratch, their r = 0 infos read
-                // from HBM in the chain)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    if (lane < nl) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i)
-                            if (8 * c + i < 21) tmpw[8 * lane + i] = info[8 * c + i];
-                    }
-                    wave_lds_sync();
-                    if (mine && 8 * c + j < 21) {
-                        const int e = 8 * c + j;
-                        double Se = sumEG[e];
-                        const double* rr = recG + (size_t)s0 * CUT_REC + CUT_FAST + e;
-                        for (int l = 0; l < nl; ++l) Se = (Se - rr[(size_t)l * CUT_REC]) + tmpw[8 * l + j];
-                        sumEG[e] = Se;
-                    }
-                    wave_lds_sync();
-                }
-#else
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
                     if (lane < nl) {
@@ -915,7 +893,6 @@ __device__ __attribute__((noinline)) CutX cut_exact_round(bool exact, int valid,
                     }
                     wave_lds_sync();
                 }
-#endif
             }
             if (mine) m_sync = me;
         }
