@@ -109,6 +109,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-sweep-seconds", type=float, default=2.5,
+                    help="timed seconds per point of the CPU baseline's 1/2/4/8 thread sweep (0: no sweep)")
     ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
     ap.add_argument("--dump-records", default=None,
                     help="save every sequence's record of the last timed step (gfpl_debug_step_records, .npy) "
@@ -352,6 +354,23 @@ def cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, n_threads, target_s, cores_info, 
                       f"sequence per host thread ({timed:.1f} s timed; oracle/ C++ -O3 restatement; input "
                       f"generation and initialisation excluded)",
             "host": cores_info}
+
+
+def cpu_thread_sweep(cam, cfg, sp, kp_cap, kl_cap, n_threads, seconds, gen_threads, n_frames, full, b1_ms):
+    """The CPU baseline at 1, 2, 4, 8 threads (and the full count from `full`), a few seconds of
+    timed work each: per-thread ms/frame shows whether the n-thread rate is n x the 1-thread rate
+    (efficiency) or loses to a shared resource (cgroup quota, memory, frequency)."""
+    pts = {}
+    for t in sorted({t for t in (1, 2, 4, 8) if t < n_threads}):
+        r = cpu_baseline(cam, cfg, sp, kp_cap, kl_cap, t, seconds, None, gen_threads, n_frames)
+        pts[str(t)] = r["value"]
+    pts[str(n_threads)] = full["value"]
+    one = pts["1"] if "1" in pts else full["value"] / n_threads
+    return {"frames_per_s": {k: round(v, 1) for k, v in pts.items()},
+            "ms_per_frame_per_thread": {k: round(1e3 * int(k) / v, 2) for k, v in pts.items()},
+            "efficiency_vs_1thread": {k: round(v / (int(k) * one), 3) for k, v in pts.items()},
+            "b1_leg_cpu_1thread_ms_per_frame": b1_ms,
+            "note": f"{seconds:.1f} s timed per point; same frames and workload as the baseline"}
 
 
 def latency_b1(ctx, cam, cfg, sp, kp_cap, kl_cap, seq, warmup, steps):
@@ -843,6 +862,10 @@ def main():
         if world == 1 and not args.no_cpu:
             nt = args.cpu_threads or cores
             cpu = cpu_baseline(cam, cfg, sp, KP, KL, nt, args.cpu_seconds, cores_info, gen_threads, W + K)
+            if args.cpu_sweep_seconds > 0:
+                cpu["thread_sweep"] = cpu_thread_sweep(cam, cfg, sp, KP, KL, nt, args.cpu_sweep_seconds,
+                                                       gen_threads, W + K, cpu,
+                                                       b1.get("cpu_1thread_ms_per_frame") if b1 else None)
         det = None
         if world == 1 and not args.no_detect:
             up_Bps = host_fed["upload_GBps"] * 1e9 if host_fed and host_fed.get("upload_GBps") else 0.0

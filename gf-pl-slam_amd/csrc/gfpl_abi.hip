@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -25,7 +28,10 @@ struct gfpl_ctx {
     hipEvent_t ev[GFPL_NEV]{};
     float stage_ms[7]{};
     std::vector<gfpl_seqbatch*> sbs;   // live seqbatches: their match-list capacities bound gfpl_set_config
-    int n_detectors = 0;   // live ORB / LBD / LSD objects: they hold the context's stream (and ORB its camera)
+    // live ORB / LBD / LSD / detector objects: they hold the context's stream and camera; they may be
+    // created and destroyed from different host threads
+    std::atomic<int> n_detectors{0};
+    std::mutex host_mu;   // the host-buffer matchers (gfpl_*_host): one call at a time per context
 };
 
 struct gfpl_seqbatch {
@@ -66,8 +72,8 @@ int gfpl_ctx_device(const gfpl_ctx* c) { return c->device; }
 void* gfpl_ctx_stream(const gfpl_ctx* c) { return (void*)c->stream; }
 const gfpl_camera* gfpl_ctx_camera(const gfpl_ctx* c) { return c->has_cam ? &c->cam : nullptr; }
 int64_t gfpl_event_records(const gfpl_event* e) { return e->records; }
-void gfpl_ctx_attach(gfpl_ctx* c) { ++c->n_detectors; }
-void gfpl_ctx_detach(gfpl_ctx* c) { --c->n_detectors; }
+void gfpl_ctx_attach(gfpl_ctx* c) { c->n_detectors.fetch_add(1); }
+void gfpl_ctx_detach(gfpl_ctx* c) { c->n_detectors.fetch_sub(1); }
 
 
 namespace {
@@ -260,6 +266,12 @@ int cfg_supported(const gfpl_config& c) {
     // the certified cut search needs a margin far above its ~1e-13 error
     if (!(c.cut_certify == 0.0 || (c.cut_certify >= 1e-10 && c.cut_certify < 1.0))) return GFPL_E_INVALID;
     if (c.cut_proof != 0 && c.cut_proof != 1) return GFPL_E_INVALID;
+    // the search's ratio keys and their +-s links are formed from a positive finite step
+    // (params(): with s <= 0 or NaN no key would exist and the proven search would follow
+    // zeroed links); the range must be an ordered finite interval
+    if (!(std::isfinite(c.cut_step) && c.cut_step > 0.0)) return GFPL_E_INVALID;
+    if (!(std::isfinite(c.cut_rng[0]) && std::isfinite(c.cut_rng[1]) && c.cut_rng[0] <= c.cut_rng[1]))
+        return GFPL_E_INVALID;
     return GFPL_OK;
 }
 
@@ -305,7 +317,7 @@ int gfpl_create_async(int device, gfpl_ctx** out) {
 int gfpl_destroy(gfpl_ctx* c) {
     if (!c) return GFPL_E_INVALID;
     if (!c->sbs.empty()) return GFPL_E_STATE;   // its seqbatches use the context's stream and config
-    if (c->n_detectors != 0) return GFPL_E_STATE;   // so do its ORB / LBD / LSD objects
+    if (c->n_detectors.load() != 0) return GFPL_E_STATE;   // so do its ORB / LBD / LSD objects
     for (int i = 0; i < GFPL_NEV; ++i)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->own_stream) {
@@ -370,6 +382,9 @@ int gfpl_event_synchronize(gfpl_event* e) {
 
 int gfpl_set_camera(gfpl_ctx* c, const gfpl_camera* cam) {
     if (!c || !cam || cam->n_levels < 1 || cam->n_levels > GFPL_MAX_LEVELS) return GFPL_E_INVALID;
+    // seqbatches (their device pyramid builder) and detectors (ORB / LSD geometry) are laid out
+    // for the camera they were created on
+    if (!c->sbs.empty() || c->n_detectors.load() != 0) return GFPL_E_STATE;
     int64_t need = 0;
     for (int i = 0; i < cam->n_levels; ++i) {
         if (cam->lvl_cols[i] < 1 || cam->lvl_rows[i] < 1 || cam->lvl_offset[i] < 0) return GFPL_E_INVALID;
@@ -789,6 +804,114 @@ int gfpl_knn2_hamming(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, i
     if (nt < 2) return GFPL_E_TOO_FEW_TRAIN;
     if (nq == 0) return GFPL_OK;
     HIPCHK(launch_knn2(q, nq, t, nt, cell, idx, dist, c->stream));
+    return GFPL_OK;
+}
+
+// ------------------------------------------------- host-facing matchers --
+// StereoFrame's matcher members as MapHandler calls them: host buffers in and out, one device
+// scratch per call (keyframe rate), serialised per context (two std::async tasks share it).
+namespace {
+struct Scratch {
+    char* p = nullptr;
+    ~Scratch() { if (p) (void)hipFree(p); }
+};
+}  // namespace
+
+int gfpl_knn2_hamming_host(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* idx,
+                           float* dist) {
+    if (!c || !q || !t || !idx || !dist || nq < 0 || (cell != 1 && cell != 2)) return GFPL_E_INVALID;
+    if (nt < 2) return GFPL_E_TOO_FEW_TRAIN;
+    if (nq == 0) return GFPL_OK;
+    std::lock_guard<std::mutex> lk(c->host_mu);
+    HIPCHK(hipSetDevice(c->device));
+    const size_t bq = 32 * (size_t)nq, bt = 32 * (size_t)nt, bo = 2 * (size_t)nq * 4;
+    Scratch s;
+    HIPCHK(hipMalloc(&s.p, bq + bt + 2 * bo + 64));
+    uint8_t* dq = reinterpret_cast<uint8_t*>(s.p);
+    uint8_t* dt = dq + bq;
+    int32_t* di = reinterpret_cast<int32_t*>(dt + bt);
+    float* dd = reinterpret_cast<float*>(di + 2 * (size_t)nq);
+    HIPCHK(hipMemcpyAsync(dq, q, bq, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dt, t, bt, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_knn2(dq, nq, dt, nt, cell, di, dd, c->stream));
+    HIPCHK(hipMemcpyAsync(idx, di, bo, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(dist, dd, bo, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GFPL_OK;
+}
+
+int gfpl_radius_hamming(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, float max_dist,
+                        int32_t* row_off, int cap, int32_t* idx, float* dist) {
+    if (!c || (!q && nq) || (!t && nt) || !row_off || nq < 0 || nt < 0 || cap < 0 || (cell != 1 && cell != 2) ||
+        max_dist != max_dist)
+        return GFPL_E_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<int32_t> h(nq + 1, 0);
+    if (nq > 0 && nt > 0) {
+        HIPCHK(launch_radius_count(q, nq, t, nt, cell, max_dist, row_off + 1, c->stream));
+        HIPCHK(hipMemcpyAsync(h.data() + 1, row_off + 1, 4 * (size_t)nq, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    for (int i = 0; i < nq; ++i) h[i + 1] += h[i];
+    HIPCHK(hipMemcpyAsync(row_off, h.data(), 4 * (size_t)(nq + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));   // (h is pageable stack memory)
+    if (h[nq] > cap) return GFPL_E_CAPACITY;
+    if (h[nq] > 0) {
+        if (!idx || !dist) return GFPL_E_INVALID;
+        HIPCHK(launch_radius_rows(q, nq, t, nt, cell, max_dist, row_off, idx, dist, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GFPL_OK;
+}
+
+int gfpl_radius_hamming_host(gfpl_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, float max_dist,
+                             int32_t* row_off, int cap, int32_t* idx, float* dist) {
+    if (!c || (!q && nq) || (!t && nt) || !row_off || nq < 0 || nt < 0 || cap < 0 || (cell != 1 && cell != 2) ||
+        max_dist != max_dist)
+        return GFPL_E_INVALID;
+    std::lock_guard<std::mutex> lk(c->host_mu);
+    HIPCHK(hipSetDevice(c->device));
+    const size_t bq = 32 * (size_t)nq, bt = 32 * (size_t)nt, bo = 4 * ((size_t)nq + 1);
+    Scratch s;
+    HIPCHK(hipMalloc(&s.p, bq + bt + bo + 64));
+    uint8_t* dq = reinterpret_cast<uint8_t*>(s.p);
+    uint8_t* dt = dq + bq;
+    int32_t* dro = reinterpret_cast<int32_t*>(dt + bt + (16 - (bq + bt) % 16) % 16);
+    if (bq) HIPCHK(hipMemcpyAsync(dq, q, bq, hipMemcpyHostToDevice, c->stream));
+    if (bt) HIPCHK(hipMemcpyAsync(dt, t, bt, hipMemcpyHostToDevice, c->stream));
+    // sizes first (rows are ragged), then the rows into a scratch of exactly that size
+    int e = gfpl_radius_hamming(c, dq, nq, dt, nt, cell, max_dist, dro, 0, nullptr, nullptr);
+    if (e != GFPL_OK && e != GFPL_E_CAPACITY) return e;
+    HIPCHK(hipMemcpy(row_off, dro, bo, hipMemcpyDeviceToHost));
+    const int total = row_off[nq];
+    if (total > cap) return GFPL_E_CAPACITY;
+    if (total == 0) return GFPL_OK;
+    if (!idx || !dist) return GFPL_E_INVALID;
+    Scratch r;
+    HIPCHK(hipMalloc(&r.p, 8 * (size_t)total + 64));
+    int32_t* ri = reinterpret_cast<int32_t*>(r.p);
+    float* rd = reinterpret_cast<float*>(ri + total);
+    HIPCHK(launch_radius_rows(dq, nq, dt, nt, cell, max_dist, dro, ri, rd, c->stream));
+    HIPCHK(hipMemcpyAsync(idx, ri, 4 * (size_t)total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(dist, rd, 4 * (size_t)total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GFPL_OK;
+}
+
+int gfpl_match_stats_host(gfpl_ctx* c, int kind, const float* d0, const float* d1, int n, int max_num, double* out) {
+    if (!c || !d0 || !d1 || !out || n < 1 || max_num < 1 || (kind != 0 && kind != 1)) return GFPL_E_INVALID;
+    std::lock_guard<std::mutex> lk(c->host_mu);
+    HIPCHK(hipSetDevice(c->device));
+    Scratch s;
+    HIPCHK(hipMalloc(&s.p, 8 * (size_t)n + 64));
+    float* a = reinterpret_cast<float*>(s.p);
+    float* b = a + n;
+    double* o = reinterpret_cast<double*>(s.p + ((8 * (size_t)n + 7) & ~(size_t)7));
+    HIPCHK(hipMemcpyAsync(a, d0, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(b, d1, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_match_stats(kind, a, b, n, max_num, o, c->stream));
+    HIPCHK(hipMemcpyAsync(out, o, 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return GFPL_OK;
 }
 

@@ -120,6 +120,9 @@ int run(gfpl_detector* d, DetSet& S, int n, gfpl_frames* out) {
     const uint8_t* right = S.img + (size_t)n * img;
     DET_CHK(gfpl_event_record(S.copied, d->c_lines));
     DET_CHK(gfpl_event_wait(d->c_orb, S.copied));
+    // the caller's stream is ordered after the input copies: work it enqueues after this call
+    // (e.g. writing the next frame into the same img_l / img_r / time_stamp) cannot overtake them
+    DET_CHK(gfpl_event_wait(d->ctx, S.copied));
     for (int side = 0; side < 2; ++side)
         DET_CHK(gfpl_orb_extract_async(d->orb, side ? right : left, n, S.kp[side], S.pdesc[side], S.n_kp[side], nullptr,
                                        nullptr, S.pyr[side], d->pyr_bytes));

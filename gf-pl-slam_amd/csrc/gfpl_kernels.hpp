@@ -10,6 +10,13 @@ hipError_t launch_line_uncertainty(const KParams& p, hipStream_t s);
 hipError_t launch_init(const KParams& p, hipStream_t s);
 hipError_t launch_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* idx, float* dist,
                        hipStream_t s);
+// k_match.hip: radiusMatch rows (count pass, then the rows at row_off) and knn-2 list statistics
+hipError_t launch_radius_count(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, float radius,
+                               int32_t* cnt, hipStream_t s);
+hipError_t launch_radius_rows(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, float radius,
+                              const int32_t* row_off, int32_t* idx, float* dist, hipStream_t s);
+hipError_t launch_match_stats(int kind, const float* d0, const float* d1, int n, int max_num, double* out,
+                              hipStream_t s);
 hipError_t launch_cross_points(const KParams& p, hipStream_t s);
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s);
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks /* [2] or null */);

@@ -252,9 +252,6 @@ __device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutDat
 }
 
 // ------------------------------------------------------------------ prep --
-#ifndef GFPL_PREP_STAGE
-#define GFPL_PREP_STAGE 1
-#endif
 __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
     __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
     const int b = blockIdx.x;
@@ -299,20 +296,6 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
                 cut_poly_data(Dl, d, homog, fd);
                 fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
-#if !GFPL_PREP_STAGE && !defined(GFPL_PREP_PROBE)
-                // the record written 16 B per lane and store
-                double2* rq = reinterpret_cast<double2*>(rec_l + (size_t)m * CUT_REC);
-#pragma unroll
-                for (int i = 0; i < 10; ++i) rq[CUT_FAST / 2 + i] = make_double2(info[2 * i], info[2 * i + 1]);   // k_cut_search subtracts it
-                rq[CUT_FAST / 2 + 10] = make_double2(info[20], 0.0);
-#pragma unroll
-                for (int i = 0; i < CUT_FAST / 2; ++i) rq[i] = make_double2(fd[2 * i], fd[2 * i + 1]);
-#endif
-#ifdef GFPL_PREP_PROBE   // (timing probe: without the comparison-data stores; the search then runs exact)
-                rec_l[(size_t)m * CUT_REC + PD_OK] = 0.0;   // (every step exact: the index field stays valid)
-                rec_l[(size_t)m * CUT_REC + PD_NEXT] = fd[PD_NEXT];
-                if (fd[0] == 12345.678) rec_l[(size_t)m * CUT_REC] = fd[1];
-#endif
             } else {
                 const size_t q = pbase + mpt[m];
                 double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
@@ -328,7 +311,6 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                     for (int j = 0; j <= i; ++j) info[tri(i, j)] = J[i] * J[j];
             }
         }
-#if GFPL_PREP_STAGE && !defined(GFPL_PREP_PROBE)
         if (lines) {   // (wave-uniform)
             // The chunk's records (comparison data | r = 0 info | pad) leave in five slices of 16
             // doubles staged through the chunk buffer (idle until the sums): a store instruction then
@@ -359,7 +341,6 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
                 __syncthreads();
             }
         }
-#endif
         if (lane < cnt) {
 #pragma unroll
             for (int i = 0; i < 21; ++i) chunk[i][lane] = info[i];

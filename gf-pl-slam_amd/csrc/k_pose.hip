@@ -178,19 +178,12 @@ struct PoseCtx {
 // Issue priority by progress: 3 in the first half of the first GN run, down to 0 in the second half
 // of the second, so the waves dispatched last are not starved by the older ones (the arbiter favours
 // the older of two ready waves) at the end of the grid: 4.92 -> 4.76 ms (profiles/r04_t)
-#ifndef GFPL_POSE_FAIR
-#define GFPL_POSE_FAIR 1
-#endif
 __device__ __forceinline__ void pose_prio(int stage, int it, int n) {
-#if GFPL_POSE_FAIR
     const int q = 2 * stage + (2 * it >= n ? 1 : 0);
     if (q <= 0) __builtin_amdgcn_s_setprio(3);
     else if (q == 1) __builtin_amdgcn_s_setprio(2);
     else if (q == 2) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-#else
-    (void)stage; (void)it; (void)n;
-#endif
 }
 
 __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl,

@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <unordered_map>
 
 namespace StVO {
@@ -85,6 +87,130 @@ int StereoFrame::descriptorDistance(const Descriptor& a, const Descriptor& b) {
     int d = 0;
     for (int i = 0; i < GFPL_DESC_BYTES; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
     return d;
+}
+
+// ------------------------------------------------------------ BFMatcher --
+namespace {
+void abi_check(int rc, const char* what) {
+    if (rc != GFPL_OK) throw std::runtime_error(std::string(what) + ": " + gfpl_strerror(rc));
+}
+std::vector<uint8_t> pack_rows(const std::vector<Descriptor>& d) {
+    std::vector<uint8_t> o(32 * d.size());
+    for (size_t i = 0; i < d.size(); ++i) std::memcpy(&o[32 * i], d[i].data(), 32);
+    return o;
+}
+}  // namespace
+
+BFMatcher::BFMatcher(int normType_, bool crossCheck_, int device) : normType(normType_), crossCheck(crossCheck_) {
+    if (normType != NORM_HAMMING && normType != NORM_HAMMING2)
+        throw std::invalid_argument("BFMatcher: NORM_HAMMING / NORM_HAMMING2 only (binary descriptors)");
+    if (crossCheck) throw std::invalid_argument("BFMatcher: crossCheck = true is not supported (the reference never sets it)");
+    abi_check(gfpl_create_async(device, &ctx_), "gfpl_create_async");
+}
+
+BFMatcher::~BFMatcher() {
+    if (ctx_) gfpl_destroy(ctx_);
+}
+
+void BFMatcher::knnMatch(const std::vector<Descriptor>& query, const std::vector<Descriptor>& train,
+                         std::vector<std::vector<DMatch>>& matches, int k) const {
+    if (k != 2) throw std::invalid_argument("BFMatcher::knnMatch: k = 2 only (every call site of the reference)");
+    const int nq = (int)query.size(), nt = (int)train.size();
+    matches.assign(nq, std::vector<DMatch>());
+    if (nq == 0) return;
+    const std::vector<uint8_t> q = pack_rows(query), t = pack_rows(train);
+    std::vector<int32_t> idx(2 * (size_t)nq);
+    std::vector<float> dist(2 * (size_t)nq);
+    abi_check(gfpl_knn2_hamming_host(ctx_, q.data(), nq, t.data(), nt, cell(), idx.data(), dist.data()),
+              "gfpl_knn2_hamming_host");
+    for (int i = 0; i < nq; ++i) {
+        matches[i].push_back(DMatch(i, idx[2 * i], dist[2 * i]));
+        matches[i].push_back(DMatch(i, idx[2 * i + 1], dist[2 * i + 1]));
+    }
+}
+
+void BFMatcher::radiusMatch(const std::vector<Descriptor>& query, const std::vector<Descriptor>& train,
+                            std::vector<std::vector<DMatch>>& matches, float maxDistance) const {
+    const int nq = (int)query.size(), nt = (int)train.size();
+    matches.assign(nq, std::vector<DMatch>());
+    if (nq == 0) return;
+    const std::vector<uint8_t> q = pack_rows(query), t = pack_rows(train);
+    std::vector<int32_t> off(nq + 1);
+    // sizes first (ragged rows), then the rows
+    int rc = gfpl_radius_hamming_host(ctx_, q.data(), nq, t.data(), nt, cell(), maxDistance, off.data(), 0, nullptr,
+                                      nullptr);
+    if (rc == GFPL_OK) return;   // no match at all
+    if (rc != GFPL_E_CAPACITY) abi_check(rc, "gfpl_radius_hamming_host");
+    std::vector<int32_t> idx(off[nq]);
+    std::vector<float> dist(off[nq]);
+    abi_check(gfpl_radius_hamming_host(ctx_, q.data(), nq, t.data(), nt, cell(), maxDistance, off.data(), off[nq],
+                                       idx.data(), dist.data()),
+              "gfpl_radius_hamming_host");
+    for (int i = 0; i < nq; ++i)
+        for (int k = off[i]; k < off[i + 1]; ++k) matches[i].push_back(DMatch(i, idx[k], dist[k]));
+}
+
+// ---------------------------------------------- StereoFrame frame members --
+namespace {
+std::mutex g_engine_mu;
+std::map<const PinholeStereoCamera*, std::unique_ptr<StereoFrameHandler>>& engines() {
+    static std::map<const PinholeStereoCamera*, std::unique_ptr<StereoFrameHandler>> m;
+    return m;
+}
+}  // namespace
+
+StereoFrameHandler& StereoFrame::engine() {
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    auto& e = engines()[cam];
+    if (!e) e.reset(new StereoFrameHandler(cam));
+    return *e;
+}
+
+void StereoFrame::extractInitialStereoFeatures(int /*fast_th*/) { engine().frame_stereo(this, true); }
+void StereoFrame::extractStereoFeatures_ORBSLAM(int /*fast_th*/) { engine().frame_stereo(this, false); }
+void StereoFrame::estimateStereoUncertainty() { engine().frame_uncertainty(this); }
+
+void StereoFrame::matchPointFeatures(BFMatcher* bfm, const std::vector<Descriptor>& pdesc_1,
+                                     const std::vector<Descriptor>& pdesc_2,
+                                     std::vector<std::vector<DMatch>>& pmatches_12) {
+    bfm->knnMatch(pdesc_1, pdesc_2, pmatches_12, 2);
+}
+void StereoFrame::matchLineFeatures(BFMatcher* bfm, const std::vector<Descriptor>& ldesc_1,
+                                    const std::vector<Descriptor>& ldesc_2,
+                                    std::vector<std::vector<DMatch>>& lmatches_12) {
+    bfm->knnMatch(ldesc_1, ldesc_2, lmatches_12, 2);
+}
+void StereoFrame::matchPointFeatures_radius(BFMatcher* bfm, const std::vector<Descriptor>& pdesc_1,
+                                            const std::vector<Descriptor>& pdesc_2,
+                                            std::vector<std::vector<DMatch>>& pmatches_12) {
+    bfm->radiusMatch(pdesc_1, pdesc_2, pmatches_12, (float)Config::pointMatchRadius());
+}
+void StereoFrame::matchLineFeatures_radius(BFMatcher* bfm, const std::vector<Descriptor>& ldesc_1,
+                                           const std::vector<Descriptor>& ldesc_2,
+                                           std::vector<std::vector<DMatch>>& lmatches_12) {
+    bfm->radiusMatch(ldesc_1, ldesc_2, lmatches_12, (float)Config::lineMatchRadius());
+}
+void StereoFrame::pointDescriptorMAD(const std::vector<std::vector<DMatch>> matches, double& nn_mad, double& nn12_mad) {
+    double o[3];
+    engine().frame_stats(0, matches, 1, o);
+    nn_mad = o[0];
+    nn12_mad = o[1];
+}
+void StereoFrame::lineDescriptorMAD(const std::vector<std::vector<DMatch>> matches, double& nn_mad, double& nn12_mad) {
+    double o[3];
+    engine().frame_stats(1, matches, 1, o);
+    nn_mad = o[0];
+    nn12_mad = o[1];
+}
+void StereoFrame::pointDescriptorBudgetThres(const std::vector<std::vector<DMatch>> matches, double& thres_budget) {
+    double o[3];
+    engine().frame_stats(0, matches, Config::maxPointMatchNum(), o);
+    thres_budget = o[2];
+}
+void StereoFrame::lineDescriptorBudgetThres(const std::vector<std::vector<DMatch>> matches, double& thres_budget) {
+    double o[3];
+    engine().frame_stats(1, matches, Config::maxLineMatchNum(), o);
+    thres_budget = o[2];
 }
 
 // ---------------------------------------------------- StereoFrameHandler --
@@ -473,58 +599,60 @@ void StereoFrameHandler::updateFrame() {
     matched_ls.clear();
 }
 
+void StereoFrameHandler::push_frame(int which, StereoFrame* f) {
+    HostBuf& h = *buf_;
+    if (!f) return;
+    gfpl_frame_host& o = h.fh;
+    o.n_pt = (int)f->stereo_pt.size();
+    o.n_ls = (int)f->stereo_ls.size();
+    if (o.n_pt > kp_cap_ || o.n_ls > kl_cap_) throw std::length_error("pushState: capacity");
+    for (int i = 0; i < o.n_pt; ++i) {
+        const PointFeature& p = *f->stereo_pt[i];
+        o.pt_idx[i] = p.idx;
+        for (int k = 0; k < 2; ++k) { o.pt_pl[2 * i + k] = p.pl(k); o.pt_pl_obs[2 * i + k] = p.pl_obs(k); }
+        o.pt_disp[i] = p.disp;
+        for (int k = 0; k < 3; ++k) o.pt_P[3 * i + k] = p.P(k);
+        o.pt_inlier[i] = p.inlier ? 1 : 0;
+        o.pt_level[i] = p.level;
+        o.pt_sigma2[i] = p.sigma2;
+        std::memcpy(o.pdesc + 32 * (size_t)i, f->pdesc_l.at(i).data(), 32);
+    }
+    for (int i = 0; i < o.n_ls; ++i) {
+        const LineFeature& l = *f->stereo_ls[i];
+        o.ls_idx[i] = l.idx;
+        for (int k = 0; k < 2; ++k) {
+            o.ls_spl[2 * i + k] = l.spl(k); o.ls_epl[2 * i + k] = l.epl(k);
+            o.ls_spl_obs[2 * i + k] = l.spl_obs(k); o.ls_epl_obs[2 * i + k] = l.epl_obs(k);
+            o.ls_cut[2 * i + k] = l.cutRatio[k];
+        }
+        o.ls_sdisp[i] = l.sdisp; o.ls_edisp[i] = l.edisp;
+        o.ls_sdisp_obs[i] = l.sdisp_obs; o.ls_edisp_obs[i] = l.edisp_obs;
+        o.ls_angle[i] = l.angle;
+        for (int k = 0; k < 3; ++k) {
+            o.ls_sP[3 * i + k] = l.sP(k); o.ls_eP[3 * i + k] = l.eP(k);
+            o.ls_le[3 * i + k] = l.le(k); o.ls_le_obs[3 * i + k] = l.le_obs(k);
+        }
+        for (int k = 0; k < 9; ++k) { o.ls_covS[9 * i + k] = l.covSpt3D.v[k]; o.ls_covE[9 * i + k] = l.covEpt3D.v[k]; }
+        for (int k = 0; k < 36; ++k) o.ls_invcov[36 * i + k] = l.invCovPose.v[k];
+        o.ls_inlier[i] = l.inlier ? 1 : 0;
+        o.ls_level[i] = l.level;
+        o.ls_sigma2[i] = l.sigma2;
+        std::memcpy(o.ldesc + 32 * (size_t)i, f->ldesc_l.at(i).data(), 32);
+    }
+    std::memcpy(o.Tfw, f->Tfw.v, sizeof o.Tfw);
+    std::memcpy(o.DT, f->DT.v, sizeof o.DT);
+    std::memcpy(o.DT_cov, f->DT_cov.v, sizeof o.DT_cov);
+    std::memcpy(o.Tfw_cov, f->Tfw_cov.v, sizeof o.Tfw_cov);
+    std::memcpy(o.DT_cov_eig, f->DT_cov_eig.v, sizeof o.DT_cov_eig);
+    o.err_norm = f->err_norm;
+    o.time_stamp = f->time_stamp;
+    check(gfpl_write_frame(sb_, which, 0, &o), "gfpl_write_frame");
+}
+
 void StereoFrameHandler::pushState() {
     HostBuf& h = *buf_;
-    auto push = [&](int which, StereoFrame* f) {
-        if (!f) return;
-        gfpl_frame_host& o = h.fh;
-        o.n_pt = (int)f->stereo_pt.size();
-        o.n_ls = (int)f->stereo_ls.size();
-        if (o.n_pt > kp_cap_ || o.n_ls > kl_cap_) throw std::length_error("pushState: capacity");
-        for (int i = 0; i < o.n_pt; ++i) {
-            const PointFeature& p = *f->stereo_pt[i];
-            o.pt_idx[i] = p.idx;
-            for (int k = 0; k < 2; ++k) { o.pt_pl[2 * i + k] = p.pl(k); o.pt_pl_obs[2 * i + k] = p.pl_obs(k); }
-            o.pt_disp[i] = p.disp;
-            for (int k = 0; k < 3; ++k) o.pt_P[3 * i + k] = p.P(k);
-            o.pt_inlier[i] = p.inlier ? 1 : 0;
-            o.pt_level[i] = p.level;
-            o.pt_sigma2[i] = p.sigma2;
-            std::memcpy(o.pdesc + 32 * (size_t)i, f->pdesc_l.at(i).data(), 32);
-        }
-        for (int i = 0; i < o.n_ls; ++i) {
-            const LineFeature& l = *f->stereo_ls[i];
-            o.ls_idx[i] = l.idx;
-            for (int k = 0; k < 2; ++k) {
-                o.ls_spl[2 * i + k] = l.spl(k); o.ls_epl[2 * i + k] = l.epl(k);
-                o.ls_spl_obs[2 * i + k] = l.spl_obs(k); o.ls_epl_obs[2 * i + k] = l.epl_obs(k);
-                o.ls_cut[2 * i + k] = l.cutRatio[k];
-            }
-            o.ls_sdisp[i] = l.sdisp; o.ls_edisp[i] = l.edisp;
-            o.ls_sdisp_obs[i] = l.sdisp_obs; o.ls_edisp_obs[i] = l.edisp_obs;
-            o.ls_angle[i] = l.angle;
-            for (int k = 0; k < 3; ++k) {
-                o.ls_sP[3 * i + k] = l.sP(k); o.ls_eP[3 * i + k] = l.eP(k);
-                o.ls_le[3 * i + k] = l.le(k); o.ls_le_obs[3 * i + k] = l.le_obs(k);
-            }
-            for (int k = 0; k < 9; ++k) { o.ls_covS[9 * i + k] = l.covSpt3D.v[k]; o.ls_covE[9 * i + k] = l.covEpt3D.v[k]; }
-            for (int k = 0; k < 36; ++k) o.ls_invcov[36 * i + k] = l.invCovPose.v[k];
-            o.ls_inlier[i] = l.inlier ? 1 : 0;
-            o.ls_level[i] = l.level;
-            o.ls_sigma2[i] = l.sigma2;
-            std::memcpy(o.ldesc + 32 * (size_t)i, f->ldesc_l.at(i).data(), 32);
-        }
-        std::memcpy(o.Tfw, f->Tfw.v, sizeof o.Tfw);
-        std::memcpy(o.DT, f->DT.v, sizeof o.DT);
-        std::memcpy(o.DT_cov, f->DT_cov.v, sizeof o.DT_cov);
-        std::memcpy(o.Tfw_cov, f->Tfw_cov.v, sizeof o.Tfw_cov);
-        std::memcpy(o.DT_cov_eig, f->DT_cov_eig.v, sizeof o.DT_cov_eig);
-        o.err_norm = f->err_norm;
-        o.time_stamp = f->time_stamp;
-        check(gfpl_write_frame(sb_, which, 0, &o), "gfpl_write_frame");
-    };
-    push(GFPL_PREV, prev_frame);
-    push(GFPL_CURR, curr_frame);
+    push_frame(GFPL_PREV, prev_frame);
+    push_frame(GFPL_CURR, curr_frame);
     if (prev_frame) {
         std::unordered_map<const void*, int> pi, li;
         for (size_t i = 0; i < prev_frame->stereo_pt.size(); ++i) pi[prev_frame->stereo_pt[i]] = (int)i;
@@ -538,6 +666,55 @@ void StereoFrameHandler::pushState() {
         t.num_frame_loss = numFrameLoss;
         check(gfpl_write_track(sb_, 0, &t), "gfpl_write_track");
     }
+}
+
+// ------------------------------------------------------------ frame engine --
+// The frame-level members of StereoFrame run on a per-camera handler that never owns the frame:
+// its seqbatch is initialised once with an empty frame, so the stage entry points run
+void StereoFrameHandler::engine_ready() {
+    if (engine_init_) return;
+    StereoFrame empty(0, cam, 0.0, {}, {}, {}, {}, {}, {}, {}, {}, {});
+    gfpl_frames dev{};
+    upload(&empty, &dev);
+    check(gfpl_initialize(sb_, &dev), "gfpl_initialize");
+    engine_init_ = true;
+}
+
+void StereoFrameHandler::frame_stereo(StereoFrame* f, bool initial) {
+    std::lock_guard<std::mutex> lk(engine_mu_);
+    sync_config();
+    engine_ready();
+    gfpl_frames dev{};
+    upload(f, &dev);   // (an image frame is detected here: points_* / lines_* / *desc_* filled)
+    if (initial) {
+        check(gfpl_initialize(sb_, &dev), "gfpl_initialize");   // extractInitialStereoFeatures (the init frame)
+        pull(GFPL_PREV, f, true, false);
+    } else {
+        check(gfpl_stereo_points(sb_, &dev), "gfpl_stereo_points");
+        check(gfpl_stereo_lines(sb_, &dev), "gfpl_stereo_lines");
+        pull(GFPL_CURR, f, true, false);
+    }
+}
+
+void StereoFrameHandler::frame_uncertainty(StereoFrame* f) {
+    std::lock_guard<std::mutex> lk(engine_mu_);
+    sync_config();
+    engine_ready();
+    push_frame(GFPL_PREV, f);
+    check(gfpl_line_uncertainty(sb_), "gfpl_line_uncertainty");   // prev_frame->estimateStereoUncertainty()
+    pull(GFPL_PREV, f, true, false);
+}
+
+void StereoFrameHandler::frame_stats(int kind, const std::vector<std::vector<DMatch>>& m, int max_num, double* out3) {
+    std::vector<float> d0(m.size()), d1(m.size());
+    for (size_t i = 0; i < m.size(); ++i) {
+        if (m[i].size() < 2) throw std::invalid_argument("descriptor MAD: every knn row needs two matches");
+        d0[i] = m[i][0].distance;
+        d1[i] = m[i][1].distance;
+    }
+    std::lock_guard<std::mutex> lk(engine_mu_);
+    check(gfpl_match_stats_host(ctx_, kind, d0.data(), d1.data(), (int)m.size(), max_num, out3),
+          "gfpl_match_stats_host");
 }
 
 }  // namespace StVO

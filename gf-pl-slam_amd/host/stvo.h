@@ -24,8 +24,10 @@
 //    prev_frame->stereo_pt / stereo_ls, mutated in place).
 #pragma once
 #include <array>
+#include <cfloat>
 #include <cstdint>
 #include <list>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -75,6 +77,43 @@ struct KeyLine {
 };
 using Descriptor = std::array<uint8_t, GFPL_DESC_BYTES>;   // one row of pdesc_* / ldesc_*
 
+// cv::DMatch (the fields the reference's matchers fill and its callers read)
+struct DMatch {
+    int queryIdx = -1, trainIdx = -1, imgIdx = -1;
+    float distance = FLT_MAX;
+    DMatch() = default;
+    DMatch(int q, int t, float d) : queryIdx(q), trainIdx(t), imgIdx(0), distance(d) {}
+    bool operator<(const DMatch& o) const { return distance < o.distance; }
+};
+// cv::NormTypes the path uses (OpenCV's values)
+enum NormTypes { NORM_HAMMING = 6, NORM_HAMMING2 = 7 };
+
+// cv::BFMatcher subset the reference builds (`new BFMatcher(NORM_HAMMING[2], false)`,
+// src/stereoFrame.cpp:176,636, src/mapHandler.cpp:213,345,551,679): knnMatch with k = 2
+// (gfpl_knn2_hamming_host: i8 MFMA, the OpenCV tie rule) and radiusMatch
+// (gfpl_radius_hamming_host), both on the GPU over the matcher's own context and stream.
+// Thread-safe: MapHandler runs two matches on one matcher from two std::async tasks.
+// Not supported (std::invalid_argument): crossCheck = true, k != 2 (the reference uses
+// neither); fewer than 2 train rows throws (GFPL_E_TOO_FEW_TRAIN: the reference then reads
+// a missing second neighbour, ledger U4).
+class BFMatcher {
+public:
+    explicit BFMatcher(int normType = NORM_HAMMING, bool crossCheck = false, int device = 0);
+    ~BFMatcher();
+    BFMatcher(const BFMatcher&) = delete;
+    BFMatcher& operator=(const BFMatcher&) = delete;
+    void knnMatch(const std::vector<Descriptor>& query, const std::vector<Descriptor>& train,
+                  std::vector<std::vector<DMatch>>& matches, int k) const;
+    void radiusMatch(const std::vector<Descriptor>& query, const std::vector<Descriptor>& train,
+                     std::vector<std::vector<DMatch>>& matches, float maxDistance) const;
+    const int normType;
+    const bool crossCheck;
+
+private:
+    int cell() const { return normType == NORM_HAMMING2 ? 2 : 1; }
+    gfpl_ctx* ctx_ = nullptr;
+};
+
 // ---------------------------------------------------------------- Config --
 // The path's subset of Config (include/config.h:28-141, defaults src/config.cpp:26-154),
 // same static accessor names.  Changes take effect at the next handler call.
@@ -90,6 +129,7 @@ public:
     static int& maxLineMatchNum() { return getInstance().c.max_line_match_num; }
     static int& maxPointMatchNum() { return getInstance().c.max_point_match_num; }
     static double& maxDistEpip() { return getInstance().c.max_dist_epip; }
+    static double& lineMatchRadius() { return getInstance().line_match_radius; }   // src/config.cpp:111
     static double& minDisp() { return getInstance().c.min_disp; }
     static double& maxRatio12P() { return getInstance().c.max_ratio_12_p; }
     static double& pointMatchRadius() { return getInstance().c.point_match_radius; }
@@ -123,6 +163,7 @@ private:
     bool best_lr_matches = true, lr_in_parallel = true, use_line_conf_cut = true, max_vol_line_cut = true;
     int orb_nfeatures = 1000, lsd_nfeatures = 300;
     double min_line_length = 0.025;
+    double line_match_radius = 80.0;
 };
 
 // ---------------------------------------------------- PinholeStereoCamera --
@@ -201,6 +242,8 @@ struct TimeLog {
     double num_ln_cross = 0;
 };
 
+class StereoFrameHandler;
+
 // ----------------------------------------------------------- StereoFrame --
 // include/stereoFrame.h:89-260.  Built from a grey stereo pair (the handler
 // detects it on the GPU and fills points_* / lines_* / *desc_* as
@@ -250,6 +293,40 @@ public:
 
     // Hamming distance of two 32-byte rows (include/stereoFrame.h:185-201)
     static int descriptorDistance(const Descriptor& a, const Descriptor& b);
+
+    // --- the frame-level members the reference's callers use (include/stereoFrame.h:104-148) ---
+    // Detection + stereo matching of this frame on the GPU (src/stereoFrame.cpp:148-336 /
+    // 411-768): an image frame is detected first (ORB, LSD, LBD); stereo_pt / stereo_ls and the
+    // reordered pdesc_l / ldesc_l are filled as the reference leaves them.  The pose members are
+    // untouched.  fast_th is accepted and unused, as in the reference (its use is commented out,
+    // src/stereoFrame.cpp:1131-1145).  Runs on the camera's frame engine (a one-sequence GPU
+    // tracker per PinholeStereoCamera, created on first use, one call at a time).
+    void extractInitialStereoFeatures(int fast_th = 20);
+    void extractStereoFeatures_ORBSLAM(int fast_th = 20);
+    // covSpt3D / covEpt3D of every stereo line (src/stereoFrame.cpp:1448-1484), on the GPU
+    void estimateStereoUncertainty();
+    // BFMatcher::knnMatch(k = 2) / radiusMatch (Config::pointMatchRadius / lineMatchRadius)
+    // wrappers (src/stereoFrame.cpp:1229-1257), as MapHandler calls them through std::async
+    void matchPointFeatures(BFMatcher* bfm, const std::vector<Descriptor>& pdesc_1,
+                            const std::vector<Descriptor>& pdesc_2, std::vector<std::vector<DMatch>>& pmatches_12);
+    void matchLineFeatures(BFMatcher* bfm, const std::vector<Descriptor>& ldesc_1,
+                           const std::vector<Descriptor>& ldesc_2, std::vector<std::vector<DMatch>>& lmatches_12);
+    void matchPointFeatures_radius(BFMatcher* bfm, const std::vector<Descriptor>& pdesc_1,
+                                   const std::vector<Descriptor>& pdesc_2,
+                                   std::vector<std::vector<DMatch>>& pmatches_12);
+    void matchLineFeatures_radius(BFMatcher* bfm, const std::vector<Descriptor>& ldesc_1,
+                                  const std::vector<Descriptor>& ldesc_2,
+                                  std::vector<std::vector<DMatch>>& lmatches_12);
+    // statistics of a knn-2 list (src/stereoFrame.cpp:1259-1341; gfpl_match_stats_host: ledger U1,
+    // U12); every row must hold two matches (GFPL_E_INVALID on an empty list, as the reference
+    // reads element size/2 of it)
+    void pointDescriptorMAD(const std::vector<std::vector<DMatch>> matches, double& nn_mad, double& nn12_mad);
+    void lineDescriptorMAD(const std::vector<std::vector<DMatch>> matches, double& nn_mad, double& nn12_mad);
+    void pointDescriptorBudgetThres(const std::vector<std::vector<DMatch>> matches, double& thres_budget);
+    void lineDescriptorBudgetThres(const std::vector<std::vector<DMatch>> matches, double& thres_budget);
+
+private:
+    StereoFrameHandler& engine();
 };
 
 // ---------------------------------------------------- StereoFrameHandler --
@@ -304,6 +381,14 @@ public:
     Matrix6d cov_prevKF_currF;
 
 private:
+    friend class StereoFrame;   // frame-level members run on a per-camera handler (the frame engine)
+    void frame_stereo(StereoFrame* f, bool initial);
+    void frame_uncertainty(StereoFrame* f);
+    void frame_stats(int kind, const std::vector<std::vector<DMatch>>& m, int max_num, double* out3);
+    void engine_ready();
+    void push_frame(int which, StereoFrame* f);
+    std::mutex engine_mu_;
+    bool engine_init_ = false;
     void sync_config();
     void upload(StereoFrame* f, gfpl_frames* dev);   // detects an image frame, uploads an injected one
     void detect(StereoFrame* f, gfpl_frames* dev);

@@ -270,6 +270,9 @@ int  gfpl_event_record_count(const gfpl_event* ev, int64_t* count);
 /* GFPL_E_STATE while seqbatches or ORB / LBD / LSD objects created on the context
  * are still alive (they use its stream; ORB also reads its camera).           */
 int  gfpl_destroy(gfpl_ctx* ctx);
+/* GFPL_E_STATE while seqbatches or detector objects of the context live (their pyramid
+ * builders and ORB / LSD geometry are laid out for the camera they were created on).
+ * GFPL_E_INVALID for bad level tables.                                                 */
 int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
 /* max_point_match_num / max_line_match_num size the matched lists and the cut /
  * pose scratch of a seqbatch when it is created; while any seqbatch of the
@@ -375,6 +378,32 @@ int  gfpl_line_cut(gfpl_seqbatch* sb);
  * Returns GFPL_E_TOO_FEW_TRAIN when nt < 2 (reference UB).        */
 int  gfpl_knn2_hamming(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
                        int cell, int32_t* out_idx, float* out_dist);
+/* The same on HOST buffers (copied in and out; synchronous): StereoFrame::matchPointFeatures /
+ * matchLineFeatures (src/stereoFrame.cpp:1229-1241), which MapHandler calls from two std::async
+ * tasks (src/mapHandler.cpp:223-226,355-356,558-559,686-687).  Thread-safe per context.      */
+int  gfpl_knn2_hamming_host(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                            int cell, int32_t* out_idx, float* out_dist);
+/* cv::BFMatcher::radiusMatch with NORM_HAMMING (cell 1) / NORM_HAMMING2 (cell 2):
+ * StereoFrame::matchPointFeatures_radius / matchLineFeatures_radius (src/stereoFrame.cpp:
+ * 1243-1257).  Row i holds every train row j with distance <= max_dist (ledger T1), sorted by
+ * distance, equal distances in train order (T2); rows are ragged: row i is
+ * [row_off[i], row_off[i+1]) of out_idx / out_dist (row_off has nq + 1 entries, always
+ * filled).  When row_off[nq] > cap nothing else is written and GFPL_E_CAPACITY is returned
+ * (call again with cap >= row_off[nq]).  _host: HOST buffers, synchronous; the device form
+ * takes DEVICE q / t / row_off / out_* and returns after the rows are written.              */
+int  gfpl_radius_hamming(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell,
+                         float max_dist, int32_t* row_off, int cap, int32_t* out_idx, float* out_dist);
+int  gfpl_radius_hamming_host(gfpl_ctx* ctx, const uint8_t* q, int nq, const uint8_t* t, int nt, int cell,
+                              float max_dist, int32_t* row_off, int cap, int32_t* out_idx, float* out_dist);
+/* Statistics of a knn-2 match list, HOST d0[n] / d1[n] = the best / second distances of each
+ * row (vector<vector<DMatch>> rows [0] / [1]): kind 0 pointDescriptorMAD + pointDescriptor-
+ * BudgetThres, kind 1 lineDescriptorMAD + lineDescriptorBudgetThres (src/stereoFrame.cpp:
+ * 1259-1341).  out[0] nn_mad, out[1] nn12_mad, out[2] thres_budget for max_num (the
+ * Config::max*MatchNum the reference reads).  nn_dist_median is the reference's
+ * uninitialised value pinned to 0.0 (ledger U1); NaN ratios order above +inf (U12).
+ * GFPL_E_INVALID for n < 1 or max_num < 1 (the reference indexes element -1).  Synchronous.   */
+int  gfpl_match_stats_host(gfpl_ctx* ctx, int kind, const float* d0, const float* d1, int n, int max_num,
+                           double* out);
 
 /* --------------------------------------------- ORB extraction (§8(f)1) ---- */
 /* ORB_SLAM2::ORBextractor (src/ORBextractor.cc:410-470 constructor, :1043-1105
@@ -505,7 +534,10 @@ int  gfpl_detector_destroy(gfpl_detector* det);
  * time_stamp DEVICE [n], produced on the context's stream (the detection waits for it).
  * *out is the view of the next buffer set (valid until that set is detected into again).
  * GFPL_E_STATE when the set's previous view was never read by a tracker call (nor
- * released with gfpl_detector_discard): at most `sets` views may be outstanding.       */
+ * released with gfpl_detector_discard): at most `sets` views may be outstanding.
+ * The inputs are copied on the detector's stream and the context's stream is made to wait
+ * for that copy, so the caller may overwrite img_l / img_r / time_stamp with work it
+ * enqueues on the context's stream after this call returns.                            */
 int  gfpl_detect_stereo_async(gfpl_detector* det, const uint8_t* img_l, const uint8_t* img_r, int n,
                               const double* time_stamp, gfpl_frames* out);
 /* The same from HOST images / time stamps (copied before it returns; the detection

@@ -717,7 +717,16 @@ std::vector<Desc> collect(const uint8_t* (Frame::*f)(int) const, const Frame& fr
 
 }  // namespace
 
-static int64_t g_cut_stats[8];   // line-cut work counters (analysis only)
+// Line-cut work counters and duplicate-evaluation scans: analysis only, compiled in with
+// -DGFPL_ORACLE_CUT_STATS (off in liboracle.so, which is also the timed CPU baseline: shared
+// counters bumped from every worker thread and the linear duplicate scans cost more than the
+// search itself at 16 threads).
+#ifdef GFPL_ORACLE_CUT_STATS
+static int64_t g_cut_stats[8];
+#define CUT_STAT(stmt) do { stmt; } while (0)
+#else
+#define CUT_STAT(stmt) do { } while (0)
+#endif
 
 struct gfplo_handler {
     Cam cam;
@@ -1326,12 +1335,15 @@ struct gfplo_handler {
             poseInfoPoint(DT_inv, prev->pt[pi], tmp);
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] + tmp[i];
         }
+#ifdef GFPL_ORACLE_CUT_STATS
         bool prev_moved = true;
         double sum_before[36];
+#endif
         for (int li : matched_ls) {
             LineF& L = prev->ls[li];
             double Jl[2] = {L.le_obs[0], L.le_obs[1]};
             double metric_back = logdet6(sum);
+#ifdef GFPL_ORACLE_CUT_STATS
             g_cut_stats[0]++;   // lines
             if (!prev_moved) {
                 bool same = true;
@@ -1340,20 +1352,24 @@ struct gfplo_handler {
             }
             std::memcpy(sum_before, sum, sizeof sum);
             std::vector<std::pair<uint64_t, uint64_t>> seen, last_step, this_step;
-            bool moved = false;
+#endif
+            [[maybe_unused]] bool moved = false;
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] - L.invCov[i];
             while (L.cut[0] + L.cut[1] <= 1.0) {
                 bool hit = false;
                 double cand[2] = {0, 0};
                 double cand_info[36];
                 double metric_init = metric_back;
-                g_cut_stats[1]++;   // steps
+                CUT_STAT(g_cut_stats[1]++);   // steps
+#ifdef GFPL_ORACLE_CUT_STATS
                 this_step.clear();
+#endif
                 for (int j = 0; j < 8; ++j) {
                     double rt[2] = {L.cut[0] + nb[j][0], L.cut[1] + nb[j][1]};
                     if (rt[0] + rt[1] > 1.0) continue;
                     if (rt[0] < cfg.cut_rng[0] || rt[0] > cfg.cut_rng[1]) continue;
                     if (rt[1] < cfg.cut_rng[0] || rt[1] > cfg.cut_rng[1]) continue;
+#ifdef GFPL_ORACLE_CUT_STATS
                     g_cut_stats[2]++;   // valid evaluations
                     uint64_t k0, k1;
                     std::memcpy(&k0, &rt[0], 8); std::memcpy(&k1, &rt[1], 8);
@@ -1365,6 +1381,7 @@ struct gfplo_handler {
                     for (auto& pr : last_step) dup1 = dup1 || (pr.first == k0 && pr.second == k1);
                     if (!dup1) g_cut_stats[6]++;
                     this_step.push_back({k0, k1});
+#endif
                     double tmp[36], tot[36];
                     poseInfoOnLine(DT_inv, Jl, L, rt, tmp);
                     for (int i = 0; i < 36; ++i) tot[i] = tmp[i] + sum[i];
@@ -1376,17 +1393,19 @@ struct gfplo_handler {
                         hit = true;
                     }
                 }
+#ifdef GFPL_ORACLE_CUT_STATS
                 last_step = this_step;
+#endif
                 if (hit) {
-                    if (cand[0] < L.cut[0] || cand[1] < L.cut[1]) g_cut_stats[7]++;   // a ratio moved back
+                    CUT_STAT(if (cand[0] < L.cut[0] || cand[1] < L.cut[1]) g_cut_stats[7]++);   // a ratio moved back
                     L.cut[0] = cand[0]; L.cut[1] = cand[1];
                     std::memcpy(L.invCov, cand_info, sizeof cand_info);
                     metric_back = metric_init;
                     moved = true;
                 } else break;
             }
-            if (!moved) g_cut_stats[4]++;   // lines that never moved
-            prev_moved = moved;
+            CUT_STAT(if (!moved) g_cut_stats[4]++);   // lines that never moved
+            CUT_STAT(prev_moved = moved);
             updateEndPointByRatio(L);
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] + L.invCov[i];
         }
@@ -1857,6 +1876,69 @@ int gfplo_write_track(gfplo_handler* h, const gfpl_track_host* in) {
 
 int gfplo_hamming(const uint8_t* a, const uint8_t* b, int cell) { return hamming(a, b, cell); }
 
+// BFMatcher::radiusMatch rows (StereoFrame::matchPointFeatures_radius / matchLineFeatures_radius,
+// src/stereoFrame.cpp:1243-1257): every train row with distance <= max_dist (ledger T1), sorted by
+// distance; OpenCV's std::sort of DMatch leaves ties unspecified — pinned to train order (T2) by a
+// stable sort.  row_off[nq + 1]; GFPL_E_CAPACITY (row_off filled) when the rows exceed cap.
+int gfplo_radius_match(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, float max_dist, int32_t* row_off,
+                       int cap, int32_t* out_idx, float* out_dist) {
+    std::vector<std::vector<std::pair<int, float>>> rows(nq);
+    row_off[0] = 0;
+    for (int i = 0; i < nq; ++i) {
+        for (int j = 0; j < nt; ++j) {
+            const float d = (float)hamming(q + 32 * (size_t)i, t + 32 * (size_t)j, cell);
+            if (d <= max_dist) rows[i].push_back(std::make_pair(j, d));
+        }
+        std::stable_sort(rows[i].begin(), rows[i].end(),
+                         [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; });
+        row_off[i + 1] = row_off[i] + (int)rows[i].size();
+    }
+    if (row_off[nq] > cap) return GFPL_E_CAPACITY;
+    for (int i = 0; i < nq; ++i)
+        for (size_t k = 0; k < rows[i].size(); ++k) {
+            out_idx[row_off[i] + k] = rows[i][k].first;
+            out_dist[row_off[i] + k] = rows[i][k].second;
+        }
+    return 0;
+}
+
+// pointDescriptorMAD / lineDescriptorMAD + *DescriptorBudgetThres (src/stereoFrame.cpp:1259-1341) on a
+// knn-2 list given as its best / second distances; the reference's std::sort calls restated with a
+// total order (NaN above +inf, ledger U12; equal keys are interchangeable, so the element at a rank
+// is the reference's), nn_dist_median pinned to 0.0 where the reference reads it uninitialised (U1).
+namespace {
+struct NanLast {
+    bool operator()(float a, float b) const {
+        if (a != a) return false;
+        if (b != b) return true;
+        return a < b;
+    }
+};
+float kth(std::vector<float> v, size_t k) {
+    std::sort(v.begin(), v.end(), NanLast());
+    return v[k];
+}
+}  // namespace
+int gfplo_match_stats(int kind, const float* d0, const float* d1, int n, int max_num, double* out) {
+    if (n < 1 || max_num < 1 || (kind != 0 && kind != 1)) return GFPL_E_INVALID;
+    const double nn_dist_median = 0.0;   // U1
+    std::vector<float> v(n);
+    for (int j = 0; j < n; ++j) v[j] = std::fabs((float)((double)d0[j] - nn_dist_median));
+    out[0] = 1.4826 * (double)kth(v, n / 2);
+    if (kind == 1) {   // lineDescriptorMAD :1287-1313
+        for (int j = 0; j < n; ++j) v[j] = std::fabs((float)((double)(d1[j] - d0[j]) - nn_dist_median));
+        out[1] = 1.4826 * (double)kth(v, n / 2);
+    } else {           // pointDescriptorMAD :1259-1285: the ratio order is descending (NN12_ratio's >)
+        for (int j = 0; j < n; ++j) v[j] = d0[j] / d1[j];
+        const double med = (double)kth(v, (size_t)(n - 1 - n / 2));
+        for (int j = 0; j < n; ++j) v[j] = std::fabs((float)((double)(d0[j] / d1[j]) - med));
+        out[1] = 1.4826 * (double)kth(v, n / 2);
+    }
+    for (int j = 0; j < n; ++j) v[j] = d0[j];
+    out[2] = (double)kth(v, (size_t)(std::min(max_num, n) - 1));   // :1315-1341
+    return 0;
+}
+
 int gfplo_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int cell, int32_t* out_idx, float* out_dist) {
     if (nt < 2) return GFPL_E_TOO_FEW_TRAIN;
     std::vector<Desc> Q(nq), T(nt);
@@ -1889,7 +1971,11 @@ int gfplo_inverse_se3(const double* T, double* out) { inverse_se3(T, out); retur
  * lines that never moved, setup logdets not implied by the previous line, (7) moves that
  * decrease a ratio */
 extern "C" void gfplo_cut_stats(int64_t* out8) {
+#ifdef GFPL_ORACLE_CUT_STATS
     for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
+#else
+    for (int i = 0; i < 8; ++i) out8[i] = -1;   // not compiled in
+#endif
 }
 
 // ============================================== keyframe consumers ==

@@ -43,6 +43,9 @@ def lib() -> C.CDLL:
         L.gfplo_optimize_pose_ini.argtypes = [P, P]; L.gfplo_optimize_pose_ini.restype = C.c_int
         L.gfplo_hamming.argtypes = [P, P, C.c_int]; L.gfplo_hamming.restype = C.c_int
         L.gfplo_knn2.argtypes = [P, C.c_int, P, C.c_int, C.c_int, P, P]; L.gfplo_knn2.restype = C.c_int
+        L.gfplo_radius_match.argtypes = [P, C.c_int, P, C.c_int, C.c_int, C.c_float, P, C.c_int, P, P]
+        L.gfplo_radius_match.restype = C.c_int
+        L.gfplo_match_stats.argtypes = [C.c_int, P, P, C.c_int, C.c_int, P]; L.gfplo_match_stats.restype = C.c_int
         L.gfplo_kf_common_matches.argtypes = [P, P, P, P, P, P, P, P]
         L.gfplo_kf_common_matches.restype = C.c_int
         L.gfplo_kf_local_map_matches.argtypes = [P, P, P, P, C.c_double, C.c_double, P, P, P, P]
@@ -203,6 +206,28 @@ def knn2(q: np.ndarray, t: np.ndarray, cell: int = 1):
     idx = np.zeros((len(q), 2), np.int32); dist = np.zeros((len(q), 2), np.float32)
     rc = lib().gfplo_knn2(_p(q), len(q), _p(t), len(t), cell, _p(idx), _p(dist))
     return rc, idx, dist
+
+
+def radius_match(q, t, max_dist: float, cell: int = 1):
+    """BFMatcher::radiusMatch rows: (row_off[nq + 1], train idx, dist) (ledger T1 / T2)."""
+    q = np.ascontiguousarray(q, np.uint8).reshape(-1, 32); t = np.ascontiguousarray(t, np.uint8).reshape(-1, 32)
+    off = np.zeros(len(q) + 1, np.int32)
+    cap = len(q) * len(t)
+    idx = np.zeros(max(cap, 1), np.int32); dist = np.zeros(max(cap, 1), np.float32)
+    rc = lib().gfplo_radius_match(_p(q), len(q), _p(t), len(t), cell, max_dist, _p(off), cap, _p(idx), _p(dist))
+    if rc:
+        raise RuntimeError(f"gfplo_radius_match: {rc}")
+    return off, idx[: off[-1]], dist[: off[-1]]
+
+
+def match_stats(kind: int, d0, d1, max_num: int):
+    """(nn_mad, nn12_mad, thres_budget) of a knn-2 list: kind 0 point, 1 line."""
+    d0 = np.ascontiguousarray(d0, np.float32); d1 = np.ascontiguousarray(d1, np.float32)
+    out = np.zeros(3, np.float64)
+    rc = lib().gfplo_match_stats(kind, _p(d0), _p(d1), len(d0), max_num, _p(out))
+    if rc:
+        raise RuntimeError(f"gfplo_match_stats: {rc}")
+    return tuple(float(x) for x in out)
 
 
 def log(x: float) -> float: return lib().gfplo_log(x)

@@ -192,3 +192,65 @@ def test_host_mirror_from_images_matches_the_oracle_chain(tmp_path):
         n_kp_l = len(O.orb_extract(imgs[k][0], nfeatures=NFEAT, kp_cap=KP)["kps"])
         assert int(f[11]) == n_kp_l and int(f[12]) == len(O.lsd_detect(imgs[k][0])[0]), (k, f[11:13])
     assert lines[-1]["matched_pt"] > 20 and lines[-1]["matched_ls"] > 5, lines[-1]   # (tracking, not lost)
+
+
+def test_detector_inputs_reusable_once_detect_returns():
+    """gfpl_detect_stereo_async copies the caller's device images on the detector's stream and
+    orders the context's stream after that copy: overwriting the same input tensors on the
+    context's stream right after detect() returns leaves the detections those of the first
+    images (include/gfpl.h, gfpl_detect_stereo_async)."""
+    import torch
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    W, H = int(cam.width), int(cam.height)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev)
+    ctx = gfpl.Context(cam, cfg, stream=s.cuda_stream)
+    det = gfpl.StereoDetector(ctx, 1, KP, KL, gfpl.DetectorParams.reference(cam, cfg, nfeatures=NFEAT), sets=2)
+    L, R = synth_stereo_steps(3, 1, W, H)[:2]
+    L2, R2 = synth_stereo_steps(4, 2, W, H)[:2]
+    ref = det.read(det.detect_host(L, R, 0.1), 0)
+    left = torch.from_numpy(L[None].copy()).to(dev)
+    right = torch.from_numpy(R[None].copy()).to(dev)
+    ts = torch.tensor([0.1], dtype=torch.float64, device=dev)
+    nl = torch.from_numpy(L2[None].copy()).to(dev)
+    nr = torch.from_numpy(R2[None].copy()).to(dev)
+    torch.cuda.synchronize()
+    fr = det.detect(left, right, ts, n=1)
+    with torch.cuda.stream(s):   # the next frame written into the same buffers at once
+        left.copy_(nl)
+        right.copy_(nr)
+        ts.fill_(0.2)
+    got = det.read(fr, 0)
+    for k in ref:
+        assert got[k].tobytes() == ref[k].tobytes(), k
+    det.status()
+    det.close()
+    ctx.close()
+
+
+def test_camera_and_cut_config_state_rules():
+    """gfpl_set_camera is refused (GFPL_E_STATE) while a seqbatch or a detector object of the
+    context lives; gfpl_set_config rejects a cut step that is not a positive finite number and
+    an unordered cut range (GFPL_E_INVALID)."""
+    cfg = gfpl.default_config()
+    cam = gfpl.make_camera("vga", cfg)
+    ctx = gfpl.Context(cam, cfg)
+    L = ctx.L
+    for bad in (0.0, -0.05, float("nan"), float("inf")):
+        c = gfpl.default_config()
+        c.cut_step = bad
+        assert L.gfpl_set_config(ctx.h, gfpl.C.byref(c)) == -1, bad
+    c = gfpl.default_config()
+    c.cut_rng[0], c.cut_rng[1] = 0.5, 0.25
+    assert L.gfpl_set_config(ctx.h, gfpl.C.byref(c)) == -1
+    assert L.gfpl_set_config(ctx.h, gfpl.C.byref(gfpl.default_config())) == 0
+    assert L.gfpl_set_camera(ctx.h, gfpl.C.byref(cam)) == 0          # nothing built on it yet
+    h = gfpl.StereoFrameHandler(ctx, 2, 256, 64)
+    assert L.gfpl_set_camera(ctx.h, gfpl.C.byref(cam)) == -6
+    h.close()
+    orb = gfpl.ORBextractor(500, 1.2, 3, 20, 7, int(cam.width), int(cam.height), ctx=ctx)
+    assert L.gfpl_set_camera(ctx.h, gfpl.C.byref(cam)) == -6
+    orb.close()
+    assert L.gfpl_set_camera(ctx.h, gfpl.C.byref(cam)) == 0
+    ctx.close()
