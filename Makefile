@@ -20,7 +20,8 @@ HIP_HDR  := $(wildcard $(PKG)/csrc/*.hpp) include/gfpl.h
 
 BINDIR   := $(PKG)/bin
 
-all: $(LIBDIR)/libgfpl_hip.so $(LIBDIR)/libgfpl_synth.so oracle/liboracle.so $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu
+all: $(LIBDIR)/libgfpl_hip.so $(LIBDIR)/libgfpl_synth.so oracle/liboracle.so $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu \
+     $(BINDIR)/mirror_maphandler
 
 $(LIBDIR)/libgfpl_hip.so: $(HIP_SRC) $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
@@ -36,6 +37,12 @@ $(LIBDIR)/libgfpl_stvo.so: $(PKG)/host/stvo.cpp $(PKG)/host/stvo.h include/gfpl.
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -lgfpl_hip -Wl,-rpath,'$$ORIGIN'
 
 $(BINDIR)/plslam_gpu: $(PKG)/host/plslam_gpu.cpp $(LIBDIR)/libgfpl_stvo.so $(LIBDIR)/libgfpl_synth.so
+	@mkdir -p $(BINDIR)
+	$(CXX) -O2 -std=c++17 -ffp-contract=off -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lgfpl_stvo -lgfpl_hip -l:libgfpl_synth.so -lpthread \
+	    -Wl,-rpath,'$$ORIGIN/../lib'
+
+# a MapHandler-shaped caller of the mirror's StereoFrame members (tests/test_mirror_members.py)
+$(BINDIR)/mirror_maphandler: tests/mirror_maphandler.cpp $(LIBDIR)/libgfpl_stvo.so $(LIBDIR)/libgfpl_synth.so
 	@mkdir -p $(BINDIR)
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lgfpl_stvo -lgfpl_hip -l:libgfpl_synth.so -lpthread \
 	    -Wl,-rpath,'$$ORIGIN/../lib'
@@ -59,9 +66,9 @@ oracle-asan: oracle/build/asan_driver
 oracle: oracle/liboracle.so
 synth: $(LIBDIR)/libgfpl_synth.so
 hip: $(LIBDIR)/libgfpl_hip.so
-host: $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu
+host: $(LIBDIR)/libgfpl_stvo.so $(BINDIR)/plslam_gpu $(BINDIR)/mirror_maphandler
 
 clean:
-	rm -f $(LIBDIR)/*.so oracle/liboracle.so $(BINDIR)/plslam_gpu oracle/build/asan_driver
+	rm -f $(LIBDIR)/*.so oracle/liboracle.so $(BINDIR)/plslam_gpu $(BINDIR)/mirror_maphandler oracle/build/asan_driver
 
 .PHONY: all clean oracle oracle-asan synth hip host

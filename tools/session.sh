@@ -4,7 +4,7 @@
 # Every step runs under its own time limit; the steps are chained and the session stops at
 # the first failure (no GPU step after a fault, abort or timeout).  Output: gpurun_out/NAME/.
 # Steps:
-#   tests[:EXPR]        pytest -m gpu (optionally -k EXPR)
+#   tests[:A,B,...]     pytest -m gpu (optionally -k "A or B or ...")
 #   smoke               __graft_entry__.smoke()
 #   bench[:ARGS]        bench.py --steps 20 --warmup 5 ARGS (ARGS: comma-separated, e.g. bench:--cut-proof,--no-cpu)
 #   quick[:ARGS]        bench.py --steps 5 --warmup 2, tracking only (no CPU / detection / host-fed / B=1 legs)
@@ -27,7 +27,8 @@ for step in "$@"; do
   echo "== $step"
   case $kind in
     tests)
-      timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu ${arg:+-k "$arg"} --timeout 300 --timeout-method thread \
+      kexpr=$(echo "$arg" | sed "s/,/ or /g")
+      timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu ${kexpr:+-k "$kexpr"} --timeout 300 --timeout-method thread \
           > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error|passed|failed" $O/pytest_gpu.log | tail -15; exit 1; }
       tail -1 $O/pytest_gpu.log ;;
     smoke)
