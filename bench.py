@@ -60,6 +60,8 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # per SIMD (MI355X_MICROARCH.md §Wave scheduling) = 1228.8 G wave-instructions/s
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2
 
+CUT_MODES = {0: "measured", 1: "proven", 2: "proven-eager", 3: "proven-redo-all"}
+
 # Every workload re-spawns its landmarks (gfpl_synth `respawn`: each pool slot is re-sampled in
 # the current frustum every `respawn` frames, phases spread), so 90 % of the detections observe a
 # landmark at every frame (10 % distractors) and the per-step work is stationary.
@@ -117,8 +119,10 @@ def parse(argv=None):
                          "and the instrumented builds' clocks (gfpl_debug_clocks, *_clk.npy)")
     ap.add_argument("--cut-certify", type=float, default=None,
                     help="gfpl_config.cut_certify (the certified line-cut margin; default: the library's)")
-    ap.add_argument("--cut-proof", action="store_true",
-                    help="gfpl_config.cut_proof = 1: margined line-cut decisions only under the proven bound")
+    ap.add_argument("--cut-proof", type=int, nargs="?", const=1, default=None,
+                    help="gfpl_config.cut_proof: 0 measured, 1 proven (the recorded search proven after the fact, "
+                         "unproven sequences redone eagerly), 2 eager-proven search (DESIGN.md §3); default: the "
+                         "library's")
     ap.add_argument("--b1-steps", type=int, default=40, help="timed steps of the B = 1 latency leg")
     ap.add_argument("--parity-seqs", type=int, default=16, help="sampled sequences replayed on the oracle per rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -634,8 +638,8 @@ def main():
     cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     if args.cut_certify is not None:
         cfg.cut_certify = args.cut_certify
-    if args.cut_proof:
-        cfg.cut_proof = 1
+    if args.cut_proof is not None:
+        cfg.cut_proof = args.cut_proof
     cam = gfpl.make_camera(cam_name, cfg)
     if world > 1:
         # RCCL broadcast of the camera + config block; every rank
@@ -782,7 +786,7 @@ def main():
     if sampler:
         sampler.initialize(h)
     step_s = []
-    stage_ms, stage_bytes, kern_ms, kern_bytes, counts, cutc = [], [], [], [], [], []
+    stage_ms, stage_bytes, kern_ms, kern_bytes, counts, cutc, proofc = [], [], [], [], [], [], []
     ctx.set_timing(True)
     for k in range(1, 1 + W + K):
         t0 = time.perf_counter()
@@ -803,6 +807,7 @@ def main():
             kern_bytes.append(h.last_step_kernel_bytes())
             counts.append(h.last_step_counts())
             cutc.append(h.last_step_track_counts())
+            proofc.append(h.last_step_cut_proof())
         if sampler:
             sampler.step(h, k)
         if rank == 0:   # progress (stderr): long runs under a watchdog keep writing
@@ -927,7 +932,17 @@ def main():
                                            "cut endpoints, pose (DT, Tfw, DT_cov, Tfw_cov, eig, err_norm) bitwise "
                                            "vs the CPU oracle (oracle/)",
                                "first": sampler.msgs[:3] if sampler else []},
-            "cut_search": {"mode": "proven" if cfg.cut_proof else "measured", "cut_certify": float(cfg.cut_certify),
+            "cut_search": {"mode": CUT_MODES[int(cfg.cut_proof)], "cut_certify": float(cfg.cut_certify),
+                           "proof": ({"redone_sequences": int(sum(c["redone"] for c in proofc)),
+                                      "redone_frac": float(sum(c["redone"] for c in proofc) / (B * K)),
+                                      "steps_proven_after_the_fact": int(sum(c["steps_proven"] for c in proofc)),
+                                      "vref_evals_per_line": float(sum(c["vref_evals"] for c in proofc) /
+                                                                   max(1, sum(c["lines"] for c in proofc))),
+                                      "note": "k_cut_verify: every margined decision of the recorded search proven "
+                                              "with the reference's own endpoint variances at the compared ratios "
+                                              "and the two running invCov_sums; unproven sequences redone by the "
+                                              "eager-proven search (DESIGN.md §3)"}
+                                     if cfg.cut_proof == 1 else None),
                            "steps": int(sum(c["steps"] for c in cutc)),
                            "exact_steps": int(sum(c["exact_steps"] for c in cutc)),
                            "exact_frac": float(sum(c["exact_steps"] for c in cutc) / max(1, sum(c["steps"] for c in cutc))),

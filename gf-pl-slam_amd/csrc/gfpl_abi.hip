@@ -157,6 +157,8 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cross_tinv = c.take<double>(B * 16);
     sb->scr.dbg = c.take<int64_t>(B * 8);
     sb->scr.cut_prog = c.take<int32_t>((size_t)1 << 17);
+    sb->scr.cut_path = c.take<uint8_t>(B * sb->mls_cap * CUT_PATH);
+    sb->scr.cut_flag = c.take<int32_t>(B);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);
@@ -265,7 +267,7 @@ int cfg_supported(const gfpl_config& c) {
     if (c.max_line_match_num < 1 || c.max_line_match_num > GFPL_MAX_MATCHED_LS) return GFPL_E_INVALID;
     // the certified cut search needs a margin far above its ~1e-13 error
     if (!(c.cut_certify == 0.0 || (c.cut_certify >= 1e-10 && c.cut_certify < 1.0))) return GFPL_E_INVALID;
-    if (c.cut_proof != 0 && c.cut_proof != 1) return GFPL_E_INVALID;
+    if (c.cut_proof < 0 || c.cut_proof > 3) return GFPL_E_INVALID;
     // the search's ratio keys and their +-s links are formed from a positive finite step
     // (params(): with s <= 0 or NaN no key would exist and the proven search would follow
     // zeroed links); the range must be an ordered finite interval
@@ -1328,6 +1330,16 @@ int gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4) {
     int e = step_rec_sums(sb, v);
     if (e) return e;
     for (int s = 0; s < 4; ++s) counts4[s] = v[16 + s];
+    return GFPL_OK;
+}
+
+int gfpl_last_step_cut_proof(gfpl_seqbatch* sb, int64_t* counts4) {
+    if (!sb || !counts4) return GFPL_E_INVALID;
+    int64_t v[STEP_REC];
+    int e = step_rec_sums(sb, v);
+    if (e) return e;
+    const bool on = sb->ctx->cfg.cut_proof == 1 || sb->ctx->cfg.cut_proof == 3;
+    for (int s = 0; s < 4; ++s) counts4[s] = on ? v[20 + s] : 0;
     return GFPL_OK;
 }
 

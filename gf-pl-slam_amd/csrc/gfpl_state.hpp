@@ -72,11 +72,17 @@ struct DevTrack {
     int32_t* kf_flag;      // [B] last needNewKF decision
 };
 
-#define STEP_REC 20   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
+#define STEP_REC 24   // int64 per sequence in DevScratch::bytes: [0..5] stage bytes, [6] total, [7] k_cut_search,
                       // [8..15] counts N_o N_k M_o S_p' S_l' M_p M_l n_inliers (gfpl_last_step_counts),
                       // [16] line-cut search steps, [17] of them evaluated exactly (k_cut_search),
                       // [18] n_inliers after optimize_pose (k_pose_finish), [19] lines whose agreement bound
-                      // was unusable (k_cut_search: R0 <= 0 or a term not finite; their steps are exact)
+                      // was unusable (k_cut_search: R0 <= 0 or a term not finite; their steps are exact),
+                      // proven mode (k_cut_verify): [20] 1 if the recorded search was not proven (the
+                      // eager-proven search redid it), [21] margined steps verified, [22] the reference's
+                      // endpoint variances evaluated, [23] lines with margined steps
+#define CUT_PATH 64   // proven mode: recorded search steps per line (k_cut_search -> k_cut_verify)
+#define CUT_P_STAY 8  //   step byte: no neighbour beat the centre (the line ends), else the move j (0-7)
+#define CUT_P_EXACT 16 //  step byte flag: the step was decided by the reference's arithmetic (exact round)
 #define CUT_KS 22     // proven line cut: ratio keys per side (KParams::cut_keys)
 #define CUT_FAST 56   // doubles of per-line comparison data (k_cut.hip, PD_*): polynomials, flags, error bounds
 #define CUT_REC 80    // doubles of a per-line cut record: comparison data | r = 0 info (21) | pad (640 B)
@@ -104,6 +110,8 @@ struct DevScratch {
     double* cross_tinv; // [B*16] inverse of the predicted curr.Tfw (k_predict_pose -> k_cross_points)
     int64_t* dbg;       // [B*8] diagnostic clocks (only builds with -DGFPL_SP_CLOCK write them)
     int32_t* cut_prog;  // [1 << 17] k_cut_search: lines done per (XCC, SE, SH, CU, SIMD, wave slot)
+    uint8_t* cut_path;  // [B*mls_cap*CUT_PATH] proven mode: every line's recorded search steps
+    int32_t* cut_flag;  // [B] proven mode: 1 = the recorded search was not proven (redo it eagerly)
 };
 
 // Everything a kernel needs, passed by value (kernarg segment).

@@ -14,6 +14,8 @@
 //               the cut endpoints of every matched line.
 // Only the lower triangle is carried through the search: LLT reads nothing
 // else (ledger Q11).
+#include <cstdlib>
+
 #include "gfpl_kernels.hpp"
 
 namespace gfpl {
@@ -405,7 +407,7 @@ __global__ void __launch_bounds__(256) k_cut_vtab(KParams p) {
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
     const int nk = p.cut_nkeys;
-    if (nls == 0 || nk == 0) return;
+    if (nls == 0 || nk == 0 || (p.cfg.cut_proof != 2 && p.scr.cut_flag[b] == 0)) return;
     const DevLines& L = p.prev.ls;
     const double* Dl = p.scr.cut_dtinv + 16 * (size_t)b;
     const int per = 2 * nk;
@@ -418,23 +420,17 @@ __global__ void __launch_bounds__(256) k_cut_vtab(KParams p) {
     }
 }
 
-__global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
-    const int b = blockIdx.y;
-    const int m = blockIdx.x * 64 + threadIdx.x;
-    const int nls = p.tr.n_matched_ls[b];
-    if (m >= nls) return;
+// the line's operand error bounds (above) for line q of sequence b: eb[0..5] / [7..12] the start /
+// end side's |P - P*| in P units, eb[6] / [13] the blended depth's relative error bound; +inf: no
+// usable bound (the line's steps are then exact)
+__device__ __attribute__((noinline)) void cut_line_bounds(const KParams& p, size_t q, bool pd_ok, const double* Dl,
+                                                          float* eb) {
     const DevLines& L = p.prev.ls;
-    const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
-    double* rec = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
-    double Dl[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     const double C = fmax(rhi, 0.0), T = fmax(fabs(rlo), fabs(rhi));
-    float eb[14];
 #pragma unroll
     for (int i = 0; i < 14; ++i) eb[i] = __builtin_inff();
-    bool ok = rlo >= 0.0 && rhi <= 1.0 && rec[PD_OK] != 0.0 && p.cam.fx > 0.0;
+    bool ok = rlo >= 0.0 && rhi <= 1.0 && pd_ok && p.cam.fx > 0.0;
     RB sP[3], eP[3], cS[9], cE[9], Jl[2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) { sP[k] = RB(L.sP[3 * q + k]); eP[k] = RB(L.eP[3 * q + k]); }
@@ -468,19 +464,18 @@ __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
     }
     if (ok) {
         const double cam_fx = p.cam.fx;
-        const double s1 = zmax * zmax / cam_fx, s2 = s1 * s1;   // 1 / fgz2*_min, its square
+        const double s1 = zmax * zmax / cam_fx;   // 1 / fgz2*_min
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             RB o7[7];
             cut_endpoint_t<RB, false>(p.cam, p.cfg.homog_th, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS,
-                               side ? cS : cE, RB(C, 0.0, 0.0), o7, zlo);
+                                      side ? cS : cE, RB(C, 0.0, 0.0), o7, zlo);
             // 1% slop: the bound arithmetic's own rounding
 #pragma unroll
             for (int i = 0; i < 6; ++i) eb[7 * side + i] = ceil_f32(1.01 * (eo[side][i] + o7[1 + i].e * s1));
             // v': the proven search evaluates with the reference's own endpoint variances scaled by
             // fgz2 = fx / gz^2 of the blended point (its v'-table): slot 6 is gz's relative error
             // bound over the range (the blend and DT_inv's rounding), which the scaling carries x 4
-            (void)s2;
             {
                 const RB c(C, 0.0, 0.0);
                 const RB* Q0 = side ? eP : sP;
@@ -494,6 +489,22 @@ __global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
             }
         }
     }
+}
+
+// eager-proven mode (cut_proof 2, or the sequences cut_proof 1 could not verify): the bounds into
+// the records, one thread per line
+__global__ void __launch_bounds__(64) k_cut_bounds(KParams p) {
+    const int b = blockIdx.y;
+    const int m = blockIdx.x * 64 + threadIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    if (m >= nls || (p.cfg.cut_proof != 2 && p.scr.cut_flag[b] == 0)) return;
+    const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+    double* rec = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
+    float eb[14];
+    cut_line_bounds(p, q, rec[PD_OK] != 0.0, Dl, eb);
     float* out = reinterpret_cast<float*>(rec + PD_ERR);
 #pragma unroll
     for (int i = 0; i < 14; ++i) out[i] = eb[i];
@@ -636,6 +647,23 @@ __device__ __forceinline__ double h4abs(const double* c, double t) {
 }
 __device__ __forceinline__ double h2(double c0, double c1, double c2, double t) {
     return __builtin_fma(t, __builtin_fma(t, c2, c1), c0);
+}
+
+// The measured search's own (approximate) info of a finished line at its final ratios, which it adds
+// to its running invCov_sum: xs = [v'_s, P_s[6], v'_e, P_e[6]] from the line's comparison data (or the
+// reference-order endpoints when PD_OK = 0), entry (ra, cb) = Ps Ps^T / v'_s + Pe Pe^T / v'_e.  Shared
+// by k_cut_search and k_cut_verify, which replays the search's running sum bit for bit.
+__device__ __forceinline__ double cut_ours_P(const double* fd, int side, int i, double t) {
+    const int o = side ? PD_PE : PD_PS;
+    return h2(fd[o + i], fd[o + 6 + i], fd[o + 12 + i], t);
+}
+__device__ __forceinline__ double cut_ours_V(const double* fd, int side, double t) {
+    const int o = side ? PD_VE : PD_VS;
+    return __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, fd[o + 4], fd[o + 3]), fd[o + 2]),
+                                          fd[o + 1]), fd[o]);
+}
+__device__ __forceinline__ double cut_ours_info(const double* xs, double is, double ie, int ra, int cb) {
+    return __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
 }
 
 // Comparison polynomials of the current line, one copy per lane (registers).
@@ -1053,8 +1081,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
-    const bool live = b < p.B;
+    // proven mode (cut_proof 1 / 3): the eager-proven search runs only for the sequences whose
+    // recorded search k_cut_verify did not prove (cut_flag); cut_proof 2 runs it for all of them
+    const bool live = b < p.B && (!PROOF || p.cfg.cut_proof == 2 || p.scr.cut_flag[b] != 0);
     const int nls = live ? p.tr.n_matched_ls[b] : 0;
+    // proven mode, first pass (the measured search): every step's decision is recorded for
+    // k_cut_verify — one byte per step and line, CUT_PATH per line
+    const bool rec = !PROOF && p.cfg.cut_proof != 0;
+    uint8_t* const path = p.scr.cut_path + (size_t)(live ? b : 0) * p.mls_cap * CUT_PATH;
+    int lstep = 0;       // steps taken on the current line
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     const double tau = p.cfg.cut_certify;
@@ -1299,6 +1334,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (exact) { dnext = sd; cnext = sb; }
         }
         int finalize = 0;
+        if (rec && act && j == 0) {   // move j | CUT_P_STAY (no better neighbour) | CUT_P_EXACT
+            if (lstep < CUT_PATH)
+                path[(size_t)m * CUT_PATH + lstep] =
+                    (uint8_t)((best >= 0 ? best : CUT_P_STAY) | (exact ? CUT_P_EXACT : 0));
+            ++lstep;
+        }
         if (act) {
             first = 0;
             if (best >= 0) {
@@ -1346,13 +1387,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 // being the same matrix as P P^T / v'
                 if (!PROOF && fst[g][PD_OK] != 0.0) {   // (proven mode: the reference's endpoints, below)
                     if (j < 6) {
-                        xs[1 + j] = h2(fst[g][PD_PS + j], fst[g][PD_PS + 6 + j], fst[g][PD_PS + 12 + j], r0);
-                        xs[8 + j] = h2(fst[g][PD_PE + j], fst[g][PD_PE + 6 + j], fst[g][PD_PE + 12 + j], r1);
+                        xs[1 + j] = cut_ours_P(fst[g], 0, j, r0);
+                        xs[8 + j] = cut_ours_P(fst[g], 1, j, r1);
                     } else {
-                        const int o = j == 6 ? PD_VS : PD_VE;
-                        const double t = j == 6 ? r0 : r1;
-                        xs[7 * (j - 6)] = __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, fst[g][o + 4], fst[g][o + 3]),
-                                                       fst[g][o + 2]), fst[g][o + 1]), fst[g][o]);
+                        xs[7 * (j - 6)] = cut_ours_V(fst[g], j - 6, j == 6 ? r0 : r1);
                     }
                 } else if (j < 2) {
                     double o7[7];
@@ -1377,7 +1415,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                         const double T0 = xs[1 + ra] * i00 + xs[8 + ra] * i10, T1 = xs[1 + ra] * i01 + xs[8 + ra] * i11;
                         info[kk] = T0 * xs[1 + cb] + T1 * xs[8 + cb];
                     } else {
-                        info[kk] = __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
+                        info[kk] = cut_ours_info(xs, is, ie, ra, cb);
                     }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
@@ -1401,6 +1439,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 q_nx = lb + (size_t)(int)fst[g][PD_NEXT];
                 if (PROOF) m_sync = m;   // sumE was brought up to line m above
                 first = 1;
+                lstep = 0;
                 r0 = 0.0;
                 r1 = 0.0;
 #pragma unroll
@@ -1452,6 +1491,314 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
 }
 
+// ------------------------------------------------------- small-batch search --
+// One sequence per wave, for small batches (B <= CUT_WAVE_MAX_B: the latency of one sequence, e.g. the
+// reference app's one stream per process, app/plslam_mod.cpp:387-411).  Same decisions, same bits as
+// k_cut_search<false> (measured mode, with the proven mode's step record): a round evaluates d on the 7 x 7
+// grid of ratios around the centre (lane a * 7 + c: offsets a - 3, c - 3, 49 lanes), which holds the 8
+// neighbours of every position up to three greedy steps away, then resolves up to three steps in order
+// from those values — each with the one-step search's first-strict-maximum rule and margin tests.  The
+// grid's ratios are accumulated as the search's moves accumulate them (r + s + s, r + (-s) + (-s)); a
+// step whose neighbours' ratio bits differ from the grid's (a ratio that moved back), or that a margin
+// test sends to the exact path, ends the round.  Exact steps and the lazy exact invCov_sum are
+// cut_exact_round's, run by the wave as group 0.  Line transitions run on the whole wave at once.
+#ifndef CUT_WAVE_MAX_B
+#define CUT_WAVE_MAX_B 2048
+#endif
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int nb_da(int j, int side) {   // neighbour j's offset on a side (nb_step's sign)
+    if (side == 0) return (j == 0 || j == 4 || j == 5) ? 1 : ((j == 1 || j == 6 || j == 7) ? -1 : 0);
+    return (j == 2 || j == 4 || j == 6) ? 1 : ((j == 3 || j == 5 || j == 7) ? -1 : 0);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search_w(KParams p) {
+    __shared__ double sumA[25];                 // approximate S of the current line
+    __shared__ double sumE[25];                 // exact invCov_sum before line m_sync (lazy, exact steps)
+    __shared__ double fst[CUT_FAST + 1];        // comparison data of the current line
+    __shared__ double tmp[CUT_G][CUT_EP + 25 + 1];   // exact round: row 0 | the flush staging (all rows)
+    __shared__ double wgs[64];                  // line open: W [6][6] | Gram (21) at 36
+    __shared__ double xsl[16];                  // transition: the finished line's [v'_s, P_s, v'_e, P_e]
+    __shared__ CutCmp cmpl;
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    const DevCam& cam = p.cam;
+    const double homog = p.cfg.homog_th;
+    const double tau = p.cfg.cut_certify;
+    const double tq = p.cut_tq;
+    DevLines& L = p.prev.ls;
+    const size_t lb = (size_t)b * p.kl_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
+    const double* rec_l = p.scr.cut_rec + (size_t)b * p.mls_cap * CUT_REC;
+    const double* Dl = p.scr.cut_dtinv + 16 * (size_t)b;
+    const double st = p.cfg.cut_step;
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const bool rec = p.cfg.cut_proof != 0;
+    uint8_t* const path = p.scr.cut_path + (size_t)b * p.mls_cap * CUT_PATH;
+    constexpr unsigned long long TRI_ROW = tri_pack(1), TRI_COL = tri_pack(0);
+    int m = 0, m_sync = 0, first = 1, line_ok = 0, c_ok = 0, lstep = 0;
+    double r0 = 0.0, r1 = 0.0, dc = 0.0;
+    size_t q_cur = 0;
+    int n_steps = 0, n_exact = 0;
+    // A line opens (fst and sumA hold its data): the k_cut_search<false> open, one lane per role
+    auto open_line = [&]() {
+        double o[28];
+        {
+            double S[21];
+#pragma unroll
+            for (int e = 0; e < 21; ++e) S[e] = sumA[e];
+            chol_s(S, o);
+        }
+        line_ok = (o[27] != 0.0) && (fst[PD_OK] != 0.0);
+        if (lane < 6) {
+            double w[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double u = fst[6 * lane + i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) u = __builtin_fma(-o[tri(i, k)], w[k], u);
+                w[i] = u * o[21 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) wgs[6 * lane + i] = w[i];
+        }
+        wave_lds_sync();
+        if (lane < 21) {
+            const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
+            double s = wgs[6 * ra] * wgs[6 * cb];
+#pragma unroll
+            for (int i = 1; i < 6; ++i) s = __builtin_fma(wgs[6 * ra + i], wgs[6 * cb + i], s);
+            wgs[36 + lane] = s;
+        }
+        wave_lds_sync();
+        const double* gm = wgs + 36;
+        double* cl = reinterpret_cast<double*>(&cmpl);
+        if (lane < 2) {
+            const int a = 3 * lane, b2 = a + 1, c2 = a + 2;
+            double* oo = cl + 5 * lane;   // ns | ne
+            oo[0] = gm[tri(a, a)];
+            oo[1] = 2.0 * gm[tri(b2, a)];
+            oo[2] = __builtin_fma(2.0, gm[tri(c2, a)], gm[tri(b2, b2)]);
+            oo[3] = 2.0 * gm[tri(c2, b2)];
+            oo[4] = gm[tri(c2, c2)];
+        } else if (lane < 4) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) cl[10 + 5 * (lane - 2) + i] = fst[PD_VS + 5 * (lane - 2) + i];
+        } else if (lane < 7) {
+            const int i = lane - 4;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cl[20 + 3 * i + k] = gm[tri(3 + k, i)];
+            const double gs = fmax(gm[tri(i, i)], 0.0), ge = fmax(gm[tri(3 + i, 3 + i)], 0.0);
+            cl[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
+            cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+        }
+        wave_lds_sync();
+        const double T = fmax(fabs(rlo), fabs(rhi));
+        if (lane == 7) {
+            const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
+            const double VsA = h4abs(cl + 10, T), VeA = h4abs(cl + 15, T);
+            const double Bs2 = Bs * Bs, Be2 = Be * Be;
+            cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+            cl[36] = VsA;
+            cl[37] = VeA;
+        }
+        wave_lds_sync();
+        dc = cut_dcore_p1<false>(cl[0], cl[10], cl[5], cl[15], cl[20], cl[35], cl[36], cl[37], cmpl.eb, tq, c_ok);
+    };
+    if (nls > 0) {
+        q_cur = lb + mls[0];
+        for (int e = lane; e < CUT_FAST; e += 64) fst[e] = rec_l[e];
+        if (lane < 21) {
+            const double s0 = p.scr.cut_sum[24 * b + lane];
+            sumA[lane] = s0 - rec_l[CUT_FAST + lane];
+            sumE[lane] = s0;
+        }
+        wave_lds_sync();
+        open_line();
+    }
+    while (m < nls) {   // (wave-uniform)
+        // ---- the 7 x 7 grid of ratios around the centre, as the moves accumulate them
+        double g0[7], g1[7];
+        g0[3] = r0;
+        g1[3] = r1;
+#pragma unroll
+        for (int k = 4; k < 7; ++k) { g0[k] = g0[k - 1] + st; g1[k] = g1[k - 1] + st; }
+#pragma unroll
+        for (int k = 2; k >= 0; --k) { g0[k] = g0[k + 1] + (-st); g1[k] = g1[k + 1] + (-st); }
+        int dj_valid = 0, bok = 0;
+        double dj = 0.0;
+        if (lane < 49) {
+            const int a = lane / 7, c = lane - 7 * (lane / 7);
+            double t0 = g0[0], t1 = g1[0];
+#pragma unroll
+            for (int k = 1; k < 7; ++k) { t0 = a == k ? g0[k] : t0; t1 = c == k ? g1[k] : t1; }
+            int valid = 1;
+            if (t0 + t1 > 1.0) valid = 0;
+            if (t0 < rlo || t0 > rhi) valid = 0;
+            if (t1 < rlo || t1 > rhi) valid = 0;
+            dj_valid = valid;
+            CutReg cr;
+            cut_reg_load(cmpl, cr);
+            dj = cut_dval<false>(cr, t0, t1, tq, bok);
+        }
+        // ---- up to three steps from the grid
+        int pa = 3, pc = 3;
+        int exact = 0, finalize = 0;
+        double vj[8];
+        int bj[8], valj[8];
+        for (int sstep = 0; sstep < 3; ++sstep) {   // (wave-uniform)
+            // the 8 neighbours' ratios must be the grid's bits
+            bool cons = true;
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const int pp = side ? pc : pa;
+                const double* gg = side ? g1 : g0;
+                double cur = gg[0], up = gg[0], dn = gg[0];
+#pragma unroll
+                for (int k = 0; k < 7; ++k) {
+                    cur = pp == k ? gg[k] : cur;
+                    up = pp + 1 == k ? gg[k] : up;
+                    dn = pp - 1 == k ? gg[k] : dn;
+                }
+                cons = cons && pp >= 1 && pp <= 5 &&
+                       __double_as_longlong(cur + st) == __double_as_longlong(up) &&
+                       __double_as_longlong(cur + (-st)) == __double_as_longlong(dn);
+            }
+            if (!cons) break;
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                const int l = (pa + nb_da(jn, 0)) * 7 + (pc + nb_da(jn, 1));
+                vj[jn] = readlane_f64(dj, l);
+                bj[jn] = __builtin_amdgcn_readlane(bok, l);
+                valj[jn] = __builtin_amdgcn_readlane(dj_valid, l);
+            }
+            // k_cut_search's group decision and margin tests (group_first_max, f1-f5), on the 8 values
+            double mx = -__builtin_inf();
+            double x[8];
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                x[jn] = (valj[jn] && vj[jn] == vj[jn]) ? vj[jn] : -__builtin_inf();
+                mx = fmax(mx, x[jn]);
+            }
+            int kf = 8;
+#pragma unroll
+            for (int jn = 7; jn >= 0; --jn) kf = (x[jn] == mx && mx > -__builtin_inf()) ? jn : kf;
+            const int best = (kf < 8 && mx > dc) ? kf : -1;
+            const double top = mx;
+            const bool has = best >= 0;
+            bool ok = !(has & !(top - dc > tau * top)) && ((tau > 0.0) & (line_ok != 0) & (c_ok != 0) & (dc == dc));
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                const bool vl = valj[jn] != 0;
+                const bool f1 = vl & !bj[jn];
+                const bool f2 = has & vl & (jn != best) & !(top - vj[jn] > tau * top);
+                const bool f4 = !has & vl & !(dc - vj[jn] > tau * dc);
+                ok = ok && !(f1 | f2 | f4);
+            }
+            if (!ok) { exact = 1; break; }
+            ++n_steps;
+            if (rec && lane == 0) {
+                if (lstep < CUT_PATH) path[(size_t)m * CUT_PATH + lstep] = (uint8_t)(has ? best : CUT_P_STAY);
+            }
+            ++lstep;
+            first = 0;
+            if (!has) { finalize = 1; break; }
+            pa += nb_da(best, 0);
+            pc += nb_da(best, 1);
+            dc = vj[best];
+            c_ok = bj[best];
+            r0 = r0 + nb_step(best, 0, st);
+            r1 = r1 + nb_step(best, 1, st);
+            if (!(r0 + r1 <= 1.0)) { finalize = 1; break; }
+        }
+        if (exact) {
+            // the reference's evaluation of this step (group 0 = lanes 0-7; the flush uses the wave);
+            // the neighbours' values were gathered by the step that stopped
+            int myv = 0;
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) myv = lane == jn ? valj[jn] : myv;
+            const CutX xr = cut_exact_round(lane < 8, myv, first, m, m_sync, r0, r1, q_cur, lb, -1, mls, rec_l, L.sP,
+                                            L.eP, L.covS, L.covE, L.le_obs, L.cut, sumE, tmp[0], &tmp[0][0], Dl,
+                                            cam.fx, cam.b, homog, st);
+            const int best = __builtin_amdgcn_readfirstlane(xr.best);
+            m_sync = __builtin_amdgcn_readfirstlane(xr.m_sync);
+            ++n_steps;
+            ++n_exact;
+            if (rec && lane == 0) {
+                if (lstep < CUT_PATH)
+                    path[(size_t)m * CUT_PATH + lstep] = (uint8_t)((best >= 0 ? best : CUT_P_STAY) | CUT_P_EXACT);
+            }
+            ++lstep;
+            first = 0;
+            if (best < 0) {
+                finalize = 1;
+            } else {
+                double vb = vj[0];
+                int bb = bj[0];
+#pragma unroll
+                for (int jn = 1; jn < 8; ++jn) { vb = best == jn ? vj[jn] : vb; bb = best == jn ? bj[jn] : bb; }
+                dc = vb;
+                c_ok = bb;
+                r0 = r0 + nb_step(best, 0, st);
+                r1 = r1 + nb_step(best, 1, st);
+                if (!(r0 + r1 <= 1.0)) finalize = 1;
+            }
+        }
+        if (finalize) {
+            if (lane == 0) {
+                L.cut[2 * q_cur] = r0;
+                L.cut[2 * q_cur + 1] = r1;
+            }
+            // the approximate invCov_sum += the finished line's info (k_cut_search's transition)
+            if (fst[PD_OK] != 0.0) {
+                if (lane < 6) {
+                    xsl[1 + lane] = cut_ours_P(fst, 0, lane, r0);
+                    xsl[8 + lane] = cut_ours_P(fst, 1, lane, r1);
+                } else if (lane < 8) {
+                    xsl[7 * (lane - 6)] = cut_ours_V(fst, lane - 6, lane == 6 ? r0 : r1);
+                }
+            } else if (lane < 2) {
+                double o7[7];
+                exact_endpoint(cam, homog, Dl, L, q_cur, lane, lane ? r1 : r0, o7);
+#pragma unroll
+                for (int i = 0; i < 7; ++i) xsl[7 * lane + i] = o7[i];
+            }
+            ++m;
+            wave_lds_sync();
+            if (m < nls) {
+                double info = 0.0;
+                if (lane < 21) {
+                    const double is = rcp_fast(xsl[0]), ie = rcp_fast(xsl[7]);
+                    const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
+                    info = cut_ours_info(xsl, is, ie, ra, cb);
+                }
+                const double* rn = rec_l + (size_t)m * CUT_REC;
+                const double i0n = lane < 21 ? rn[CUT_FAST + lane] : 0.0;
+                double f0 = rn[lane < CUT_FAST ? lane : 0];
+                wave_lds_sync();
+                if (lane < CUT_FAST) fst[lane] = f0;
+                if (lane < 21) sumA[lane] = (sumA[lane] + info) - i0n;
+                q_cur = lb + mls[m];
+                first = 1;
+                lstep = 0;
+                r0 = 0.0;
+                r1 = 0.0;
+                wave_lds_sync();
+                open_line();
+            }
+        }
+    }
+    if (lane == 0) {
+        p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
+        p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
+        p.scr.bytes[(size_t)STEP_REC * b + 19] = 0;
+    }
+}
+
 // ---------------------------------------------------------------- finish --
 // invCovPose of the chosen ratio + updateEndPointByRatio (ledger Q4)
 #ifndef GFPL_FIN_WAVES
@@ -1460,7 +1807,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
-    if (nls == 0) return;
+    // proven mode (cut_proof 1 / 3): k_cut_verify finished the proven sequences, this kernel the redone ones
+    if (nls == 0 || ((p.cfg.cut_proof == 1 || p.cfg.cut_proof == 3) && p.scr.cut_flag[b] == 0)) return;
     const DevCam& cam = p.cam;
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)b * p.kl_cap;
@@ -1511,19 +1859,347 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     }
 }
 
+// ---------------------------------------------------------------- verify --
+// Proven mode (cut_proof 1): the measured search (k_cut_search<false>) decided every margined step on
+// our comparison operands and recorded its decisions (cut_path); this kernel proves, after the fact,
+// that each of those decisions is the reference's, with the agreement bound of DESIGN.md §3 — now
+// evaluated with the operands' *actual* differences instead of eager reference operands in the search:
+//   * v' (Lemma 2): at every ratio the recorded steps compared, the reference's own endpoint variance
+//     (ref_vprime: cut_endpoint_t<double>'s expression tree, scaled by its fgz2) against the quartic the
+//     search used, r_v(t) = |v'_ours - v'_ref| / v'_ref plus the scaling's bound (RB, cut_line_bounds);
+//   * S (Lemma 3): the search's running invCov_sum (replayed bit for bit in list order: r = 0 infos of
+//     k_cut_prep, the search's own info of each finished line — cut_ours_*) against the reference's (the
+//     same list order with the reference-order info of each line at its final ratios), their difference
+//     whitened by diag(S^-1): eps_S = sum_ik |dS_ik| sqrt(s_i s_k) + our factor's backward error;
+//   * P (Lemma 2): the RB error bounds of our polynomial coefficients and of the reference's Jacobian.
+// Per line: E = K0 + A1 max(1/v's) + 4.12 bs^2 max(r_v,s / v's) + (end side) <= R0 = tau/8 - 1.01 K0,
+// with every maximum over the ratios of the line's margined steps (each step's comparisons then have
+// gaps > tau in d, > tau/2 in exact arithmetic (forward bound), > tau/4 between the reference's metrics).
+// Steps the search decided exactly need nothing.  A sequence with any line not proven (or a path that
+// does not replay to the search's final ratios) is flagged; the eager-proven search then redoes its line
+// cut (k_cut_bounds, k_cut_vtab, k_cut_search<true>, k_cut_finish, gated by the flag).  This kernel is
+// also k_cut_finish for the proven sequences: invCovPose of every line (written for all; a redone
+// sequence overwrites it) and, once the whole sequence is proven, the cut endpoints.
+// One wave per sequence; lines in chunks of 64, one per lane.
+__device__ __forceinline__ double verify_vref(const KParams& p, const double* Dl, size_t q, int side, double t) {
+    return ref_vprime(p.cam, p.cfg.homog_th, Dl, p.prev.ls, q, side, t);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_verify(KParams p) {
+    __shared__ double fo[21][65];   // the chunk's lines: our info, then S_ours of the line
+    __shared__ double fr[21][65];   // the reference's info, then dS = S_ours - S_ref
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int nls = p.tr.n_matched_ls[b];
+    const DevCam& cam = p.cam;
+    const double homog = p.cfg.homog_th;
+    DevLines& L = p.prev.ls;
+    const size_t lb = (size_t)b * p.kl_cap;
+    const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
+    const double* rec_l = p.scr.cut_rec + (size_t)b * p.mls_cap * CUT_REC;
+    const uint8_t* path = p.scr.cut_path + (size_t)b * p.mls_cap * CUT_PATH;
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
+    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const double T = fmax(fabs(rlo), fabs(rhi));
+    const double tau = p.cfg.cut_certify;
+    constexpr double u = 0x1p-53;
+    int bad = p.cfg.cut_proof == 3 ? 1 : 0;   // (cut_proof 3: every sequence redone eagerly — a test hook)
+    int64_t n_marg = 0, n_eval = 0, n_mline = 0;
+    // the running sums of the search (sA: ours, S of the line being opened) and of the reference (sE:
+    // the whole sum before the line's r = 0 info is taken out), lanes 0-20 hold entry lane
+    double sA = 0.0, sE = 0.0;
+    if (nls > 0 && lane < 21) {
+        const double s0 = p.scr.cut_sum[24 * b + lane];
+        sA = s0 - rec_l[CUT_FAST + lane];
+        sE = s0;
+    }
+    for (int c0 = 0; c0 < nls; c0 += 64) {   // (wave-uniform)
+        const int m = c0 + lane;
+        const bool on = m < nls;
+        const size_t q = lb + (on ? mls[m] : mls[0]);
+        const double* fd = rec_l + (size_t)(on ? m : 0) * CUT_REC;
+        const double r0f = L.cut[2 * q], r1f = L.cut[2 * q + 1];
+        // (1) the reference's info at the final ratios: invCovPose (k_cut_finish's), and its lower triangle
+        {
+            LineCutData d;
+            load_line(L, q, d);
+            double info[36];
+            poseInfoOnLine<true>(cam, homog, Dl, d, r0f, r1f, info);
+            if (on) {
+                double2* iv = reinterpret_cast<double2*>(L.invcov + 36 * q);
+#pragma unroll
+                for (int i = 0; i < 18; ++i) iv[i] = make_double2(info[2 * i], info[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int k = 0; k <= i; ++k) fr[tri(i, k)][lane] = info[i * 6 + k];
+            }
+        }
+        // (2) the search's own info of the line (its transition's expressions, cut_ours_*)
+        const bool pdok = fd[PD_OK] != 0.0;
+        {
+            double xs[14];
+            if (pdok) {
+                xs[0] = cut_ours_V(fd, 0, r0f);
+                xs[7] = cut_ours_V(fd, 1, r1f);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) { xs[1 + i] = cut_ours_P(fd, 0, i, r0f); xs[8 + i] = cut_ours_P(fd, 1, i, r1f); }
+            } else {
+                exact_endpoint(cam, homog, Dl, L, q, 0, r0f, xs);
+                exact_endpoint(cam, homog, Dl, L, q, 1, r1f, xs + 7);
+            }
+            const double is = rcp_fast(xs[0]), ie = rcp_fast(xs[7]);
+            if (on) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int k = 0; k <= i; ++k) fo[tri(i, k)][lane] = cut_ours_info(xs, is, ie, i, k);
+            }
+        }
+        // (3) replay the recorded steps: the ratios every margined step compared, their v' both ways
+        double ivs = 0.0, rivs = 0.0, ive = 0.0, rive = 0.0, rvmax = 0.0;
+        int marg = 0;
+        float eb[14];
+#pragma unroll
+        for (int i = 0; i < 14; ++i) eb[i] = 0.0f;
+        if (on) {
+            double r0 = 0.0, r1 = 0.0;
+            bool done = false;
+            // the reference's v' at the last ratios evaluated, per side (t bits, value); the quartic is
+            // re-evaluated (four FMAs)
+            double ct[2][4], cv[2][4];
+            int cn[2] = {0, 0};
+            for (int k = 0; k < CUT_PATH && !done; ++k) {
+                const int by = path[(size_t)m * CUT_PATH + k];
+                if (!(by & CUT_P_EXACT)) {
+                    ++marg;
+                    // the six ratios the step compared (superset: every t in range, both sides)
+                    for (int w = 0; w < 6; ++w) {
+                        const int side = w / 3, o = w % 3;
+                        const double rc = side ? r1 : r0;
+                        const double t = o == 0 ? rc + (-st) : (o == 2 ? rc + st : rc);   // (nb_step's bits)
+                        if (!(t >= rlo && t <= rhi)) continue;
+                        double vr = 0.0;
+                        bool hit = false;
+                        for (int z = 0; z < cn[side]; ++z)
+                            if (__double_as_longlong(ct[side][z]) == __double_as_longlong(t)) { vr = cv[side][z]; hit = true; }
+                        if (!hit) {
+                            vr = verify_vref(p, Dl, q, side, t);
+                            ++n_eval;
+                            const int z = cn[side] < 4 ? cn[side]++ : (k & 3);
+                            ct[side][z] = t;
+                            cv[side][z] = vr;
+                        }
+                        const double vo = cut_ours_V(fd, side, t);
+                        const double lo = fmin(vr, vo);
+                        const double rv = fabs(vo - vr) / vr;
+                        if (!(lo > 0.0 && rv < 0.25)) { bad = 1; continue; }
+                        const double iv = 1.0 / lo;
+                        rvmax = fmax(rvmax, rv);
+                        if (side) { ive = fmax(ive, iv); rive = fmax(rive, rv * iv); }
+                        else { ivs = fmax(ivs, iv); rivs = fmax(rivs, rv * iv); }
+                    }
+                }
+                if (by & CUT_P_STAY) {
+                    done = true;
+                } else {
+                    const int jj = by & 7;
+                    r0 = r0 + nb_step(jj, 0, st);
+                    r1 = r1 + nb_step(jj, 1, st);
+                    if (!(r0 + r1 <= 1.0)) done = true;
+                }
+            }
+            // the replay must end where the search did
+            if (!done || __double_as_longlong(r0) != __double_as_longlong(r0f) ||
+                __double_as_longlong(r1) != __double_as_longlong(r1f))
+                bad = 1;
+            n_marg += marg;
+            if (marg) {
+                ++n_mline;
+                cut_line_bounds(p, q, pdok, Dl, eb);
+            }
+        }
+        wave_lds_sync();
+        // (4) the two running sums in list order (lanes 0-20, entry lane): S_ours and dS of each line
+        //     replace its infos in fo / fr
+        const int cnt = min(64, nls - c0);
+        if (lane < 21) {
+            for (int l = 0; l < cnt; ++l) {
+                const double i0 = rec_l[(size_t)(c0 + l) * CUT_REC + CUT_FAST + lane];
+                const double i0n = c0 + l + 1 < nls ? rec_l[(size_t)(c0 + l + 1) * CUT_REC + CUT_FAST + lane] : 0.0;
+                const double sref = sE - i0;                 // the reference's S of line c0 + l
+                const double sours = sA;                     // the search's
+                const double f_o = fo[lane][l], f_r = fr[lane][l];
+                fo[lane][l] = sours;
+                fr[lane][l] = sours - sref;
+                sE = sref + f_r;
+                sA = (sA + f_o) - i0n;
+            }
+        }
+        wave_lds_sync();
+        // (5) the agreement bound of each line with margined steps
+        if (on && marg) {
+            double o28[28];
+            {
+                double S[21];
+#pragma unroll
+                for (int e = 0; e < 21; ++e) S[e] = fo[e][lane];
+                chol_s(S, o28);   // (the search's factorization: pivots >= 1e-2 of the diagonal, 1 / L_kk)
+            }
+            if (o28[27] == 0.0) bad = 1;
+            // s_i = |L^-1 e_i|^2, W_k = L^-1 P_k (the comparison data's six coefficient vectors)
+            double sg[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double x[6], a = 0.0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    double uu = i == j ? 1.0 : 0.0;
+#pragma unroll
+                    for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * x[k];
+                    x[i] = uu * o28[21 + i];
+                    a = a + x[i] * x[i];
+                }
+                sg[j] = 1.002 * a;
+            }
+            double Bn[2] = {0.0, 0.0};
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                double tk = 1.0;
+#pragma unroll
+                for (int kk = 0; kk < 3; ++kk) {
+                    double w[6], a = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        double uu = fd[(side ? PD_PE : PD_PS) + 6 * kk + i];
+#pragma unroll
+                        for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * w[k];
+                        w[i] = uu * o28[21 + i];
+                        a = a + w[i] * w[i];
+                    }
+                    Bn[side] = Bn[side] + 1.01 * sqrt(a) * tk;
+                    tk = tk * T;
+                }
+            }
+            double Kc = 0.0, xi = 0.0, Qs = 0.0, Qe = 0.0, hs0 = 0.0, he0 = 0.0, Lam = 0.0, dSn = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double Sii = fo[tri(i, i)][lane];
+                const double es = eb[i], ee = eb[7 + i];
+                const double ps = fabs(fd[PD_PS + i]) + T * (fabs(fd[PD_PS + 6 + i]) + T * fabs(fd[PD_PS + 12 + i])) + es;
+                const double pe = fabs(fd[PD_PE + i]) + T * (fabs(fd[PD_PE + 6 + i]) + T * fabs(fd[PD_PE + 12 + i])) + ee;
+                const double kc = Sii * sg[i];
+                Kc = Kc + kc;
+                xi = xi + sqrt(kc);
+                Qs = Qs + sg[i] * ps * ps;
+                Qe = Qe + sg[i] * pe * pe;
+                hs0 = hs0 + es * sqrt(sg[i]);
+                he0 = he0 + ee * sqrt(sg[i]);
+                Lam = Lam + ((Sii > 0.0 && Sii < 1e300) ? 0.6931471805599453 * (double)(abs(__builtin_amdgcn_frexp_exp(Sii)) + 1)
+                                                         : __builtin_inf());
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    // |dS_ik| (+ the rounding of its own subtraction, u |S_ik|), whitened
+                    const int e = tri(i > k ? i : k, i > k ? k : i);
+                    const double dd = fabs(fr[e][lane]) + u * fabs(fo[e][lane]);
+                    dSn = dSn + dd * sqrt(sg[i] * sg[k]);
+                }
+            }
+            const double epsS = 1.01 * dSn + (7.01 * u) * xi * xi;
+            const double hs = hs0 + (6.01 * u) * Bn[0] * xi, he = he0 + (6.01 * u) * Bn[1] * xi;
+            const double ck = 110.0 * u;
+            const double K0 = 1.002 * epsS + ck * Kc + (7.1 * u) * Lam;
+            const double bs = Bn[0] + hs, be = Bn[1] + he;
+            // the v'-table's own error (the blended depth's relative error x 4 + the scaling's roundings)
+            const double rts = 4.1 * (double)eb[6] + 16.0 * u, rte = 4.1 * (double)eb[13] + 16.0 * u;
+            const double A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs), B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be);
+            const double E = K0 + A1 * ivs + 4.12 * bs * bs * (1.01 * rivs + rts * ivs) +
+                             B1 * ive + 4.12 * be * be * (1.01 * rive + rte * ive);
+            const double R0 = fmin(0.125 * tau, 1e-3) - 1.01 * K0;
+            const bool ok = epsS <= 1e-3 && Kc <= 1e8 && R0 > 0.0 && E * 1.0001 <= R0 && rvmax + rts + rte <= 0.25 &&
+                            rlo >= 0.0 && rhi <= 1.0 && tau > 0.0;
+            if (!ok) bad = 1;
+        }
+        wave_lds_sync();
+    }
+    bad = __any(bad) ? 1 : 0;
+    // k_cut_finish's endpoint update, for a proven sequence
+    if (!bad) {
+        for (int m = lane; m < nls; m += 64) {
+            const size_t q = lb + mls[m];
+            const double r0 = L.cut[2 * q], r1 = L.cut[2 * q + 1];
+            if (fabs(r0) < 0.0001 && fabs(r1) < 0.0001) continue;
+            double sP[3], eP[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { sP[k] = L.sP[3 * q + k]; eP[k] = L.eP[3 * q + k]; }
+            if (fabs(r0) > 0.0001) {
+                double s3[3];
+                for (int k = 0; k < 3; ++k) s3[k] = (1 - r0) * sP[k] + r0 * eP[k];
+                for (int k = 0; k < 3; ++k) { sP[k] = s3[k]; L.sP[3 * q + k] = s3[k]; }
+                double uv[2];
+                projection(cam, sP, uv);
+                L.spl[2 * q] = uv[0]; L.spl[2 * q + 1] = uv[1];
+                L.sdisp[q] = (cam.fx * cam.b) / sP[2];
+            }
+            if (fabs(r1) > 0.0001) {
+                double e3[3];
+                for (int k = 0; k < 3; ++k) e3[k] = (1 - r1) * eP[k] + r1 * sP[k];
+                for (int k = 0; k < 3; ++k) { eP[k] = e3[k]; L.eP[3 * q + k] = e3[k]; }
+                double uv[2];
+                projection(cam, eP, uv);
+                L.epl[2 * q] = uv[0]; L.epl[2 * q + 1] = uv[1];
+                L.edisp[q] = (cam.fx * cam.b) / eP[2];
+            }
+        }
+    }
+    // counters: lanes' partial counts summed
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        n_marg += __shfl_xor(n_marg, o);
+        n_eval += __shfl_xor(n_eval, o);
+        n_mline += __shfl_xor(n_mline, o);
+    }
+    if (lane == 0) {
+        p.scr.cut_flag[b] = bad;
+        p.scr.bytes[(size_t)STEP_REC * b + 20] = bad;
+        p.scr.bytes[(size_t)STEP_REC * b + 21] = n_marg;
+        p.scr.bytes[(size_t)STEP_REC * b + 22] = n_eval;
+        p.scr.bytes[(size_t)STEP_REC * b + 23] = n_mline;
+    }
+}
+
+// the batch size up to which the one-sequence-per-wave search runs (GFPL_CUT_WAVE_MAX_B overrides:
+// tests run both searches on the same batch)
+static int cut_wave_max_b() {
+    const char* e = getenv("GFPL_CUT_WAVE_MAX_B");
+    return e ? atoi(e) : CUT_WAVE_MAX_B;
+}
+
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
+    const int mode = p.cfg.cut_proof;   // 0 measured, 1 proven (recorded search + verify), 2 eager-proven, 3 (test)
+    const dim3 gsearch((p.B + CUT_G - 1) / CUT_G);
     hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
-    // proven mode: the per-line operand error bounds the agreement bound starts from
-    if (p.cfg.cut_proof) {
+    if (mode == 2) {   // the per-line operand error bounds the eager agreement bound starts from
         hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);
     }
     if (marks) (void)hipEventRecord(marks[0], s);
-    if (p.cfg.cut_proof)
-        hipLaunchKernelGGL(k_cut_search<true>, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+    if (mode == 2)
+        hipLaunchKernelGGL(k_cut_search<true>, gsearch, dim3(64), 0, s, p);
+    else if (p.B <= cut_wave_max_b())   // small batches: one sequence per wave, three steps per round
+        hipLaunchKernelGGL(k_cut_search_w, dim3(p.B), dim3(64), 0, s, p);
     else
-        hipLaunchKernelGGL(k_cut_search<false>, dim3((p.B + CUT_G - 1) / CUT_G), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_search<false>, gsearch, dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[1], s);
+    if (mode == 1 || mode == 3) {
+        // prove the recorded decisions (and finish those sequences); redo the others eagerly
+        hipLaunchKernelGGL(k_cut_verify, dim3(p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(k_cut_search<true>, gsearch, dim3(64), 0, s, p);
+    }
     hipLaunchKernelGGL(k_cut_finish, dim3(p.B), dim3(64), 0, s, p);
     return hipGetLastError();
 }

@@ -353,6 +353,7 @@ def hiplib() -> C.CDLL:
             "gfpl_last_step_stage_bytes": ([P, P], C.c_int),
             "gfpl_last_step_counts": ([P, P], C.c_int),
             "gfpl_last_step_track_counts": ([P, P], C.c_int),
+            "gfpl_last_step_cut_proof": ([P, P], C.c_int),
             "gfpl_debug_cut_records": ([P, C.c_int, P, C.c_int], C.c_int),
             "gfpl_debug_step_records": ([P, P], C.c_int),
             "gfpl_debug_clocks": ([P, P], C.c_int),
@@ -1020,6 +1021,15 @@ class StereoFrameHandler:
         return {"steps": int(v[0]), "exact_steps": int(v[1]), "inliers_after_pose": int(v[2]),
                 "lines_unbounded": int(v[3])}
 
+    def last_step_cut_proof(self) -> dict:
+        """Proven line cut (cut_proof 1) of the last step, summed over the batch
+        (gfpl_last_step_cut_proof): sequences redone by the eager-proven search because the
+        recorded search could not be proven, margined steps proven, reference variances
+        evaluated, lines with margined steps."""
+        v = np.zeros(4, np.int64)
+        check(self.L.gfpl_last_step_cut_proof(self.h, v.ctypes.data), "last_step_cut_proof")
+        return {"redone": int(v[0]), "steps_proven": int(v[1]), "vref_evals": int(v[2]), "lines": int(v[3])}
+
     def debug_cut_records(self, b: int, n_lines: int) -> np.ndarray:
         """gfpl_debug_cut_records: sequence b's line-cut records [n_lines][80] (float64)."""
         out = np.zeros((n_lines, 80), np.float64)
@@ -1027,8 +1037,8 @@ class StereoFrameHandler:
         return out
 
     def debug_step_records(self) -> np.ndarray:
-        """gfpl_debug_step_records: every sequence's record of the last step [B][20] (int64)."""
-        out = np.zeros((self.B, 20), np.int64)
+        """gfpl_debug_step_records: every sequence's record of the last step [B][24] (int64)."""
+        out = np.zeros((self.B, 24), np.int64)
         check(self.L.gfpl_debug_step_records(self.h, out.ctypes.data), "debug_step_records")
         return out
 

@@ -673,11 +673,16 @@ int  gfpl_last_step_counts(gfpl_seqbatch* sb, int64_t* counts8);
  * insert's list sizes), searched lines whose agreement bound was unusable —
  * every step of such a line is exact].  Synchronises.                                */
 int  gfpl_last_step_track_counts(gfpl_seqbatch* sb, int64_t* counts4);
+/* Proven line cut (cut_proof 1) of the last step, summed over the batch: [sequences whose
+ * recorded search k_cut_verify could not prove (their line cut was redone by the eager-proven
+ * search), margined steps proven after the fact, the reference's endpoint variances evaluated
+ * for them, lines with margined steps].  Zeros in the other modes.  Synchronises.        */
+int  gfpl_last_step_cut_proof(gfpl_seqbatch* sb, int64_t* counts4);
 /* Diagnostics: the line-cut records of sequence b's first n_lines matched lines of the last
  * insert (80 doubles each: comparison data, bounds, r = 0 info, the agreement bound as
  * k_cut_search formed it — DESIGN.md §3; layout in k_cut.hip).  Synchronises.      */
 int  gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines);
-/* Every sequence's record of the last step: B x 20 int64 — stage bytes [0..7], the counts of
+/* Every sequence's record of the last step: B x 24 int64 — stage bytes [0..7], the counts of
  * gfpl_last_step_counts [8..15], line-cut steps / exact steps [16..17], inliers after the pose
  * [18], lines without a usable bound [19] (layout: STEP_REC in gfpl_state.hpp).  Synchronises. */
 int  gfpl_debug_step_records(gfpl_seqbatch* sb, int64_t* out);

@@ -10,6 +10,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <utility>
@@ -723,6 +724,8 @@ std::vector<Desc> collect(const uint8_t* (Frame::*f)(int) const, const Frame& fr
 // search itself at 16 threads).
 #ifdef GFPL_ORACLE_CUT_STATS
 static int64_t g_cut_stats[8];
+// per line: the smallest metric gap a step decision rests on (histogram by decade, 1e-16 .. 1e3)
+static int64_t g_cut_gap_hist[20];
 #define CUT_STAT(stmt) do { stmt; } while (0)
 #else
 #define CUT_STAT(stmt) do { } while (0)
@@ -1352,6 +1355,7 @@ struct gfplo_handler {
             }
             std::memcpy(sum_before, sum, sizeof sum);
             std::vector<std::pair<uint64_t, uint64_t>> seen, last_step, this_step;
+            double line_gap = 1e300;
 #endif
             [[maybe_unused]] bool moved = false;
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] - L.invCov[i];
@@ -1361,6 +1365,10 @@ struct gfplo_handler {
                 double cand_info[36];
                 double metric_init = metric_back;
                 CUT_STAT(g_cut_stats[1]++);   // steps
+#ifdef GFPL_ORACLE_CUT_STATS
+                double mv[8];
+                int nv = 0;
+#endif
 #ifdef GFPL_ORACLE_CUT_STATS
                 this_step.clear();
 #endif
@@ -1386,6 +1394,9 @@ struct gfplo_handler {
                     poseInfoOnLine(DT_inv, Jl, L, rt, tmp);
                     for (int i = 0; i < 36; ++i) tot[i] = tmp[i] + sum[i];
                     double m = logdet6(tot);
+#ifdef GFPL_ORACLE_CUT_STATS
+                    mv[nv++] = m;
+#endif
                     if (m > metric_init) {
                         metric_init = m;
                         cand[0] = rt[0]; cand[1] = rt[1];
@@ -1395,6 +1406,14 @@ struct gfplo_handler {
                 }
 #ifdef GFPL_ORACLE_CUT_STATS
                 last_step = this_step;
+                {   // the gaps the decision rests on: winner vs every other value and vs the centre
+                    const double top = hit ? metric_init : metric_back;
+                    double g = 1e300;
+                    for (int i = 0; i < nv; ++i)
+                        if (mv[i] != top) g = std::min(g, std::fabs(top - mv[i]));
+                    if (hit) g = std::min(g, std::fabs(top - metric_back));
+                    line_gap = std::min(line_gap, g);
+                }
 #endif
                 if (hit) {
                     CUT_STAT(if (cand[0] < L.cut[0] || cand[1] < L.cut[1]) g_cut_stats[7]++);   // a ratio moved back
@@ -1405,6 +1424,12 @@ struct gfplo_handler {
                 } else break;
             }
             CUT_STAT(if (!moved) g_cut_stats[4]++);   // lines that never moved
+#ifdef GFPL_ORACLE_CUT_STATS
+            {
+                int b = line_gap > 0 ? (int)std::floor(std::log10(line_gap)) + 16 : 0;
+                g_cut_gap_hist[std::max(0, std::min(19, b))]++;
+            }
+#endif
             CUT_STAT(prev_moved = moved);
             updateEndPointByRatio(L);
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] + L.invCov[i];
@@ -1973,6 +1998,8 @@ int gfplo_inverse_se3(const double* T, double* out) { inverse_se3(T, out); retur
 extern "C" void gfplo_cut_stats(int64_t* out8) {
 #ifdef GFPL_ORACLE_CUT_STATS
     for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
+    for (int i = 0; i < 20; ++i) { fprintf(stderr, "%lld ", (long long)g_cut_gap_hist[i]); g_cut_gap_hist[i] = 0; }
+    fprintf(stderr, "\n");
 #else
     for (int i = 0; i < 8; ++i) out8[i] = -1;   // not compiled in
 #endif

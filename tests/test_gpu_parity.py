@@ -87,17 +87,26 @@ def test_vga_default_pose_bitexact(vga_default):
     assert all(vga_default["pose_exact"]), vga_default["pose_exact"]
 
 
-def test_bench_config_parity():
-    # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop
+@pytest.mark.parametrize("wave_max", ["0", "4096"])
+def test_bench_config_parity(monkeypatch, wave_max):
+    # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop; both line-cut searches
+    monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)
     rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
                         n_seq=2, n_frames=4, kp_cap=2048, kl_cap=512, seed=7)
     _check(rep)
 
 
-def test_proven_cut_parity():
-    """Proven-mode line cut (gfpl_config.cut_proof = 1) against the oracle: the v'-table of the
-    reference's own endpoint variances, the exact running invCov_sum and the per-step bound."""
-    rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0, cut_proof=1),
+@pytest.mark.parametrize("proof,wave_max", [(1, "0"), (1, "4096"), (2, "0"), (3, "0")])
+def test_proven_cut_parity(monkeypatch, proof, wave_max):
+    """Proven-mode line cut against the oracle: cut_proof 1 — the recorded measured
+    search proven after the fact by k_cut_verify (the reference's own endpoint variances at every
+    compared ratio, the two running invCov_sums), unproven sequences redone eagerly; 2 — the eager
+    proven search for every sequence (v'-tables, exact running sum, per-step bound); 3 — every
+    sequence sent through the redo path (the fallback of mode 1).  Both searches record: the
+    8-sequence-per-wave one and the small-batch one (GFPL_CUT_WAVE_MAX_B)."""
+    monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)
+    rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0,
+                                    cut_proof=proof),
                         n_seq=3, n_frames=5, kp_cap=2048, kl_cap=512, seed=9)
     _check(rep)
 
@@ -414,11 +423,13 @@ def test_cut_certify_margin_validated():
             gfpl.Context(cam, gfpl.default_config(cut_certify=bad))
 
 
-def test_line_cut_certified_matches_exact_at_scale():
+@pytest.mark.parametrize("wave_max", ["0", "4096"])
+def test_line_cut_certified_matches_exact_at_scale(monkeypatch, wave_max):
     """512 sequences x 3 frames on the GPU three times — the margined search in measured mode,
     in proven mode (gfpl_config.cut_proof: a margined decision only under the proven per-step
     agreement bound) and exact steps only — cut ratios, invCovPose of every
     matched line and the poses bit-identical; proven mode certifies most steps."""
+    monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)   # 0: the 8-sequence-per-wave search, else one per wave
     n, F, KP, KL = 512, 3, 2048, 512
     base = dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     cam = gfpl.make_camera("vga", gfpl.default_config(**base))
@@ -426,17 +437,22 @@ def test_line_cut_certified_matches_exact_at_scale():
     D = gfpl.DeviceFrames(H)
     out = []
     proven = {"steps": 0, "exact_steps": 0, "lines_unbounded": 0}
-    for margin, proof in ((1e-9, 0), (1e-9, 1), (0.0, 0)):
+    verified = {"redone": 0, "steps_proven": 0, "vref_evals": 0, "lines": 0}
+    for margin, proof in ((1e-9, 0), (1e-9, 2), (1e-9, 1), (0.0, 0)):
         ctx = gfpl.Context(cam, gfpl.default_config(cut_certify=margin, cut_proof=proof, **base))
         h = gfpl.StereoFrameHandler(ctx, n, KP, KL)
         h.initialize(D.frames(0))
         res = []
         for k in range(1, F):
             h.insertStereoPair(D.frames(k))
-            if proof:
+            if proof == 2:
                 tc = h.last_step_track_counts()
                 for key in proven:
                     proven[key] += tc[key]
+            if proof == 1:
+                vc = h.last_step_cut_proof()
+                for key in verified:
+                    verified[key] += vc[key]
             h.optimizePose()
             for b in range(n):
                 tr = h.read_track(b)
@@ -446,7 +462,7 @@ def test_line_cut_certified_matches_exact_at_scale():
                             h.read_frame(gfpl.CURR, b).get("Tfw")))
             h.updateFrame()
         out.append(res)
-    for other in (out[1], out[2]):
+    for other in (out[1], out[2], out[3]):
         n_lines = 0
         for (ma, ca, ia, ta), (mb, cb, ib, tb) in zip(out[0], other):
             assert np.array_equal(ma, mb)
@@ -455,8 +471,10 @@ def test_line_cut_certified_matches_exact_at_scale():
             assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64))
             n_lines += len(ma)
         assert n_lines > 100 * n
-    print("proven mode:", proven)
+    print("eager proven mode:", proven, "verified proven mode:", verified)
     assert proven["steps"] > 0 and proven["exact_steps"] < 0.05 * proven["steps"], proven
+    # the recorded search is proven for (nearly) every sequence: a redo is the exception
+    assert verified["steps_proven"] > 0.9 * proven["steps"] and verified["redone"] <= 0.01 * n * (F - 1), verified
 
 
 # ---- keyframe decision: needNewKF / currFrameIsKF
