@@ -530,7 +530,11 @@ def detection_rates(cam, upload_Bps, n_img=256, n_lines=300, steps=5):
     return out
 
 
-def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False):
+PIPE_BARS = 600         # bars per Mpx of scene plane: ~2000 ORB + 300 LSD keylines per VGA image (north-star load)
+PIPE_SCENES = 128       # distinct scenes of the images -> poses legs (sequence b shows scene b % PIPE_SCENES)
+
+
+def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False, bars=PIPE_BARS):
     """Images in HBM to poses on one device (gfpl.pipeline), measured after the
     timed tracking steps (not part of `value`): per step ORB on both images of B stereo frames,
     LBD (and LSD when lsd) on the pipeline's detection stream, one StereoFrameHandler step on
@@ -550,7 +554,7 @@ def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False):
     det = (lambda f: pipe.detect_images(f[0], f[1], f[6])) if lsd else (lambda f: pipe.detect(*f))
     frames = []
     for k in range(2 + 2 * steps):
-        sc = [synth_stereo_steps(b, k, W, H) for b in range(B)]
+        sc = [synth_stereo_steps(b % PIPE_SCENES, k, W, H, bars=bars) for b in range(B)]
         if progress:
             print(f"[pipeline_rate] frame {k} of {2 + 2 * steps} generated", file=sys.stderr, flush=True)
         kl = [np.zeros((B, KL), gfpl.KEYLINE_DT) for _ in range(2)]
@@ -590,6 +594,7 @@ def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False):
     t_ovl = time.perf_counter() - t0
     pipe.status()
     tr = g.read_last_track(0)
+    sc_counts = g.last_step_counts()   # per-sequence means of the last step: S_p', S_l', M_p, M_l
     g.close()
     pipe.close()
     ctx.close()
@@ -598,7 +603,12 @@ def pipeline_rate(cam, cfg, B=1024, steps=3, lsd=False, progress=False):
             "serial": {"value": B * steps / (t_det + t_trk), "detect_ms_per_step": 1e3 * t_det / steps,
                        "track_ms_per_step": 1e3 * t_trk / steps},
             "matched_pt_seq0": len(tr["matched_pt"]), "matched_ls_seq0": len(tr["matched_ls"]),
-            "scene": "staircase bands at disparity 2/12/20/8 px, 2000 ORB, " +
+            "per_frame_mean": {"stereo_pt": round(sc_counts["S_p"], 1), "stereo_ls": round(sc_counts["S_l"], 1),
+                               "matched_pt": round(sc_counts["M_p"], 1), "matched_ls": round(sc_counts["M_l"], 1),
+                               "keypoints_both_sides": round(sc_counts["N_o"], 1),
+                               "keylines_both_sides": round(sc_counts["N_k"], 1)},
+            "scene": f"staircase bands at disparity 2/12/20/8 px, {bars} anti-aliased bars per Mpx of plane "
+                     f"({PIPE_SCENES} distinct scenes), 2000 ORB, " +
                      ("LSD on the device (<= 300 keylines per side)" if lsd else "300 given keylines per side"),
             "overlap": "detection of frame k+1 (detection stream) beside the tracking of frame k (tracking stream)"}
 
@@ -876,7 +886,7 @@ def main():
             up_Bps = host_fed["upload_GBps"] * 1e9 if host_fed and host_fed.get("upload_GBps") else 0.0
             det = detection_rates(cam, up_Bps)
             try:
-                det["images_to_poses"] = pipeline_rate(cam, cfg)
+                det["images_to_poses"] = pipeline_rate(cam, cfg, bars=0)
                 det["images_to_poses_lsd"] = pipeline_rate(cam, cfg, B=1536, lsd=True)
             except Exception as e:   # reported, never fatal to the contract line
                 det["images_to_poses"] = {"error": f"{type(e).__name__}: {e}"}

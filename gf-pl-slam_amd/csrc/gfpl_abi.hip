@@ -159,6 +159,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cut_prog = c.take<int32_t>((size_t)1 << 17);
     sb->scr.cut_path = c.take<uint8_t>(B * sb->mls_cap * CUT_PATH);
     sb->scr.cut_flag = c.take<int32_t>(B);
+    sb->scr.cut_vmax = c.take<double>(B * sb->mls_cap * CUT_VMAX);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);

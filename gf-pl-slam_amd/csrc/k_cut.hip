@@ -85,11 +85,13 @@ __device__ __forceinline__ void cut_endpoint_t(const DevCam& cam, double homog, 
     T Pt[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) Pt[k] = (T(1.0) - c) * P0[k] + c * P1[k];
-    const T a = (T(1.0) - c) * (T(1.0) - c), q = c * c;
-    T cov[9];
+    if (VAR) {   // (VAR = false: C0 / C1 are not read)
+        const T a = (T(1.0) - c) * (T(1.0) - c), q = c * c;
+        T cov[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
-    if (VAR) out7[0] = endpointVar_t<T>(cam, DT_inv, Jl, Pt, cov, zlo);
+        for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + q * C1[i];
+        out7[0] = endpointVar_t<T>(cam, DT_inv, Jl, Pt, cov, zlo);
+    }
     T cur[3];
     se3_apply_t<T, double>(DT_inv, Pt, cur);
     rb_floor(cur[2], zlo);
@@ -423,8 +425,7 @@ __global__ void __launch_bounds__(256) k_cut_vtab(KParams p) {
 // the line's operand error bounds (above) for line q of sequence b: eb[0..5] / [7..12] the start /
 // end side's |P - P*| in P units, eb[6] / [13] the blended depth's relative error bound; +inf: no
 // usable bound (the line's steps are then exact)
-__device__ __attribute__((noinline)) void cut_line_bounds(const KParams& p, size_t q, bool pd_ok, const double* Dl,
-                                                          float* eb) {
+__device__ __forceinline__ void cut_line_bounds(const KParams& p, size_t q, bool pd_ok, const double* Dl, float* eb) {
     const DevLines& L = p.prev.ls;
     const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     const double C = fmax(rhi, 0.0), T = fmax(fabs(rlo), fabs(rhi));
@@ -488,6 +489,64 @@ __device__ __attribute__((noinline)) void cut_line_bounds(const KParams& p, size
                 eb[7 * side + 6] = cur[2].lo > 0.0 ? ceil_f32(1.01 * cur[2].e / cur[2].lo) : __builtin_inff();
             }
         }
+    }
+}
+
+// k_cut_verify's variant: the same P bounds (our coefficients' RB error + the reference's Jacobian's)
+// and the blended depth's relative error, without the v' coefficients' bound (the verification
+// measures v' against the reference's own values instead) — so without R C R^T in RB
+__device__ __forceinline__ void cut_line_bounds_p(const KParams& p, size_t q, bool pd_ok, const double* Dl, float* eb) {
+    const DevLines& L = p.prev.ls;
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const double C = fmax(rhi, 0.0), T = fmax(fabs(rlo), fabs(rhi));
+#pragma unroll
+    for (int i = 0; i < 14; ++i) eb[i] = __builtin_inff();
+    if (!(rlo >= 0.0 && rhi <= 1.0 && pd_ok && p.cam.fx > 0.0)) return;
+    RB sP[3], eP[3], Jl[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sP[k] = RB(L.sP[3 * q + k]); eP[k] = RB(L.eP[3 * q + k]); }
+    Jl[0] = RB(L.le_obs[3 * q]);
+    Jl[1] = RB(L.le_obs[3 * q + 1]);
+    RB g[6];
+    se3_apply_t<RB, double>(Dl, sP, g);
+    se3_apply_t<RB, double>(Dl, eP, g + 3);
+    double gd[6];
+    {
+        const double s3[3] = {L.sP[3 * q], L.sP[3 * q + 1], L.sP[3 * q + 2]};
+        const double e3[3] = {L.eP[3 * q], L.eP[3 * q + 1], L.eP[3 * q + 2]};
+        se3_apply(Dl, s3, gd);
+        se3_apply(Dl, e3, gd + 3);
+    }
+    const double zlo = fmin(fabs(gd[2]) - g[2].e, fabs(gd[5]) - g[5].e);
+    const double zmax = fmax(fabs(gd[2]) + g[2].e, fabs(gd[5]) + g[5].e);
+    if (!(zlo > 0.0)) return;
+    const double s1 = zmax * zmax / p.cam.fx;   // 1 / fgz2*_min
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        double eo[6] = {0, 0, 0, 0, 0, 0};
+        double tk = 1.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {   // (cut_poly_coef_t's P part: coefficient k of the side's P(t))
+            RB Pk[6];
+            cut_poly_coeff_t<RB>(g + 3 * side, g + 3 * (1 - side), Jl[0], Jl[1], k, Pk);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) eo[i] = eo[i] + tk * Pk[i].e;
+            tk = tk * T;
+        }
+        RB o7[7];
+        cut_endpoint_t<RB, false>(p.cam, p.cfg.homog_th, Dl, Jl, side ? eP : sP, side ? sP : eP, nullptr, nullptr,
+                                  RB(C, 0.0, 0.0), o7, zlo);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) eb[7 * side + i] = ceil_f32(1.01 * (eo[i] + o7[1 + i].e * s1));
+        const RB c(C, 0.0, 0.0);
+        const RB* Q0 = side ? eP : sP;
+        const RB* Q1 = side ? sP : eP;
+        RB Pt[3], cur[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Pt[k] = (RB(1.0) - c) * Q0[k] + c * Q1[k];
+        se3_apply_t<RB, double>(Dl, Pt, cur);
+        rb_floor(cur[2], zlo);
+        eb[7 * side + 6] = cur[2].lo > 0.0 ? ceil_f32(1.01 * cur[2].e / cur[2].lo) : __builtin_inff();
     }
 }
 
@@ -579,15 +638,17 @@ __device__ __forceinline__ void exact_endpoint(const DevCam& cam, double homog, 
     cut_endpoint(cam, homog, Dl, Jl, side ? eP : sP, side ? sP : eP, side ? cE : cS, side ? cS : cE, t, o7);
 }
 
+// neighbour j's offset on a side (src/stereoFrameHandler.cpp:1624-1633): bit masks of the moves that
+// grow (0x31 / 0x54) and shrink (0xC2 / 0xA8) the start / end ratio, so a data-dependent j costs no branch
+__device__ __forceinline__ int nb_off(int j, int side) {
+    const unsigned pl = side == 0 ? 0x31u : 0x54u, mi = side == 0 ? 0xC2u : 0xA8u;
+    return (int)((pl >> j) & 1u) - (int)((mi >> j) & 1u);
+}
 __device__ __forceinline__ double nb_step(int j, int side, double st) {
-    // neighbour j of (r0, r1) (src/stereoFrameHandler.cpp:1624-1633)
-    const int a = side == 0 ? ((j == 0 || j == 4 || j == 5) ? 1 : ((j == 1 || j == 6 || j == 7) ? -1 : 0))
-                            : ((j == 2 || j == 4 || j == 6) ? 1 : ((j == 3 || j == 5 || j == 7) ? -1 : 0));
-    return a > 0 ? st : (a < 0 ? -st : 0.0);
+    return (double)nb_off(j, side) * st;   // (st, -st or +0.0: the bits of the ternary it replaces)
 }
 __device__ __forceinline__ int nb_slot(int j, int side) {   // endpoint slot: 0: -s, 1: 0, 2: +s
-    if (side == 0) return (j == 0 || j == 4 || j == 5) ? 2 : ((j == 1 || j == 6 || j == 7) ? 0 : 1);
-    return (j == 2 || j == 4 || j == 6) ? 2 : ((j == 3 || j == 5 || j == 7) ? 0 : 1);
+    return 1 + nb_off(j, side);
 }
 
 // S = L L^T for the margined comparisons (out: L strictly lower 21, 1/L_kk 6, ok).  ok = 0
@@ -1494,12 +1555,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // ------------------------------------------------------- small-batch search --
 // One sequence per wave, for small batches (B <= CUT_WAVE_MAX_B: the latency of one sequence, e.g. the
 // reference app's one stream per process, app/plslam_mod.cpp:387-411).  Same decisions, same bits as
-// k_cut_search<false> (measured mode, with the proven mode's step record): a round evaluates d on the 7 x 7
-// grid of ratios around the centre (lane a * 7 + c: offsets a - 3, c - 3, 49 lanes), which holds the 8
-// neighbours of every position up to three greedy steps away, then resolves up to three steps in order
-// from those values — each with the one-step search's first-strict-maximum rule and margin tests.  The
-// grid's ratios are accumulated as the search's moves accumulate them (r + s + s, r + (-s) + (-s)); a
-// step whose neighbours' ratio bits differ from the grid's (a ratio that moved back), or that a margin
+// k_cut_search<false> (measured mode, with the proven mode's step record): a round evaluates d on the 8 x 8
+// grid of ratios at offsets -1 .. 6 from the centre on both sides (lane a * 8 + c), which holds the 8
+// neighbours of every position a path that only grows the ratios reaches in five steps — the greedy cut
+// almost always grows them (final r0 + r1 ~ 1 after ~20 steps) — then resolves up to five steps in order
+// from those values, each with the one-step search's first-strict-maximum rule and margin tests.  The
+// grid's ratios are accumulated as the search's moves accumulate them (r + s + s ...); a step whose
+// neighbours' ratio bits differ from the grid's or leave it (a ratio that moved back), or that a margin
 // test sends to the exact path, ends the round.  Exact steps and the lazy exact invCov_sum are
 // cut_exact_round's, run by the wave as group 0.  Line transitions run on the whole wave at once.
 #ifndef CUT_WAVE_MAX_B
@@ -1511,8 +1573,7 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ int nb_da(int j, int side) {   // neighbour j's offset on a side (nb_step's sign)
-    if (side == 0) return (j == 0 || j == 4 || j == 5) ? 1 : ((j == 1 || j == 6 || j == 7) ? -1 : 0);
-    return (j == 2 || j == 4 || j == 6) ? 1 : ((j == 3 || j == 5 || j == 7) ? -1 : 0);
+    return nb_off(j, side);
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search_w(KParams p) {
@@ -1523,6 +1584,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double wgs[64];                  // line open: W [6][6] | Gram (21) at 36
     __shared__ double xsl[16];                  // transition: the finished line's [v'_s, P_s, v'_e, P_e]
     __shared__ CutCmp cmpl;
+    __shared__ double dgx[82];                  // decision pass: the grid's values (-inf: invalid / NaN), padded
+    __shared__ int dgf[82];                     // and flags (bok | valid << 1 | valid NaN << 2)
     const int lane = threadIdx.x;
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -1620,22 +1683,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         wave_lds_sync();
         open_line();
     }
+#ifdef GFPL_CUTW_CLOCK   // (diagnostic build: shader-clock cycles per phase and counts in scr.dbg)
+    uint64_t ck_eval = 0, ck_dec = 0, ck_walk = 0, ck_trans = 0, ck_exact = 0, n_rounds = 0, n_trans = 0;
+    uint64_t ck0 = clock64();
+#define CUTW_CK(acc) do { const uint64_t ck1 = clock64(); acc += ck1 - ck0; ck0 = ck1; } while (0)
+#else
+#define CUTW_CK(acc) do { } while (0)
+#endif
     while (m < nls) {   // (wave-uniform)
-        // ---- the 7 x 7 grid of ratios around the centre, as the moves accumulate them
-        double g0[7], g1[7];
-        g0[3] = r0;
-        g1[3] = r1;
+        // ---- the 8 x 8 grid of ratios at offsets -1 .. 6 from the centre, as the moves accumulate
+        //      them (the greedy path almost always grows both ratios: up to five steps per round)
+        double g0[8], g1[8];
+        g0[1] = r0;
+        g1[1] = r1;
+        g0[0] = r0 + (-st);
+        g1[0] = r1 + (-st);
 #pragma unroll
-        for (int k = 4; k < 7; ++k) { g0[k] = g0[k - 1] + st; g1[k] = g1[k - 1] + st; }
-#pragma unroll
-        for (int k = 2; k >= 0; --k) { g0[k] = g0[k + 1] + (-st); g1[k] = g1[k + 1] + (-st); }
+        for (int k = 2; k < 8; ++k) { g0[k] = g0[k - 1] + st; g1[k] = g1[k - 1] + st; }
         int dj_valid = 0, bok = 0;
         double dj = 0.0;
-        if (lane < 49) {
-            const int a = lane / 7, c = lane - 7 * (lane / 7);
-            double t0 = g0[0], t1 = g1[0];
+        double t0 = g0[0], t1 = g1[0];   // the lane's grid ratios
+        {
+            const int a = lane >> 3, c = lane & 7;
 #pragma unroll
-            for (int k = 1; k < 7; ++k) { t0 = a == k ? g0[k] : t0; t1 = c == k ? g1[k] : t1; }
+            for (int k = 1; k < 8; ++k) { t0 = a == k ? g0[k] : t0; t1 = c == k ? g1[k] : t1; }
             int valid = 1;
             if (t0 + t1 > 1.0) valid = 0;
             if (t0 < rlo || t0 > rhi) valid = 0;
@@ -1645,76 +1716,109 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             cut_reg_load(cmpl, cr);
             dj = cut_dval<false>(cr, t0, t1, tq, bok);
         }
-        // ---- up to three steps from the grid
-        int pa = 3, pc = 3;
+        CUTW_CK(ck_eval);
+        // ---- every grid position's decision at once: lane (a, c), 1 <= a, c <= 6, gathers its 8
+        //      neighbours' values (bpermute) and takes k_cut_search's group decision and margin tests
+        //      (group_first_max, f1-f5) with its own value as the centre: a move j, CUT_P_STAY, or
+        //      WAVE_EXACT / WAVE_STOP (a margin test failed / a neighbour's ratio bits are not the grid's)
+        constexpr int WAVE_EXACT = 16, WAVE_STOP = 32;
+        int dec = WAVE_STOP;
+        {
+            const int a = lane >> 3, c = lane & 7;
+            // a position's neighbour ratios are the grid's iff r - s of its ratio has the bits of the grid
+            // value below (r + s is the value above by construction, and so is g[0] + s = g[1])
+            int cm0 = 2, cm1 = 2;
+#pragma unroll
+            for (int k = 2; k <= 6; ++k) {
+                cm0 |= (__double_as_longlong(g0[k] + (-st)) == __double_as_longlong(g0[k - 1])) ? (1 << k) : 0;
+                cm1 |= (__double_as_longlong(g1[k] + (-st)) == __double_as_longlong(g1[k - 1])) ? (1 << k) : 0;
+            }
+            const bool cons = ((cm0 >> a) & (cm1 >> c) & 1) != 0;
+            // the neighbours' values and flags through LDS (8 reads each; border lanes read padding)
+            const double xo = (dj_valid && dj == dj) ? dj : -__builtin_inf();
+            dgx[9 + lane] = xo;
+            dgf[9 + lane] = bok | (dj_valid << 1) | ((dj_valid && !(dj == dj)) ? 4 : 0);
+            wave_lds_sync();
+            double vjn[8];
+            int fl[8];
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                const int l = 9 + lane + 8 * nb_da(jn, 0) + nb_da(jn, 1);
+                vjn[jn] = dgx[l];
+                fl[jn] = dgf[l];
+            }
+            const double dcl = dj;
+            const int cok = bok;
+            // the first strict maximum (group_first_max's rule): a tree maximum, then the lowest index at it
+            const double m01 = fmax(vjn[0], vjn[1]), m23 = fmax(vjn[2], vjn[3]);
+            const double m45 = fmax(vjn[4], vjn[5]), m67 = fmax(vjn[6], vjn[7]);
+            const double mx = fmax(fmax(m01, m23), fmax(m45, m67));
+            int atm = 0;
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) atm |= (vjn[jn] == mx) ? (1 << jn) : 0;
+            const int kf = (mx > -__builtin_inf()) ? __builtin_ctz(atm | 256) : 8;
+            const int best = (kf < 8 && mx > dcl) ? kf : -1;
+            const double top = mx;
+            const bool has = best >= 0;
+            const double ttop = tau * top, tdc = tau * dcl;
+            bool ok = !(has & !(top - dcl > ttop)) && ((tau > 0.0) & (line_ok != 0) & (cok != 0) & (dcl == dcl));
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                const double v = vjn[jn];
+                const bool vl = (fl[jn] & 2) != 0;
+                const bool f1 = vl & !(fl[jn] & 1);
+                const bool f2 = has & vl & (jn != best) & !(top - v > ttop);
+                const bool f4 = !has & vl & !(dcl - v > tdc);
+                const bool f3 = (fl[jn] & 4) != 0;   // (a valid NaN: the raw value fails f2 / f4 in the group search)
+                ok = ok && !(f1 | f2 | f3 | f4);
+            }
+            dec = !cons ? WAVE_STOP : (!ok ? WAVE_EXACT : (has ? best : CUT_P_STAY));
+            // the walk's word: the decision, whether the move ends the line (r0 + r1 > 1 after it: the moved
+            // ratios are the neighbour's grid values, bit for bit, at a consistent position) and the lane moved to
+            const int mv = has ? best : 0;
+            const double n0 = t0 + nb_step(mv, 0, st), n1 = t1 + nb_step(mv, 1, st);
+            const int fin = (has && !(n0 + n1 <= 1.0)) ? 64 : 0;
+            dec |= fin | ((lane + 8 * nb_da(mv, 0) + nb_da(mv, 1)) & 63) << 8;
+        }
+        CUTW_CK(ck_dec);
+        // ---- follow the decisions from the centre: up to five steps
+        int pos = 9;   // (a, c) = (1, 1): the centre
         int exact = 0, finalize = 0;
         double vj[8];
         int bj[8], valj[8];
-        for (int sstep = 0; sstep < 3; ++sstep) {   // (wave-uniform)
-            // the 8 neighbours' ratios must be the grid's bits
-            bool cons = true;
+        for (int sstep = 0; sstep < 5; ++sstep) {   // (wave-uniform)
+            const int w = __builtin_amdgcn_readlane(dec, pos);
+            const int dpos = w & 63;
+            const int pa = pos >> 3, pc = pos & 7;
+            if (dpos == WAVE_STOP) break;
+            if (dpos == WAVE_EXACT) {   // the exact round needs the position's neighbours
 #pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const int pp = side ? pc : pa;
-                const double* gg = side ? g1 : g0;
-                double cur = gg[0], up = gg[0], dn = gg[0];
-#pragma unroll
-                for (int k = 0; k < 7; ++k) {
-                    cur = pp == k ? gg[k] : cur;
-                    up = pp + 1 == k ? gg[k] : up;
-                    dn = pp - 1 == k ? gg[k] : dn;
+                for (int jn = 0; jn < 8; ++jn) {
+                    const int l = (pa + nb_da(jn, 0)) * 8 + (pc + nb_da(jn, 1));
+                    vj[jn] = readlane_f64(dj, l);
+                    bj[jn] = __builtin_amdgcn_readlane(bok, l);
+                    valj[jn] = __builtin_amdgcn_readlane(dj_valid, l);
                 }
-                cons = cons && pp >= 1 && pp <= 5 &&
-                       __double_as_longlong(cur + st) == __double_as_longlong(up) &&
-                       __double_as_longlong(cur + (-st)) == __double_as_longlong(dn);
+                exact = 1;
+                break;
             }
-            if (!cons) break;
-#pragma unroll
-            for (int jn = 0; jn < 8; ++jn) {
-                const int l = (pa + nb_da(jn, 0)) * 7 + (pc + nb_da(jn, 1));
-                vj[jn] = readlane_f64(dj, l);
-                bj[jn] = __builtin_amdgcn_readlane(bok, l);
-                valj[jn] = __builtin_amdgcn_readlane(dj_valid, l);
-            }
-            // k_cut_search's group decision and margin tests (group_first_max, f1-f5), on the 8 values
-            double mx = -__builtin_inf();
-            double x[8];
-#pragma unroll
-            for (int jn = 0; jn < 8; ++jn) {
-                x[jn] = (valj[jn] && vj[jn] == vj[jn]) ? vj[jn] : -__builtin_inf();
-                mx = fmax(mx, x[jn]);
-            }
-            int kf = 8;
-#pragma unroll
-            for (int jn = 7; jn >= 0; --jn) kf = (x[jn] == mx && mx > -__builtin_inf()) ? jn : kf;
-            const int best = (kf < 8 && mx > dc) ? kf : -1;
-            const double top = mx;
-            const bool has = best >= 0;
-            bool ok = !(has & !(top - dc > tau * top)) && ((tau > 0.0) & (line_ok != 0) & (c_ok != 0) & (dc == dc));
-#pragma unroll
-            for (int jn = 0; jn < 8; ++jn) {
-                const bool vl = valj[jn] != 0;
-                const bool f1 = vl & !bj[jn];
-                const bool f2 = has & vl & (jn != best) & !(top - vj[jn] > tau * top);
-                const bool f4 = !has & vl & !(dc - vj[jn] > tau * dc);
-                ok = ok && !(f1 | f2 | f4);
-            }
-            if (!ok) { exact = 1; break; }
             ++n_steps;
             if (rec && lane == 0) {
-                if (lstep < CUT_PATH) path[(size_t)m * CUT_PATH + lstep] = (uint8_t)(has ? best : CUT_P_STAY);
+                if (lstep < CUT_PATH) path[(size_t)m * CUT_PATH + lstep] = (uint8_t)dpos;
             }
             ++lstep;
             first = 0;
-            if (!has) { finalize = 1; break; }
-            pa += nb_da(best, 0);
-            pc += nb_da(best, 1);
-            dc = vj[best];
-            c_ok = bj[best];
-            r0 = r0 + nb_step(best, 0, st);
-            r1 = r1 + nb_step(best, 1, st);
-            if (!(r0 + r1 <= 1.0)) { finalize = 1; break; }
+            if (dpos == CUT_P_STAY) { finalize = 1; break; }
+            pos = w >> 8;
+            if (w & 64) { finalize = 1; break; }
         }
+        // the ratios where the walk stopped: that lane's grid values (r + s accumulated, bit for bit)
+        r0 = readlane_f64(t0, pos);
+        r1 = readlane_f64(t1, pos);
+        CUTW_CK(ck_walk);
+#ifdef GFPL_CUTW_CLOCK
+        ++n_rounds;
+#endif
         if (exact) {
             // the reference's evaluation of this step (group 0 = lanes 0-7; the flush uses the wave);
             // the neighbours' values were gathered by the step that stopped
@@ -1748,7 +1852,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (!(r0 + r1 <= 1.0)) finalize = 1;
             }
         }
+        CUTW_CK(ck_exact);
         if (finalize) {
+#ifdef GFPL_CUTW_CLOCK
+            ++n_trans;
+#endif
             if (lane == 0) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
@@ -1791,11 +1899,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 open_line();
             }
         }
+        CUTW_CK(ck_trans);
     }
     if (lane == 0) {
         p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
         p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;
         p.scr.bytes[(size_t)STEP_REC * b + 19] = 0;
+#ifdef GFPL_CUTW_CLOCK
+        int64_t* d = p.scr.dbg + 8 * (size_t)b;
+        d[0] = ck_eval; d[1] = ck_dec; d[2] = ck_walk; d[3] = ck_exact; d[4] = ck_trans; d[5] = n_rounds; d[6] = n_trans;
+        d[7] = n_steps;
+#endif
     }
 }
 
@@ -1885,9 +1999,539 @@ __device__ __forceinline__ double verify_vref(const KParams& p, const double* Dl
     return ref_vprime(p.cam, p.cfg.homog_th, Dl, p.prev.ls, q, side, t);
 }
 
+// Proven mode, first verification pass: one lane per matched line of every sequence (no serial
+// dependence between lines here).  The line's recorded steps are replayed and, at every ratio a
+// margined step compared, the reference's own scaled endpoint variance v'_ref (ref_vprime, from
+// the line's data held in registers) is set against the quartic v'_ours the search used:
+// per side, max 1.01 / min(v'_ours, v'_ref) and max r_v / min(...) with r_v = |v'_ours - v'_ref| / v'_ref.
+// k_cut_verify combines these maxima with the line's S-dependent bound terms.
+__device__ __forceinline__ double vref_regs(const DevCam& cam, double homog, const double* Dl, const double* P0,
+                                            const double* P1, const double* C0, const double* C1, const double* Jl,
+                                            double c) {
+    double Pt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Pt[k] = (1.0 - c) * P0[k] + c * P1[k];
+    const double a = (1.0 - c) * (1.0 - c), qq = c * c;
+    double cov[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + qq * C1[i];
+    const double v = endpointVar_t<double>(cam, Dl, Jl, Pt, cov, 0.0);
+    double cur[3];
+    se3_apply(Dl, Pt, cur);
+    const double f = cam.fx / ref_max(homog, cur[2] * cur[2]);
+    return v / (f * f);
+}
+
+// The line's replay with a small cache of evaluated ratios per side: the fallback of k_cut_vref for a
+// line whose compared ratios leave the key table (a ratio moved back: rare), one lane.
+__device__ __forceinline__ void vref_replay(const KParams& p, int b, int m) {
+    const double* fd = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
+    double* out = p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX;
+    const uint8_t* path = p.scr.cut_path + ((size_t)b * p.mls_cap + m) * CUT_PATH;
+    const DevLines& L = p.prev.ls;
+    const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+    const double* Dl = p.scr.cut_dtinv + 16 * (size_t)b;
+    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    double sP[3], eP[3], cS[9], cE[9], Jl[2], qs[5], qe[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sP[k] = L.sP[3 * q + k]; eP[k] = L.eP[3 * q + k]; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { cS[k] = L.covS[9 * q + k]; cE[k] = L.covE[9 * q + k]; }
+    Jl[0] = L.le_obs[3 * q];
+    Jl[1] = L.le_obs[3 * q + 1];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { qs[k] = fd[PD_VS + k]; qe[k] = fd[PD_VE + k]; }
+    double r0 = 0.0, r1 = 0.0;
+    bool done = false;
+    // the reference's v' at the last four ratios evaluated per side (t bits, value), in registers:
+    // a ratio step moves the window by one, so a step evaluates at most one new ratio per side
+    long long ct0[4] = {-1, -1, -1, -1}, ct1[4] = {-1, -1, -1, -1};
+    double cv0[4] = {0, 0, 0, 0}, cv1[4] = {0, 0, 0, 0};
+    int slot0 = 0, slot1 = 0;
+    double ivm[2] = {0.0, 0.0}, rim[2] = {0.0, 0.0};
+    int marg = 0, nbad = 0, nev = 0;
+    for (int k = 0; k < CUT_PATH && !done; ++k) {
+        const int by = path[k];
+        if (!(by & CUT_P_EXACT)) {
+            ++marg;
+            for (int w = 0; w < 6; ++w) {
+                const int side = w >= 3 ? 1 : 0, o = w - 3 * side;
+                const double rc = side ? r1 : r0;
+                const double t = o == 0 ? rc + (-st) : (o == 2 ? rc + st : rc);   // (nb_step's bits)
+                if (!(t >= rlo && t <= rhi)) continue;
+                const long long tb = __double_as_longlong(t);
+                double vr = 0.0;
+                bool hit = false;
+#pragma unroll
+                for (int z = 0; z < 4; ++z) {
+                    const bool h = side ? ct1[z] == tb : ct0[z] == tb;
+                    vr = h ? (side ? cv1[z] : cv0[z]) : vr;
+                    hit = hit || h;
+                }
+                if (!hit) {
+                    vr = side ? vref_regs(p.cam, p.cfg.homog_th, Dl, eP, sP, cE, cS, Jl, t)
+                              : vref_regs(p.cam, p.cfg.homog_th, Dl, sP, eP, cS, cE, Jl, t);
+                    ++nev;
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        if (side && slot1 == z) { ct1[z] = tb; cv1[z] = vr; }
+                        if (!side && slot0 == z) { ct0[z] = tb; cv0[z] = vr; }
+                    }
+                    if (side) slot1 = (slot1 + 1) & 3; else slot0 = (slot0 + 1) & 3;
+                }
+                const double* qc = side ? qe : qs;
+                const double vo = __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, qc[4], qc[3]), qc[2]),
+                                                                 qc[1]), qc[0]);   // (cut_ours_V's expression)
+                const double lo = fmin(vr, vo);
+                const double rv = fabs(vo - vr) / vr;
+                if (!(lo > 0.0 && rv < 0.01)) { ++nbad; continue; }
+                const double iv = 1.01 / lo;
+                ivm[side] = fmax(ivm[side], iv);
+                rim[side] = fmax(rim[side], rv * iv);
+            }
+        }
+        if (by & CUT_P_STAY) {
+            done = true;
+        } else {
+            const int jj = by & 7;
+            r0 = r0 + nb_step(jj, 0, st);
+            r1 = r1 + nb_step(jj, 1, st);
+            if (!(r0 + r1 <= 1.0)) done = true;
+        }
+    }
+    // a path that does not end where the search's final ratios are counts as a failure
+    if (!done || __double_as_longlong(r0) != __double_as_longlong(L.cut[2 * q]) ||
+        __double_as_longlong(r1) != __double_as_longlong(L.cut[2 * q + 1]))
+        nbad += 1 << 20;
+    out[0] = ivm[0];
+    out[1] = rim[0];
+    out[2] = ivm[1];
+    out[3] = rim[1];
+    out[4] = (double)marg + 1024.0 * (double)nev;   // (marg <= CUT_PATH)
+    out[5] = (double)nbad;
+}
+
+
+// Lines in chunks of 64 (one wave), in two passes.  (A) lane per line: the recorded steps replayed on
+// the ratio-key links (cut_knxt / cut_kprv, the bits of r + s and r - s), marking per side every key a
+// margined step compared; (B) the marked (line, side, key) items, compacted in LDS, evaluated by the
+// whole wave (consecutive items share a line: its data loads broadcast), the per-side maxima by LDS
+// atomics.  A line whose compared ratios leave the table takes vref_replay.
+__global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
+    __shared__ double keys[CUT_KS];
+    __shared__ int8_t knx[CUT_KS], kpv[CUT_KS];
+    __shared__ uint16_t items[64 * 2 * CUT_KS];
+    __shared__ unsigned long long red[4][64];   // ivm0, rim0, ivm1, rim1 (non-negative doubles' bits)
+    __shared__ int nbl[64];
+    const int b = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int m = blockIdx.x * 64 + lane;
+    const int nls = p.tr.n_matched_ls[b];
+    if (blockIdx.x * 64 >= nls) return;   // (wave-uniform)
+    const int nk = p.cut_nkeys;
+    if (lane < CUT_KS) {
+        keys[lane] = p.cut_keys[lane];
+        knx[lane] = p.cut_knxt[lane];
+        kpv[lane] = p.cut_kprv[lane];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[i][lane] = 0ull;
+    nbl[lane] = 0;
+    wave_lds_sync();
+    const bool on = m < nls;
+    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    // (A) replay on the key links
+    uint32_t mk[2] = {0u, 0u};
+    int marg = 0, nbad = 0;
+    bool off = nk == 0;
+    if (on && !off) {
+        // the line's 64 path bytes in one go (16-byte loads), not a memory round trip per step
+        const uint4* pv = reinterpret_cast<const uint4*>(p.scr.cut_path + ((size_t)b * p.mls_cap + m) * CUT_PATH);
+        uint32_t pw[CUT_PATH / 4];
+#pragma unroll
+        for (int i = 0; i < CUT_PATH / 16; ++i) {
+            const uint4 v = pv[i];
+            pw[4 * i] = v.x; pw[4 * i + 1] = v.y; pw[4 * i + 2] = v.z; pw[4 * i + 3] = v.w;
+        }
+        double r[2] = {0.0, 0.0};
+        int kc[2] = {0, 0};   // (keys[0] is 0.0)
+        bool done = false;
+        for (int k = 0; k < CUT_PATH && !done && !off; ++k) {
+            uint32_t wd = pw[0];
+#pragma unroll
+            for (int i = 1; i < CUT_PATH / 4; ++i) wd = (k >> 2) == i ? pw[i] : wd;
+            const int by = (int)((wd >> (8 * (k & 3))) & 255u);
+            if (!(by & CUT_P_EXACT)) {
+                ++marg;
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+#pragma unroll
+                    for (int o = 0; o < 3; ++o) {
+                        const double t = o == 0 ? r[side] + (-st) : (o == 2 ? r[side] + st : r[side]);
+                        if (!(t >= rlo && t <= rhi)) continue;
+                        const int kk = kc[side] < 0 ? -1 : (o == 0 ? kpv[kc[side]] : (o == 2 ? knx[kc[side]] : kc[side]));
+                        if (kk < 0 || __double_as_longlong(keys[kk]) != __double_as_longlong(t)) { off = true; continue; }
+                        mk[side] |= 1u << kk;
+                    }
+                }
+            }
+            if (by & CUT_P_STAY) {
+                done = true;
+            } else {
+                const int jj = by & 7;
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const double sv = nb_step(jj, side, st);
+                    r[side] = r[side] + sv;
+                    if (kc[side] >= 0) kc[side] = sv > 0.0 ? knx[kc[side]] : (sv < 0.0 ? kpv[kc[side]] : kc[side]);
+                }
+                if (!(r[0] + r[1] <= 1.0)) done = true;
+            }
+        }
+        const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+        // a path that does not end where the search's final ratios are counts as a failure
+        if (!done || __double_as_longlong(r[0]) != __double_as_longlong(p.prev.ls.cut[2 * q]) ||
+            __double_as_longlong(r[1]) != __double_as_longlong(p.prev.ls.cut[2 * q + 1]))
+            nbad += 1 << 20;
+    }
+    if (off) mk[0] = mk[1] = 0u;
+    // compaction: the lane's items at its exclusive prefix of the counts
+    const int cnt = __popc(mk[0]) + __popc(mk[1]);
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o);
+        if (lane >= o) inc += v;
+    }
+    const int total = __shfl(inc, 63);
+    {
+        int w = inc - cnt;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            uint32_t x = mk[side];
+            while (x) {
+                const int kk = __ffs(x) - 1;
+                x &= x - 1u;
+                items[w++] = (uint16_t)((lane << 6) | (side << 5) | kk);
+            }
+        }
+    }
+    wave_lds_sync();
+    // (B) the items, one per lane per round
+    const DevLines& L = p.prev.ls;
+    const double* Dl = p.scr.cut_dtinv + 16 * (size_t)b;
+    for (int i0 = 0; i0 < total; i0 += 64) {   // (wave-uniform)
+        const int i = i0 + lane;
+        if (i < total) {
+            const int it = items[i];
+            const int ln = it >> 6, side = (it >> 5) & 1, kk = it & 31;
+            const int mm = blockIdx.x * 64 + ln;
+            const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + mm];
+            const double* fd = p.scr.cut_rec + ((size_t)b * p.mls_cap + mm) * CUT_REC;
+            double P0[3], P1[3], C0[9], C1[9], Jl[2], qc[5];
+            const double* A3 = side ? L.eP : L.sP;
+            const double* B3 = side ? L.sP : L.eP;
+            const double* A9 = side ? L.covE : L.covS;
+            const double* B9 = side ? L.covS : L.covE;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { P0[k] = A3[3 * q + k]; P1[k] = B3[3 * q + k]; }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { C0[k] = A9[9 * q + k]; C1[k] = B9[9 * q + k]; }
+            Jl[0] = L.le_obs[3 * q];
+            Jl[1] = L.le_obs[3 * q + 1];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) qc[k] = fd[(side ? PD_VE : PD_VS) + k];
+            const double t = keys[kk];
+            const double vr = vref_regs(p.cam, p.cfg.homog_th, Dl, P0, P1, C0, C1, Jl, t);
+            const double vo = __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, __builtin_fma(t, qc[4], qc[3]), qc[2]),
+                                                             qc[1]), qc[0]);   // (cut_ours_V's expression)
+            const double lo = fmin(vr, vo);
+            const double rv = fabs(vo - vr) / vr;
+            if (!(lo > 0.0 && rv < 0.01)) {
+                atomicAdd(&nbl[ln], 1);
+            } else {
+                const double iv = 1.01 / lo;
+                atomicMax(&red[2 * side][ln], (unsigned long long)__double_as_longlong(iv));
+                atomicMax(&red[2 * side + 1][ln], (unsigned long long)__double_as_longlong(rv * iv));
+            }
+        }
+    }
+    wave_lds_sync();
+    if (!on) return;
+    double* out = p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX;
+    if (off) {   // (k_cut_vref_off replays the line)
+        out[4] = -1.0;
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = __longlong_as_double((long long)red[i][lane]);
+    out[4] = (double)marg + 1024.0 * (double)cnt;   // (marg <= CUT_PATH)
+    out[5] = (double)(nbad + nbl[lane]);
+}
+
+// the lines k_cut_vref left (out[4] = -1: a compared ratio off the key table), one lane each; its own
+// kernel, so that the replay's registers do not set k_cut_vref's occupancy
+__global__ void __launch_bounds__(64) k_cut_vref_off(KParams p) {
+    const int b = blockIdx.y;
+    const int m = blockIdx.x * 64 + threadIdx.x;
+    if (m >= p.tr.n_matched_ls[b]) return;
+    if (p.scr.cut_vmax[((size_t)b * p.mls_cap + m) * CUT_VMAX + 4] < 0.0) vref_replay(p, b, m);
+}
+
+// Proven mode: the operand error bounds of every matched line (cut_line_bounds_p, P only) into
+// cut_vmax[6..13] as 14 floats, one lane per line — no dependence between lines, so out of
+// k_cut_verify's serial sequence pass (and its register budget)
+__global__ void __launch_bounds__(64) k_cut_ebound(KParams p) {
+    const int b = blockIdx.y;
+    const int m = blockIdx.x * 64 + threadIdx.x;
+    if (m >= p.tr.n_matched_ls[b]) return;
+    const double* fd = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
+    if (fd[PD_OK] == 0.0) return;
+    const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+    double Dl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
+    float eb[14];
+    cut_line_bounds_p(p, q, true, Dl, eb);
+    float* o = reinterpret_cast<float*>(p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX + 6);
+#pragma unroll
+    for (int i = 0; i < 14; ++i) o[i] = eb[i];
+}
+
+// A recorded step the bound does not cover, checked with the reference's own arithmetic: its 6
+// endpoint slots (reference order), every valid neighbour's logdet(S_ref + info) and the centre
+// metric (logdet(invCov_sum) on a line's first step), the reference's first strict maximum against
+// the recorded decision.  Out of line: rare, and its two 6x6 LLTs per neighbour would set the
+// register budget of the replay.  Returns 1 when the decisions agree.
+__device__ __attribute__((noinline)) int verify_exact_step(const KParams& p, const double* Dl, size_t q, double r0,
+                                                           double r1, int first, const double* Sref, const double* Sfull,
+                                                           int recorded) {
+    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    double ep[6][7];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int side = j < 3 ? 0 : 1;
+        const double eoff = (j % 3) == 0 ? -st : ((j % 3) == 2 ? st : 0.0);
+        exact_endpoint(p.cam, p.cfg.homog_th, Dl, p.prev.ls, q, side, (side == 0 ? r0 : r1) + eoff, ep[j]);
+    }
+    double tot[21], tmp[21];
+    double mc;
+    if (first) {
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = Sfull[i];
+    } else {
+        cut_assemble<false>(ep[1], ep[4], tmp);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + Sref[i];
+    }
+    mc = logdet6_lower(tot);
+    double mx = -__builtin_inf();
+    int best = -1;
+    for (int jn = 0; jn < 8; ++jn) {
+        const double t0 = r0 + nb_step(jn, 0, st), t1 = r1 + nb_step(jn, 1, st);
+        if (t0 + t1 > 1.0 || t0 < rlo || t0 > rhi || t1 < rlo || t1 > rhi) continue;
+        cut_assemble<false>(ep[nb_slot(jn, 0)], ep[3 + nb_slot(jn, 1)], tmp);
+#pragma unroll
+        for (int i = 0; i < 21; ++i) tot[i] = tmp[i] + Sref[i];
+        const double v = logdet6_lower(tot);
+        if (v == v && v > mx) { mx = v; best = jn; }   // the first strict maximum (ties: lowest j)
+    }
+    const int ref = (best >= 0 && mx > mc) ? best : CUT_P_STAY;
+    return ref == recorded ? 1 : 0;
+}
+
+// k_cut_verify's step-by-step replay of one line the line-level bound did not cover (rare): per margined
+// step the reference's v' at the step's ratios and the step's own bound, a step no bound covers
+// re-decided by the reference's arithmetic (verify_exact_step).  Sfull: the LDS column of the
+// reference's whole invCov_sum at the line's start (stride 65).  Returns a reason mask.
+__device__ __attribute__((noinline)) int verify_line_detail(const KParams& p, const double* Dl, size_t q,
+                                                            const uint8_t* path_m, const double* fd, double r0f,
+                                                            double r1f, double K0, double A1, double B1, double cs,
+                                                            double ce, double R0, double rts, double rte, bool line_ok,
+                                                            const double* Scol, int& n_xchk) {
+    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const bool pdok = fd[PD_OK] != 0.0;
+    int bad = 0;
+    {
+            double r0 = 0.0, r1 = 0.0;
+            bool done = false;
+            int first = 1;
+            // the reference's v' at the last ratios evaluated, per side (t bits, value); the quartic is
+            // re-evaluated (four FMAs)
+            double ct[2][4], cv[2][4];
+            int cn[2] = {0, 0};
+            for (int k = 0; k < CUT_PATH && !done; ++k) {
+                const int by = path_m[k];
+                if (!(by & CUT_P_EXACT)) {
+                    // (a margined step)
+                    double ivm[2] = {0.0, 0.0}, rim[2] = {0.0, 0.0};
+                    bool vok = pdok;
+                    for (int w = 0; w < 6 && vok; ++w) {
+                        const int side = w / 3, o = w % 3;
+                        const double rc = side ? r1 : r0;
+                        const double t = o == 0 ? rc + (-st) : (o == 2 ? rc + st : rc);   // (nb_step's bits)
+                        if (!(t >= rlo && t <= rhi)) continue;
+                        double vr = 0.0;
+                        bool hit = false;
+                        for (int z = 0; z < cn[side]; ++z)
+                            if (__double_as_longlong(ct[side][z]) == __double_as_longlong(t)) { vr = cv[side][z]; hit = true; }
+                        if (!hit) {
+                            vr = verify_vref(p, Dl, q, side, t);
+                            const int z = cn[side] < 4 ? cn[side]++ : (k & 3);
+                            ct[side][z] = t;
+                            cv[side][z] = vr;
+                        }
+                        const double vo = cut_ours_V(fd, side, t);
+                        const double lo = fmin(vr, vo);
+                        const double rv = fabs(vo - vr) / vr;
+                        if (!(lo > 0.0 && rv < 0.01)) { vok = false; continue; }
+                        const double iv = 1.01 / lo;
+                        ivm[side] = fmax(ivm[side], iv);
+                        rim[side] = fmax(rim[side], (1.01 * rv + (side ? rte : rts)) * iv);
+                    }
+                    const double E = K0 + A1 * ivm[0] + cs * rim[0] + B1 * ivm[1] + ce * rim[1];
+                    if (!(vok && line_ok && E * 1.0001 <= R0)) {
+                        // not covered by the bound: the reference's own evaluation of the step
+                        double Sref[21], Sfull[21];
+#pragma unroll
+                        for (int e = 0; e < 21; ++e) { Sfull[e] = Scol[65 * e]; Sref[e] = Sfull[e] - fd[CUT_FAST + e]; }
+                        ++n_xchk;
+                        if (!verify_exact_step(p, Dl, q, r0, r1, first, Sref, Sfull, (by & CUT_P_STAY) ? CUT_P_STAY : (by & 7)))
+                            bad |= 512;
+                    }
+                }
+                first = 0;
+                if (by & CUT_P_STAY) {
+                    done = true;
+                } else {
+                    const int jj = by & 7;
+                    r0 = r0 + nb_step(jj, 0, st);
+                    r1 = r1 + nb_step(jj, 1, st);
+                    if (!(r0 + r1 <= 1.0)) done = true;
+                }
+            }
+            // the replay must end where the search did
+            if (!done || __double_as_longlong(r0) != __double_as_longlong(r0f) ||
+                __double_as_longlong(r1) != __double_as_longlong(r1f))
+                bad |= 1;
+        }
+    return bad;
+}
+
+// k_cut_verify: the S-dependent bound terms of one line from S_ours (LDS column So),
+// the reference's whole sum at the line's start (column Sf; S_ref = Sf - i0) and the operand bounds.
+// Out of line: its unrolled 6 x 6 loops would otherwise set the kernel's register budget.
+struct LineBound {
+    double K0, A1, B1, cs, ce, R0, rts, rte, epsS, kt;
+    int ok;
+};
+__device__ __forceinline__ LineBound verify_line_bound(const KParams& p, size_t q, const double* fd, const double* vmx,
+                                                      const double* Dl, const double* So, const double* Sf) {
+    const double rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
+    const double T = fmax(fabs(rlo), fabs(rhi));
+    const double tau = p.cfg.cut_certify;
+    constexpr double u = 0x1p-53;
+    LineBound lbd;
+    double K0, A1, B1, cs, ce, R0, rts, rte, epsS_l, kt_l;
+    bool line_ok;
+        float eb[14];
+        {
+            const float* ebg = reinterpret_cast<const float*>(vmx + 6);   // (k_cut_ebound's)
+#pragma unroll
+            for (int i = 0; i < 14; ++i) eb[i] = ebg[i];
+        }
+        double o28[28];
+        {
+            double S[21];
+#pragma unroll
+            for (int e = 0; e < 21; ++e) S[e] = So[65 * e];
+            chol_s(S, o28);   // (the search's factorization: pivots >= 1e-2 of the diagonal, 1 / L_kk)
+        }
+        double sg[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double x[6], a = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double uu = i == j ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * x[k];
+                x[i] = uu * o28[21 + i];
+                a = a + x[i] * x[i];
+            }
+            sg[j] = 1.002 * a;
+        }
+        double Bn[2] = {0.0, 0.0};
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            double tk = 1.0;
+#pragma unroll
+            for (int kk = 0; kk < 3; ++kk) {
+                double w[6], a = 0.0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    double uu = fd[(side ? PD_PE : PD_PS) + 6 * kk + i];
+#pragma unroll
+                    for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * w[k];
+                    w[i] = uu * o28[21 + i];
+                    a = a + w[i] * w[i];
+                }
+                Bn[side] = Bn[side] + 1.01 * sqrt(a) * tk;
+                tk = tk * T;
+            }
+        }
+        double Kc = 0.0, xi = 0.0, Qs = 0.0, Qe = 0.0, hs0 = 0.0, he0 = 0.0, Lam = 0.0, dSn = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double Sii = So[65 * tri(i, i)];
+            const double es = eb[i], ee = eb[7 + i];
+            const double ps = fabs(fd[PD_PS + i]) + T * (fabs(fd[PD_PS + 6 + i]) + T * fabs(fd[PD_PS + 12 + i])) + es;
+            const double pe = fabs(fd[PD_PE + i]) + T * (fabs(fd[PD_PE + 6 + i]) + T * fabs(fd[PD_PE + 12 + i])) + ee;
+            const double kc = Sii * sg[i];
+            Kc = Kc + kc;
+            xi = xi + sqrt(kc);
+            Qs = Qs + sg[i] * ps * ps;
+            Qe = Qe + sg[i] * pe * pe;
+            hs0 = hs0 + es * sqrt(sg[i]);
+            he0 = he0 + ee * sqrt(sg[i]);
+            Lam = Lam + ((Sii > 0.0 && Sii < 1e300) ? 0.6931471805599453 * (double)(abs(__builtin_amdgcn_frexp_exp(Sii)) + 1)
+                                                     : __builtin_inf());
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                // |S_ours - S_ref| of entry (i, k), S_ref = sE - i0 as the reference forms it; the
+                // difference of two such close values is exact (Sterbenz), 2u |.| covers the rest
+                const int e = tri(i > k ? i : k, i > k ? k : i);
+                const double sref = Sf[65 * e] - fd[CUT_FAST + e];
+                const double dd = 1.0000000000000004 * fabs(So[65 * e] - sref);
+                dSn = dSn + dd * sqrt(sg[i] * sg[k]);
+            }
+        }
+        const double epsS = 1.01 * dSn + (7.01 * u) * xi * xi;
+        const double hs = hs0 + (6.01 * u) * Bn[0] * xi, he = he0 + (6.01 * u) * Bn[1] * xi;
+        const double ck = 110.0 * u;
+        K0 = 1.002 * epsS + ck * Kc + (7.1 * u) * Lam;
+        const double bs = Bn[0] + hs, be = Bn[1] + he;
+        // the v'-table's own error (the blended depth's relative error x 4 + the scaling's roundings)
+        rts = 4.1 * (double)eb[6] + 16.0 * u;
+        rte = 4.1 * (double)eb[13] + 16.0 * u;
+        A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs);
+        B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be);
+        cs = 4.12 * bs * bs;
+        ce = 4.12 * be * be;
+        R0 = fmin(0.125 * tau, 1e-3) - 1.01 * K0;
+        line_ok = o28[27] != 0.0 && epsS <= 1e-3 && Kc <= 1e8 && R0 > 0.0 && rlo >= 0.0 && rhi <= 1.0 &&
+                  tau > 0.0 && rts + rte <= 0.01;
+        epsS_l = 1.002 * epsS;
+        kt_l = ck * Kc + (7.1 * u) * Lam;
+
+    lbd.K0 = K0; lbd.A1 = A1; lbd.B1 = B1; lbd.cs = cs; lbd.ce = ce; lbd.R0 = R0; lbd.rts = rts; lbd.rte = rte;
+    lbd.epsS = epsS_l; lbd.kt = kt_l; lbd.ok = line_ok ? 1 : 0;
+    return lbd;
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_verify(KParams p) {
     __shared__ double fo[21][65];   // the chunk's lines: our info, then S_ours of the line
-    __shared__ double fr[21][65];   // the reference's info, then dS = S_ours - S_ref
+    __shared__ double fr[21][65];   // the reference's info, then its whole invCov_sum at the line's start
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -1901,12 +2545,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     double Dl[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
-    const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
-    const double T = fmax(fabs(rlo), fabs(rhi));
-    const double tau = p.cfg.cut_certify;
-    constexpr double u = 0x1p-53;
-    int bad = p.cfg.cut_proof == 3 ? 1 : 0;   // (cut_proof 3: every sequence redone eagerly — a test hook)
-    int64_t n_marg = 0, n_eval = 0, n_mline = 0;
+    int bad = p.cfg.cut_proof == 3 ? 256 : 0;   // (cut_proof 3: every sequence redone eagerly — a test hook)
+    // bad is a reason mask (diagnostics, scr.dbg): 1 replay != search, 2 v' <= 0 or r_v >= 1/4, 512 a step
+    // the bound does not cover decided otherwise by the reference's arithmetic
+    double worst = 0.0;   // max E / R0 over the margined steps
+    double tS = 0.0, tK = 0.0, tA = 0.0, tV = 0.0;   // its terms: eps_S, K0's rest, A1 / B1, the v' terms
+    int64_t n_marg = 0, n_eval = 0, n_mline = 0, n_xchk = 0, n_dline = 0;
     // the running sums of the search (sA: ours, S of the line being opened) and of the reference (sE:
     // the whole sum before the line's r = 0 info is taken out), lanes 0-20 hold entry lane
     double sA = 0.0, sE = 0.0;
@@ -1915,6 +2559,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         sA = s0 - rec_l[CUT_FAST + lane];
         sE = s0;
     }
+#ifdef GFPL_VERIFY_CLOCK   // (diagnostic build: shader-clock cycles per phase in scr.dbg 0-4)
+    uint64_t vk[5] = {0, 0, 0, 0, 0};
+    uint64_t vk0 = clock64();
+#define VK(i) do { const uint64_t vk1 = clock64(); vk[i] += vk1 - vk0; vk0 = vk1; } while (0)
+#else
+#define VK(i) do { } while (0)
+#endif
     for (int c0 = 0; c0 < nls; c0 += 64) {   // (wave-uniform)
         const int m = c0 + lane;
         const bool on = m < nls;
@@ -1937,6 +2588,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int k = 0; k <= i; ++k) fr[tri(i, k)][lane] = info[i * 6 + k];
             }
         }
+        VK(0);
         // (2) the search's own info of the line (its transition's expressions, cut_ours_*)
         const bool pdok = fd[PD_OK] != 0.0;
         {
@@ -1958,173 +2610,94 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int k = 0; k <= i; ++k) fo[tri(i, k)][lane] = cut_ours_info(xs, is, ie, i, k);
             }
         }
-        // (3) replay the recorded steps: the ratios every margined step compared, their v' both ways
-        double ivs = 0.0, rivs = 0.0, ive = 0.0, rive = 0.0, rvmax = 0.0;
-        int marg = 0;
-        float eb[14];
-#pragma unroll
-        for (int i = 0; i < 14; ++i) eb[i] = 0.0f;
-        if (on) {
-            double r0 = 0.0, r1 = 0.0;
-            bool done = false;
-            // the reference's v' at the last ratios evaluated, per side (t bits, value); the quartic is
-            // re-evaluated (four FMAs)
-            double ct[2][4], cv[2][4];
-            int cn[2] = {0, 0};
-            for (int k = 0; k < CUT_PATH && !done; ++k) {
-                const int by = path[(size_t)m * CUT_PATH + k];
-                if (!(by & CUT_P_EXACT)) {
-                    ++marg;
-                    // the six ratios the step compared (superset: every t in range, both sides)
-                    for (int w = 0; w < 6; ++w) {
-                        const int side = w / 3, o = w % 3;
-                        const double rc = side ? r1 : r0;
-                        const double t = o == 0 ? rc + (-st) : (o == 2 ? rc + st : rc);   // (nb_step's bits)
-                        if (!(t >= rlo && t <= rhi)) continue;
-                        double vr = 0.0;
-                        bool hit = false;
-                        for (int z = 0; z < cn[side]; ++z)
-                            if (__double_as_longlong(ct[side][z]) == __double_as_longlong(t)) { vr = cv[side][z]; hit = true; }
-                        if (!hit) {
-                            vr = verify_vref(p, Dl, q, side, t);
-                            ++n_eval;
-                            const int z = cn[side] < 4 ? cn[side]++ : (k & 3);
-                            ct[side][z] = t;
-                            cv[side][z] = vr;
-                        }
-                        const double vo = cut_ours_V(fd, side, t);
-                        const double lo = fmin(vr, vo);
-                        const double rv = fabs(vo - vr) / vr;
-                        if (!(lo > 0.0 && rv < 0.25)) { bad = 1; continue; }
-                        const double iv = 1.0 / lo;
-                        rvmax = fmax(rvmax, rv);
-                        if (side) { ive = fmax(ive, iv); rive = fmax(rive, rv * iv); }
-                        else { ivs = fmax(ivs, iv); rivs = fmax(rivs, rv * iv); }
-                    }
-                }
-                if (by & CUT_P_STAY) {
-                    done = true;
-                } else {
-                    const int jj = by & 7;
-                    r0 = r0 + nb_step(jj, 0, st);
-                    r1 = r1 + nb_step(jj, 1, st);
-                    if (!(r0 + r1 <= 1.0)) done = true;
-                }
-            }
-            // the replay must end where the search did
-            if (!done || __double_as_longlong(r0) != __double_as_longlong(r0f) ||
-                __double_as_longlong(r1) != __double_as_longlong(r1f))
-                bad = 1;
-            n_marg += marg;
-            if (marg) {
-                ++n_mline;
-                cut_line_bounds(p, q, pdok, Dl, eb);
-            }
-        }
         wave_lds_sync();
-        // (4) the two running sums in list order (lanes 0-20, entry lane): S_ours and dS of each line
-        //     replace its infos in fo / fr
+        VK(1);
+        // (3) the two running sums in list order (lanes 0-20, entry lane): S_ours and the reference's
+        //     whole sum at each line's start replace its infos in fo / fr
         const int cnt = min(64, nls - c0);
         if (lane < 21) {
-            for (int l = 0; l < cnt; ++l) {
-                const double i0 = rec_l[(size_t)(c0 + l) * CUT_REC + CUT_FAST + lane];
-                const double i0n = c0 + l + 1 < nls ? rec_l[(size_t)(c0 + l + 1) * CUT_REC + CUT_FAST + lane] : 0.0;
-                const double sref = sE - i0;                 // the reference's S of line c0 + l
-                const double sours = sA;                     // the search's
-                const double f_o = fo[lane][l], f_r = fr[lane][l];
-                fo[lane][l] = sours;
-                fr[lane][l] = sours - sref;
-                sE = sref + f_r;
-                sA = (sA + f_o) - i0n;
+            // the r = 0 infos are fetched 16 lines at a time (one memory round trip per batch, not per line)
+            for (int l0 = 0; l0 < cnt; l0 += 16) {
+                double iv[17];
+#pragma unroll
+                for (int k = 0; k < 17; ++k) {
+                    const int mm = c0 + l0 + k;
+                    iv[k] = (l0 + k <= cnt && mm < nls) ? rec_l[(size_t)mm * CUT_REC + CUT_FAST + lane] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int l = l0 + k;
+                    if (l < cnt) {
+                        const double sref = sE - iv[k];                // the reference's S of line c0 + l
+                        const double f_o = fo[lane][l], f_r = fr[lane][l];
+                        fo[lane][l] = sA;
+                        fr[lane][l] = sE;
+                        sE = sref + f_r;
+                        sA = (sA + f_o) - iv[k + 1];
+                    }
+                }
             }
         }
         wave_lds_sync();
-        // (5) the agreement bound of each line with margined steps
-        if (on && marg) {
-            double o28[28];
-            {
-                double S[21];
-#pragma unroll
-                for (int e = 0; e < 21; ++e) S[e] = fo[e][lane];
-                chol_s(S, o28);   // (the search's factorization: pivots >= 1e-2 of the diagonal, 1 / L_kk)
-            }
-            if (o28[27] == 0.0) bad = 1;
-            // s_i = |L^-1 e_i|^2, W_k = L^-1 P_k (the comparison data's six coefficient vectors)
-            double sg[6];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double x[6], a = 0.0;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) {
-                    double uu = i == j ? 1.0 : 0.0;
-#pragma unroll
-                    for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * x[k];
-                    x[i] = uu * o28[21 + i];
-                    a = a + x[i] * x[i];
-                }
-                sg[j] = 1.002 * a;
-            }
-            double Bn[2] = {0.0, 0.0};
-#pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                double tk = 1.0;
-#pragma unroll
-                for (int kk = 0; kk < 3; ++kk) {
-                    double w[6], a = 0.0;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) {
-                        double uu = fd[(side ? PD_PE : PD_PS) + 6 * kk + i];
-#pragma unroll
-                        for (int k = 0; k < i; ++k) uu = uu - o28[tri(i, k)] * w[k];
-                        w[i] = uu * o28[21 + i];
-                        a = a + w[i] * w[i];
-                    }
-                    Bn[side] = Bn[side] + 1.01 * sqrt(a) * tk;
-                    tk = tk * T;
+        VK(2);
+        // (4) the line's bound terms from S_ours, S_ref = sE - i0, and the operand bounds
+        double K0 = 0.0, A1 = 0.0, B1 = 0.0, cs = 0.0, ce = 0.0, R0 = -1.0, rts = 0.0, rte = 0.0;
+        double epsS_l = 0.0, kt_l = 0.0;
+        bool line_ok = false;
+        if (on && pdok) {
+            const LineBound lbd = verify_line_bound(p, q, fd, p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX, Dl,
+                                                    &fo[0][0] + lane, &fr[0][0] + lane);
+            K0 = lbd.K0; A1 = lbd.A1; B1 = lbd.B1; cs = lbd.cs; ce = lbd.ce; R0 = lbd.R0; rts = lbd.rts; rte = lbd.rte;
+            epsS_l = lbd.epsS; kt_l = lbd.kt; line_ok = lbd.ok != 0;
+        }
+        VK(3);
+        // (5) the line's margined steps: with k_cut_vref's maxima over the compared ratios, one bound for
+        //     every step of the line; a line it does not cover is replayed step by step (the reference's v'
+        //     at each step's ratios, the step's own bound) and a step no bound covers is re-decided exactly
+        int marg = 0;
+        bool detail = false;
+        if (on) {
+            const double* vm = p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX;
+            const double mv = vm[4];
+            marg = (int)fmod(mv, 1024.0);
+            n_eval += (int64_t)(mv / 1024.0);
+            if (marg) {
+                const double E = K0 + A1 * vm[0] + cs * (1.01 * vm[1] + rts * vm[0]) + B1 * vm[2] +
+                                 ce * (1.01 * vm[3] + rte * vm[2]);
+                detail = !(vm[5] == 0.0 && line_ok && E * 1.0001 <= R0);
+                if (!detail && E / R0 > worst) {   // (diagnostics: the worst line's terms, relative to R0)
+                    worst = E / R0;
+                    tS = epsS_l / R0;
+                    tK = kt_l / R0;
+                    tA = (A1 * vm[0] + B1 * vm[2]) / R0;
+                    tV = (cs * (1.01 * vm[1] + rts * vm[0]) + ce * (1.01 * vm[3] + rte * vm[2])) / R0;
                 }
             }
-            double Kc = 0.0, xi = 0.0, Qs = 0.0, Qe = 0.0, hs0 = 0.0, he0 = 0.0, Lam = 0.0, dSn = 0.0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double Sii = fo[tri(i, i)][lane];
-                const double es = eb[i], ee = eb[7 + i];
-                const double ps = fabs(fd[PD_PS + i]) + T * (fabs(fd[PD_PS + 6 + i]) + T * fabs(fd[PD_PS + 12 + i])) + es;
-                const double pe = fabs(fd[PD_PE + i]) + T * (fabs(fd[PD_PE + 6 + i]) + T * fabs(fd[PD_PE + 12 + i])) + ee;
-                const double kc = Sii * sg[i];
-                Kc = Kc + kc;
-                xi = xi + sqrt(kc);
-                Qs = Qs + sg[i] * ps * ps;
-                Qe = Qe + sg[i] * pe * pe;
-                hs0 = hs0 + es * sqrt(sg[i]);
-                he0 = he0 + ee * sqrt(sg[i]);
-                Lam = Lam + ((Sii > 0.0 && Sii < 1e300) ? 0.6931471805599453 * (double)(abs(__builtin_amdgcn_frexp_exp(Sii)) + 1)
-                                                         : __builtin_inf());
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    // |dS_ik| (+ the rounding of its own subtraction, u |S_ik|), whitened
-                    const int e = tri(i > k ? i : k, i > k ? k : i);
-                    const double dd = fabs(fr[e][lane]) + u * fabs(fo[e][lane]);
-                    dSn = dSn + dd * sqrt(sg[i] * sg[k]);
-                }
-            }
-            const double epsS = 1.01 * dSn + (7.01 * u) * xi * xi;
-            const double hs = hs0 + (6.01 * u) * Bn[0] * xi, he = he0 + (6.01 * u) * Bn[1] * xi;
-            const double ck = 110.0 * u;
-            const double K0 = 1.002 * epsS + ck * Kc + (7.1 * u) * Lam;
-            const double bs = Bn[0] + hs, be = Bn[1] + he;
-            // the v'-table's own error (the blended depth's relative error x 4 + the scaling's roundings)
-            const double rts = 4.1 * (double)eb[6] + 16.0 * u, rte = 4.1 * (double)eb[13] + 16.0 * u;
-            const double A1 = 1.03 * (2.0 * ck * Qs + 4.0 * hs * bs), B1 = 1.03 * (2.0 * ck * Qe + 4.0 * he * be);
-            const double E = K0 + A1 * ivs + 4.12 * bs * bs * (1.01 * rivs + rts * ivs) +
-                             B1 * ive + 4.12 * be * be * (1.01 * rive + rte * ive);
-            const double R0 = fmin(0.125 * tau, 1e-3) - 1.01 * K0;
-            const bool ok = epsS <= 1e-3 && Kc <= 1e8 && R0 > 0.0 && E * 1.0001 <= R0 && rvmax + rts + rte <= 0.25 &&
-                            rlo >= 0.0 && rhi <= 1.0 && tau > 0.0;
-            if (!ok) bad = 1;
+            n_marg += marg;
+            n_mline += marg ? 1 : 0;
+            n_dline += detail ? 1 : 0;
+        }
+        VK(4);
+        if (detail) {
+            int nx = 0;
+            bad |= verify_line_detail(p, Dl, q, path + (size_t)m * CUT_PATH, fd, r0f, r1f, K0, A1, B1, cs, ce, R0, rts, rte,
+                                      line_ok, &fr[0][0] + lane, nx);
+            n_xchk += nx;
         }
         wave_lds_sync();
     }
-    bad = __any(bad) ? 1 : 0;
+    // the reason mask and the worst E / R0 over the wave's lanes (diagnostics)
+    int mask = bad;
+    int wl = lane;   // the lane holding the worst step
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mask |= __shfl_xor(mask, o);
+        const double ow = __shfl_xor(worst, o);
+        const int ol = __shfl_xor(wl, o);
+        if (ow > worst || (ow == worst && ol < wl)) { worst = ow; wl = ol; }
+    }
+    tS = __shfl(tS, wl); tK = __shfl(tK, wl); tA = __shfl(tA, wl); tV = __shfl(tV, wl);
+    bad = mask != 0 ? 1 : 0;
     // k_cut_finish's endpoint update, for a proven sequence
     if (!bad) {
         for (int m = lane; m < nls; m += 64) {
@@ -2160,6 +2733,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         n_marg += __shfl_xor(n_marg, o);
         n_eval += __shfl_xor(n_eval, o);
         n_mline += __shfl_xor(n_mline, o);
+        n_xchk += __shfl_xor(n_xchk, o);
+        n_dline += __shfl_xor(n_dline, o);
     }
     if (lane == 0) {
         p.scr.cut_flag[b] = bad;
@@ -2167,6 +2742,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         p.scr.bytes[(size_t)STEP_REC * b + 21] = n_marg;
         p.scr.bytes[(size_t)STEP_REC * b + 22] = n_eval;
         p.scr.bytes[(size_t)STEP_REC * b + 23] = n_mline;
+        p.scr.dbg[8 * (size_t)b + 4] = mask;
+        p.scr.dbg[8 * (size_t)b + 5] = __double_as_longlong(worst);
+        p.scr.dbg[8 * (size_t)b + 6] = n_xchk;
+        p.scr.dbg[8 * (size_t)b + 7] = n_dline;
+        p.scr.dbg[8 * (size_t)b + 0] = __double_as_longlong(tS);
+        p.scr.dbg[8 * (size_t)b + 1] = __double_as_longlong(tK);
+        p.scr.dbg[8 * (size_t)b + 2] = __double_as_longlong(tA);
+        p.scr.dbg[8 * (size_t)b + 3] = __double_as_longlong(tV);
+#ifdef GFPL_VERIFY_CLOCK
+        for (int i = 0; i < 5; ++i) p.scr.dbg[8 * (size_t)b + i] = (int64_t)vk[i];
+#endif
     }
 }
 
@@ -2195,6 +2781,9 @@ hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* ma
     if (marks) (void)hipEventRecord(marks[1], s);
     if (mode == 1 || mode == 3) {
         // prove the recorded decisions (and finish those sequences); redo the others eagerly
+        hipLaunchKernelGGL(k_cut_vref, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_vref_off, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_ebound, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_verify, dim3(p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);

@@ -18,9 +18,26 @@
 //    update element-parallel (se3_update_wave).
 // The outlier pass takes the MAD medians by bitwise selection over register-held
 // residuals (wave_select; lists above 512 entries sort in LDS).
+#include <cstdlib>
+
 #include "gfpl_kernels.hpp"
 
 namespace gfpl {
+
+// Small batches (B <= POSE_MULTI_MAX_B) run k_pose<POSE_W>: W waves per sequence, wave 0 the
+// solver as in k_pose<1> and waves 1.. helpers that evaluate a GN chunk each per round (the
+// list-ordered reduction stays wave 0's, so H keeps its bits).  Wave 0's own phases then
+// synchronise as one wave (pose_bar<W>); the block barriers are the helper protocol's alone.
+template <int W>
+__device__ __forceinline__ void pose_bar() {
+    if (W == 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
 
 struct PoseLDS {
     double DT[16];
@@ -32,6 +49,7 @@ struct PoseLDS {
     int ninl;
     int cnt[2];
     double err;
+    int cmd, c0, np_act, nl_act, nch;   // k_pose<W > 1>: helper command (0 exit, 1 evaluate chunks c0 + w)
 };
 
 // DT <- DT * inverse_se3(expmap_se3(inc)) (gaussNewtonOptimization, src/stereoFrameHandler.cpp:
@@ -41,6 +59,7 @@ struct PoseLDS {
 // Out of line: inlined into the GN loop it raised k_pose to 172 VGPRs (2 waves / SIMD, 6.31 ms);
 // as a call it costs a 48-B stack save and the kernel keeps 3 waves / SIMD (5.82 ms; the serial
 // lane-0 update ran 5.95 ms)
+template <int W>
 __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, double* DT, double* X) {
     const int lane = threadIdx.x;
     double* E = X;        // [16] expmap_se3(inc)
@@ -55,7 +74,7 @@ __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, dou
                             : lane == 6 ? -w1 : lane == 7 ? w0 : 0.0;
             Sm[lane] = sk / theta;
         }
-        __syncthreads();
+        pose_bar<W>();
         const double st = det_sin(theta), ct = det_cos(theta);
         double Vi = 0.0;
         if (lane < 9) {
@@ -67,16 +86,16 @@ __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, dou
             const double tms = theta - st;
             Vi = (Ii + (si * omc) / theta) + (ssi * tms) / theta;
         }
-        __syncthreads();
+        pose_bar<W>();
         if (lane < 9) Sm[lane] = Vi;
-        __syncthreads();
+        pose_bar<W>();
         if (lane < 3) E[lane * 4 + 3] = (Sm[lane * 3 + 0] * inc[0] + Sm[lane * 3 + 1] * inc[1]) + Sm[lane * 3 + 2] * inc[2];
     } else {
         if (lane < 9) E[r9 * 4 + c9] = (r9 == c9) ? 1.0 : 0.0;
         if (lane < 3) E[lane * 4 + 3] = inc[lane];
     }
     if (lane >= 12 && lane < 16) E[lane] = (lane == 15) ? 1.0 : 0.0;
-    __syncthreads();
+    pose_bar<W>();
     const int r = (lane >> 2) & 3, c = lane & 3;
     if (lane < 16) {
         double ei;
@@ -85,14 +104,14 @@ __device__ __attribute__((noinline)) void se3_update_wave(const double* inc, dou
         else ei = (c == 3) ? 1.0 : 0.0;
         Ei[lane] = ei;
     }
-    __syncthreads();
+    pose_bar<W>();
     double dn = 0.0;
     if (lane < 16)
         dn = ((DT[r * 4 + 0] * Ei[0 * 4 + c] + DT[r * 4 + 1] * Ei[1 * 4 + c]) + DT[r * 4 + 2] * Ei[2 * 4 + c]) +
              DT[r * 4 + 3] * Ei[3 * 4 + c];
-    __syncthreads();
+    pose_bar<W>();
     if (lane < 16) DT[lane] = dn;
-    __syncthreads();
+    pose_bar<W>();
 }
 
 #define PT_K 6    // X Y Z ox oy sigma2
@@ -174,6 +193,54 @@ struct PoseCtx {
     int npt, nls;
 };
 
+// k_pose<W > 1>: chunk c0 + w of the active entries (points and lines) evaluated into wave w's rows
+template <int W>
+__device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx& X, const double* DT, int c0,
+                                                int np_act, int nl_act, int ntot, double* cp, double* cl, int w) {
+    const int lane = threadIdx.x & 63;
+    const int c = c0 + w;
+    const int f = (c << 6) + lane;
+    double* cpw = cp + w * (16 * CH_STRIDE);
+    double* clw = cl + w * (16 * CH_STRIDE);
+    const uint32_t ix = f < ntot ? X.idx[f] : 0u;
+    double o[8], in[LS_K];
+    if (f < np_act) {
+        const int fp = (int)(ix & 0xFFFFu);
+#pragma unroll
+        for (int i = 0; i < PT_K; ++i) in[i] = X.pin[i * X.mpt_cap + fp];
+        eval_point(p.cam, p.cfg.homog_th, DT, in, o);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cpw[i * CH_STRIDE + lane] = o[i];
+    if (f < nl_act) {
+        const int fl = (int)(ix >> 16);
+#pragma unroll
+        for (int i = 0; i < LS_K; ++i) in[i] = X.lin[i * X.mls_cap + fl];
+        eval_line(p.cam, p.cfg.homog_th, DT, in, o);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) clw[i * CH_STRIDE + lane] = o[i];
+}
+
+// the helper waves of k_pose<W > 1>: evaluate chunk c0 + w on every command until the exit command
+template <int W>
+__device__ void pose_helper(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl) {
+    const int w = threadIdx.x >> 6;
+    for (;;) {
+        __syncthreads();   // (A)
+        if (S.cmd == 0) return;
+        const int c0 = S.c0, nch = S.nch;
+        if (c0 + w < nch) pose_eval_chunk<W>(p, X, S.DT, c0, S.np_act, S.nl_act, max(S.np_act, S.nl_act), cp, cl, w);
+        __syncthreads();   // (B)
+    }
+}
+
 // gaussNewtonOptimization (:2032-2056): DT updated in place in S, H = last evaluated
 // Issue priority by progress: 3 in the first half of the first GN run, down to 0 in the second half
 // of the second, so the waves dispatched last are not starved by the older ones (the arbiter favours
@@ -186,6 +253,7 @@ __device__ __forceinline__ void pose_prio(int stage, int it, int n) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
+template <int W>
 __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl,
                              int max_iters, int stage) {
     const int lane = threadIdx.x;
@@ -222,7 +290,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             if (a) reinterpret_cast<uint16_t*>(X.idx + nl_act + __popcll(m & lt))[1] = (uint16_t)f;
             nl_act += __popcll(m);
         }
-        __syncthreads();
+        pose_bar<W>();
     }
     const int ntot = max(np_act, nl_act), nch = (ntot + 63) >> 6;
     // a chunk's list positions are loaded one chunk ahead of its inputs (the inputs' loads
@@ -249,53 +317,79 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
 #pragma unroll
             for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
         };
-        load_chunk(0, load_idx(0));
-        uint32_t ix = load_idx(1);
-        for (int c = 0; c < nch; ++c) {
-            const int f = (c << 6) + lane;
-            double o[8];
-            if (f < np_act) eval_point(cam, homog, DT, pv, o);
-            else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = 0.0;
+        if (W == 1) {
+            load_chunk(0, load_idx(0));
+            uint32_t ix = load_idx(1);
+            for (int c = 0; c < nch; ++c) {
+                const int f = (c << 6) + lane;
+                double o[8];
+                if (f < np_act) eval_point(cam, homog, DT, pv, o);
+                else {
+    #pragma unroll
+                    for (int i = 0; i < 8; ++i) o[i] = 0.0;
+                }
+    #pragma unroll
+                for (int i = 0; i < 8; ++i) cp[i * CH_STRIDE + lane] = o[i];
+                if (f < nl_act) eval_line(cam, homog, DT, lv, o);
+                else {
+    #pragma unroll
+                    for (int i = 0; i < 8; ++i) o[i] = 0.0;
+                }
+    #pragma unroll
+                for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
+                if (c + 1 < nch) {
+                    load_chunk(c + 1, ix);
+                    ix = load_idx(c + 2);
+                }
+                pose_bar<W>();
+                const double* A = buf + ia * CH_STRIDE;
+                const double* Bv = buf + ib * CH_STRIDE;
+                const double* Wr = buf + 7 * CH_STRIDE;
+                const double2* A2 = reinterpret_cast<const double2*>(A);
+                const double2* B2 = reinterpret_cast<const double2*>(Bv);
+                const double2* W2 = reinterpret_cast<const double2*>(Wr);
+    #pragma unroll GFPL_POSE_RED_UNROLL
+                for (int k = 0; k < 32; ++k) {
+                    const double2 a = A2[k], bb = B2[k], w = W2[k];
+                    s = s + (a.x * bb.x) * w.x;
+                    s = s + (a.y * bb.y) * w.y;
+                }
+                pose_bar<W>();
             }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) cp[i * CH_STRIDE + lane] = o[i];
-            if (f < nl_act) eval_line(cam, homog, DT, lv, o);
-            else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
-            if (c + 1 < nch) {
-                load_chunk(c + 1, ix);
-                ix = load_idx(c + 2);
-            }
-            __syncthreads();
-            const double* A = buf + ia * CH_STRIDE;
-            const double* Bv = buf + ib * CH_STRIDE;
-            const double* W = buf + 7 * CH_STRIDE;
-            const double2* A2 = reinterpret_cast<const double2*>(A);
-            const double2* B2 = reinterpret_cast<const double2*>(Bv);
-            const double2* W2 = reinterpret_cast<const double2*>(W);
+        } else {
+            // rounds of W chunks: wave w evaluates chunk c0 + w (the helpers on a command), then
+            // the reduction lanes add the round's chunks in list order
+            if (lane == 0) { S.np_act = np_act; S.nl_act = nl_act; S.nch = nch; }
+            for (int c0 = 0; c0 < nch; c0 += W) {
+                if (lane == 0) { S.cmd = 1; S.c0 = c0; }
+                __syncthreads();   // (A) the helpers read the command, DT and the positions
+                pose_eval_chunk<W>(p, X, S.DT, c0, np_act, nl_act, ntot, cp, cl, 0);
+                __syncthreads();   // (B) the round's rows are in LDS
+                const int nw = min(W, nch - c0);
+                for (int wb = 0; wb < nw; ++wb) {
+                    const double* bw = (list == 0 ? cp : cl) + wb * (16 * CH_STRIDE);
+                    const double2* A2 = reinterpret_cast<const double2*>(bw + ia * CH_STRIDE);
+                    const double2* B2 = reinterpret_cast<const double2*>(bw + ib * CH_STRIDE);
+                    const double2* W2 = reinterpret_cast<const double2*>(bw + 7 * CH_STRIDE);
 #pragma unroll GFPL_POSE_RED_UNROLL
-            for (int k = 0; k < 32; ++k) {
-                const double2 a = A2[k], bb = B2[k], w = W2[k];
-                s = s + (a.x * bb.x) * w.x;
-                s = s + (a.y * bb.y) * w.y;
+                    for (int k = 0; k < 32; ++k) {
+                        const double2 a = A2[k], bb = B2[k], w = W2[k];
+                        s = s + (a.x * bb.x) * w.x;
+                        s = s + (a.y * bb.y) * w.y;
+                    }
+                }
             }
-            __syncthreads();
+            pose_bar<W>();
         }
         part[lane] = s;
-        __syncthreads();
+        pose_bar<W>();
         // H = H_p + H_l, one element per lane (the symmetric pair gets the same sum)
         if (lane < 36) {
             const int r = lane / 6, c = lane - 6 * (lane / 6);
             const int t = r >= c ? tri(r, c) : tri(c, r);
             S.H[lane] = part[t] + part[28 + t];
         }
-        __syncthreads();
+        pose_bar<W>();
         if (lane == 0) {
             double H[36], g[6];
             for (int i = 0; i < 36; ++i) H[i] = S.H[i];
@@ -319,20 +413,22 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             S.brk = brk;
             S.upd = upd;
         }
-        __syncthreads();
-        if (S.upd) se3_update_wave(incs, S.DT, xs);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
+        pose_bar<W>();
+        if (S.upd) se3_update_wave<W>(incs, S.DT, xs);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
         if (S.brk) break;
     }
 }
 
 // vector_stdv_mad on buf[0..n) (LDS, destroyed); buf has NP2 entries
+template <int W>
 __device__ double stdv_mad(double* buf, int n, int NP2) {
+    const int nthr = W == 1 ? (int)blockDim.x : 64;   // (W > 1: wave 0 alone)
     if (n == 0) return 0.0;   // uniform
-    for (int i = threadIdx.x + n; i < NP2; i += blockDim.x) buf[i] = __builtin_inf();
-    __syncthreads();
+    for (int i = threadIdx.x + n; i < NP2; i += nthr) buf[i] = __builtin_inf();
+    pose_bar<W>();
     for (int k = 2; k <= NP2; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < NP2; i += blockDim.x) {
+            for (int i = threadIdx.x; i < NP2; i += nthr) {
                 int ixj = i ^ j;
                 if (ixj > i) {
                     bool up = ((i & k) == 0);
@@ -340,15 +436,15 @@ __device__ double stdv_mad(double* buf, int n, int NP2) {
                     if ((x > y) == up) { buf[i] = y; buf[ixj] = x; }
                 }
             }
-            __syncthreads();
+            pose_bar<W>();
         }
     const double median = buf[n / 2];
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) buf[i] = (double)fabsf((float)(buf[i] - median));
-    __syncthreads();
+    pose_bar<W>();
+    for (int i = threadIdx.x; i < n; i += nthr) buf[i] = (double)fabsf((float)(buf[i] - median));
+    pose_bar<W>();
     for (int k = 2; k <= NP2; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < NP2; i += blockDim.x) {
+            for (int i = threadIdx.x; i < NP2; i += nthr) {
                 int ixj = i ^ j;
                 if (ixj > i) {
                     bool up = ((i & k) == 0);
@@ -356,10 +452,10 @@ __device__ double stdv_mad(double* buf, int n, int NP2) {
                     if ((x > y) == up) { buf[i] = y; buf[ixj] = x; }
                 }
             }
-            __syncthreads();
+            pose_bar<W>();
         }
     const double mad = buf[n / 2];
-    __syncthreads();
+    pose_bar<W>();
     return 1.4826 * mad;
 }
 
@@ -417,14 +513,15 @@ __device__ __forceinline__ int wave_sum(int v) {
 #ifndef GFPL_POSE_WAVES
 #define GFPL_POSE_WAVES 4
 #endif
-__global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2) {
+template <int W>
+__global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(KParams p, int NP2) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ PoseLDS S;
     const int b = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x;   // (W > 1: wave 0's lanes; the helpers branch off below)
     const int npt = p.tr.n_matched_pt[b], nls = p.tr.n_matched_ls[b];
     // the GN chunk rows and the outlier residuals are never live together
-    const int region = max(16 * CH_STRIDE, NP2);
+    const int region = max(W * 16 * CH_STRIDE, NP2);
     double* cp = (double*)smem;
     double* cl = cp + 8 * CH_STRIDE;
     double* buf = cp;   // MAD sort buffer: never live together with the GN chunk rows
@@ -441,6 +538,10 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     double* lin = pin + PT_K * p.mpt_cap;
     X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
     X.idx = p.scr.pose_idx + (size_t)b * (size_t)max(p.mpt_cap, p.mls_cap);
+    if (W > 1 && threadIdx.x >= 64) {   // helper waves: GN chunk evaluation on wave 0's commands
+        pose_helper<W>(p, X, S, cp, cl);
+        return;
+    }
     if (lane < 16) {   // Q2: the app passes prev_frame->DT (app/plslam_mod.cpp:408)
         S.DTini[lane] = p.dt_ini ? p.dt_ini[16 * b + lane] : PP.DT[16 * b + lane];
         S.DT[lane] = S.DTini[lane];
@@ -471,11 +572,11 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
     cpn = wave_sum(cpn);
     cln = wave_sum(cln);
     if (lane == 0) { S.cnt[0] = cpn; S.cnt[1] = cln; }
-    __syncthreads();
+    pose_bar<W>();
     int ok = 0;        // 1: stage-2 DT usable
     double err = 0.0;  // err of the last GN run (reference: uninitialised when no GN runs, pinned 0)
     if (S.ninl > p.cfg.min_features) {
-        gauss_newton(p, X, S, cp, cl, p.cfg.max_iters, 0);
+        gauss_newton<W>(p, X, S, cp, cl, p.cfg.max_iters, 0);
         err = S.err;
         double DTs[16];
         for (int i = 0; i < 16; ++i) DTs[i] = S.DT[i];
@@ -513,7 +614,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
             // bits).  Duplicates of one prev point share P, pl_obs and sigma2, hence the
             // residual: flagging per list position equals the reference's per-feature flag.
             int op = 0, ol = 0;
-            __syncthreads();
+            pose_bar<W>();
             if (npt <= 64 * POSE_MAD_R) {
                 double r[POSE_MAD_R];
 #pragma unroll
@@ -526,12 +627,12 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
                 }
             } else {
                 for (int k = lane; k < npt; k += 64) buf[k] = res_p(k);
-                __syncthreads();
-                const double th_p = p.cfg.inlier_k * stdv_mad(buf, npt, NP2);
+                pose_bar<W>();
+                const double th_p = p.cfg.inlier_k * stdv_mad<W>(buf, npt, NP2);
                 for (int k = lane; k < npt; k += 64)
                     if (res_p(k) > th_p) { P.inlier[pb + mpt[k]] = 0; act[k] = 0; ++op; }
             }
-            __syncthreads();
+            pose_bar<W>();
             if (nls <= 64 * POSE_MAD_R) {
                 double r[POSE_MAD_R];
 #pragma unroll
@@ -544,8 +645,8 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
                 }
             } else {
                 for (int k = lane; k < nls; k += 64) buf[k] = res_l(k);
-                __syncthreads();
-                const double th_l = p.cfg.inlier_k * stdv_mad(buf, nls, NP2);
+                pose_bar<W>();
+                const double th_l = p.cfg.inlier_k * stdv_mad<W>(buf, nls, NP2);
                 for (int k = lane; k < nls; k += 64)
                     if (res_l(k) > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
             }
@@ -553,7 +654,7 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
             ol = wave_sum(ol);
             // active counts for stage 2
             int ap = 0, al = 0;
-            __syncthreads();
+            pose_bar<W>();
             for (int k = lane; k < npt; k += 64) ap += act[k];
             for (int k = lane; k < nls; k += 64) al += act[npt + k];
             ap = wave_sum(ap);
@@ -565,15 +666,19 @@ __global__ void __launch_bounds__(64, GFPL_POSE_WAVES) k_pose(KParams p, int NP2
                 p.tr.n_inliers_ls[b] -= ol;
                 S.cnt[0] = ap; S.cnt[1] = al;
             }
-            __syncthreads();
+            pose_bar<W>();
             if (S.ninl > p.cfg.min_features) {
                 if (lane < 16) S.DT[lane] = S.DTini[lane];   // Q3: stage 2 restarts from DT_ini
-                __syncthreads();
-                gauss_newton(p, X, S, cp, cl, p.cfg.max_iters_ref, 1);
+                pose_bar<W>();
+                gauss_newton<W>(p, X, S, cp, cl, p.cfg.max_iters_ref, 1);
                 err = S.err;
                 ok = 1;
             }
         }
+    }
+    if (W > 1) {   // release the helpers
+        if (lane == 0) S.cmd = 0;
+        __syncthreads();
     }
     if (lane == 0) {
         for (int i = 0; i < 16; ++i) p.scr.pose_DT[16 * b + i] = S.DT[i];
@@ -727,12 +832,28 @@ hipError_t launch_curr_frame_is_kf(const KParams& p, const int32_t* mask, hipStr
     return hipGetLastError();
 }
 
+#ifndef POSE_W
+#define POSE_W 4
+#endif
+#ifndef POSE_MULTI_MAX_B
+#define POSE_MULTI_MAX_B 1024
+#endif
+// the batch size up to which k_pose runs POSE_W waves per sequence (GFPL_POSE_MULTI_MAX_B overrides)
+static int pose_multi_max_b() {
+    const char* e = getenv("GFPL_POSE_MULTI_MAX_B");
+    return e ? atoi(e) : POSE_MULTI_MAX_B;
+}
+
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
-    const size_t region = (size_t)std::max(16 * CH_STRIDE, NP2);
+    const bool multi = p.B <= pose_multi_max_b();   // small batches: POSE_W waves per sequence
+    const size_t region = (size_t)std::max((multi ? POSE_W : 1) * 16 * CH_STRIDE, NP2);
     const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 16;
-    hipLaunchKernelGGL(k_pose, dim3(p.B), dim3(64), lds, s, p, NP2);
+    if (multi)
+        hipLaunchKernelGGL(k_pose<POSE_W>, dim3(p.B), dim3(64 * POSE_W), lds, s, p, NP2);
+    else
+        hipLaunchKernelGGL(k_pose<1>, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
     hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
     return hipGetLastError();

@@ -22,9 +22,41 @@ from . import (DESC, KEYLINE_DT, KEYPOINT_DT, BinaryDescriptor, Context, Event, 
                ORBextractor, make_frames, synth_image, synth_keylines)
 
 
+def _draw_bars(img: np.ndarray, n: int, seed: int) -> np.ndarray:
+    """n anti-aliased bars (rotated rectangles 30-110 px long, 8-24 px wide, dark or bright, none
+    within 20 degrees of horizontal) over img: straight high-contrast edges LSD finds as segments
+    (an aliased staircase edge breaks its level-line regions) and corners for FAST."""
+    rng = np.random.default_rng(seed)
+    h, w = img.shape
+    out = img.astype(np.float32)
+    for _ in range(n):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        ln, wd = rng.uniform(30, 110), rng.uniform(8, 24)
+        a = rng.uniform(0.35, np.pi - 0.35)
+        ca, sa = np.float32(np.cos(a)), np.float32(np.sin(a))
+        r = ln / 2 + wd / 2 + 2
+        x0, x1 = int(max(0, cx - r)), int(min(w, cx + r + 1))
+        y0, y1 = int(max(0, cy - r)), int(min(h, cy + r + 1))
+        if x0 >= x1 or y0 >= y1:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1].astype(np.float32)
+        X, Y = xx - np.float32(cx), yy - np.float32(cy)
+        d = np.maximum(np.abs(X * ca + Y * sa) - np.float32(ln / 2), np.abs(Y * ca - X * sa) - np.float32(wd / 2))
+        cov = np.clip(0.5 - d, 0.0, 1.0)
+        val = np.float32(rng.integers(0, 2) * 190 + rng.integers(15, 50))
+        blk = out[y0:y1, x0:x1]
+        out[y0:y1, x0:x1] = blk + (val - blk) * cov
+    return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
 @functools.lru_cache(maxsize=4096)
-def _plane(seq: int, base_w: int, height: int, n_segs: int):
+def _plane(seq: int, base_w: int, height: int, n_segs: int, bars: int = 0, flat: bool = False):
     base = synth_image(0xB45E + seq, 0, base_w, height)
+    if flat:   # a plain grey plane with mild noise (only the bars give features)
+        rng = np.random.default_rng(0xF1A7 + seq)
+        base = (118 + rng.integers(0, 21, base.shape)).astype(np.uint8)
+    if bars:
+        base = _draw_bars(base, bars, 0xBA25 + seq)
     base.setflags(write=False)
     segs = synth_keylines(n_segs, base_w, height, 0x5E65 + seq, min_len=8.0, max_len=120.0)
     segs.setflags(write=False)
@@ -54,7 +86,7 @@ def synth_stereo_scene(seq: int, frame: int, width: int, height: int, disparity:
 
 
 def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparities=(2, 12, 20, 8), band: int = 96,
-                       n_lines: int = 300, frames: int = 64):
+                       n_lines: int = 300, frames: int = 64, bars: int = 0, bar_min_disp: int = 0):
     """A staircase of fronto-parallel textured bands (world columns [band i, band (i+1)) at
     disparity disparities[i % len]) seen from a camera translating along x by half a baseline
     per frame: band b moves d_b / 2 px per frame in the left image and sits d_b px further
@@ -63,12 +95,19 @@ def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparitie
     information of the lines well conditioned (the single plane couples rotation and
     translation, and the line cut then takes the reference's exact step at every step).
     Keylines are the plane segments lying inside one band, shifted per view and kept when both
-    endpoints stay in the image.  Returns (left, right, kl_left, kl_right)."""
+    endpoints stay in the image.  bars: anti-aliased bars drawn over the plane's texture per
+    `bars` per 1000 x 1000 px of it (the north-star load: ~2000 ORB keypoints and >= 300 LSD
+    keylines per VGA image at 500; 0 keeps the plain texture, ~50 keylines per image).
+    Returns (left, right, kl_left, kl_right)."""
     ds = [int(d) for d in disparities]
     assert all(d % 2 == 0 and d > 0 for d in ds)
     dmax = max(ds)
     base_w = width + dmax * (frames // 2 + 1) + band
-    base, segs = _plane(seq, base_w, height, n_lines * 6)
+    nb = int(round(bars * base_w * height / 1e6))
+    base, segs = _plane(seq, base_w, height, n_lines * 6, nb)
+    # bar_min_disp > 0: bands at that disparity or more show bars on a plain plane instead (their
+    # features are then the bars' edges and corners; the textured near-field bands carry the points)
+    base_b = _plane(seq, base_w, height, n_lines * 6, nb, True)[0] if bar_min_disp else base
     n_band = (base_w + band - 1) // band
     disp = [ds[i % len(ds)] for i in range(n_band)]
     far = min(ds)
@@ -81,7 +120,8 @@ def synth_stereo_steps(seq: int, frame: int, width: int, height: int, disparitie
             x0, x1 = u0 - shift(disp[i]), u1 - shift(disp[i])
             c0, c1 = max(x0, 0), min(x1, width)
             if c0 < c1:
-                img[:, c0:c1] = base[:, u0 + (c0 - x0):u0 + (c1 - x0)]
+                src = base_b if bar_min_disp and disp[i] >= bar_min_disp else base
+                img[:, c0:c1] = src[:, u0 + (c0 - x0):u0 + (c1 - x0)]
         views.append(img)
     bi = np.floor(segs["sx"] / band).astype(np.int64)
     same = (bi == np.floor(segs["ex"] / band).astype(np.int64))

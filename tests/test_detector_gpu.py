@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "gf-pl-slam_amd", "bin", "plslam_gpu")
 NFEAT, KP, KL = 2000, 2320, 320
+BARS = 600   # the dense scene: ~2000 ORB keypoints and 300 LSD keylines per image (the north-star load)
 
 
 def _oracle_scene(L, R):
@@ -46,7 +47,7 @@ def test_detector_images_to_poses_match_the_oracle_chain():
     orc = [O.OracleHandler(cam, cfg, KP, KL) for _ in range(B)]
 
     def detect(k):
-        imgs = [synth_stereo_steps(b, k, W, H)[:2] for b in range(B)]
+        imgs = [synth_stereo_steps(b, k, W, H, bars=BARS)[:2] for b in range(B)]
         left = torch.from_numpy(np.stack([i[0] for i in imgs])).to(dev)
         right = torch.from_numpy(np.stack([i[1] for i in imgs])).to(dev)
         ts = torch.full((B,), 0.05 * k, dtype=torch.float64, device=dev)
@@ -88,7 +89,7 @@ def test_detector_images_to_poses_match_the_oracle_chain():
             bad += compare_track(g.read_last_track(b), tr, f"f{k} s{b} ")
     det.status()
     assert not bad, "\n".join(bad[:30])
-    assert all(c[0] > 30 and c[1] > 5 for c in counts), counts
+    assert all(c[0] > 100 and c[1] > 100 for c in counts), counts   # tracking at the dense scene's load
     g.close()
     det.close()
 
@@ -149,7 +150,7 @@ def test_host_mirror_from_images_matches_the_oracle_chain(tmp_path):
     W, H = int(cam.width), int(cam.height)
     for side in ("left", "right"):
         (tmp_path / side).mkdir()
-    imgs = [synth_stereo_steps(7, k, W, H)[:2] for k in range(n)]
+    imgs = [synth_stereo_steps(7, k, W, H, bars=BARS)[:2] for k in range(n)]
     ts = [1403636579.763555527 + 0.05 * k for k in range(n)]
     for k, (L, R) in enumerate(imgs):
         _write_pgm(tmp_path / "left" / f"{k:06d}.pgm", L)
@@ -191,7 +192,9 @@ def test_host_mirror_from_images_matches_the_oracle_chain(tmp_path):
         f = t.split(" ")
         n_kp_l = len(O.orb_extract(imgs[k][0], nfeatures=NFEAT, kp_cap=KP)["kps"])
         assert int(f[11]) == n_kp_l and int(f[12]) == len(O.lsd_detect(imgs[k][0])[0]), (k, f[11:13])
-    assert lines[-1]["matched_pt"] > 20 and lines[-1]["matched_ls"] > 5, lines[-1]   # (tracking, not lost)
+    # tracking at the dense scene's load (2000 ORB + 300 LSD per image; stereo points stop at ~5 px of
+    # disparity, ledger Q1, so the 2 px band carries them)
+    assert lines[-1]["matched_pt"] > 100 and lines[-1]["matched_ls"] > 100, lines[-1]
 
 
 def test_detector_inputs_reusable_once_detect_returns():

@@ -90,7 +90,9 @@ def test_vga_default_pose_bitexact(vga_default):
 @pytest.mark.parametrize("wave_max", ["0", "4096"])
 def test_bench_config_parity(monkeypatch, wave_max):
     # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop; both line-cut searches
+    # and both pose layouts (one wave per sequence, and the small-batch 4 waves per sequence)
     monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)
+    monkeypatch.setenv("GFPL_POSE_MULTI_MAX_B", wave_max)
     rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
                         n_seq=2, n_frames=4, kp_cap=2048, kl_cap=512, seed=7)
     _check(rep)
@@ -430,6 +432,7 @@ def test_line_cut_certified_matches_exact_at_scale(monkeypatch, wave_max):
     agreement bound) and exact steps only — cut ratios, invCovPose of every
     matched line and the poses bit-identical; proven mode certifies most steps."""
     monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)   # 0: the 8-sequence-per-wave search, else one per wave
+    monkeypatch.setenv("GFPL_POSE_MULTI_MAX_B", wave_max)  # 0: one wave per sequence in k_pose, else four
     n, F, KP, KL = 512, 3, 2048, 512
     base = dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     cam = gfpl.make_camera("vga", gfpl.default_config(**base))

@@ -174,3 +174,18 @@ def test_lsd_parity_large_batch_small_lds_sort():
     imgs = np.stack([_dense_image(1000 + i, w, h) if i % 50 == 0 else gfpl.synth_image(i, 0, w, h)
                      for i in range(n)])
     assert _check(imgs, kl_cap=64) > 0
+
+
+def test_lsd_parity_dense_bar_scene():
+    """The images -> poses bench scene at the north-star load (gfpl.pipeline: 600 anti-aliased bars
+    per Mpx over the staircase): several hundred segments per image, the 300-keyline response cut
+    (S7) deciding among them, and the keep-all budget — bit-exact against the oracle."""
+    w, h = 640, 480
+    imgs = []
+    for seq, fr in ((0, 0), (9, 3), (31, 7)):
+        left, right, _, _ = P.synth_stereo_steps(seq, fr, w, h, bars=600)
+        imgs += [left, right]
+    imgs = np.stack(imgs)
+    tot = _check(imgs)
+    assert tot == 300 * len(imgs), tot   # every image fills lsdNFeatures
+    _check(imgs[:2], gfpl.LsdParams.reference(w, h, n_features=0), kl_cap=2048)
