@@ -114,6 +114,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-sweep-seconds", type=float, default=2.5,
                     help="timed seconds per point of the CPU baseline's 1/2/4/8 thread sweep (0: no sweep)")
     ap.add_argument("--no-b1", action="store_true", help="skip the one-sequence latency leg (B = 1)")
+    ap.add_argument("--proven-steps", type=int, default=5,
+                    help="N = 1, measured mode: after the timed window, this many further steps (one more untimed) "
+                         "in proven mode (cut_proof 1), reported as cut_search.proven_leg (0: skip)")
     ap.add_argument("--dump-records", default=None,
                     help="save every sequence's record of the last timed step (gfpl_debug_step_records, .npy) "
                          "and the instrumented builds' clocks (gfpl_debug_clocks, *_clk.npy)")
@@ -708,7 +711,9 @@ def main():
     # cores cannot generate all B sequences' frames within --gen-budget (8 ranks sharing one
     # host's quota), one chunk of distinct sequences is generated per frame and uploaded into
     # every chunk of the batch — every sequence is still tracked on the GPU from its own state
-    n_frames_gen = W + K + 1 + (0 if (world > 1 or args.no_host_fed or dry) else 2)
+    n_proven = args.proven_steps + 1 if (world == 1 and args.proven_steps > 0 and not dry and
+                                         int(cfg.cut_proof) == 0) else 0
+    n_frames_gen = W + K + 1 + n_proven + (0 if (world > 1 or args.no_host_fed or dry) else 2)
     probe_n = min(chunk, 128)
     t0 = time.perf_counter()
     ring[1].fill(0, gen_threads, seq0=seq0, n=probe_n)
@@ -837,9 +842,38 @@ def main():
     else:
         t_max, frames_total = elapsed, B * K
 
+    proven = None
+    if n_proven:
+        # the same sequences, tracked on in proven mode: one untimed step (the mode's first launches),
+        # then timed steps bracketed like the window's; the mode is restored afterwards
+        cfg1 = gfpl.Config()
+        C.memmove(C.byref(cfg1), C.byref(cfg), C.sizeof(cfg))
+        cfg1.cut_proof = 1
+        ctx.set_config(cfg1)
+        p_s, p_cut, p_redone = [], [], 0
+        for i in range(n_proven):
+            t0 = time.perf_counter()
+            dv = stage_frame(W + K + 1 + i)
+            t_gen += time.perf_counter() - t0
+            sync_all()
+            ts0 = time.perf_counter()
+            h.frameStep(dv)
+            sync_all()
+            ts1 = time.perf_counter()
+            if i > 0:
+                p_s.append(ts1 - ts0)
+                p_cut.append(float(ctx.stage_times()[4]))
+                p_redone += int(h.last_step_cut_proof()["redone"])
+        ctx.set_config(cfg)
+        n_p = len(p_s)
+        proven = {"value": B * n_p / float(np.sum(p_s)), "ms_per_step": 1e3 * float(np.mean(p_s)),
+                  "line_cut_ms": float(np.mean(p_cut)), "steps": n_p, "redone_sequences": p_redone,
+                  "note": "cut_proof 1 on the same sequences right after the timed window (frames "
+                          f"{W + K + 2}..{W + K + n_proven}): the measured-mode line's decisions proven after the "
+                          "fact, unproven sequences redone by the eager-proven search (DESIGN.md §3)"}
     host_fed = None
     if world == 1 and not args.no_host_fed:
-        host_fed = host_fed_rate(h, cam, sp_up, B, KP, KL, seq0, W + K + 1, gen_threads, per_up, dev,
+        host_fed = host_fed_rate(h, cam, sp_up, B, KP, KL, seq0, W + K + 1 + n_proven, gen_threads, per_up, dev,
                                  distinct=distinct if replicate else B)
 
     if rank == 0:
@@ -953,6 +987,7 @@ def main():
                                               "and the two running invCov_sums; unproven sequences redone by the "
                                               "eager-proven search (DESIGN.md §3)"}
                                      if cfg.cut_proof == 1 else None),
+                           "proven_leg": proven,
                            "steps": int(sum(c["steps"] for c in cutc)),
                            "exact_steps": int(sum(c["exact_steps"] for c in cutc)),
                            "exact_frac": float(sum(c["exact_steps"] for c in cutc) / max(1, sum(c["steps"] for c in cutc))),

@@ -1556,11 +1556,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // One sequence per wave, for small batches (B <= CUT_WAVE_MAX_B: the latency of one sequence, e.g. the
 // reference app's one stream per process, app/plslam_mod.cpp:387-411).  Same decisions, same bits as
 // k_cut_search<false> (measured mode, with the proven mode's step record): a round evaluates d on the 8 x 8
-// grid of ratios at offsets -1 .. 6 from the centre on both sides (lane a * 8 + c), which holds the 8
-// neighbours of every position a path that only grows the ratios reaches in five steps — the greedy cut
-// almost always grows them (final r0 + r1 ~ 1 after ~20 steps) — then resolves up to five steps in order
-// from those values, each with the one-step search's first-strict-maximum rule and margin tests.  The
-// grid's ratios are accumulated as the search's moves accumulate them (r + s + s ...); a step whose
+// grid of ratios at offsets -1 .. 6 from the centre on both sides (lane a * 8 + c), takes every interior
+// position's decision at once (the one-step search's first-strict-maximum rule and margin tests over its
+// 8 neighbours' values), then follows the decisions from the centre as far as they stay inside the grid.
+// The greedy paths are runs of moves growing both ratios followed by runs growing one (oracle move
+// statistics on cfg2: 80% (+,+), 10% (+,0), 10% (0,+), moves back 0.03%): 2.3 rounds per line against
+// 3.0 with a five-step cap, and no 64-cell shape of the grid does better (profiles/r05_cutw).  The grid's
+// ratios are accumulated as the search's moves accumulate them (r + s + s ...); a position whose
 // neighbours' ratio bits differ from the grid's or leave it (a ratio that moved back), or that a margin
 // test sends to the exact path, ends the round.  Exact steps and the lazy exact invCov_sum are
 // cut_exact_round's, run by the wave as group 0.  Line transitions run on the whole wave at once.
@@ -1584,8 +1586,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double wgs[64];                  // line open: W [6][6] | Gram (21) at 36
     __shared__ double xsl[16];                  // transition: the finished line's [v'_s, P_s, v'_e, P_e]
     __shared__ CutCmp cmpl;
-    __shared__ double dgx[82];                  // decision pass: the grid's values (-inf: invalid / NaN), padded
-    __shared__ int dgf[82];                     // and flags (bok | valid << 1 | valid NaN << 2)
+    __shared__ double dgx[100];                 // decision pass: the grid's values (-inf: invalid / NaN), padded,
+    __shared__ int dgf[100];                    // and flags (bok | valid << 1 | valid NaN << 2); alt values at 82
     const int lane = threadIdx.x;
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
@@ -1683,6 +1685,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         wave_lds_sync();
         open_line();
     }
+    // the next line's record and list entry, fetched while this line is searched (vector loads: the
+    // line transition then waits for no memory round trip)
+    double pf_f0 = 0.0, pf_i0 = 0.0;
+    int pf_q = 0;
+    auto prefetch = [&](int mn) {
+        if (mn < nls) {   // (wave-uniform)
+            int iv = mn;
+            asm volatile("" : "+v"(iv));   // (a per-lane index: vector loads, counted apart from LDS)
+            const double* rn = rec_l + (size_t)iv * CUT_REC;
+            pf_i0 = lane < 21 ? rn[CUT_FAST + lane] : 0.0;
+            pf_f0 = rn[lane < CUT_FAST ? lane : 0];
+            pf_q = mls[iv];
+        }
+    };
+    prefetch(1);
 #ifdef GFPL_CUTW_CLOCK   // (diagnostic build: shader-clock cycles per phase and counts in scr.dbg)
     uint64_t ck_eval = 0, ck_dec = 0, ck_walk = 0, ck_trans = 0, ck_exact = 0, n_rounds = 0, n_trans = 0;
     uint64_t ck0 = clock64();
@@ -1692,7 +1709,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     while (m < nls) {   // (wave-uniform)
         // ---- the 8 x 8 grid of ratios at offsets -1 .. 6 from the centre, as the moves accumulate
-        //      them (the greedy path almost always grows both ratios: up to five steps per round)
+        //      them
         double g0[8], g1[8];
         g0[1] = r0;
         g1[1] = r1;
@@ -1700,9 +1717,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         g1[0] = r1 + (-st);
 #pragma unroll
         for (int k = 2; k < 8; ++k) { g0[k] = g0[k - 1] + st; g1[k] = g1[k - 1] + st; }
+        // an interior index k whose r - s is not the grid value below (k = 3 and 20 of 0, s, 2s, ... for
+        // s = 0.05: 0.15 - 0.05 != 0.1): its positions' lower neighbours are evaluated apart (alt values);
+        // the lowest such index per side is served, positions at any other one stop the walk
+        int inc0 = 0, inc1 = 0;
+#pragma unroll
+        for (int k = 2; k <= 6; ++k) {
+            inc0 |= (__double_as_longlong(g0[k] + (-st)) != __double_as_longlong(g0[k - 1])) ? (1 << k) : 0;
+            inc1 |= (__double_as_longlong(g1[k] + (-st)) != __double_as_longlong(g1[k - 1])) ? (1 << k) : 0;
+        }
+        const int k0 = inc0 ? __builtin_ctz(inc0) : -1, k1 = inc1 ? __builtin_ctz(inc1) : -1;
         int dj_valid = 0, bok = 0;
         double dj = 0.0;
         double t0 = g0[0], t1 = g1[0];   // the lane's grid ratios
+        CutReg cr;
+        cut_reg_load(cmpl, cr);
         {
             const int a = lane >> 3, c = lane & 7;
 #pragma unroll
@@ -1712,9 +1741,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (t0 < rlo || t0 > rhi) valid = 0;
             if (t1 < rlo || t1 > rhi) valid = 0;
             dj_valid = valid;
-            CutReg cr;
-            cut_reg_load(cmpl, cr);
             dj = cut_dval<false>(cr, t0, t1, tq, bok);
+        }
+        if (inc0 | inc1) {   // (wave-uniform) the alt values: lanes 0-7 (h0, g1[c]), 8-15 (g0[a], h1), 16 (h0, h1)
+            double h0 = g0[0], h1 = g1[0];
+#pragma unroll
+            for (int k = 2; k <= 6; ++k) { h0 = k == k0 ? g0[k] + (-st) : h0; h1 = k == k1 ? g1[k] + (-st) : h1; }
+            double u0 = h0, u1 = h1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { u1 = lane == k ? g1[k] : u1; u0 = lane == 8 + k ? g0[k] : u0; }
+            int valid = (lane < 8 && k0 >= 0) || (lane >= 8 && lane < 16 && k1 >= 0) || (lane == 16 && k0 >= 0 && k1 >= 0);
+            if (u0 + u1 > 1.0) valid = 0;
+            if (u0 < rlo || u0 > rhi) valid = 0;
+            if (u1 < rlo || u1 > rhi) valid = 0;
+            int abok = 0;
+            const double da = cut_dval<false>(cr, u0, u1, tq, abok);
+            if (lane < 17) {
+                dgx[82 + lane] = (valid && da == da) ? da : -__builtin_inf();
+                dgf[82 + lane] = abok | (valid << 1) | ((valid && !(da == da)) ? 4 : 0);
+            }
         }
         CUTW_CK(ck_eval);
         // ---- every grid position's decision at once: lane (a, c), 1 <= a, c <= 6, gathers its 8
@@ -1725,15 +1770,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         int dec = WAVE_STOP;
         {
             const int a = lane >> 3, c = lane & 7;
-            // a position's neighbour ratios are the grid's iff r - s of its ratio has the bits of the grid
-            // value below (r + s is the value above by construction, and so is g[0] + s = g[1])
-            int cm0 = 2, cm1 = 2;
-#pragma unroll
-            for (int k = 2; k <= 6; ++k) {
-                cm0 |= (__double_as_longlong(g0[k] + (-st)) == __double_as_longlong(g0[k - 1])) ? (1 << k) : 0;
-                cm1 |= (__double_as_longlong(g1[k] + (-st)) == __double_as_longlong(g1[k - 1])) ? (1 << k) : 0;
-            }
-            const bool cons = ((cm0 >> a) & (cm1 >> c) & 1) != 0;
+            // a position's neighbour ratios are the grid's (r + s is the value above by construction, r - s
+            // the value below unless the index is inconsistent) or the alt values of the served index
+            const int bad0 = inc0 & ~(k0 >= 0 ? 1 << k0 : 0), bad1 = inc1 & ~(k1 >= 0 ? 1 << k1 : 0);
+            const bool cons = a >= 1 && a <= 6 && c >= 1 && c <= 6 && !((bad0 >> a) & 1) && !((bad1 >> c) & 1);
+            const bool ia = a == k0, ic = c == k1;
             // the neighbours' values and flags through LDS (8 reads each; border lanes read padding)
             const double xo = (dj_valid && dj == dj) ? dj : -__builtin_inf();
             dgx[9 + lane] = xo;
@@ -1743,7 +1784,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             int fl[8];
 #pragma unroll
             for (int jn = 0; jn < 8; ++jn) {
-                const int l = 9 + lane + 8 * nb_da(jn, 0) + nb_da(jn, 1);
+                const int da = nb_da(jn, 0), dc = nb_da(jn, 1);
+                const bool xa = ia && da < 0, xc = ic && dc < 0;
+                const int l = (xa && xc) ? 82 + 16 : (xa ? 82 + c + dc : (xc ? 90 + a + da : 9 + lane + 8 * da + dc));
                 vjn[jn] = dgx[l];
                 fl[jn] = dgf[l];
             }
@@ -1761,18 +1804,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const double top = mx;
             const bool has = best >= 0;
             const double ttop = tau * top, tdc = tau * dcl;
-            bool ok = !(has & !(top - dcl > ttop)) && ((tau > 0.0) & (line_ok != 0) & (cok != 0) & (dcl == dcl));
+            // (bitwise, not short-circuit: every flag read is issued at once instead of one LDS round trip per
+            // neighbour behind a branch)
+            int fail = (int)(has & !(top - dcl > ttop)) | (int)!((tau > 0.0) & (line_ok != 0) & (cok != 0) & (dcl == dcl));
 #pragma unroll
             for (int jn = 0; jn < 8; ++jn) {
                 const double v = vjn[jn];
-                const bool vl = (fl[jn] & 2) != 0;
-                const bool f1 = vl & !(fl[jn] & 1);
-                const bool f2 = has & vl & (jn != best) & !(top - v > ttop);
-                const bool f4 = !has & vl & !(dcl - v > tdc);
-                const bool f3 = (fl[jn] & 4) != 0;   // (a valid NaN: the raw value fails f2 / f4 in the group search)
-                ok = ok && !(f1 | f2 | f3 | f4);
+                const int f = fl[jn];
+                const int vl = (f >> 1) & 1;
+                const int f1 = vl & ~f & 1;
+                const int f2 = (int)has & vl & (int)(jn != best) & (int)!(top - v > ttop);
+                const int f4 = (int)!has & vl & (int)!(dcl - v > tdc);
+                const int f3 = (f >> 2) & 1;   // (a valid NaN: the raw value fails f2 / f4 in the group search)
+                fail |= f1 | f2 | f3 | f4;
             }
-            dec = !cons ? WAVE_STOP : (!ok ? WAVE_EXACT : (has ? best : CUT_P_STAY));
+            const bool ok = fail == 0;
+            // a move below a served index leaves the grid, and the exact round reads the grid's neighbours:
+            // both stop the walk (the next round, centred there, has them on its grid)
+            const bool off = has && ((ia && nb_da(best, 0) < 0) || (ic && nb_da(best, 1) < 0));
+            dec = !cons ? WAVE_STOP : (!ok ? ((ia || ic) ? WAVE_STOP : WAVE_EXACT) : (off ? WAVE_STOP : (has ? best : CUT_P_STAY)));
             // the walk's word: the decision, whether the move ends the line (r0 + r1 > 1 after it: the moved
             // ratios are the neighbour's grid values, bit for bit, at a consistent position) and the lane moved to
             const int mv = has ? best : 0;
@@ -1781,36 +1831,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             dec |= fin | ((lane + 8 * nb_da(mv, 0) + nb_da(mv, 1)) & 63) << 8;
         }
         CUTW_CK(ck_dec);
-        // ---- follow the decisions from the centre: up to five steps
+        // ---- follow the decisions from the centre while they stay inside the grid
         int pos = 9;   // (a, c) = (1, 1): the centre
         int exact = 0, finalize = 0;
         double vj[8];
         int bj[8], valj[8];
-        for (int sstep = 0; sstep < 5; ++sstep) {   // (wave-uniform)
+        // scalar walk: one readlane per step, the step's record byte parked in lane ns of pathv (one vector
+        // store after the walk, no per-step exec-masked store)
+        int pathv = 0, ns = 0;
+        for (int sstep = 0; sstep < 64; ++sstep) {   // (wave-uniform; the grid ends a path: its edge positions stop)
             const int w = __builtin_amdgcn_readlane(dec, pos);
             const int dpos = w & 63;
-            const int pa = pos >> 3, pc = pos & 7;
-            if (dpos == WAVE_STOP) break;
-            if (dpos == WAVE_EXACT) {   // the exact round needs the position's neighbours
-#pragma unroll
-                for (int jn = 0; jn < 8; ++jn) {
-                    const int l = (pa + nb_da(jn, 0)) * 8 + (pc + nb_da(jn, 1));
-                    vj[jn] = readlane_f64(dj, l);
-                    bj[jn] = __builtin_amdgcn_readlane(bok, l);
-                    valj[jn] = __builtin_amdgcn_readlane(dj_valid, l);
-                }
-                exact = 1;
+            if (dpos >= WAVE_EXACT) {   // WAVE_STOP / WAVE_EXACT
+                exact = dpos == WAVE_EXACT;
                 break;
             }
-            ++n_steps;
-            if (rec && lane == 0) {
-                if (lstep < CUT_PATH) path[(size_t)m * CUT_PATH + lstep] = (uint8_t)dpos;
-            }
-            ++lstep;
-            first = 0;
+            pathv = lane == ns ? dpos : pathv;
+            ++ns;
             if (dpos == CUT_P_STAY) { finalize = 1; break; }
             pos = w >> 8;
             if (w & 64) { finalize = 1; break; }
+        }
+        if (ns) {
+            if (rec && lane < ns && lstep + lane < CUT_PATH) path[(size_t)m * CUT_PATH + lstep + lane] = (uint8_t)pathv;
+            n_steps += ns;
+            lstep += ns;
+            first = 0;
+        }
+        if (exact) {   // the exact round needs the position's neighbours
+            const int pa = pos >> 3, pc = pos & 7;
+#pragma unroll
+            for (int jn = 0; jn < 8; ++jn) {
+                const int l = (pa + nb_da(jn, 0)) * 8 + (pc + nb_da(jn, 1));
+                vj[jn] = readlane_f64(dj, l);
+                bj[jn] = __builtin_amdgcn_readlane(bok, l);
+                valj[jn] = __builtin_amdgcn_readlane(dj_valid, l);
+            }
         }
         // the ratios where the walk stopped: that lane's grid values (r + s accumulated, bit for bit)
         r0 = readlane_f64(t0, pos);
@@ -1884,19 +1940,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
                     info = cut_ours_info(xsl, is, ie, ra, cb);
                 }
-                const double* rn = rec_l + (size_t)m * CUT_REC;
-                const double i0n = lane < 21 ? rn[CUT_FAST + lane] : 0.0;
-                double f0 = rn[lane < CUT_FAST ? lane : 0];
                 wave_lds_sync();
-                if (lane < CUT_FAST) fst[lane] = f0;
-                if (lane < 21) sumA[lane] = (sumA[lane] + info) - i0n;
-                q_cur = lb + mls[m];
+                if (lane < CUT_FAST) fst[lane] = pf_f0;
+                if (lane < 21) sumA[lane] = (sumA[lane] + info) - pf_i0;
+                q_cur = lb + __builtin_amdgcn_readfirstlane(pf_q);
                 first = 1;
                 lstep = 0;
                 r0 = 0.0;
                 r1 = 0.0;
                 wave_lds_sync();
                 open_line();
+                prefetch(m + 1);
             }
         }
         CUTW_CK(ck_trans);

@@ -50,7 +50,16 @@ struct PoseLDS {
     int cnt[2];
     double err;
     int cmd, c0, np_act, nl_act, nch;   // k_pose<W > 1>: helper command (0 exit, 1 evaluate chunks c0 + w)
+    int gen;                            // k_pose<W > 1>: GN run number (the helpers' register-held inputs)
+#ifdef GFPL_POSE_CLOCK   // (diagnostic build: wave 0's shader-clock cycles per phase, scr.dbg 0-7)
+    unsigned long long ck[8], ck0;
+#endif
 };
+#ifdef GFPL_POSE_CLOCK
+#define POSE_CK(S, i) do { if (threadIdx.x == 0) { const unsigned long long t_ = clock64(); (S).ck[i] += t_ - (S).ck0; (S).ck0 = t_; } } while (0)
+#else
+#define POSE_CK(S, i) do { } while (0)
+#endif
 
 // DT <- DT * inverse_se3(expmap_se3(inc)) (gaussNewtonOptimization, src/stereoFrameHandler.cpp:
 // 2046-2050) by the wave, element-parallel: every element is formed by the expression the serial
@@ -193,22 +202,30 @@ struct PoseCtx {
     int npt, nls;
 };
 
-// k_pose<W > 1>: chunk c0 + w of the active entries (points and lines) evaluated into wave w's rows
+// k_pose<W > 1>: chunk c0 + w of the active entries (points and lines) evaluated into wave w's rows.
+// The chunk's inputs are gathered into pv / lv when `load`; a GN run whose chunks fit one round
+// (nch <= W) evaluates the same entries every iteration, so the callers keep them in registers and
+// load once per run (only DT changes between iterations).
 template <int W>
 __device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx& X, const double* DT, int c0,
-                                                int np_act, int nl_act, int ntot, double* cp, double* cl, int w) {
+                                                int np_act, int nl_act, int ntot, double* cp, double* cl, int w,
+                                                double* pv, double* lv, bool load) {
     const int lane = threadIdx.x & 63;
     const int c = c0 + w;
     const int f = (c << 6) + lane;
     double* cpw = cp + w * (16 * CH_STRIDE);
     double* clw = cl + w * (16 * CH_STRIDE);
-    const uint32_t ix = f < ntot ? X.idx[f] : 0u;
-    double o[8], in[LS_K];
-    if (f < np_act) {
-        const int fp = (int)(ix & 0xFFFFu);
+    if (load) {
+        const uint32_t ix = f < ntot ? X.idx[f] : 0u;
+        const int fp = f < np_act ? (int)(ix & 0xFFFFu) : 0, fl = f < nl_act ? (int)(ix >> 16) : 0;
 #pragma unroll
-        for (int i = 0; i < PT_K; ++i) in[i] = X.pin[i * X.mpt_cap + fp];
-        eval_point(p.cam, p.cfg.homog_th, DT, in, o);
+        for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
+#pragma unroll
+        for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
+    }
+    double o[8];
+    if (f < np_act) {
+        eval_point(p.cam, p.cfg.homog_th, DT, pv, o);
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = 0.0;
@@ -216,10 +233,7 @@ __device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx&
 #pragma unroll
     for (int i = 0; i < 8; ++i) cpw[i * CH_STRIDE + lane] = o[i];
     if (f < nl_act) {
-        const int fl = (int)(ix >> 16);
-#pragma unroll
-        for (int i = 0; i < LS_K; ++i) in[i] = X.lin[i * X.mls_cap + fl];
-        eval_line(p.cam, p.cfg.homog_th, DT, in, o);
+        eval_line(p.cam, p.cfg.homog_th, DT, lv, o);
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = 0.0;
@@ -229,14 +243,22 @@ __device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx&
 }
 
 // the helper waves of k_pose<W > 1>: evaluate chunk c0 + w on every command until the exit command
+// (inputs kept in registers across the iterations of a one-round GN run: S.gen numbers the runs)
 template <int W>
 __device__ void pose_helper(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl) {
     const int w = threadIdx.x >> 6;
+    double pv[PT_K], lv[LS_K];
+    int gen = -1;
     for (;;) {
         __syncthreads();   // (A)
         if (S.cmd == 0) return;
         const int c0 = S.c0, nch = S.nch;
-        if (c0 + w < nch) pose_eval_chunk<W>(p, X, S.DT, c0, S.np_act, S.nl_act, max(S.np_act, S.nl_act), cp, cl, w);
+        if (c0 + w < nch) {
+            const bool keep = W >= 8 && nch <= W;   // (see gauss_newton)
+            pose_eval_chunk<W>(p, X, S.DT, c0, S.np_act, S.nl_act, max(S.np_act, S.nl_act), cp, cl, w, pv, lv,
+                               !(keep && gen == S.gen));
+            gen = keep ? S.gen : -1;
+        }
         __syncthreads();   // (B)
     }
 }
@@ -297,9 +319,15 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     // depend on them); chunk 0's are reloaded per iteration (kept in a register across the
     // iterations and the se3_update_wave call, they cost 45 VGPR spills at 128 registers)
     auto load_idx = [&](int c) { const int f = (c << 6) + lane; return f < ntot ? X.idx[f] : 0u; };
+    // k_pose<W >= 8>: wave 0's chunk inputs, kept over a one-round run (k_pose<4> at B <= 1024 keeps its
+    // occupancy: 4 waves / SIMD need <= 128 VGPRs)
+    constexpr bool KEEP = W >= 8;
+    double pv0[PT_K], lv0[LS_K];
+    if (W > 1 && lane == 0) S.gen = S.gen + 1;
     double* part = cp;        // [64] the 28 + 28 reduction partials
     double* incs = cp + 64;   // [6] the increment
     double* xs = cp + 72;     // [48] se3_update_wave scratch
+    POSE_CK(S, 7);
     for (int it = 0; it < max_iters; ++it) {
         pose_prio(stage, it, max_iters);
         // the evaluations read DT from LDS (wave-uniform broadcast reads) instead of
@@ -363,8 +391,9 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             for (int c0 = 0; c0 < nch; c0 += W) {
                 if (lane == 0) { S.cmd = 1; S.c0 = c0; }
                 __syncthreads();   // (A) the helpers read the command, DT and the positions
-                pose_eval_chunk<W>(p, X, S.DT, c0, np_act, nl_act, ntot, cp, cl, 0);
+                pose_eval_chunk<W>(p, X, S.DT, c0, np_act, nl_act, ntot, cp, cl, 0, pv0, lv0, !(KEEP && nch <= W && it > 0));
                 __syncthreads();   // (B) the round's rows are in LDS
+                POSE_CK(S, 5);
                 const int nw = min(W, nch - c0);
                 for (int wb = 0; wb < nw; ++wb) {
                     const double* bw = (list == 0 ? cp : cl) + wb * (16 * CH_STRIDE);
@@ -381,6 +410,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             }
             pose_bar<W>();
         }
+        POSE_CK(S, 1);
         part[lane] = s;
         pose_bar<W>();
         // H = H_p + H_l, one element per lane (the symmetric pair gets the same sum)
@@ -414,7 +444,9 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             S.upd = upd;
         }
         pose_bar<W>();
+        POSE_CK(S, 2);
         if (S.upd) se3_update_wave<W>(incs, S.DT, xs);   // DT * inverse_se3(expmap_se3(inc)), before the nrm break
+        POSE_CK(S, 3);
         if (S.brk) break;
     }
 }
@@ -546,7 +578,11 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
         S.DTini[lane] = p.dt_ini ? p.dt_ini[16 * b + lane] : PP.DT[16 * b + lane];
         S.DT[lane] = S.DTini[lane];
     }
-    if (lane == 0) S.ninl = p.tr.n_inliers[b];
+    if (lane == 0) { S.ninl = p.tr.n_inliers[b]; S.gen = 0; }
+#ifdef GFPL_POSE_CLOCK
+    if (lane < 8) S.ck[lane] = 0;
+    if (lane == 0) S.ck0 = clock64();
+#endif
     // gather the matched lists once (lane l owns positions l, l+64, ...)
     int cpn = 0, cln = 0;
     for (int f = lane; f < npt; f += 64) {
@@ -573,10 +609,12 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
     cln = wave_sum(cln);
     if (lane == 0) { S.cnt[0] = cpn; S.cnt[1] = cln; }
     pose_bar<W>();
+    POSE_CK(S, 0);
     int ok = 0;        // 1: stage-2 DT usable
     double err = 0.0;  // err of the last GN run (reference: uninitialised when no GN runs, pinned 0)
     if (S.ninl > p.cfg.min_features) {
         gauss_newton<W>(p, X, S, cp, cl, p.cfg.max_iters, 0);
+        POSE_CK(S, 7);
         err = S.err;
         double DTs[16];
         for (int i = 0; i < 16; ++i) DTs[i] = S.DT[i];
@@ -667,6 +705,7 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
                 S.cnt[0] = ap; S.cnt[1] = al;
             }
             pose_bar<W>();
+            POSE_CK(S, 4);
             if (S.ninl > p.cfg.min_features) {
                 if (lane < 16) S.DT[lane] = S.DTini[lane];   // Q3: stage 2 restarts from DT_ini
                 pose_bar<W>();
@@ -676,10 +715,14 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
             }
         }
     }
+    POSE_CK(S, 7);
     if (W > 1) {   // release the helpers
         if (lane == 0) S.cmd = 0;
         __syncthreads();
     }
+#ifdef GFPL_POSE_CLOCK
+    if (lane < 8) p.scr.dbg[8 * (size_t)b + lane] = (int64_t)S.ck[lane];
+#endif
     if (lane == 0) {
         for (int i = 0; i < 16; ++i) p.scr.pose_DT[16 * b + i] = S.DT[i];
         for (int i = 0; i < 36; ++i) p.scr.pose_H[36 * b + i] = S.H[i];
@@ -843,14 +886,34 @@ static int pose_multi_max_b() {
     const char* e = getenv("GFPL_POSE_MULTI_MAX_B");
     return e ? atoi(e) : POSE_MULTI_MAX_B;
 }
+// ... and up to which it runs 8 (a list of <= 512 active entries is then one round of chunks per GN
+// iteration; 1 workgroup of 8 waves per CU at B <= 256); GFPL_POSE_W8_MAX_B overrides
+#ifndef POSE_W8_MAX_B
+#define POSE_W8_MAX_B 256
+#endif
+static int pose_w8_max_b() {
+    const char* e = getenv("GFPL_POSE_W8_MAX_B");
+    return e ? atoi(e) : POSE_W8_MAX_B;
+}
 
 hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     int NP2 = 1;
     while (NP2 < p.mpt_cap || NP2 < p.mls_cap) NP2 <<= 1;
+    const bool w8 = p.B <= pose_w8_max_b();
     const bool multi = p.B <= pose_multi_max_b();   // small batches: POSE_W waves per sequence
-    const size_t region = (size_t)std::max((multi ? POSE_W : 1) * 16 * CH_STRIDE, NP2);
+    const int Wl = w8 ? 8 : (multi ? POSE_W : 1);
+    const size_t region = (size_t)std::max(Wl * 16 * CH_STRIDE, NP2);
     const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 16;
-    if (multi)
+    if (w8) {
+        static bool attr = false;   // (dynamic LDS above the 64 KB default)
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_pose<8>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_pose<8>, dim3(p.B), dim3(64 * 8), lds, s, p, NP2);
+    } else if (multi)
         hipLaunchKernelGGL(k_pose<POSE_W>, dim3(p.B), dim3(64 * POSE_W), lds, s, p, NP2);
     else
         hipLaunchKernelGGL(k_pose<1>, dim3(p.B), dim3(64), lds, s, p, NP2);

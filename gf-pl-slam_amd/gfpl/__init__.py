@@ -762,6 +762,11 @@ class Context:
         dev = torch.device("cuda", self.device)
         return torch.cuda.ExternalStream(self.stream, device=dev) if self.stream else torch.cuda.default_stream(dev)
 
+    def set_config(self, cfg: Config):
+        """gfpl_set_config between steps (e.g. the line cut's proof mode); the context keeps a copy."""
+        check(self.L.gfpl_set_config(self.h, C.byref(cfg)), "set_config")
+        self.cfg = cfg
+
     def set_timing(self, on: bool):
         check(self.L.gfpl_set_timing(self.h, int(on)), "set_timing")
 

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -726,6 +727,10 @@ std::vector<Desc> collect(const uint8_t* (Frame::*f)(int) const, const Frame& fr
 static int64_t g_cut_stats[8];
 // per line: the smallest metric gap a step decision rests on (histogram by decade, 1e-16 .. 1e3)
 static int64_t g_cut_gap_hist[20];
+// moves by (sign of the start-ratio change + 1) * 3 + (sign of the end-ratio change + 1); [9]: a
+// single-ratio move right after one on the same ratio in the same direction; [10]: lines
+static int64_t g_cut_moves[11];
+static std::string g_cut_paths;   // per line: the move classes, one character each ('0' + class, 'S' stay)
 #define CUT_STAT(stmt) do { stmt; } while (0)
 #else
 #define CUT_STAT(stmt) do { } while (0)
@@ -1356,6 +1361,8 @@ struct gfplo_handler {
             std::memcpy(sum_before, sum, sizeof sum);
             std::vector<std::pair<uint64_t, uint64_t>> seen, last_step, this_step;
             double line_gap = 1e300;
+            int prev_mc = -1;
+            g_cut_moves[10]++;
 #endif
             [[maybe_unused]] bool moved = false;
             for (int i = 0; i < 36; ++i) sum[i] = sum[i] - L.invCov[i];
@@ -1415,6 +1422,16 @@ struct gfplo_handler {
                     line_gap = std::min(line_gap, g);
                 }
 #endif
+#ifdef GFPL_ORACLE_CUT_STATS
+                if (hit) {
+                    const int s0 = (cand[0] > L.cut[0]) - (cand[0] < L.cut[0]), s1 = (cand[1] > L.cut[1]) - (cand[1] < L.cut[1]);
+                    const int mc = (s0 + 1) * 3 + (s1 + 1);
+                    g_cut_moves[mc]++;
+                    g_cut_paths.push_back((char)('0' + mc));
+                    if ((s0 == 0) != (s1 == 0) && mc == prev_mc) g_cut_moves[9]++;
+                    prev_mc = mc;
+                }
+#endif
                 if (hit) {
                     CUT_STAT(if (cand[0] < L.cut[0] || cand[1] < L.cut[1]) g_cut_stats[7]++);   // a ratio moved back
                     L.cut[0] = cand[0]; L.cut[1] = cand[1];
@@ -1423,6 +1440,9 @@ struct gfplo_handler {
                     moved = true;
                 } else break;
             }
+#ifdef GFPL_ORACLE_CUT_STATS
+            g_cut_paths.push_back('\n');
+#endif
             CUT_STAT(if (!moved) g_cut_stats[4]++);   // lines that never moved
 #ifdef GFPL_ORACLE_CUT_STATS
             {
@@ -1999,6 +2019,10 @@ extern "C" void gfplo_cut_stats(int64_t* out8) {
 #ifdef GFPL_ORACLE_CUT_STATS
     for (int i = 0; i < 8; ++i) { out8[i] = g_cut_stats[i]; g_cut_stats[i] = 0; }
     for (int i = 0; i < 20; ++i) { fprintf(stderr, "%lld ", (long long)g_cut_gap_hist[i]); g_cut_gap_hist[i] = 0; }
+    if (FILE* f = fopen("/tmp/gfplo_cut_paths.txt", "w")) { fputs(g_cut_paths.c_str(), f); fclose(f); }
+    g_cut_paths.clear();
+    fprintf(stderr, "\nmoves:");
+    for (int i = 0; i < 11; ++i) { fprintf(stderr, " %lld", (long long)g_cut_moves[i]); g_cut_moves[i] = 0; }
     fprintf(stderr, "\n");
 #else
     for (int i = 0; i < 8; ++i) out8[i] = -1;   // not compiled in

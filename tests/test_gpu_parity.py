@@ -87,12 +87,13 @@ def test_vga_default_pose_bitexact(vga_default):
     assert all(vga_default["pose_exact"]), vga_default["pose_exact"]
 
 
-@pytest.mark.parametrize("wave_max", ["0", "4096"])
-def test_bench_config_parity(monkeypatch, wave_max):
+@pytest.mark.parametrize("wave_max,w8_max", [("0", "0"), ("4096", "0"), ("4096", "4096")])
+def test_bench_config_parity(monkeypatch, wave_max, w8_max):
     # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop; both line-cut searches
-    # and both pose layouts (one wave per sequence, and the small-batch 4 waves per sequence)
+    # and the three pose layouts (one wave per sequence; the small-batch 4 and 8 waves per sequence)
     monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)
     monkeypatch.setenv("GFPL_POSE_MULTI_MAX_B", wave_max)
+    monkeypatch.setenv("GFPL_POSE_W8_MAX_B", w8_max)
     rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
                         n_seq=2, n_frames=4, kp_cap=2048, kl_cap=512, seed=7)
     _check(rep)
@@ -433,6 +434,7 @@ def test_line_cut_certified_matches_exact_at_scale(monkeypatch, wave_max):
     matched line and the poses bit-identical; proven mode certifies most steps."""
     monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)   # 0: the 8-sequence-per-wave search, else one per wave
     monkeypatch.setenv("GFPL_POSE_MULTI_MAX_B", wave_max)  # 0: one wave per sequence in k_pose, else four
+    monkeypatch.setenv("GFPL_POSE_W8_MAX_B", "0")         # (eight: test_bench_config_parity)
     n, F, KP, KL = 512, 3, 2048, 512
     base = dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
     cam = gfpl.make_camera("vga", gfpl.default_config(**base))
