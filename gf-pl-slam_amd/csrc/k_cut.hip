@@ -1610,6 +1610,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     size_t q_cur = 0;
     int n_steps = 0, n_exact = 0;
     // A line opens (fst and sumA hold its data): the k_cut_search<false> open, one lane per role
+#ifdef GFPL_CUTW_TCLOCK   // (diagnostic build: line-transition phases in scr.dbg 0-7)
+    uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tk0 = clock64();
+#define TCK(i) do { const uint64_t t_ = clock64(); tk[i] += t_ - tk0; tk0 = t_; } while (0)
+#else
+#define TCK(i) do { } while (0)
+#endif
     auto open_line = [&]() {
         double o[28];
         {
@@ -1618,6 +1625,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             for (int e = 0; e < 21; ++e) S[e] = sumA[e];
             chol_s(S, o);
         }
+        TCK(2);
         line_ok = (o[27] != 0.0) && (fst[PD_OK] != 0.0);
         if (lane < 6) {
             double w[6];
@@ -1632,6 +1640,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             for (int i = 0; i < 6; ++i) wgs[6 * lane + i] = w[i];
         }
         wave_lds_sync();
+        TCK(3);
         if (lane < 21) {
             const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
             double s = wgs[6 * ra] * wgs[6 * cb];
@@ -1640,39 +1649,50 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             wgs[36 + lane] = s;
         }
         wave_lds_sync();
+        TCK(4);
+        // the line's comparison data (cmpl), formed by every lane in registers (no per-role branches and
+        // LDS round trips), stored by lane 0 for the rounds' cut_reg_load
         const double* gm = wgs + 36;
         double* cl = reinterpret_cast<double*>(&cmpl);
-        if (lane < 2) {
-            const int a = 3 * lane, b2 = a + 1, c2 = a + 2;
-            double* oo = cl + 5 * lane;   // ns | ne
-            oo[0] = gm[tri(a, a)];
-            oo[1] = 2.0 * gm[tri(b2, a)];
-            oo[2] = __builtin_fma(2.0, gm[tri(c2, a)], gm[tri(b2, b2)]);
-            oo[3] = 2.0 * gm[tri(c2, b2)];
-            oo[4] = gm[tri(c2, c2)];
-        } else if (lane < 4) {
+        double G[21], cv[38];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) cl[10 + 5 * (lane - 2) + i] = fst[PD_VS + 5 * (lane - 2) + i];
-        } else if (lane < 7) {
-            const int i = lane - 4;
+        for (int e = 0; e < 21; ++e) G[e] = gm[e];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) cl[20 + 3 * i + k] = gm[tri(3 + k, i)];
-            const double gs = fmax(gm[tri(i, i)], 0.0), ge = fmax(gm[tri(3 + i, 3 + i)], 0.0);
-            cl[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
-            cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+        for (int i = 0; i < 10; ++i) cv[10 + i] = fst[PD_VS + i];
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+            const int a0 = 3 * sd, b2 = a0 + 1, c2 = a0 + 2;
+            cv[5 * sd + 0] = G[tri(a0, a0)];
+            cv[5 * sd + 1] = 2.0 * G[tri(b2, a0)];
+            cv[5 * sd + 2] = __builtin_fma(2.0, G[tri(c2, a0)], G[tri(b2, b2)]);
+            cv[5 * sd + 3] = 2.0 * G[tri(c2, b2)];
+            cv[5 * sd + 4] = G[tri(c2, c2)];
         }
-        wave_lds_sync();
-        const double T = fmax(fabs(rlo), fabs(rhi));
-        if (lane == 7) {
-            const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
-            const double VsA = h4abs(cl + 10, T), VeA = h4abs(cl + 15, T);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cv[20 + 3 * i + k] = G[tri(3 + k, i)];
+            const double gs = fmax(G[tri(i, i)], 0.0), ge = fmax(G[tri(3 + i, 3 + i)], 0.0);
+            cv[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
+            cv[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+        }
+        {
+            const double T = fmax(fabs(rlo), fabs(rhi));
+            const double Bs = h2(cv[29], cv[30], cv[31], T), Be = h2(cv[32], cv[33], cv[34], T);
+            const double VsA = h4abs(cv + 10, T), VeA = h4abs(cv + 15, T);
             const double Bs2 = Bs * Bs, Be2 = Be * Be;
-            cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
-            cl[36] = VsA;
-            cl[37] = VeA;
+            cv[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+            cv[36] = VsA;
+            cv[37] = VeA;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 38; ++i) cl[i] = cv[i];
         }
         wave_lds_sync();
-        dc = cut_dcore_p1<false>(cl[0], cl[10], cl[5], cl[15], cl[20], cl[35], cl[36], cl[37], cmpl.eb, tq, c_ok);
+        TCK(5);
+        dc = cut_dcore_p1<false>(cv[0], cv[10], cv[5], cv[15], cv[20], cv[35], cv[36], cv[37], cmpl.eb, tq, c_ok);
+        TCK(6);
     };
     if (nls > 0) {
         q_cur = lb + mls[0];
@@ -1913,33 +1933,40 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #ifdef GFPL_CUTW_CLOCK
             ++n_trans;
 #endif
+#ifdef GFPL_CUTW_TCLOCK
+            tk0 = clock64();
+#endif
             if (lane == 0) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
             }
-            // the approximate invCov_sum += the finished line's info (k_cut_search's transition)
-            if (fst[PD_OK] != 0.0) {
-                if (lane < 6) {
-                    xsl[1 + lane] = cut_ours_P(fst, 0, lane, r0);
-                    xsl[8 + lane] = cut_ours_P(fst, 1, lane, r1);
-                } else if (lane < 8) {
-                    xsl[7 * (lane - 6)] = cut_ours_V(fst, lane - 6, lane == 6 ? r0 : r1);
-                }
-            } else if (lane < 2) {
-                double o7[7];
-                exact_endpoint(cam, homog, Dl, L, q_cur, lane, lane ? r1 : r0, o7);
+            // the approximate invCov_sum += the finished line's info (k_cut_search's transition): lane
+            // e < 21 forms its entry from the comparison data directly (cut_ours_* expressions, the bits of
+            // cut_ours_info over the [v'_s, P_s, v'_e, P_e] vector), or from the reference-order endpoints
+            double info = 0.0;
+            {
+                const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
+                if (fst[PD_OK] != 0.0) {   // (wave-uniform)
+                    if (lane < 21) {
+                        const double is = rcp_fast(cut_ours_V(fst, 0, r0)), ie = rcp_fast(cut_ours_V(fst, 1, r1));
+                        const double psr = cut_ours_P(fst, 0, ra, r0), psc = cut_ours_P(fst, 0, cb, r0);
+                        const double per = cut_ours_P(fst, 1, ra, r1), pec = cut_ours_P(fst, 1, cb, r1);
+                        info = __builtin_fma(psr * is, psc, (per * ie) * pec);
+                    }
+                } else {
+                    if (lane < 2) {
+                        double o7[7];
+                        exact_endpoint(cam, homog, Dl, L, q_cur, lane, lane ? r1 : r0, o7);
 #pragma unroll
-                for (int i = 0; i < 7; ++i) xsl[7 * lane + i] = o7[i];
+                        for (int i = 0; i < 7; ++i) xsl[7 * lane + i] = o7[i];
+                    }
+                    wave_lds_sync();
+                    if (lane < 21) info = cut_ours_info(xsl, rcp_fast(xsl[0]), rcp_fast(xsl[7]), ra, cb);
+                }
             }
             ++m;
-            wave_lds_sync();
+            TCK(0);
             if (m < nls) {
-                double info = 0.0;
-                if (lane < 21) {
-                    const double is = rcp_fast(xsl[0]), ie = rcp_fast(xsl[7]);
-                    const int ra = (int)((TRI_ROW >> (3 * lane)) & 7), cb = (int)((TRI_COL >> (3 * lane)) & 7);
-                    info = cut_ours_info(xsl, is, ie, ra, cb);
-                }
                 wave_lds_sync();
                 if (lane < CUT_FAST) fst[lane] = pf_f0;
                 if (lane < 21) sumA[lane] = (sumA[lane] + info) - pf_i0;
@@ -1949,6 +1976,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 r0 = 0.0;
                 r1 = 0.0;
                 wave_lds_sync();
+                TCK(1);
                 open_line();
                 prefetch(m + 1);
             }
@@ -1963,6 +1991,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         int64_t* d = p.scr.dbg + 8 * (size_t)b;
         d[0] = ck_eval; d[1] = ck_dec; d[2] = ck_walk; d[3] = ck_exact; d[4] = ck_trans; d[5] = n_rounds; d[6] = n_trans;
         d[7] = n_steps;
+#endif
+#ifdef GFPL_CUTW_TCLOCK
+        for (int i = 0; i < 7; ++i) p.scr.dbg[8 * (size_t)b + i] = (int64_t)tk[i];
 #endif
     }
 }

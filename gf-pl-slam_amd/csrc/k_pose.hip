@@ -400,11 +400,22 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
                     const double2* A2 = reinterpret_cast<const double2*>(bw + ia * CH_STRIDE);
                     const double2* B2 = reinterpret_cast<const double2*>(bw + ib * CH_STRIDE);
                     const double2* W2 = reinterpret_cast<const double2*>(bw + 7 * CH_STRIDE);
+                    if (W >= 8) {
+                        // the add chain is the serial part (list order): reads issued 16 entries ahead of
+                        // it (the 8-wave kernel has the registers)
+#pragma unroll 8
+                        for (int k = 0; k < 32; ++k) {
+                            const double2 a = A2[k], bb = B2[k], w = W2[k];
+                            s = s + (a.x * bb.x) * w.x;
+                            s = s + (a.y * bb.y) * w.y;
+                        }
+                    } else {
 #pragma unroll GFPL_POSE_RED_UNROLL
-                    for (int k = 0; k < 32; ++k) {
-                        const double2 a = A2[k], bb = B2[k], w = W2[k];
-                        s = s + (a.x * bb.x) * w.x;
-                        s = s + (a.y * bb.y) * w.y;
+                        for (int k = 0; k < 32; ++k) {
+                            const double2 a = A2[k], bb = B2[k], w = W2[k];
+                            s = s + (a.x * bb.x) * w.x;
+                            s = s + (a.y * bb.y) * w.y;
+                        }
                     }
                 }
             }
