@@ -1073,33 +1073,16 @@ __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, c
 // Issue priority by progress.  A SIMD holds two search waves with the same work (B = 16384: 300
 // lines per sequence, the greedy steps per wave within 2%), yet measured per wave
 // (-DGFPL_CUT_CLOCK, profiles/r04_o, r04_r) the one in wave slot 0 finished in 5.2 ms and the one in
-// slot 1 in 5.6 ms (up to 6.3), which then ran its end alone.  GFPL_CUT_FAIR 1: the priority falls
-// one level per quarter of the wave's lines; 2: the two waves of a SIMD publish their progress (lines
-// done) in HBM at every line transition and the one ahead of its partner yields (priority 0 vs 2).
-#ifndef GFPL_CUT_FAIR
-#define GFPL_CUT_FAIR 2
-#endif
-// proven mode: 16-B pieces per lane of the next line's record prefetched into LDS (1: none, the
-// record is read from HBM when the line opens; 3: its first 48 doubles, 3 KB per wave — with the
-// v'-tables a fourth piece passes the 20 KB that keeps 8 waves per CU — measured 10.32 vs 10.25 ms,
-// profiles/r04_ab: the proven transitions are bound by their exact endpoint work, not this read)
-#ifndef CUT_PF_PROOF
-#define CUT_PF_PROOF 1
-#endif
+// slot 1 in 5.6 ms (up to 6.3), which then ran its end alone.  The two waves of a SIMD publish their
+// progress (lines done) in HBM at every line transition and the one ahead of its partner yields
+// (priority 0 vs 2); a per-quarter priority ladder measured 6.21 -> 6.15 ms against 6.14 -> 5.84
+// (profiles/r04_q, r04_r) and was removed.  The partner is the wave slot ^ 1, checked on the GPU by
+// test_cut_progress_partner_slots.
 __device__ __forceinline__ int wave_sum8(int v) {   // sum over the wave's 8 groups of lane 8g's value
     v += __shfl_xor(v, 8);
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void cut_progress_prio(int done, int total) {
-    done = wave_sum8(done);
-    total = wave_sum8(total);
-    const int q = total > 0 ? (4 * done) / total : 4;
-    if (q <= 0) __builtin_amdgcn_s_setprio(3);
-    else if (q == 1) __builtin_amdgcn_s_setprio(2);
-    else if (q == 2) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
 }
 // the wave's progress slot and its SIMD partner's (slot ^ 1) in scr.cut_prog: one entry per
 // (XCC, SE, SH, CU, SIMD, wave slot) from the HW_ID / XCC_ID registers
@@ -1123,7 +1106,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // nxl[k][16 g + ...] (the DMA writes base + 16 * lane)
     // (proven mode: no prefetch buffer — its v'-tables take the LDS, and 5 KB more would cost the
     // eighth wave of a CU; the record is read from HBM when the line opens)
-    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? CUT_PF_PROOF : 5][128];
+    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? 1 : 5][128];
     // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
     //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
     //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
@@ -1142,6 +1125,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     const int g = lane >> 3, j = lane & 7;
     const int b = blockIdx.x * CUT_G + g;
+    if (!PROOF && p.cfg.cut_proof == 0 && j == 0 && b < p.B) {
+        // the wave's HW_ID / XCC_ID in the debug slots 6 / 7 of its sequences (measured mode; read by
+        // tests/test_gpu_parity.py::test_cut_progress_partner_slots: the progress exchange's slot ^ 1)
+        p.scr.dbg[8 * (size_t)b + 6] = (int64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        p.scr.dbg[8 * (size_t)b + 7] = (int64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
     // proven mode (cut_proof 1 / 3): the eager-proven search runs only for the sequences whose
     // recorded search k_cut_verify did not prove (cut_flag); cut_proof 2 runs it for all of them
     const bool live = b < p.B && (!PROOF || p.cfg.cut_proof == 2 || p.scr.cut_flag[b] != 0);
@@ -1311,10 +1300,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
     auto pf_issue = [&](int mm) {
-        if (PROOF && CUT_PF_PROOF < 2) return;
+        if (PROOF) return;
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
-        for (int k = 0; k < (PROOF ? CUT_PF_PROOF : 5); ++k)
+        for (int k = 0; k < (PROOF ? 1 : 5); ++k)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
                                              (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
     };
@@ -1334,14 +1323,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     int n_steps = 0, n_exact = 0;   // this sequence's search steps, and those evaluated exactly
-#if GFPL_CUT_FAIR == 1
-    cut_progress_prio(0, j == 0 ? nls : 0);
-#elif GFPL_CUT_FAIR == 2
     const CutProg prog = cut_prog_slots(p.scr.cut_prog);
     if (lane == 0) __hip_atomic_store(prog.own, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int partner_done = 0;   // the partner's lines done as read at the previous transition
     __builtin_amdgcn_s_setprio(2);
-#endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -1480,7 +1465,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
-                if (PROOF && CUT_PF_PROOF < 2) {
+                if (PROOF) {
 #pragma unroll
                     for (int k = 0; k < CUT_FAST / 8; ++k) fst[g][j + 8 * k] = rec_l[(size_t)m * CUT_REC + j + 8 * k];
                 } else {
@@ -1489,8 +1474,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int k = 0; k < CUT_FAST / 8; ++k) {
                         const int e = j + 8 * k;
                         // (proven mode: the entries past the prefetched pieces from HBM)
-                        fst[g][e] = (PROOF && e >= 16 * CUT_PF_PROOF) ? rec_l[(size_t)m * CUT_REC + e]
-                                                                       : nxl[e >> 4][16 * g + (e & 15)];
+                        fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
                     }
                 }
             }
@@ -1509,8 +1493,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
                     if (e < 21) {
                         const double mid = sumA[g][e] + info[kk];
-                        const double nw = mid - ((PROOF && (CUT_PF_PROOF < 2 || x >= 16 * CUT_PF_PROOF))
-                                                 ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
+                        const double nw = mid - (PROOF ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
                         sumA[g][e] = nw;
                         if (PROOF) sumE[g][e] = mid;   // the exact invCov_sum, kept current (m_sync = m)
                     }
@@ -1522,9 +1505,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
-#if GFPL_CUT_FAIR == 1
-            cut_progress_prio(j == 0 ? m : 0, j == 0 ? nls : 0);
-#elif GFPL_CUT_FAIR == 2
             {
                 const int done = wave_sum8(j == 0 ? m : 0);
                 if (done > __builtin_amdgcn_readfirstlane(partner_done)) __builtin_amdgcn_s_setprio(0);
@@ -1532,7 +1512,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (lane == 0) __hip_atomic_store(prog.own, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 partner_done = __hip_atomic_load(prog.partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used next time
             }
-#endif
         } else if (pend) {
             ++wait;
         }

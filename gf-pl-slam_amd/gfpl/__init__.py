@@ -1048,7 +1048,8 @@ class StereoFrameHandler:
         return out
 
     def debug_clocks(self) -> np.ndarray:
-        """gfpl_debug_clocks: the instrumented builds' per-sequence clocks [B][8] (int64)."""
+        """gfpl_debug_clocks: per-sequence debug slots [B][8] (int64): the instrumented builds' clocks;
+        in the product build slots 6 / 7 hold the measured-mode line-cut wave's HW_ID / XCC_ID."""
         out = np.zeros((self.B, 8), np.int64)
         check(self.L.gfpl_debug_clocks(self.h, out.ctypes.data), "debug_clocks")
         return out

@@ -99,6 +99,50 @@ def test_bench_config_parity(monkeypatch, wave_max, w8_max):
     _check(rep)
 
 
+@pytest.mark.parametrize("n_seq", [1, 8])
+def test_small_batch_parity(n_seq):
+    """The small-batch kernels at the batch sizes they serve by default (B <= 256: the wave line-cut
+    search and the 8-wave k_pose), bench config, against the oracle — B = 1 is the reference app's
+    one stream per process (app/plslam_mod.cpp:387-411)."""
+    rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
+                        n_seq=n_seq, n_frames=4, kp_cap=2048, kl_cap=512, seed=11)
+    _check(rep)
+
+
+def test_cut_progress_partner_slots():
+    """k_cut_search's progress exchange pairs each wave with wave slot ^ 1 of its SIMD (k_cut.hip
+    cut_prog_slots).  At B = 16384 (2048 search waves over 1024 SIMDs, two resident per SIMD) every
+    wave's HW_ID / XCC_ID (debug slots 6 / 7, measured mode) is read back: each SIMD holding two waves
+    must hold them in slots s and s ^ 1.  Input: 64 distinct generated sequences tiled over the batch."""
+    B, n_dist, KP, KL = 16384, 64, 2048, 512
+    cfg = gfpl.default_config(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0)
+    cam = gfpl.make_camera("vga", cfg)
+    ctx = gfpl.Context(cam, cfg)
+    h = gfpl.StereoFrameHandler(ctx, B, KP, KL)
+    hb = gfpl.HostBatch(cam, gfpl.synth_params(pyr_from_l0=2), n_dist, KP, KL, seq0=0, pinned=True)
+
+    def stage(k):
+        hb.fill(k, 8, seq0=0, n=n_dist)
+        for s0 in range(0, B, n_dist):
+            h.upload_wait(h.upload_async(hb.frames(n_dist), s0, 0, l0_stride=int(cam.pyr_bytes)))
+        return h.staged_frames(0)
+
+    h.initialize(stage(0))
+    h.frameStep(stage(1))
+    d = h.debug_clocks()[::8]   # one row per search wave (8 sequences each)
+    hw, xcc = d[:, 6].astype(np.int64), d[:, 7].astype(np.int64)
+    simd = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 + ((hw >> 4) & 3)
+    slot = hw & 15
+    per = {}
+    for s_, w_ in zip(simd.tolist(), slot.tolist()):
+        per.setdefault(s_, []).append(w_)
+    pairs = [v for v in per.values() if len(v) == 2]
+    print(f"{len(per)} SIMDs, {len(pairs)} with two waves, slot sets {sorted(set(tuple(sorted(v)) for v in pairs))[:8]}")
+    assert len(pairs) > 0.5 * len(per)
+    bad = [v for v in pairs if v[0] != (v[1] ^ 1)]
+    assert not bad, f"{len(bad)} SIMDs whose two waves are not partner slots, e.g. {bad[:4]}"
+
+
 @pytest.mark.parametrize("proof,wave_max", [(1, "0"), (1, "4096"), (2, "0"), (3, "0")])
 def test_proven_cut_parity(monkeypatch, proof, wave_max):
     """Proven-mode line cut against the oracle: cut_proof 1 — the recorded measured
