@@ -113,6 +113,7 @@ struct DevScratch {
     int32_t* cut_prog;  // [1 << 17] k_cut_search: lines done per (XCC, SE, SH, CU, SIMD, wave slot)
     uint8_t* cut_path;  // [B*mls_cap*CUT_PATH] proven mode: every line's recorded search steps
     int32_t* cut_flag;  // [B] proven mode: 1 = the recorded search was not proven (redo it eagerly)
+    int32_t* cut_offl;  // [1 + B*mls_cap] proven mode: count, then the lines (b * mls_cap + m) k_cut_vref left to k_cut_vref_off
     double* cut_vmax;   // [B*mls_cap*CUT_VMAX] proven mode (k_cut_vref -> k_cut_verify): per line, over the ratios
                         // its margined steps compared, max 1 / v' and max r_v / v' per side, the margined
                         // steps, and the ratios whose v' comparison failed

@@ -1095,7 +1095,9 @@ __device__ __forceinline__ CutProg cut_prog_slots(int* base) {
     const unsigned slot = hw & 15u;
     return CutProg{base + simd * 16u + slot, base + simd * 16u + (slot ^ 1u)};
 }
-template <bool PROOF>
+// REC (PROOF false): record every step's decision for k_cut_verify (proven mode's first pass); a
+// template parameter so that the measured mode's kernel carries none of its registers
+template <bool PROOF, bool REC = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
@@ -1137,9 +1139,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int nls = live ? p.tr.n_matched_ls[b] : 0;
     // proven mode, first pass (the measured search): every step's decision is recorded for
     // k_cut_verify — one byte per step and line, CUT_PATH per line
-    const bool rec = !PROOF && p.cfg.cut_proof != 0;
+    constexpr bool rec = !PROOF && REC;
     uint8_t* const path = p.scr.cut_path + (size_t)(live ? b : 0) * p.mls_cap * CUT_PATH;
     int lstep = 0;       // steps taken on the current line
+    unsigned long long pacc = 0ull;   // the current 8-byte block of its recorded steps
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     const double tau = p.cfg.cut_certify;
@@ -1382,8 +1385,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         int finalize = 0;
         if (rec && act && j == 0) {   // move j | CUT_P_STAY (no better neighbour) | CUT_P_EXACT
             if (lstep < CUT_PATH)
-                path[(size_t)m * CUT_PATH + lstep] =
-                    (uint8_t)((best >= 0 ? best : CUT_P_STAY) | (exact ? CUT_P_EXACT : 0));
+                pacc |= (unsigned long long)((best >= 0 ? best : CUT_P_STAY) | (exact ? CUT_P_EXACT : 0)) << (8 * (lstep & 7));
             ++lstep;
         }
         if (act) {
@@ -1406,6 +1408,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             } else {
                 finalize = 1;
             }
+        }
+        // the recorded bytes go out eight at a time (a full 8-byte block, or the line's last one)
+        if (rec && act && j == 0 && lstep <= CUT_PATH && ((lstep & 7) == 0 || finalize)) {
+            *reinterpret_cast<unsigned long long*>(path + (size_t)m * CUT_PATH + ((lstep - 1) & ~7)) = pacc;
+            pacc = 0ull;
         }
         if (act && finalize) {
             if (j == 0) {
@@ -2323,8 +2330,9 @@ __global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
     wave_lds_sync();
     if (!on) return;
     double* out = p.scr.cut_vmax + ((size_t)b * p.mls_cap + m) * CUT_VMAX;
-    if (off) {   // (k_cut_vref_off replays the line)
-        out[4] = -1.0;
+    if (off) {   // (k_cut_vref_off replays the line: appended to its list)
+        const int slot = atomicAdd(p.scr.cut_offl, 1);
+        p.scr.cut_offl[1 + slot] = b * p.mls_cap + m;
         return;
     }
 #pragma unroll
@@ -2333,13 +2341,14 @@ __global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
     out[5] = (double)(nbad + nbl[lane]);
 }
 
-// the lines k_cut_vref left (out[4] = -1: a compared ratio off the key table), one lane each; its own
-// kernel, so that the replay's registers do not set k_cut_vref's occupancy
+// the lines k_cut_vref left (a compared ratio off the key table: rare), from its list, one lane each;
+// its own kernel, so that the replay's registers do not set k_cut_vref's occupancy, over a fixed grid
 __global__ void __launch_bounds__(64) k_cut_vref_off(KParams p) {
-    const int b = blockIdx.y;
-    const int m = blockIdx.x * 64 + threadIdx.x;
-    if (m >= p.tr.n_matched_ls[b]) return;
-    if (p.scr.cut_vmax[((size_t)b * p.mls_cap + m) * CUT_VMAX + 4] < 0.0) vref_replay(p, b, m);
+    const int n = p.scr.cut_offl[0];
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
+        const int e = p.scr.cut_offl[1 + i];
+        vref_replay(p, e / p.mls_cap, e % p.mls_cap);
+    }
 }
 
 // Proven mode: the operand error bounds of every matched line (cut_line_bounds_p, P only) into
@@ -2838,15 +2847,18 @@ hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* ma
     if (marks) (void)hipEventRecord(marks[0], s);
     if (mode == 2)
         hipLaunchKernelGGL(k_cut_search<true>, gsearch, dim3(64), 0, s, p);
-    else if (p.B <= cut_wave_max_b())   // small batches: one sequence per wave, three steps per round
+    else if (p.B <= cut_wave_max_b())   // small batches: one sequence per wave, several steps per round
         hipLaunchKernelGGL(k_cut_search_w, dim3(p.B), dim3(64), 0, s, p);
+    else if (mode == 1 || mode == 3)   // (the recorded search)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_cut_search<false, true>), gsearch, dim3(64), 0, s, p);
     else
         hipLaunchKernelGGL(k_cut_search<false>, gsearch, dim3(64), 0, s, p);
     if (marks) (void)hipEventRecord(marks[1], s);
     if (mode == 1 || mode == 3) {
         // prove the recorded decisions (and finish those sequences); redo the others eagerly
+        if (hipMemsetAsync(p.scr.cut_offl, 0, sizeof(int32_t), s) != hipSuccess) return hipGetLastError();
         hipLaunchKernelGGL(k_cut_vref, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
-        hipLaunchKernelGGL(k_cut_vref_off, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_vref_off, dim3(256), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_ebound, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_verify, dim3(p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);

@@ -277,7 +277,8 @@ int  gfpl_set_camera(gfpl_ctx* ctx, const gfpl_camera* cam);
 /* max_point_match_num / max_line_match_num size the matched lists and the cut /
  * pose scratch of a seqbatch when it is created; while any seqbatch of the
  * context lives, a config with a larger budget than its capacity is refused with
- * GFPL_E_CAPACITY (lower budgets are accepted).                                */
+ * GFPL_E_CAPACITY (lower budgets are accepted).  Other fields (e.g. cut_proof) may
+ * change between steps: each step reads the config current at its launch.     */
 int  gfpl_set_config(gfpl_ctx* ctx, const gfpl_config* cfg);
 int  gfpl_get_camera(const gfpl_ctx* ctx, gfpl_camera* cam);
 int  gfpl_get_config(const gfpl_ctx* ctx, gfpl_config* cfg);
@@ -686,8 +687,10 @@ int  gfpl_debug_cut_records(gfpl_seqbatch* sb, int b, double* out, int n_lines);
  * gfpl_last_step_counts [8..15], line-cut steps / exact steps [16..17], inliers after the pose
  * [18], lines without a usable bound [19] (layout: STEP_REC in gfpl_state.hpp).  Synchronises. */
 int  gfpl_debug_step_records(gfpl_seqbatch* sb, int64_t* out);
-/* B x 8 int64 of diagnostic clocks (100 MHz wall clock) that instrumented builds of the library
- * write (e.g. -DGFPL_SP_CLOCK: k_stereo_points' phase boundaries); zeros otherwise. Synchronises. */
+/* B x 8 int64 of diagnostic slots: the clocks instrumented builds of the library write (e.g.
+ * -DGFPL_SP_CLOCK: k_stereo_points' phase boundaries); in every build, after a measured-mode step
+ * with the 8-sequence-per-wave line-cut search, slots 6 / 7 hold that search wave's HW_ID / XCC_ID
+ * (its SIMD and wave slot: the progress exchange's partner check).  Synchronises.               */
 int  gfpl_debug_clocks(gfpl_seqbatch* sb, int64_t* out);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
