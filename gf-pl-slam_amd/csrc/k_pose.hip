@@ -275,6 +275,13 @@ __device__ __forceinline__ void pose_prio(int stage, int it, int n) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
+// entry pairs of chunk c the reduction lane adds: its list's remaining entries (rounded up to a pair),
+// none for lanes 56-63
+__device__ __forceinline__ int red_pairs(int lane, int list, int np_act, int nl_act, int c) {
+    const int rem = min(64, max(0, (list == 0 ? np_act : nl_act) - (c << 6)));
+    return lane < 56 ? (rem + 1) >> 1 : 0;
+}
+
 template <int W>
 __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, double* cp, double* cl,
                              int max_iters, int stage) {
@@ -376,8 +383,12 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
                 const double2* A2 = reinterpret_cast<const double2*>(A);
                 const double2* B2 = reinterpret_cast<const double2*>(Bv);
                 const double2* W2 = reinterpret_cast<const double2*>(Wr);
+                // the entry pairs of this chunk the lane's list has (the rows past its end are zero: +0.0
+                // leaves the sum's bits); lanes 56-63 hold no entry — the LDS reads, not the adds, bound
+                // this loop at 4 waves per SIMD
+                const int kmax = red_pairs(lane, list, np_act, nl_act, c);
     #pragma unroll GFPL_POSE_RED_UNROLL
-                for (int k = 0; k < 32; ++k) {
+                for (int k = 0; k < kmax; ++k) {
                     const double2 a = A2[k], bb = B2[k], w = W2[k];
                     s = s + (a.x * bb.x) * w.x;
                     s = s + (a.y * bb.y) * w.y;
@@ -400,18 +411,19 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
                     const double2* A2 = reinterpret_cast<const double2*>(bw + ia * CH_STRIDE);
                     const double2* B2 = reinterpret_cast<const double2*>(bw + ib * CH_STRIDE);
                     const double2* W2 = reinterpret_cast<const double2*>(bw + 7 * CH_STRIDE);
+                    const int kmax = red_pairs(lane, list, np_act, nl_act, c0 + wb);
                     if (W >= 8) {
                         // the add chain is the serial part (list order): reads issued 16 entries ahead of
                         // it (the 8-wave kernel has the registers)
 #pragma unroll 8
-                        for (int k = 0; k < 32; ++k) {
+                        for (int k = 0; k < 32; ++k) {   // (a fixed trip count: the reads stay 16 entries ahead)
                             const double2 a = A2[k], bb = B2[k], w = W2[k];
                             s = s + (a.x * bb.x) * w.x;
                             s = s + (a.y * bb.y) * w.y;
                         }
                     } else {
 #pragma unroll GFPL_POSE_RED_UNROLL
-                        for (int k = 0; k < 32; ++k) {
+                        for (int k = 0; k < kmax; ++k) {
                             const double2 a = A2[k], bb = B2[k], w = W2[k];
                             s = s + (a.x * bb.x) * w.x;
                             s = s + (a.y * bb.y) * w.y;
