@@ -161,6 +161,8 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.cut_flag = c.take<int32_t>(B);
     sb->scr.cut_vmax = c.take<double>(B * sb->mls_cap * CUT_VMAX);
     sb->scr.cut_offl = c.take<int32_t>(1 + B * sb->mls_cap);
+    sb->scr.cut_dtln = c.take<int32_t>(1 + CUT_DTL * B);
+    sb->scr.cut_dtl = c.take<double>(CUT_DTL * B * 32);
     sb->scr.kf_mask = c.take<int32_t>(B);
     sb->last_n_pt = c.take<int32_t>(B);
     sb->last_n_ls = c.take<int32_t>(B);

@@ -81,6 +81,7 @@ struct DevTrack {
                       // eager-proven search redid it), [21] margined steps verified, [22] the reference's
                       // endpoint variances evaluated, [23] lines with margined steps
 #define CUT_PATH 64   // proven mode: recorded search steps per line (k_cut_search -> k_cut_verify)
+#define CUT_DTL 4     // proven mode: detail-list entries per sequence (a sequence past them is redone eagerly)
 #define CUT_VMAX 14   // proven mode: doubles per line of k_cut_vref's maxima [0..5] and k_cut_ebound's operand bounds (14 floats at [6..13]) (DevScratch::cut_vmax)
 #define CUT_P_STAY 8  //   step byte: no neighbour beat the centre (the line ends), else the move j (0-7)
 #define CUT_P_EXACT 16 //  step byte flag: the step was decided by the reference's arithmetic (exact round)
@@ -114,6 +115,8 @@ struct DevScratch {
     uint8_t* cut_path;  // [B*mls_cap*CUT_PATH] proven mode: every line's recorded search steps
     int32_t* cut_flag;  // [B] proven mode: 1 = the recorded search was not proven (redo it eagerly)
     int32_t* cut_offl;  // [1 + B*mls_cap] proven mode: count, then the lines (b * mls_cap + m) k_cut_vref left to k_cut_vref_off
+    int32_t* cut_dtln;  // [1 + CUT_DTL * B] proven mode: count, then the lines k_cut_verify left to k_cut_verify_detail
+    double* cut_dtl;    // [CUT_DTL * B * 32] their payload: S_full at the line's start (21), the bound terms (9)
     double* cut_vmax;   // [B*mls_cap*CUT_VMAX] proven mode (k_cut_vref -> k_cut_verify): per line, over the ratios
                         // its margined steps compared, max 1 / v' and max r_v / v' per side, the margined
                         // steps, and the ratios whose v' comparison failed

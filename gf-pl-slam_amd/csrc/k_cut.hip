@@ -1142,7 +1142,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     constexpr bool rec = !PROOF && REC;
     uint8_t* const path = p.scr.cut_path + (size_t)(live ? b : 0) * p.mls_cap * CUT_PATH;
     int lstep = 0;       // steps taken on the current line
-    unsigned long long pacc = 0ull;   // the current 8-byte block of its recorded steps
+    // REC: the current line's recorded steps, per group (stored to HBM when the line finishes)
+    __shared__ __attribute__((aligned(8))) uint8_t pth[REC ? CUT_G : 1][REC ? CUT_PATH : 8];
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     const double tau = p.cfg.cut_certify;
@@ -1383,10 +1384,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             if (exact) { dnext = sd; cnext = sb; }
         }
         int finalize = 0;
-        if (rec && act && j == 0) {   // move j | CUT_P_STAY (no better neighbour) | CUT_P_EXACT
-            if (lstep < CUT_PATH)
-                pacc |= (unsigned long long)((best >= 0 ? best : CUT_P_STAY) | (exact ? CUT_P_EXACT : 0)) << (8 * (lstep & 7));
-            ++lstep;
+        if (rec && act) {   // move j | CUT_P_STAY (no better neighbour) | CUT_P_EXACT, into the group's LDS row
+            if (j == 0 && lstep < CUT_PATH)
+                pth[g][lstep] = (uint8_t)((best >= 0 ? best : CUT_P_STAY) | (exact ? CUT_P_EXACT : 0));
+            ++lstep;   // (every lane of the group: they store the row's 8-byte blocks)
         }
         if (act) {
             first = 0;
@@ -1409,10 +1410,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 finalize = 1;
             }
         }
-        // the recorded bytes go out eight at a time (a full 8-byte block, or the line's last one)
-        if (rec && act && j == 0 && lstep <= CUT_PATH && ((lstep & 7) == 0 || finalize)) {
-            *reinterpret_cast<unsigned long long*>(path + (size_t)m * CUT_PATH + ((lstep - 1) & ~7)) = pacc;
-            pacc = 0ull;
+        if (rec && act && finalize) {   // the line's recorded steps to HBM: 8 bytes per group lane
+            __builtin_amdgcn_wave_barrier();
+            if (8 * j < lstep)
+                *reinterpret_cast<unsigned long long*>(path + (size_t)m * CUT_PATH + 8 * j) =
+                    *reinterpret_cast<const unsigned long long*>(&pth[g][8 * j]);
         }
         if (act && finalize) {
             if (j == 0) {
@@ -1992,8 +1994,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     const int b = blockIdx.x;
     const int nls = p.tr.n_matched_ls[b];
-    // proven mode (cut_proof 1 / 3): k_cut_verify finished the proven sequences, this kernel the redone ones
-    if (nls == 0 || ((p.cfg.cut_proof == 1 || p.cfg.cut_proof == 3) && p.scr.cut_flag[b] == 0)) return;
+    // proven mode (cut_proof 1 / 3): k_cut_verify wrote the proven sequences' invCovPose, this kernel their
+    // cut endpoints; the redone ones get both here
+    if (nls == 0) return;
+    const bool ends_only = (p.cfg.cut_proof == 1 || p.cfg.cut_proof == 3) && p.scr.cut_flag[b] == 0;
     const DevCam& cam = p.cam;
     DevLines& L = p.prev.ls;
     const size_t lb = (size_t)b * p.kl_cap;
@@ -2008,7 +2012,11 @@ __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
         LineCutData d;
         double r0 = 0.0, r1 = 0.0;
         double info[36];
-        if (live) {
+        if (live && ends_only) {
+            load_line(L, q, d);
+            r0 = L.cut[2 * q];
+            r1 = L.cut[2 * q + 1];
+        } else if (live) {
             load_line(L, q, d);
             r0 = L.cut[2 * q];
             r1 = L.cut[2 * q + 1];
@@ -2421,7 +2429,7 @@ __device__ __attribute__((noinline)) int verify_line_detail(const KParams& p, co
                                                             const uint8_t* path_m, const double* fd, double r0f,
                                                             double r1f, double K0, double A1, double B1, double cs,
                                                             double ce, double R0, double rts, double rte, bool line_ok,
-                                                            const double* Scol, int& n_xchk) {
+                                                            const double* Scol, int sstride, int& n_xchk) {
     const double st = p.cfg.cut_step, rlo = p.cfg.cut_rng[0], rhi = p.cfg.cut_rng[1];
     const bool pdok = fd[PD_OK] != 0.0;
     int bad = 0;
@@ -2467,7 +2475,7 @@ __device__ __attribute__((noinline)) int verify_line_detail(const KParams& p, co
                         // not covered by the bound: the reference's own evaluation of the step
                         double Sref[21], Sfull[21];
 #pragma unroll
-                        for (int e = 0; e < 21; ++e) { Sfull[e] = Scol[65 * e]; Sref[e] = Sfull[e] - fd[CUT_FAST + e]; }
+                        for (int e = 0; e < 21; ++e) { Sfull[e] = Scol[sstride * e]; Sref[e] = Sfull[e] - fd[CUT_FAST + e]; }
                         ++n_xchk;
                         if (!verify_exact_step(p, Dl, q, r0, r1, first, Sref, Sfull, (by & CUT_P_STAY) ? CUT_P_STAY : (by & 7)))
                             bad |= 512;
@@ -2614,7 +2622,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const size_t lb = (size_t)b * p.kl_cap;
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
     const double* rec_l = p.scr.cut_rec + (size_t)b * p.mls_cap * CUT_REC;
-    const uint8_t* path = p.scr.cut_path + (size_t)b * p.mls_cap * CUT_PATH;
     double Dl[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) Dl[i] = p.scr.cut_dtinv[16 * b + i];
@@ -2690,13 +2697,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const int cnt = min(64, nls - c0);
         if (lane < 21) {
             // the r = 0 infos are fetched 16 lines at a time (one memory round trip per batch, not per line)
-            for (int l0 = 0; l0 < cnt; l0 += 16) {
-                double iv[17];
+            auto fetch = [&](int l0, double* v) {
 #pragma unroll
                 for (int k = 0; k < 17; ++k) {
                     const int mm = c0 + l0 + k;
-                    iv[k] = (l0 + k <= cnt && mm < nls) ? rec_l[(size_t)mm * CUT_REC + CUT_FAST + lane] : 0.0;
+                    v[k] = (l0 + k <= cnt && mm < nls) ? rec_l[(size_t)mm * CUT_REC + CUT_FAST + lane] : 0.0;
                 }
+            };
+            // (a double-buffered fetch, the next batch's loads issued before this batch's sums, measured
+            // 2.21 vs 1.99 ms: its 34 live registers cost 35 more spills)
+            double iv[17];
+            for (int l0 = 0; l0 < cnt; l0 += 16) {
+                fetch(l0, iv);
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
                     const int l = l0 + k;
@@ -2751,11 +2763,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             n_dline += detail ? 1 : 0;
         }
         VK(4);
-        if (detail) {
-            int nx = 0;
-            bad |= verify_line_detail(p, Dl, q, path + (size_t)m * CUT_PATH, fd, r0f, r1f, K0, A1, B1, cs, ce, R0, rts, rte,
-                                      line_ok, &fr[0][0] + lane, nx);
-            n_xchk += nx;
+        if (detail) {   // to k_cut_verify_detail's list (out of this kernel's register budget); a full list: redo
+            const int slot = atomicAdd(p.scr.cut_dtln, 1);
+            if (slot < CUT_DTL * p.B) {
+                double* e = p.scr.cut_dtl + (size_t)slot * 32;
+#pragma unroll
+                for (int i = 0; i < 21; ++i) e[i] = fr[i][lane];
+                e[21] = K0; e[22] = A1; e[23] = B1; e[24] = cs; e[25] = ce; e[26] = R0; e[27] = rts; e[28] = rte;
+                e[29] = line_ok ? 1.0 : 0.0;
+                p.scr.cut_dtln[1 + slot] = b * p.mls_cap + m;
+            } else {
+                bad |= 1024;
+            }
         }
         wave_lds_sync();
     }
@@ -2771,35 +2790,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     tS = __shfl(tS, wl); tK = __shfl(tK, wl); tA = __shfl(tA, wl); tV = __shfl(tV, wl);
     bad = mask != 0 ? 1 : 0;
-    // k_cut_finish's endpoint update, for a proven sequence
-    if (!bad) {
-        for (int m = lane; m < nls; m += 64) {
-            const size_t q = lb + mls[m];
-            const double r0 = L.cut[2 * q], r1 = L.cut[2 * q + 1];
-            if (fabs(r0) < 0.0001 && fabs(r1) < 0.0001) continue;
-            double sP[3], eP[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { sP[k] = L.sP[3 * q + k]; eP[k] = L.eP[3 * q + k]; }
-            if (fabs(r0) > 0.0001) {
-                double s3[3];
-                for (int k = 0; k < 3; ++k) s3[k] = (1 - r0) * sP[k] + r0 * eP[k];
-                for (int k = 0; k < 3; ++k) { sP[k] = s3[k]; L.sP[3 * q + k] = s3[k]; }
-                double uv[2];
-                projection(cam, sP, uv);
-                L.spl[2 * q] = uv[0]; L.spl[2 * q + 1] = uv[1];
-                L.sdisp[q] = (cam.fx * cam.b) / sP[2];
-            }
-            if (fabs(r1) > 0.0001) {
-                double e3[3];
-                for (int k = 0; k < 3; ++k) e3[k] = (1 - r1) * eP[k] + r1 * sP[k];
-                for (int k = 0; k < 3; ++k) { eP[k] = e3[k]; L.eP[3 * q + k] = e3[k]; }
-                double uv[2];
-                projection(cam, eP, uv);
-                L.epl[2 * q] = uv[0]; L.epl[2 * q + 1] = uv[1];
-                L.edisp[q] = (cam.fx * cam.b) / eP[2];
-            }
-        }
-    }
+    // (the cut endpoints of a proven sequence: k_cut_finish, after k_cut_verify_detail has had its say)
     // counters: lanes' partial counts summed
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -2826,6 +2817,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #ifdef GFPL_VERIFY_CLOCK
         for (int i = 0; i < 5; ++i) p.scr.dbg[8 * (size_t)b + i] = (int64_t)vk[i];
 #endif
+    }
+}
+
+// The lines k_cut_verify's line-level bound did not cover, from its list, one lane each: the recorded
+// steps replayed with each step's own bound, and a step no bound covers re-decided with the
+// reference's arithmetic (verify_line_detail).  A failure flags the sequence for the eager redo.
+__global__ void __launch_bounds__(64) k_cut_verify_detail(KParams p) {
+    const int n = min(p.scr.cut_dtln[0], CUT_DTL * p.B);
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
+        const int e = p.scr.cut_dtln[1 + i];
+        const int b = e / p.mls_cap, m = e % p.mls_cap;
+        const double* pl = p.scr.cut_dtl + (size_t)i * 32;
+        const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+        const double* fd = p.scr.cut_rec + ((size_t)b * p.mls_cap + m) * CUT_REC;
+        const uint8_t* path = p.scr.cut_path + ((size_t)b * p.mls_cap + m) * CUT_PATH;
+        double Dl[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) Dl[k] = p.scr.cut_dtinv[16 * b + k];
+        int nx = 0;
+        const int bad = verify_line_detail(p, Dl, q, path, fd, p.prev.ls.cut[2 * q], p.prev.ls.cut[2 * q + 1], pl[21],
+                                           pl[22], pl[23], pl[24], pl[25], pl[26], pl[27], pl[28], pl[29] != 0.0, pl, 1,
+                                           nx);
+        if (bad) {
+            atomicOr(&p.scr.cut_flag[b], 1);
+            atomicOr(reinterpret_cast<unsigned long long*>(&p.scr.bytes[(size_t)STEP_REC * b + 20]), 1ull);
+        }
+        if (nx) atomicAdd(reinterpret_cast<unsigned long long*>(&p.scr.dbg[8 * (size_t)b + 6]), (unsigned long long)nx);
     }
 }
 
@@ -2860,7 +2878,9 @@ hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* ma
         hipLaunchKernelGGL(k_cut_vref, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_vref_off, dim3(256), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_ebound, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
+        if (hipMemsetAsync(p.scr.cut_dtln, 0, sizeof(int32_t), s) != hipSuccess) return hipGetLastError();
         hipLaunchKernelGGL(k_cut_verify, dim3(p.B), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(k_cut_verify_detail, dim3(256), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);
         hipLaunchKernelGGL(k_cut_search<true>, gsearch, dim3(64), 0, s, p);
