@@ -28,7 +28,7 @@ fi
 pmc() {   # name counters...
   local name=$1; shift
   timeout -k 10 500 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/pmc/$name -o $name -f csv -- \
-      python3 bench.py --no-cpu --parity-seqs 0 --no-detect --no-host-fed --no-b1 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
+      python3 bench.py --no-cpu --parity-seqs 0 --no-detect --no-host-fed --no-b1 --proven-steps 0 $BENCH_ARGS > $OUT/pmc/$name.log 2>&1 \
     || { echo "pmc $name failed"; tail -5 $OUT/pmc/$name.log; return 1; }
 }
 pmc fetch FETCH_SIZE && \
