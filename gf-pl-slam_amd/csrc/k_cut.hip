@@ -27,7 +27,9 @@ struct LineCutData {
 // projected residual variance of one cut endpoint (src/stereoFrameHandler.cpp:1356-1369).
 // Templated: T = double is the kernel's arithmetic, T = RB its running error bounds (the
 // point's depth then takes the lower bound zlo, see rb_floor).
-template <typename T>
+// SD (T = double only): the three divisions by pz^2 share the denominator's reciprocal refinement
+// (SharedDiv, gfpl_device.hpp: every quotient keeps the bits of '/'), for k_cut_vref's evaluations
+template <typename T, bool SD = false>
 __device__ __forceinline__ T endpointVar_t(const DevCam& cam, const double* DT_inv, const T* Jl, const T* Pt,
                                            const T* cov, double zlo) {
     T Jdt[9];
@@ -43,9 +45,17 @@ __device__ __forceinline__ T endpointVar_t(const DevCam& cam, const double* DT_i
     T Jp[9];
     Jp[0] = f / pz; Jp[3] = T(0.0); Jp[6] = T(0.0);
     Jp[1] = T(0.0); Jp[4] = f / pz; Jp[7] = T(0.0);
-    Jp[2] = ((-f) * cur[0]) / pz_2;
-    Jp[5] = ((-f) * cur[1]) / pz_2;
-    Jp[8] = ((-f) * T(cam.b)) / pz_2;
+    if constexpr (SD) {
+        const double n0 = (-f) * cur[0], n1 = (-f) * cur[1], n2 = (-f) * T(cam.b);
+        const SharedDiv dz = div_prep(pz_2, n0);
+        Jp[2] = div_by(dz, n0);
+        Jp[5] = div_by(dz, n1);
+        Jp[8] = div_by(dz, n2);
+    } else {
+        Jp[2] = ((-f) * cur[0]) / pz_2;
+        Jp[5] = ((-f) * cur[1]) / pz_2;
+        Jp[8] = ((-f) * T(cam.b)) / pz_2;
+    }
     T T1[6], T2[6], T3[6], M[4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -2094,7 +2104,7 @@ __device__ __forceinline__ double vref_regs(const DevCam& cam, double homog, con
     double cov[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) cov[i] = a * C0[i] + qq * C1[i];
-    const double v = endpointVar_t<double>(cam, Dl, Jl, Pt, cov, 0.0);
+    const double v = endpointVar_t<double, true>(cam, Dl, Jl, Pt, cov, 0.0);
     double cur[3];
     se3_apply(Dl, Pt, cur);
     const double f = cam.fx / ref_max(homog, cur[2] * cur[2]);
