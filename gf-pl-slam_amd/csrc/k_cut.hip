@@ -1800,13 +1800,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             wave_lds_sync();
             double vjn[8];
             int fl[8];
+            if (inc0 | inc1) {   // (wave-uniform) some lower neighbours are alt values
 #pragma unroll
-            for (int jn = 0; jn < 8; ++jn) {
-                const int da = nb_da(jn, 0), dc = nb_da(jn, 1);
-                const bool xa = ia && da < 0, xc = ic && dc < 0;
-                const int l = (xa && xc) ? 82 + 16 : (xa ? 82 + c + dc : (xc ? 90 + a + da : 9 + lane + 8 * da + dc));
-                vjn[jn] = dgx[l];
-                fl[jn] = dgf[l];
+                for (int jn = 0; jn < 8; ++jn) {
+                    const int da = nb_da(jn, 0), dc = nb_da(jn, 1);
+                    const bool xa = ia && da < 0, xc = ic && dc < 0;
+                    const int l = (xa && xc) ? 82 + 16 : (xa ? 82 + c + dc : (xc ? 90 + a + da : 9 + lane + 8 * da + dc));
+                    vjn[jn] = dgx[l];
+                    fl[jn] = dgf[l];
+                }
+            } else {   // every neighbour on the grid: constant offsets from the lane's slot
+#pragma unroll
+                for (int jn = 0; jn < 8; ++jn) {
+                    const int l = 9 + lane + 8 * nb_da(jn, 0) + nb_da(jn, 1);
+                    vjn[jn] = dgx[l];
+                    fl[jn] = dgf[l];
+                }
             }
             const double dcl = dj;
             const int cok = bok;
@@ -1854,21 +1863,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         int exact = 0, finalize = 0;
         double vj[8];
         int bj[8], valj[8];
-        // scalar walk: one readlane per step, the step's record byte parked in lane ns of pathv (one vector
-        // store after the walk, no per-step exec-masked store)
         int pathv = 0, ns = 0;
-        for (int sstep = 0; sstep < 64; ++sstep) {   // (wave-uniform; the grid ends a path: its edge positions stop)
-            const int w = __builtin_amdgcn_readlane(dec, pos);
-            const int dpos = w & 63;
-            if (dpos >= WAVE_EXACT) {   // WAVE_STOP / WAVE_EXACT
-                exact = dpos == WAVE_EXACT;
-                break;
+        if (!rec) {
+            // measured mode: the walk by pointer jumping (no record needed).  A position whose decision
+            // is a move that does not end the line continues at its target; every other position ends
+            // a chain.  Moves go to strictly larger d, so the chains are acyclic; six doublings cover
+            // the 64 positions.  Then lane 9's chain end and step count decide the round.
+            const int dpos = dec & 63;
+            const bool cont = dpos < CUT_P_STAY && !(dec & 64);
+            int jump = cont ? (dec >> 8) & 63 : lane;
+            int acc = cont ? 1 : 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const int jj = __shfl(jump, jump);
+                const int aa = __shfl(acc, jump);
+                acc += aa;
+                jump = jj;
             }
-            pathv = lane == ns ? dpos : pathv;
-            ++ns;
-            if (dpos == CUT_P_STAY) { finalize = 1; break; }
-            pos = w >> 8;
-            if (w & 64) { finalize = 1; break; }
+            const int T = __builtin_amdgcn_readlane(jump, 9);
+            ns = __builtin_amdgcn_readlane(acc, 9);
+            const int wT = __builtin_amdgcn_readlane(dec, T);
+            const int dT = wT & 63;
+            pos = T;
+            if (dT >= WAVE_EXACT) {
+                exact = dT == WAVE_EXACT;
+            } else {
+                ++ns;
+                finalize = 1;
+                if (dT != CUT_P_STAY) pos = wT >> 8;   // (a move that ends the line: r0 + r1 > 1 after it)
+            }
+        } else {
+            // scalar walk: one readlane per step, the step's record byte parked in lane ns of pathv (one
+            // vector store after the walk, no per-step exec-masked store)
+            for (int sstep = 0; sstep < 64; ++sstep) {   // (wave-uniform; the grid ends a path: its edge positions stop)
+                const int w = __builtin_amdgcn_readlane(dec, pos);
+                const int dpos = w & 63;
+                if (dpos >= WAVE_EXACT) {   // WAVE_STOP / WAVE_EXACT
+                    exact = dpos == WAVE_EXACT;
+                    break;
+                }
+                pathv = lane == ns ? dpos : pathv;
+                ++ns;
+                if (dpos == CUT_P_STAY) { finalize = 1; break; }
+                pos = w >> 8;
+                if (w & 64) { finalize = 1; break; }
+            }
         }
         if (ns) {
             if (rec && lane < ns && lstep + lane < CUT_PATH) path[(size_t)m * CUT_PATH + lstep + lane] = (uint8_t)pathv;
