@@ -1178,12 +1178,27 @@ __global__ void k_step_bytes(KParams p) {
 // ------------------------------------------------------------ launchers --
 static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p; }
 
+// small batches (B <= SP_WIDE_MAX_B, GFPL_SP_WIDE_MAX_B overrides): one sequence's stereo matching is
+// the latency, and a CU holds at most one or two sequences — 16 waves per sequence instead of 8
+#ifndef SP_WIDE_MAX_B
+#define SP_WIDE_MAX_B 256
+#endif
+static int sp_wide_max_b() {
+    const char* e = getenv("GFPL_SP_WIDE_MAX_B");
+    return e ? atoi(e) : SP_WIDE_MAX_B;
+}
+
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
     const int KP2 = next_pow2(p.kp_cap);
     const size_t lds = (size_t)KP2 * 18 + (size_t)((p.cam.height + 1) & ~1) * 2 + 64 * 4;
     const int nrl_seg = (p.cam.n_levels + 1) * (p.cam.height + 2 * SP_MINR_PAD) + 1;
     const size_t lds_seg = (size_t)KP2 * 18 + (size_t)((nrl_seg + 1) & ~1) * 2 + 32 * 4 + 16 +
                            (size_t)(512 / 64) * SP_CHUNK * 32;
+    const size_t lds_seg_w = lds_seg + (size_t)(512 / 64) * SP_CHUNK * 32;   // (16 waves' staging)
+    if (p.B <= sp_wide_max_b() && p.kp_cap <= 2048 && lds_seg_w <= 64 * 1024) {
+        hipLaunchKernelGGL((k_stereo_points<1024, true>), dim3(p.B), dim3(1024), lds_seg_w, s, p, KP2);
+        return hipGetLastError();
+    }
     // the large-capacity layout leaves LDS for one workgroup per CU: give it 16 waves
     if (p.kp_cap > 2048)
         hipLaunchKernelGGL((k_stereo_points<1024, false>), dim3(p.B), dim3(1024), lds, s, p, KP2);
@@ -1197,7 +1212,8 @@ hipError_t launch_stereo_points(const KParams& p, hipStream_t s) {
 size_t stereo_lines_lds(int cap) { return (size_t)cap * 32 + (size_t)cap * 16 + 260 * 4 + 64 * 4 + 1024 * 4; }
 
 hipError_t launch_stereo_lines(const KParams& p, hipStream_t s) {
-    if (p.kl_cap > 1024)   // large-capacity LDS layout: one workgroup per CU, 16 waves
+    // large-capacity LDS layout (one workgroup per CU) and small batches: 16 waves
+    if (p.kl_cap > 1024 || p.B <= sp_wide_max_b())
         hipLaunchKernelGGL((k_stereo_lines<2, false, 1024>), dim3(p.B), dim3(1024), stereo_lines_lds(p.kl_cap), s, p);
     else
         hipLaunchKernelGGL((k_stereo_lines<2, false, 512>), dim3(p.B), dim3(512), stereo_lines_lds(p.kl_cap), s, p);

@@ -89,11 +89,13 @@ def test_vga_default_pose_bitexact(vga_default):
 
 @pytest.mark.parametrize("wave_max,w8_max", [("0", "0"), ("4096", "0"), ("4096", "4096")])
 def test_bench_config_parity(monkeypatch, wave_max, w8_max):
-    # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop; both line-cut searches
-    # and the three pose layouts (one wave per sequence; the small-batch 4 and 8 waves per sequence)
+    # harness overrides of SURVEY §8(d): 10 + 10 GN iterations, no early stop; both line-cut searches,
+    # the three pose layouts (one wave per sequence; the small-batch 4 and 8 waves per sequence) and both
+    # stereo layouts (8 and 16 waves per sequence)
     monkeypatch.setenv("GFPL_CUT_WAVE_MAX_B", wave_max)
     monkeypatch.setenv("GFPL_POSE_MULTI_MAX_B", wave_max)
     monkeypatch.setenv("GFPL_POSE_W8_MAX_B", w8_max)
+    monkeypatch.setenv("GFPL_SP_WIDE_MAX_B", wave_max)   # 0: the bench batch's 8-wave stereo kernels, else 16
     rep = _run_sequence("vga", dict(max_iters=10, max_iters_ref=10, min_error=0.0, min_error_change=0.0),
                         n_seq=2, n_frames=4, kp_cap=2048, kl_cap=512, seed=7)
     _check(rep)
