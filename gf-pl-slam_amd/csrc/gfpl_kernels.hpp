@@ -4,6 +4,8 @@
 
 namespace gfpl {
 
+// the batch size up to which the stereo and cross stages run 16 waves per sequence (k_stereo.hip)
+int sp_wide_max_b();
 hipError_t launch_stereo_points(const KParams& p, hipStream_t s);
 hipError_t launch_stereo_lines(const KParams& p, hipStream_t s);
 hipError_t launch_line_uncertainty(const KParams& p, hipStream_t s);

@@ -335,7 +335,8 @@ hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
 
 hipError_t launch_cross_lines(const KParams& p, hipStream_t s) {
     const size_t lds = (size_t)p.kl_cap * 32 + (size_t)p.kl_cap * 16 + 520 * 4 + 64 * 4 + 512 * 4;
-    if (p.kl_cap > 1024)   // large-capacity LDS layout: one workgroup per CU, 16 waves
+    // large-capacity LDS layout (one workgroup per CU) and small batches: 16 waves
+    if (p.kl_cap > 1024 || p.B <= sp_wide_max_b())
         hipLaunchKernelGGL(k_cross_lines<1024>, dim3(p.B), dim3(1024), lds, s, p);
     else
         hipLaunchKernelGGL(k_cross_lines<512>, dim3(p.B), dim3(512), lds, s, p);

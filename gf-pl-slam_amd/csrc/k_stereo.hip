@@ -1183,7 +1183,7 @@ static inline int next_pow2(int v) { int p = 1; while (p < v) p <<= 1; return p;
 #ifndef SP_WIDE_MAX_B
 #define SP_WIDE_MAX_B 256
 #endif
-static int sp_wide_max_b() {
+int sp_wide_max_b() {
     const char* e = getenv("GFPL_SP_WIDE_MAX_B");
     return e ? atoi(e) : SP_WIDE_MAX_B;
 }
