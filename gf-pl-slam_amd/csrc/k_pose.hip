@@ -757,10 +757,16 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
 // Final bookkeeping of optimizePose (src/stereoFrameHandler.cpp:1983-2028), one
 // lane per sequence: inverse_se3, motion-step gate, Tfw, DT_cov = H^-1 (Q13),
 // its eigenvalues, Tfw_cov = unccomp_se3, err_norm, numFrameLoss.
-__global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+// Two waves per 64 sequences: both form DT_cov = H^-1; wave 1 takes its eigenvalues (the 6x6 cyclic
+// Jacobi, the longest serial chain here) while wave 0 does the rest, on another SIMD — the same
+// expressions, so the same bits (two lanes of one wave would run the two paths one after the other)
+__global__ void __launch_bounds__(128) k_pose_finish(KParams p) {
+    const int b = blockIdx.x * 64 + (threadIdx.x & 63), role = threadIdx.x >> 6;
     if (b >= p.B) return;
-    p.scr.bytes[(size_t)STEP_REC * b + 18] = p.tr.n_inliers[b];   // inliers after removeOutliers (step record)
+#ifdef GFPL_PFIN_CLOCK
+    const uint64_t pf0 = clock64();
+#endif
+    if (role == 0) p.scr.bytes[(size_t)STEP_REC * b + 18] = p.tr.n_inliers[b];   // inliers after removeOutliers (step record)
     DevPose& CP = p.curr.pose;
     const DevPose& PP = p.prev.pose;
     const int ok = p.scr.pose_ok[b];
@@ -779,6 +785,20 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
 #pragma unroll
         for (int i = 0; i < 36; ++i) DT_cov[i] = 0.0;
     }
+#ifdef GFPL_PFIN_CLOCK
+    const uint64_t pf1 = clock64();
+#endif
+    if (role == 1) {
+        double eig[6];
+        eig_sym<6>(DT_cov, eig);
+#ifdef GFPL_PFIN_CLOCK
+        p.scr.dbg[8 * (size_t)b + 1] = (int64_t)(clock64() - pf1);
+        p.scr.dbg[8 * (size_t)b + 0] = (int64_t)(pf1 - pf0);
+#endif
+#pragma unroll
+        for (int i = 0; i < 6; ++i) CP.DT_cov_eig[6 * b + i] = eig[i];
+        return;
+    }
     bool fin = true;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { double d = DT[i] - DT[i]; if (!(d == d)) fin = false; }
@@ -787,7 +807,7 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
     for (int i = 0; i < 16; ++i) Tp[i] = PP.Tfw[16 * b + i];
 #pragma unroll
     for (int i = 0; i < 36; ++i) Tpc[i] = PP.Tfw_cov[36 * b + i];
-    double cDT[16], Tfw[16], Tcov[36], eig[6];
+    double cDT[16], Tfw[16], Tcov[36];
     double err_norm;
     bool moved = false;
     if (fin) {
@@ -813,14 +833,14 @@ __global__ void __launch_bounds__(64) k_pose_finish(KParams p) {
         for (int i = 0; i < 36; ++i) Tcov[i] = Tpc[i];
         err_norm = -1.0;
     }
-    eig_sym<6>(DT_cov, eig);
 #pragma unroll
     for (int i = 0; i < 16; ++i) { CP.DT[16 * b + i] = cDT[i]; CP.Tfw[16 * b + i] = Tfw[i]; }
 #pragma unroll
     for (int i = 0; i < 36; ++i) { CP.DT_cov[36 * b + i] = DT_cov[i]; CP.Tfw_cov[36 * b + i] = Tcov[i]; }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) CP.DT_cov_eig[6 * b + i] = eig[i];
     CP.err_norm[b] = err_norm;
+#ifdef GFPL_PFIN_CLOCK
+    p.scr.dbg[8 * (size_t)b + 2] = (int64_t)(clock64() - pf1);
+#endif
 }
 
 // needNewKF (src/stereoFrameHandler.cpp:2309-2349), one lane per sequence, on the
@@ -941,7 +961,7 @@ hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     else
         hipLaunchKernelGGL(k_pose<1>, dim3(p.B), dim3(64), lds, s, p, NP2);
     if (mark) (void)hipEventRecord(mark, s);
-    hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(k_pose_finish, dim3((p.B + 63) / 64), dim3(128), 0, s, p);
     return hipGetLastError();
 }
 
