@@ -265,14 +265,22 @@ __device__ __forceinline__ void cut_poly_data(const double* Dl, const LineCutDat
                     ? 1.0 : 0.0;
 }
 
+// a wave's LDS stores visible to its own later loads (one wave: no barrier needed)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // ------------------------------------------------------------------ prep --
-__global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
-    __shared__ double chunk[21][65];   // lower-triangle infos of 64 list entries (padded row: lanes read 21 rows)
+// W waves per sequence (W = 1 from CUT_PREP_W8_MAX_B up; small batches W = 8): the waves compute W
+// 64-entry chunks at once, each in its own LDS buffer, then wave 0's lanes e < 21 add the W chunks'
+// infos in list order (the serial sum is the part that stays one wave's)
+template <int W>
+__global__ void __launch_bounds__(64 * W) k_cut_prep(KParams p) {
+    extern __shared__ double prep_lds[];   // W x [21][65] lower-triangle infos of 64 list entries (padded row)
     const int b = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = W > 1 ? (int)(threadIdx.x >> 6) : 0;
     const int nls = p.tr.n_matched_ls[b];
     const int npt = p.tr.n_matched_pt[b];
     if (nls == 0) return;
+    double (*chunk)[65] = reinterpret_cast<double (*)[65]>(prep_lds + (size_t)wv * 21 * 65);
     const DevCam& cam = p.cam;
     const double homog = p.cfg.homog_th;
     DevLines& L = p.prev.ls;
@@ -290,82 +298,95 @@ __global__ void __launch_bounds__(64) k_cut_prep(KParams p) {
         mat4_inv(Tc, Ti);
         mat4_mul(Ti, Tp, Dl);
     }
-    if (lane < 16) p.scr.cut_dtinv[16 * b + lane] = Dl[lane];
-    // invCov_sum: lines then points, each entry summed in list order by lane e < 21,
-    // 64 list entries at a time staged through LDS (src/stereoFrameHandler.cpp:1640-1657)
+    if (wv == 0 && lane < 16) p.scr.cut_dtinv[16 * b + lane] = Dl[lane];
+    // invCov_sum: lines then points, each entry summed in list order by lane e < 21 of wave 0,
+    // 64 list entries per wave at a time staged through LDS (src/stereoFrameHandler.cpp:1640-1657)
     double s = 0.0;
     const int nl_ch = (nls + 63) >> 6, np_ch = (npt + 63) >> 6;
-    for (int c = 0; c < nl_ch + np_ch; ++c) {
+    auto chunk_cnt = [&](int c) {
         const bool lines = c < nl_ch;
-        const int m = ((lines ? c : c - nl_ch) << 6) + lane;
-        const int cnt = min(64, (lines ? nls : npt) - (((lines ? c : c - nl_ch)) << 6));
-        double info[21];
-        double fd[CUT_FAST];   // (lines) the record's comparison data
-        if (lane < cnt) {
-            if (lines) {
-                LineCutData d;
-                load_line(L, lb + mls[m], d);
-                poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
+        return min(64, (lines ? nls : npt) - (((lines ? c : c - nl_ch)) << 6));
+    };
+    for (int c0 = 0; c0 < nl_ch + np_ch; c0 += W) {
+        const int c = c0 + wv;
+        if (c < nl_ch + np_ch) {   // (wave-uniform)
+            const bool lines = c < nl_ch;
+            const int m = ((lines ? c : c - nl_ch) << 6) + lane;
+            const int cnt = chunk_cnt(c);
+            double info[21];
+            double fd[CUT_FAST];   // (lines) the record's comparison data
+            if (lane < cnt) {
+                if (lines) {
+                    LineCutData d;
+                    load_line(L, lb + mls[m], d);
+                    poseInfoOnLine<false>(cam, homog, Dl, d, 0.0, 0.0, info);
 #pragma unroll
-                for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
-                cut_poly_data(Dl, d, homog, fd);
-                fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
-            } else {
-                const size_t q = pbase + mpt[m];
-                double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
-                double cur[3], uv[2];
-                se3_apply(Dl, Pp, cur);
-                projection(cam, cur, uv);
-                const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
-                double J[6];
-                poseJac(cam, homog, cur, dx, dy, J);   // getPoseInfoPoint (:1414-1447)
+                    for (int i = PD_ERR; i < CUT_FAST; ++i) fd[i] = 0.0;   // k_cut_bounds fills PD_ERR
+                    cut_poly_data(Dl, d, homog, fd);
+                    fd[PD_NEXT] = (double)mls[min(m + 1, nls - 1)];   // k_cut_search's next-next line
+                } else {
+                    const size_t q = pbase + mpt[m];
+                    double Pp[3] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2]};
+                    double cur[3], uv[2];
+                    se3_apply(Dl, Pp, cur);
+                    projection(cam, cur, uv);
+                    const double dx = uv[0] - P.pl_obs[2 * q], dy = uv[1] - P.pl_obs[2 * q + 1];
+                    double J[6];
+                    poseJac(cam, homog, cur, dx, dy, J);   // getPoseInfoPoint (:1414-1447)
 #pragma unroll
-                for (int i = 0; i < 6; ++i)
+                    for (int i = 0; i < 6; ++i)
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) info[tri(i, j)] = J[i] * J[j];
+                        for (int j = 0; j <= i; ++j) info[tri(i, j)] = J[i] * J[j];
+                }
             }
-        }
-        if (lines) {   // (wave-uniform)
-            // The chunk's records (comparison data | r = 0 info | pad) leave in five slices of 16
-            // doubles staged through the chunk buffer (idle until the sums): a store instruction then
-            // writes 8 whole 128-B lines of 8 records instead of 16 B of each of 64 records — stored
-            // straight from the lanes, the records took a third of the kernel
-            // (profiles/r04_s/bench_prepprobe.log)
-            double* stg = &chunk[0][0];   // [64][17] (odd row stride: the lanes' rows spread over the banks)
-            const int pl = lane >> 3, pp = lane & 7;
-            double* rc = rec_l + (size_t)(c << 6) * CUT_REC;
+            if (lines) {   // (wave-uniform)
+                // The chunk's records (comparison data | r = 0 info | pad) leave in five slices of 16
+                // doubles staged through the wave's chunk buffer (idle until the sums): a store
+                // instruction then writes 8 whole 128-B lines of 8 records instead of 16 B of each of 64
+                // records — stored straight from the lanes, the records took a third of the kernel
+                // (profiles/r04_s/bench_prepprobe.log)
+                double* stg = &chunk[0][0];   // [64][17] (odd row stride: the lanes' rows spread over the banks)
+                const int pl = lane >> 3, pp = lane & 7;
+                double* rc = rec_l + (size_t)(c << 6) * CUT_REC;
 #pragma unroll
-            for (int sl = 0; sl < CUT_REC / 16; ++sl) {
-                if (lane < cnt) {
+                for (int sl = 0; sl < CUT_REC / 16; ++sl) {
+                    if (lane < cnt) {
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        const int x = 16 * sl + k;
-                        stg[lane * 17 + k] = x < CUT_FAST ? fd[x] : (x < CUT_FAST + 21 ? info[x - CUT_FAST] : 0.0);
+                        for (int k = 0; k < 16; ++k) {
+                            const int x = 16 * sl + k;
+                            stg[lane * 17 + k] = x < CUT_FAST ? fd[x] : (x < CUT_FAST + 21 ? info[x - CUT_FAST] : 0.0);
+                        }
                     }
-                }
-                __syncthreads();
-                // (reading four slices ahead of their stores measured the same: profiles/r04_aa)
+                    wave_lds_sync();
+                    // (reading four slices ahead of their stores measured the same: profiles/r04_aa)
 #pragma unroll
-                for (int g8 = 0; g8 < 8; ++g8) {
-                    const int ln = 8 * g8 + pl;
-                    if (ln < cnt)
-                        reinterpret_cast<double2*>(rc + (size_t)ln * CUT_REC + 16 * sl)[pp] =
-                            make_double2(stg[ln * 17 + 2 * pp], stg[ln * 17 + 2 * pp + 1]);
+                    for (int g8 = 0; g8 < 8; ++g8) {
+                        const int ln = 8 * g8 + pl;
+                        if (ln < cnt)
+                            reinterpret_cast<double2*>(rc + (size_t)ln * CUT_REC + 16 * sl)[pp] =
+                                make_double2(stg[ln * 17 + 2 * pp], stg[ln * 17 + 2 * pp + 1]);
+                    }
+                    wave_lds_sync();
                 }
-                __syncthreads();
             }
-        }
-        if (lane < cnt) {
+            if (lane < cnt) {
 #pragma unroll
-            for (int i = 0; i < 21; ++i) chunk[i][lane] = info[i];
+                for (int i = 0; i < 21; ++i) chunk[i][lane] = info[i];
+            }
         }
         __syncthreads();
-        if (lane < 21)
-            for (int k = 0; k < cnt; ++k) s = s + chunk[lane][k];
+        if (wv == 0 && lane < 21) {
+            const double (*all)[21][65] = reinterpret_cast<const double (*)[21][65]>(prep_lds);
+            for (int k = 0; k < W && c0 + k < nl_ch + np_ch; ++k) {
+                const int cnt = chunk_cnt(c0 + k);
+                for (int e = 0; e < cnt; ++e) s = s + all[k][lane][e];
+            }
+        }
         __syncthreads();
     }
-    if (lane < 21) p.scr.cut_sum[24 * b + lane] = s;
+    if (wv == 0 && lane < 21) p.scr.cut_sum[24 * b + lane] = s;
 }
+constexpr size_t cut_prep_lds(int w) { return (size_t)w * 21 * 65 * sizeof(double); }
 
 // ---------------------------------------------------------------- bounds --
 // Per matched line, the error bounds of the margined comparisons' operands,
@@ -882,7 +903,6 @@ __device__ __forceinline__ int group_first_max(double v, int valid, int j, doubl
 // phase boundary only has to keep the compiler from moving LDS accesses across
 // it and drain the wave's LDS queue — unlike __syncthreads it does not wait for
 // the in-flight global prefetch loads.
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ---- exact step (X), out of line: rare, and its two 6x6 LLTs, reference-order endpoints
 // and the exact-sum flush would otherwise set the register budget of the search loop.
@@ -1761,22 +1781,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             dj_valid = valid;
             dj = cut_dval<false>(cr, t0, t1, tq, bok);
         }
-        if (inc0 | inc1) {   // (wave-uniform) the alt values: lanes 0-7 (h0, g1[c]), 8-15 (g0[a], h1), 16 (h0, h1)
-            double h0 = g0[0], h1 = g1[0];
-#pragma unroll
-            for (int k = 2; k <= 6; ++k) { h0 = k == k0 ? g0[k] + (-st) : h0; h1 = k == k1 ? g1[k] + (-st) : h1; }
-            double u0 = h0, u1 = h1;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) { u1 = lane == k ? g1[k] : u1; u0 = lane == 8 + k ? g0[k] : u0; }
-            int valid = (lane < 8 && k0 >= 0) || (lane >= 8 && lane < 16 && k1 >= 0) || (lane == 16 && k0 >= 0 && k1 >= 0);
+        if (inc0 | inc1) {   // (wave-uniform) the alt values (h0, g1[c]) -> slot 82 + c, (g0[a], h1) -> 90 + a,
+                             // (h0, h1) -> 98, each on a lane that already holds its grid ratio: row items on
+                             // lanes 0-7 (a = 0: t1 = g1[c]), column items a >= 1 on lanes 8a + 7 (t0 = g0[a]),
+                             // column item 0 on lane 8, the corner on lane 16
+            const int a = lane >> 3, c = lane & 7;
+            const int k0s = __builtin_amdgcn_readfirstlane(k0), k1s = __builtin_amdgcn_readfirstlane(k1);
+            // h = g[k] - s at the served index (t0 of lane 8k is g0[k], t1 of lane k is g1[k])
+            const double h0 = readlane_f64(t0, k0s > 0 ? 8 * k0s : 0) + (-st);
+            const double h1 = readlane_f64(t1, k1s > 0 ? k1s : 0) + (-st);
+            const bool row = lane < 8, col = lane == 8 || (c == 7 && a >= 1), cor = lane == 16;
+            const double u0 = (row || cor) ? h0 : (lane == 8 ? g0[0] : t0);
+            const double u1 = row ? t1 : h1;
+            int valid = (row && k0s >= 0) || (col && k1s >= 0) || (cor && k0s >= 0 && k1s >= 0);
             if (u0 + u1 > 1.0) valid = 0;
             if (u0 < rlo || u0 > rhi) valid = 0;
             if (u1 < rlo || u1 > rhi) valid = 0;
             int abok = 0;
             const double da = cut_dval<false>(cr, u0, u1, tq, abok);
-            if (lane < 17) {
-                dgx[82 + lane] = (valid && da == da) ? da : -__builtin_inf();
-                dgf[82 + lane] = abok | (valid << 1) | ((valid && !(da == da)) ? 4 : 0);
+            if (row | col | cor) {
+                const int slot = row ? 82 + lane : (cor ? 98 : 90 + (lane == 8 ? 0 : a));
+                dgx[slot] = (valid && da == da) ? da : -__builtin_inf();
+                dgf[slot] = abok | (valid << 1) | ((valid && !(da == da)) ? 4 : 0);
             }
         }
         CUTW_CK(ck_eval);
@@ -2903,10 +2929,24 @@ static int cut_wave_max_b() {
     return e ? atoi(e) : CUT_WAVE_MAX_B;
 }
 
+// the batch size up to which k_cut_prep runs 8 waves per sequence (GFPL_CUT_PREP_W8_MAX_B overrides)
+static int cut_prep_w8_max_b() {
+    const char* e = getenv("GFPL_CUT_PREP_W8_MAX_B");
+    return e ? atoi(e) : 256;
+}
+
 hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* marks) {
     const int mode = p.cfg.cut_proof;   // 0 measured, 1 proven (recorded search + verify), 2 eager-proven, 3 (test)
     const dim3 gsearch((p.B + CUT_G - 1) / CUT_G);
-    hipLaunchKernelGGL(k_cut_prep, dim3(p.B), dim3(64), 0, s, p);
+    if (p.B <= cut_prep_w8_max_b()) {   // small batches: 8 waves per sequence
+        static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(k_cut_prep<8>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)cut_prep_lds(8)) == hipSuccess;
+        if (!lds_ok) return hipErrorInvalidConfiguration;
+        hipLaunchKernelGGL(k_cut_prep<8>, dim3(p.B), dim3(512), cut_prep_lds(8), s, p);
+    } else {
+        hipLaunchKernelGGL(k_cut_prep<1>, dim3(p.B), dim3(64), cut_prep_lds(1), s, p);
+    }
     if (mode == 2) {   // the per-line operand error bounds the eager agreement bound starts from
         hipLaunchKernelGGL(k_cut_bounds, dim3((p.mls_cap + 63) / 64, p.B), dim3(64), 0, s, p);
         hipLaunchKernelGGL(k_cut_vtab, dim3(p.B), dim3(256), 0, s, p);

@@ -522,16 +522,49 @@ __device__ double stdv_mad(double* buf, int n, int NP2) {
 // (floats) the bit patterns order like the values, so this is the element
 // std::sort(...)[k] leaves at k (vector_stdv_mad, src/auxiliar.cpp:521-537); residuals
 // sqrt(.) * sqrt(sigma2) and fabsf(.) are never -0.0.
+template <typename K>
+__device__ __forceinline__ K readlane_key(K v, int l) {
+    if (sizeof(K) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+        return (K)(((uint64_t)hi << 32) | lo);
+    }
+    return (K)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
 template <typename K, int R>
 __device__ __forceinline__ K wave_select(const K* key, int n, int k) {
+    // two bits per pass: the three thresholds' counts are independent (one pass's compares and
+    // popcounts overlap), and the largest threshold with count <= k is the bit-by-bit choice of
+    // both bits (the counts are monotone in the threshold).  lo / hi count the keys below the
+    // window [P, P + 2^(b+2)) the choices so far leave (lo <= k < hi); once it holds one key, that
+    // key is the k-th (the remaining bits are its own) and is read out.  (Keys are non-negative
+    // doubles / floats: P + 2^b stays below the sign bit; padding keys ~0 never count.)
     K P = 0;
-    for (int b = 8 * (int)sizeof(K) - 1; b >= 0; --b) {
-        const K T = P | ((K)1 << b);
-        int c = 0;
+    int lo = 0, hi = n;
+    for (int b = 8 * (int)sizeof(K) - 2; b >= 0; b -= 2) {
+        const K T1 = P | ((K)1 << b), T2 = P | ((K)2 << b), T3 = P | ((K)3 << b);
+        int c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r * 64 < n) c += __popcll(__ballot(key[r] < T));
-        if (c <= k) P = T;
+            if (r * 64 < n) {
+                c1 += __popcll(__ballot(key[r] < T1));
+                c2 += __popcll(__ballot(key[r] < T2));
+                c3 += __popcll(__ballot(key[r] < T3));
+            }
+        if (c3 <= k) { P = T3; lo = c3; }
+        else if (c2 <= k) { P = T2; lo = c2; hi = c3; }
+        else if (c1 <= k) { P = T1; lo = c1; hi = c2; }
+        else { hi = c1; }
+        if (hi - lo == 1 && b > 0) {   // (wave-uniform) the window's one key
+            const K wd = (K)1 << b;
+            K v = 0;
+            bool in = false;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r * 64 < n && (K)(key[r] - P) < wd) { v = key[r]; in = true; }
+            return readlane_key<K>(v, __builtin_ctzll(__ballot(in)));
+        }
     }
     return P;
 }
@@ -541,7 +574,7 @@ __device__ __forceinline__ K wave_select(const K* key, int n, int k) {
 template <int R>
 __device__ __forceinline__ double stdv_mad_regs(const double* r, int n) {
     if (n == 0) return 0.0;   // uniform
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     uint64_t k64[R];
 #pragma unroll
     for (int s = 0; s < R; ++s)
@@ -560,6 +593,50 @@ __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// removeOutliers(DT_) (:2058-2116): the residual of list entry k (inputs gathered SoA in pose_in)
+__device__ __forceinline__ double point_residual(const KParams& p, const double* pin, const double* DTs, int k) {
+    const double* in = pin + k;
+    const double Pp[3] = {in[0], in[p.mpt_cap], in[2 * p.mpt_cap]};
+    double Pc[3], uv[2];
+    se3_apply(DTs, Pp, Pc);
+    projection(p.cam, Pc, uv);
+    const double ex = uv[0] - in[3 * p.mpt_cap], ey = uv[1] - in[4 * p.mpt_cap];
+    return sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
+}
+__device__ __forceinline__ double line_residual(const KParams& p, const double* lin, const double* DTs, int k) {
+    const double* in = lin + k;
+    const size_t st = p.mls_cap;
+    const double sP[3] = {in[0], in[st], in[2 * st]};
+    const double eP[3] = {in[3 * st], in[4 * st], in[5 * st]};
+    double sc[3], ec[3], su[2], eu[2];
+    se3_apply(DTs, sP, sc);
+    se3_apply(DTs, eP, ec);
+    projection(p.cam, sc, su);
+    projection(p.cam, ec, eu);
+    const double l0 = in[6 * st], l1 = in[7 * st], l2 = in[8 * st];
+    const double e0 = (l0 * su[0] + l1 * su[1]) + l2;
+    const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
+    return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
+}
+
+// the line list's outlier flags from register-held residuals (n <= 64 POSE_MAD_R): returns the
+// wave's flagged count
+__device__ __forceinline__ int line_outliers_regs(const KParams& p, const double* lin, const double* DTs,
+                                                  uint8_t* act, int npt, int nls, size_t lb, const int32_t* mls) {
+    const int lane = threadIdx.x & 63;
+    double r[POSE_MAD_R];
+#pragma unroll
+    for (int s = 0; s < POSE_MAD_R; ++s) r[s] = (lane + 64 * s < nls) ? line_residual(p, lin, DTs, lane + 64 * s) : 0.0;
+    const double th_l = p.cfg.inlier_k * stdv_mad_regs<POSE_MAD_R>(r, nls);
+    int ol = 0;
+#pragma unroll
+    for (int s = 0; s < POSE_MAD_R; ++s) {
+        const int k = lane + 64 * s;
+        if (k < nls && r[s] > th_l) { p.prev.ls.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+    }
+    return wave_sum(ol);
 }
 
 // dynamic LDS: {cp[8*CH_STRIDE] cl[8*CH_STRIDE] | buf[NP2]} f64 | act[mpt+mls] u8 (16-B padded):
@@ -645,30 +722,8 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
         for (int i = 0; i < 16; ++i) { double d = DTs[i] - DTs[i]; if (!(d == d)) fin = false; }
         if (fin) {
             // removeOutliers(DT_) (:2058-2116): residuals of every list entry
-            auto res_p = [&](int k) {
-                const double* in = pin + k;
-                const double Pp[3] = {in[0], in[p.mpt_cap], in[2 * p.mpt_cap]};
-                double Pc[3], uv[2];
-                se3_apply(DTs, Pp, Pc);
-                projection(p.cam, Pc, uv);
-                const double ex = uv[0] - in[3 * p.mpt_cap], ey = uv[1] - in[4 * p.mpt_cap];
-                return sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
-            };
-            auto res_l = [&](int k) {
-                const double* in = lin + k;
-                const size_t st = p.mls_cap;
-                const double sP[3] = {in[0], in[st], in[2 * st]};
-                const double eP[3] = {in[3 * st], in[4 * st], in[5 * st]};
-                double sc[3], ec[3], su[2], eu[2];
-                se3_apply(DTs, sP, sc);
-                se3_apply(DTs, eP, ec);
-                projection(p.cam, sc, su);
-                projection(p.cam, ec, eu);
-                const double l0 = in[6 * st], l1 = in[7 * st], l2 = in[8 * st];
-                const double e0 = (l0 * su[0] + l1 * su[1]) + l2;
-                const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
-                return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
-            };
+            auto res_p = [&](int k) { return point_residual(p, pin, DTs, k); };
+            auto res_l = [&](int k) { return line_residual(p, lin, DTs, k); };
             // Lists of up to 512 entries keep their residuals in registers and take both
             // medians by wave_select (no sort); longer lists sort in the GN chunk region (buf
             // aliases it) and the flag pass re-evaluates each residual (same operands, same
@@ -676,6 +731,8 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
             // residual: flagging per list position equals the reference's per-feature flag.
             int op = 0, ol = 0;
             pose_bar<W>();
+            // (the line list's pass on a helper wave beside the points' here measured slower: the
+            // helper's registers slowed wave 0's chunk reduction by more than the overlap saved)
             if (npt <= 64 * POSE_MAD_R) {
                 double r[POSE_MAD_R];
 #pragma unroll
@@ -695,24 +752,16 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
             }
             pose_bar<W>();
             if (nls <= 64 * POSE_MAD_R) {
-                double r[POSE_MAD_R];
-#pragma unroll
-                for (int s = 0; s < POSE_MAD_R; ++s) r[s] = (lane + 64 * s < nls) ? res_l(lane + 64 * s) : 0.0;
-                const double th_l = p.cfg.inlier_k * stdv_mad_regs<POSE_MAD_R>(r, nls);
-#pragma unroll
-                for (int s = 0; s < POSE_MAD_R; ++s) {
-                    const int k = lane + 64 * s;
-                    if (k < nls && r[s] > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
-                }
+                ol = line_outliers_regs(p, lin, DTs, act, npt, nls, lb, mls);
             } else {
                 for (int k = lane; k < nls; k += 64) buf[k] = res_l(k);
                 pose_bar<W>();
                 const double th_l = p.cfg.inlier_k * stdv_mad<W>(buf, nls, NP2);
                 for (int k = lane; k < nls; k += 64)
                     if (res_l(k) > th_l) { L.inlier[lb + mls[k]] = 0; act[npt + k] = 0; ++ol; }
+                ol = wave_sum(ol);
             }
             op = wave_sum(op);
-            ol = wave_sum(ol);
             // active counts for stage 2
             int ap = 0, al = 0;
             pose_bar<W>();
