@@ -1,63 +1,99 @@
-"""Model of k_pose's wave_select (gf-pl-slam_amd/csrc/k_pose.hip): the k-th smallest of n <= 512
-non-negative keys by two bits per pass with the early read-out once the selection window holds a
-single key.  The kernel's results are checked bit for bit against the oracle by the -m gpu outlier
-tests; this CPU test pins the algorithm itself on adversarial key sets (duplicates, runs of equal
-high bits, a single key, all keys equal), the cases where the window logic could go wrong."""
+"""Host model of k_pose's MAD medians (gf-pl-slam_amd/csrc/k_pose.hip, wave_select /
+stdv_mad_regs): the k-th smallest key is built from the top, two bits per pass, as the largest P
+with #{x < P} <= k (read out early once one key is left in the window), over the unsigned bit patterns of non-negative doubles (then of floats).  This
+restates the kernel's loop in numpy and checks it against the sort the reference takes the
+element from (vector_stdv_mad, src/auxiliar.cpp:521-537: std::sort, then [n / 2]) on ties,
+zeros, subnormals, huge values and +inf.  The GPU path itself is compared with the oracle by
+the -m gpu pose tests (tests/test_gpu_parity.py)."""
 import numpy as np
-import pytest
 
 
-def wave_select_model(keys, k, bits):
-    """Python restatement of wave_select<K, R>: keys are the valid keys only (the kernel's padding
-    keys ~0 never count)."""
-    keys = [int(x) for x in keys]
-    n = len(keys)
+def wave_select(keys, k, bits):
+    """The kernel's selection over unsigned keys (all-ones padding never counts): two bits per
+    pass — the largest of the three thresholds P | j 2^b with #{x < T} <= k, the same choice as
+    two single-bit steps since the counts are monotone in T — and the early read-out once the
+    window [P, P + 2^b) between the counts lo <= k < hi holds a single key."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    valid = keys[keys != np.uint64(~np.uint64(0))] if bits == 64 else keys[keys != np.uint64(0xFFFFFFFF)]
+    n = len(valid)
     P, lo, hi = 0, 0, n
     for b in range(bits - 2, -1, -2):
-        T1, T2, T3 = P | (1 << b), P | (2 << b), P | (3 << b)
-        c1 = sum(x < T1 for x in keys)
-        c2 = sum(x < T2 for x in keys)
-        c3 = sum(x < T3 for x in keys)
-        if c3 <= k:
-            P, lo = T3, c3
-        elif c2 <= k:
-            P, lo, hi = T2, c2, c3
-        elif c1 <= k:
-            P, lo, hi = T1, c1, c2
+        c = [int(np.count_nonzero(valid < np.uint64(P | (j << b)))) for j in (1, 2, 3)]
+        if c[2] <= k:
+            P, lo = P | (3 << b), c[2]
+        elif c[1] <= k:
+            P, lo, hi = P | (2 << b), c[1], c[2]
+        elif c[0] <= k:
+            P, lo, hi = P | (1 << b), c[0], c[1]
         else:
-            hi = c1
+            hi = c[0]
         assert lo <= k < hi
         if hi - lo == 1 and b > 0:
-            wd = 1 << b
-            inside = [x for x in keys if 0 <= x - P < wd]
+            inside = valid[(valid >= np.uint64(P)) & (valid - np.uint64(P) < np.uint64(1 << b))]
             assert len(inside) == 1
-            return inside[0]
+            return int(inside[0])
     return P
 
 
-def _f64_keys(v):
-    return np.asarray(v, dtype=np.float64).view(np.uint64)
+def stdv_mad_model(r):
+    n = len(r)
+    if n == 0:
+        return 0.0
+    k64 = r.astype(np.float64).view(np.uint64)
+    median = np.uint64(wave_select(k64, n // 2, 64)).view(np.float64)
+    dev = np.abs((r - median).astype(np.float32))            # (double)fabsf((float)(x - median))
+    k32 = dev.view(np.uint32).astype(np.uint64)
+    mad = np.float64(np.uint32(wave_select(k32, n // 2, 32)).view(np.float32))
+    return 1.4826 * mad
 
 
-def _f32_keys(v):
-    return np.asarray(v, dtype=np.float32).view(np.uint32)
+def stdv_mad_reference(r):
+    n = len(r)
+    if n == 0:
+        return 0.0
+    s = np.sort(r.astype(np.float64))
+    median = s[n // 2]
+    dev = np.sort(np.abs((s - median).astype(np.float32)).astype(np.float64))
+    return 1.4826 * dev[n // 2]
 
 
-@pytest.mark.parametrize("seed", range(6))
-def test_wave_select_model_matches_sort(seed):
-    rng = np.random.default_rng(seed)
-    for n in (1, 2, 3, 63, 64, 65, 300, 512):
-        r = np.abs(rng.standard_normal(n)) * 10.0 ** rng.uniform(-3, 2)
-        if seed % 2:   # duplicates and a cluster of equal high bits
-            r[: n // 3] = r[0]
-            r[n // 3: n // 2] = np.nextafter(r[0], np.inf)
-        for keys, bits in ((_f64_keys(r), 64), (_f32_keys(r.astype(np.float32)), 32)):
-            k = n // 2
-            assert wave_select_model(keys, k, bits) == int(np.sort(keys)[k])
+def test_select_equals_sorted_order_statistic():
+    rng = np.random.default_rng(7)
+    for trial in range(300):
+        n = int(rng.integers(1, 513))
+        kind = trial % 5
+        if kind == 0:
+            x = rng.random(n) * 10.0
+        elif kind == 1:                                   # heavy ties
+            x = rng.integers(0, 4, n).astype(np.float64) * 0.25
+        elif kind == 2:                                   # zeros, subnormals, huge
+            x = rng.choice([0.0, 5e-324, 1e-310, 1.0, 1e300, np.inf], n)
+        elif kind == 3:                                   # residual-like: sqrt(.) * sqrt(sigma2)
+            x = np.sqrt(rng.random(n) * 4.0) * np.sqrt(1.44 ** rng.integers(0, 4, n))
+        else:
+            x = np.exp(rng.normal(0.0, 20.0, n))
+        for k in (0, n // 2, n - 1):
+            got = np.uint64(wave_select(x.view(np.uint64), k, 64)).view(np.float64)
+            assert got == np.sort(x)[k]
 
 
-def test_wave_select_model_edge_sets():
-    for vals in ([0.0], [0.0, 0.0], [5.0] * 7, [0.0, 1e-300, 1e300], [1.0, 2.0]):
-        keys = _f64_keys(vals)
+def test_mad_model_equals_reference_mad():
+    rng = np.random.default_rng(11)
+    for trial in range(200):
+        n = int(rng.integers(1, 513))
+        x = np.sqrt(rng.random(n) * rng.choice([1e-6, 1.0, 1e4])) * 1.2
+        if trial % 3 == 0:
+            x[rng.integers(0, n, n // 3)] = x[0]          # duplicates of one residual
+        assert stdv_mad_model(x) == stdv_mad_reference(x)
+
+
+def test_mad_model_empty_is_zero():
+    assert stdv_mad_model(np.zeros(0)) == 0.0
+
+
+def test_select_edge_sets():
+    for vals in ([0.0], [0.0, 0.0], [5.0] * 7, [0.0, 1e-300, 1e300], [1.0, 2.0], [np.inf, 1.0, np.inf]):
+        x = np.asarray(vals, dtype=np.float64)
         for k in range(len(vals)):
-            assert wave_select_model(keys, k, 64) == int(np.sort(keys)[k])
+            got = np.uint64(wave_select(x.view(np.uint64), k, 64)).view(np.float64)
+            assert got == np.sort(x)[k]
