@@ -686,7 +686,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         int* wcnt = cnt + 128;                    // [NW][128] this round's per-wave counts
         for (int x = tid; x < 128 * (NW + 1); x += BLOCK) cnt[x] = 0;
         __syncthreads();
-        for (int i = tid; i < KP2; i += BLOCK) {
+        for (int i = tid; i < N; i += BLOCK) {   // (keys live at iL < N; the rest stay ~0)
             const uint32_t k = pairs[i];
             if (k != 0xFFFFFFFFu) atomicAdd(&cnt[k >> 16], 1);
         }
@@ -708,9 +708,9 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
         const int wave = tid >> 6, lane = tid & 63;
         const unsigned long long lt = (1ull << lane) - 1ull;
         keys = order;
-        for (int r0 = 0; r0 < KP2; r0 += BLOCK) {   // block-uniform
+        for (int r0 = 0; r0 < N; r0 += BLOCK) {   // block-uniform
             const int i = r0 + tid;
-            const uint32_t k = i < KP2 ? pairs[i] : 0xFFFFFFFFu;
+            const uint32_t k = i < N ? pairs[i] : 0xFFFFFFFFu;
             const bool v = k != 0xFFFFFFFFu;
             const int d = (int)(k >> 16) & 127;
             unsigned long long peers = __ballot(v);
