@@ -2,7 +2,23 @@
 #pragma once
 #include "gfpl_state.hpp"
 
+#include <atomic>
+
 namespace gfpl {
+
+// A kernel's dynamic-LDS ceiling above the 64 KB default, set once per device (the attribute
+// belongs to the device's kernel object; contexts on several devices may share the process).
+// *done: one bit per device id < 64 (idempotent: two threads setting it race harmlessly)
+inline hipError_t ensure_dyn_lds(const void* fn, int bytes, std::atomic<unsigned long long>* done) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
+    if (bit && (done->load(std::memory_order_acquire) & bit)) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit) done->fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 // the batch size up to which the stereo and cross stages run 16 waves per sequence (k_stereo.hip)
 int sp_wide_max_b();

@@ -2939,10 +2939,9 @@ hipError_t launch_line_cut(const KParams& p, hipStream_t s, const hipEvent_t* ma
     const int mode = p.cfg.cut_proof;   // 0 measured, 1 proven (recorded search + verify), 2 eager-proven, 3 (test)
     const dim3 gsearch((p.B + CUT_G - 1) / CUT_G);
     if (p.B <= cut_prep_w8_max_b()) {   // small batches: 8 waves per sequence
-        static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(k_cut_prep<8>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)cut_prep_lds(8)) == hipSuccess;
-        if (!lds_ok) return hipErrorInvalidConfiguration;
+        static std::atomic<unsigned long long> attr{0};
+        const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(k_cut_prep<8>), (int)cut_prep_lds(8), &attr);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_cut_prep<8>, dim3(p.B), dim3(512), cut_prep_lds(8), s, p);
     } else {
         hipLaunchKernelGGL(k_cut_prep<1>, dim3(p.B), dim3(64), cut_prep_lds(1), s, p);

@@ -997,13 +997,9 @@ hipError_t launch_pose(const KParams& p, hipStream_t s, hipEvent_t mark) {
     const size_t region = (size_t)std::max(Wl * 16 * CH_STRIDE, NP2);
     const size_t lds = region * 8 + ((p.mpt_cap + p.mls_cap + 15) & ~15) + 16;
     if (w8) {
-        static bool attr = false;   // (dynamic LDS above the 64 KB default)
-        if (!attr) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_pose<8>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        static std::atomic<unsigned long long> attr{0};   // (dynamic LDS above the 64 KB default)
+        const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(k_pose<8>), 160 * 1024 - 1024, &attr);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_pose<8>, dim3(p.B), dim3(64 * 8), lds, s, p, NP2);
     } else if (multi)
         hipLaunchKernelGGL(k_pose<POSE_W>, dim3(p.B), dim3(64 * POSE_W), lds, s, p, NP2);
