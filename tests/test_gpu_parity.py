@@ -230,8 +230,15 @@ def test_knn2_hamming_parity():
     assert ctx.knn2(qd, 700, td, 1, 1, idx, dist) == -4
 
 
-def test_ragged_inputs_parity():
-    # empty / one-line / tiny detection sets (ledger U4, U5 guards)
+@pytest.mark.parametrize("layout", ["small_batch", "bench_batch"])
+def test_ragged_inputs_parity(layout, monkeypatch):
+    # empty / one-line / tiny detection sets (ledger U4, U5 guards), through the small-batch kernels
+    # (B = 5: 8-wave k_cut_prep / k_pose, the wave search, 16-wave stereo) and through the ones the
+    # bench batch runs (every small-batch threshold forced to 0)
+    if layout == "bench_batch":
+        for v in ("GFPL_CUT_WAVE_MAX_B", "GFPL_CUT_PREP_W8_MAX_B", "GFPL_POSE_MULTI_MAX_B", "GFPL_POSE_W8_MAX_B",
+                  "GFPL_SP_WIDE_MAX_B"):
+            monkeypatch.setenv(v, "0")
     rep = _run_sequence("vga", {}, n_seq=5, n_frames=3, kp_cap=1024, kl_cap=256,
                         synth_over=dict(n_kp=600, n_kl=150, n_world_pts=800, n_world_lines=200), seed=13,
                         mutate=make_ragged)
