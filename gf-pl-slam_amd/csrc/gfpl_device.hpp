@@ -680,13 +680,20 @@ GFPL_DEV void eig_sym(const double* A, double* w) {
                 if (apq != 0.0) {
                     const double app = a[p * N + p], aqq = a[q * N + q];
                     const double theta = (aqq - app) / (2.0 * apq);
+                    // the oracle's expressions, with two shortcuts that give their bits (the late
+                    // sweeps' rotations are almost all in them): for 2^27 <= |theta| <= 1e150,
+                    // theta^2 + 1 rounds to theta^2, whose correctly rounded sqrt is |theta|, so
+                    // 1 / (|theta| + sqrt(.)) is 1 / (2 |theta|) = 0.5 / |theta|; and t^2 + 1 == 1
+                    // makes c = 1 / sqrt(1) = 1, s = t (tests/test_oracle_known_answers.py checks both)
                     double t;
-                    if (fabs(theta) > 1e150) t = 0.5 / theta;
+                    const double ath = fabs(theta);
+                    if (ath > 1e150) t = 0.5 / theta;
                     else {
-                        t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                        t = ath >= 0x1p27 ? 0.5 / ath : 1.0 / (ath + sqrt(theta * theta + 1.0));
                         if (theta < 0.0) t = -t;
                     }
-                    const double c = 1.0 / sqrt(t * t + 1.0);
+                    const double tt1 = t * t + 1.0;
+                    const double c = tt1 == 1.0 ? 1.0 : 1.0 / sqrt(tt1);
                     const double s = t * c;
 #pragma unroll
                     for (int k = 0; k < N; ++k) {

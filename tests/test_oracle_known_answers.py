@@ -150,6 +150,20 @@ def test_inverses_match_numpy():
         assert np.allclose(O.inverse4(B), np.linalg.inv(B), rtol=1e-9, atol=1e-9)
 
 
+def test_jacobi_rotation_shortcuts_are_bit_identical():
+    """eig_sym's device rotation (gfpl_device.hpp) skips two sqrt / div chains where they cannot
+    change a bit of the oracle's (oracle/gfpl_oracle.cpp eig_sym): 1 / (|th| + sqrt(th^2 + 1)) is
+    0.5 / |th| for 2^27 <= |th| <= 1e150, and t^2 + 1 == 1 gives c = 1."""
+    rng = np.random.default_rng(27)
+    e = rng.uniform(27, 498, 2_000_000)
+    th = np.exp2(e) * rng.uniform(1, 2, e.size)
+    th = np.concatenate([th[th <= 1e150], 2.0 ** 27 + np.arange(4096) * 2.0 ** -25, [1e150]])
+    assert np.array_equal(1.0 / (th + np.sqrt(th * th + 1.0)), 0.5 / th)
+    t = np.concatenate([np.exp2(rng.uniform(-600, -20, 1_000_000)), [2.0 ** -27, 2.0 ** -26]])
+    tt1 = t * t + 1.0
+    assert np.all((1.0 / np.sqrt(tt1))[tt1 == 1.0] == 1.0)
+
+
 def test_eig_sym_matches_numpy():
     rng = np.random.default_rng(8)
     for n in (3, 6):
