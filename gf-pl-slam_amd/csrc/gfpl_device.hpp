@@ -672,6 +672,22 @@ GFPL_DEV void eig_sym(const double* A, double* w) {
 #pragma unroll
             for (int q = p + 1; q < N; ++q) off = off + a[p * N + q] * a[p * N + q];
         if (!(off > 0.0)) break;
+        {   // (early exit with the oracle's bits) once the off-diagonal mass is below an eighth of the
+            // smallest gap under a diagonal entry, no later rotation moves a diagonal entry: each moves
+            // app, aqq by t apq with |t| <= 1, the rotations keep the off-diagonal Frobenius norm (up to
+            // rounding far inside the factor 8), and app -+ (less than half that gap) rounds to app.
+            // Finite diagonals only (the oracle's NaN / Inf rotations spread).
+            double thr = __builtin_inf();
+            bool fin = true;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int e = (int)((__double_as_longlong(a[i * N + i]) >> 52) & 0x7FF);
+                fin = fin && e != 0x7FF;
+                // (2^(e - 1076) / 8)^2: 2^(e - 1076) is the gap below |a_ii| (0 for zero / subnormal)
+                thr = fmin(thr, e == 0 ? 0.0 : ldexp(1.0, 2 * (e - 1076) - 6));
+            }
+            if (fin && off < thr) break;
+        }
 #pragma unroll
         for (int p = 0; p < N - 1; ++p)
 #pragma unroll

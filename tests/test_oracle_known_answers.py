@@ -164,6 +164,83 @@ def test_jacobi_rotation_shortcuts_are_bit_identical():
     assert np.all((1.0 / np.sqrt(tt1))[tt1 == 1.0] == 1.0)
 
 
+def _jacobi(A, fast):
+    """oracle/gfpl_oracle.cpp eig_sym (fast=False) and the device's eig_sym (gfpl_device.hpp: the
+    rotation shortcuts and the early exit), in Python doubles (IEEE, correctly rounded sqrt)."""
+    import math
+    n = A.shape[0]
+    a = [float(x) for x in A.ravel()]
+    for _ in range(50):
+        off = 0.0
+        for p in range(n):
+            for q in range(p + 1, n):
+                off = off + a[p * n + q] * a[p * n + q]
+        if not off > 0.0:
+            break
+        if fast:
+            thr, fin = math.inf, True
+            for i in range(n):
+                e = (np.float64(a[i * n + i]).view(np.uint64) >> np.uint64(52)) & np.uint64(0x7FF)
+                e = int(e)
+                fin = fin and e != 0x7FF
+                thr = min(thr, 0.0 if e == 0 else math.ldexp(1.0, 2 * (e - 1076) - 6))
+            if fin and off < thr:
+                break
+        for p in range(n - 1):
+            for q in range(p + 1, n):
+                apq = a[p * n + q]
+                if apq == 0.0:
+                    continue
+                app, aqq = a[p * n + p], a[q * n + q]
+                th = (aqq - app) / (2.0 * apq)
+                if abs(th) > 1e150:
+                    t = 0.5 / th
+                elif fast and abs(th) >= 2.0 ** 27:
+                    t = 0.5 / abs(th)
+                    t = -t if th < 0.0 else t
+                else:
+                    t = 1.0 / (abs(th) + math.sqrt(th * th + 1.0))
+                    t = -t if th < 0.0 else t
+                tt1 = t * t + 1.0
+                c = 1.0 if (fast and tt1 == 1.0) else 1.0 / math.sqrt(tt1)
+                s_ = t * c
+                for k in range(n):
+                    if k in (p, q):
+                        continue
+                    akp, akq = a[k * n + p], a[k * n + q]
+                    nkp, nkq = c * akp - s_ * akq, s_ * akp + c * akq
+                    a[k * n + p] = a[p * n + k] = nkp
+                    a[k * n + q] = a[q * n + k] = nkq
+                a[p * n + p] = app - t * apq
+                a[q * n + q] = aqq + t * apq
+                a[p * n + q] = a[q * n + p] = 0.0
+    return sorted(a[i * n + i] for i in range(n))
+
+
+def test_jacobi_early_exit_keeps_the_oracles_bits():
+    """The device eig_sym stops once no later rotation can move a diagonal entry; its eigenvalues
+    equal the oracle's full sweep bit for bit (random, near-degenerate, diagonal, widely scaled)."""
+    rng = np.random.default_rng(45)
+    for trial in range(600):
+        n = 3 if trial % 2 else 6
+        kind = trial % 6
+        A = rng.normal(size=(n, n))
+        A = A @ A.T if kind < 2 else A + A.T
+        if kind == 2:   # near-degenerate: a repeated eigenvalue plus a tiny perturbation
+            Q = np.linalg.qr(rng.normal(size=(n, n)))[0]
+            A = Q @ np.diag([1.0] * (n - 1) + [2.0]) @ Q.T + 1e-13 * (lambda M: M + M.T)(rng.normal(size=(n, n)))
+        if kind == 3:
+            A = np.diag(rng.normal(size=n)) + np.triu(1e-170 * rng.normal(size=(n, n)), 1)
+            A = np.triu(A) + np.triu(A, 1).T
+        if kind == 4:
+            A = A * 10.0 ** rng.uniform(-150, 150)
+        if kind == 5:
+            A[0, :] = 0.0
+            A[:, 0] = 0.0
+        got, ref = _jacobi(A, True), _jacobi(A, False)
+        assert [np.float64(x).view(np.uint64) for x in got] == [np.float64(x).view(np.uint64) for x in ref], (trial, got, ref)
+
+
 def test_eig_sym_matches_numpy():
     rng = np.random.default_rng(8)
     for n in (3, 6):
