@@ -815,6 +815,33 @@ struct LineOut {
     int level;
 };
 
+// The line gate's test "largest eigenvalue < th" (src/stereoFrame.cpp:743-751, 992-1000) settled
+// without the eigenvalues when bounds decide it the way eig_sym's values would: 1 = the largest value
+// eig_sym returns is < th, 0 = it is >= th, -1 = open (non-finite entries, or th inside the bounds).
+//  * >= th: a Jacobi rotation turns the (p, q) diagonal pair into app - t apq, aqq + t apq with
+//    t apq of the sign of aqq - app, so the larger entry only grows (rounding is monotone): the
+//    largest returned value is >= max_i c_ii.
+//  * < th: every returned value is a diagonal entry of an orthogonal similarity of C up to the
+//    rotations' rounding (<= 150 rotations, ~1e-13 M), hence <= Gershgorin's max_i (c_ii +
+//    sum_j |c_ij|) + 4e-9 M, M = max |c_ij|.
+__device__ __forceinline__ int eig_gate_bound(const double* C, double th) {
+    double M = 0.0, G = -__builtin_inf(), D = -__builtin_inf();
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { fin = fin && (C[i] - C[i] == 0.0); M = fmax(M, fabs(C[i])); }
+    if (!fin) return -1;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double d = C[4 * i];
+        const double r = (d + fabs(C[3 * i + (i + 1) % 3])) + fabs(C[3 * i + (i + 2) % 3]);
+        G = fmax(G, r);
+        D = fmax(D, d);
+    }
+    if (D >= th) return 0;
+    if (G + 4e-9 * M < th) return 1;
+    return -1;
+}
+
 // Line triangulation: initial (src/stereoFrame.cpp:301-330) / per-frame (:684-760)
 __device__ bool triangulate(const KParams& p, const gfpl_keyline& a, const gfpl_keyline& c, bool initial,
                             LineOut* L) {
@@ -837,13 +864,21 @@ __device__ bool triangulate(const KParams& p, const gfpl_keyline& a, const gfpl_
           overlap > p.cfg.stereo_overlap_th))
         return false;
     if (!initial) {
-        double cS[9], cE[9], wS[3], wE[3];
+        double cS[9], cE[9];
         endpointCov(cam, sp_l[0], sp_l[1], disp_s, cS);
         endpointCov(cam, ep_l[0], ep_l[1], disp_e, cE);
-        eig_sym<3>(cS, wS);
-        eig_sym<3>(cE, wE);
-        double max_eig = std_max(wS[2], wE[2]);
-        if (!(max_eig < p.cfg.line_cov_th)) return false;
+        // the gate max(largest eigenvalue) < th, from bounds where they settle it (eig_gate_bound),
+        // else from eig_sym's values as the oracle takes them
+        const double th = p.cfg.line_cov_th;
+        const int gS = eig_gate_bound(cS, th), gE = eig_gate_bound(cE, th);
+        if (gS == 0 || gE == 0) return false;
+        if (!(gS == 1 && gE == 1)) {
+            double wS[3], wE[3];
+            eig_sym<3>(cS, wS);
+            eig_sym<3>(cE, wE);
+            double max_eig = std_max(wS[2], wE[2]);
+            if (!(max_eig < th)) return false;
+        }
     }
     L->spl[0] = sp_l[0]; L->spl[1] = sp_l[1];
     L->epl[0] = ep_l[0]; L->epl[1] = ep_l[1];

@@ -420,3 +420,38 @@ def test_need_new_kf_entropy_and_frame_count(tmp_path):
     # the frame-count gate (numFrameSinceKeyframe > 2) fires no later than the 3rd frame after a KF
     assert any(f for _, f in seen)
     assert all(n <= 3 for n, _ in seen)
+
+
+def _gate_bound(C, th):
+    """k_stereo.hip eig_gate_bound: 1 / 0 when bounds settle "largest eigenvalue < th", else -1."""
+    import math
+    c = [float(x) for x in C.ravel()]
+    if not all(math.isfinite(x) for x in c):
+        return -1
+    M = max(abs(x) for x in c)
+    G = max((c[4 * i] + abs(c[3 * i + (i + 1) % 3])) + abs(c[3 * i + (i + 2) % 3]) for i in range(3))
+    D = max(c[4 * i] for i in range(3))
+    if D >= th:
+        return 0
+    if G + 4e-9 * M < th:
+        return 1
+    return -1
+
+
+def test_line_gate_bounds_agree_with_the_eigenvalues():
+    """The stereo line gate (src/stereoFrame.cpp:743-751) decided from bounds gives eig_sym's
+    decision whenever the bounds settle it: endpoint-covariance-like 3x3 matrices (a dominant
+    viewing-ray direction plus isotropic noise) with th swept across their largest eigenvalue."""
+    rng = np.random.default_rng(9)
+    settled = [0, 0]
+    for trial in range(3000):
+        v = rng.normal(size=3)
+        C = np.outer(v, v) * 10.0 ** rng.uniform(-6, 2) + np.diag(rng.uniform(0, 1e-3, 3))
+        C = (C + C.T) / 2.0
+        lam = _jacobi(C, True)[2]
+        th = lam * (1.0 + rng.choice([-1.0, 1.0]) * 10.0 ** rng.uniform(-14, 0.5))
+        g = _gate_bound(C, th)
+        if g >= 0:
+            settled[g] += 1
+            assert g == (1 if lam < th else 0), (trial, lam, th, g)
+    assert min(settled) > 50   # (both outcomes exercised)
