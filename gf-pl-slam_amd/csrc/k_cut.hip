@@ -2064,7 +2064,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // ---------------------------------------------------------------- finish --
 // invCovPose of the chosen ratio + updateEndPointByRatio (ledger Q4)
 #ifndef GFPL_FIN_WAVES
-#define GFPL_FIN_WAVES 1
+#define GFPL_FIN_WAVES 4   // waves per SIMD: <= 128 VGPRs (0.855 -> 0.842 ms, profiles/r05_bp)
 #endif
 __global__ void __launch_bounds__(64, GFPL_FIN_WAVES) k_cut_finish(KParams p) {
     const int b = blockIdx.x;
