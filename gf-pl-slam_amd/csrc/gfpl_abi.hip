@@ -7,6 +7,7 @@
 #include <cmath>
 #include <mutex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -59,6 +60,8 @@ struct gfpl_seqbatch {
     int32_t* last_n_pt = nullptr;   // [B] list lengths before the last gfpl_update_frame
     int32_t* last_n_ls = nullptr;   // (gfpl_read_last_track)
     PyrBuild* pyrb = nullptr;       // levels 1.. of uploaded level-0 right images (gfpl_upload_frames_l0_async)
+    int last_cut_mode = -1;         // cfg.cut_proof the last line cut ran with (-1: none since the last
+                                    // insert); gfpl_last_step_cut_proof reports on it, not on the current cfg
 };
 
 struct gfpl_event {
@@ -99,6 +102,11 @@ struct Carver {
         return p;
     }
 };
+
+int debug_fill_byte() {
+    const char* e = getenv("GFPL_DEBUG_FILL");
+    return e ? (int)(strtol(e, nullptr, 0) & 0xFF) : 0;
+}
 
 void carve(Carver& c, gfpl_seqbatch* sb) {
     const size_t B = sb->B, P = (size_t)B * sb->kp_cap, L = (size_t)B * sb->kl_cap;
@@ -152,7 +160,7 @@ void carve(Carver& c, gfpl_seqbatch* sb) {
     sb->scr.pose_err = c.take<double>(B);
     sb->scr.pose_ok = c.take<int32_t>(B);
     sb->scr.pose_in = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
-    sb->scr.pose_idx = c.take<uint32_t>(B * (size_t)std::max(sb->mpt_cap, sb->mls_cap));
+    sb->scr.pose_act = c.take<double>(B * (6 * (size_t)sb->mpt_cap + 10 * (size_t)sb->mls_cap));
     sb->scr.pose_dtini = c.take<double>(B * 16);
     sb->scr.cross_tinv = c.take<double>(B * 16);
     sb->scr.dbg = c.take<int64_t>(B * 8);
@@ -451,7 +459,10 @@ int gfpl_seqbatch_create(gfpl_ctx* c, int batch, int kp_cap, int kl_cap, gfpl_se
     carve(dry, sb);
     sb->bytes = (int64_t)dry.off;
     if (hipMalloc(&sb->base, dry.off) != hipSuccess) { delete sb; return GFPL_E_HIP; }
-    if (hipMemsetAsync(sb->base, 0, dry.off, c->stream) != hipSuccess) { (void)hipFree(sb->base); delete sb; return GFPL_E_HIP; }
+    // GFPL_DEBUG_FILL=<byte> (debug): fill the whole allocation — frame slots, track lists, every
+    // scratch field — with that byte instead of zeros (0xFF: NaN doubles, -1 ints), so a read of
+    // memory no step wrote changes results (tests/test_gpu_parity.py::test_poisoned_scratch_*)
+    if (hipMemsetAsync(sb->base, debug_fill_byte(), dry.off, c->stream) != hipSuccess) { (void)hipFree(sb->base); delete sb; return GFPL_E_HIP; }
     Carver real;
     real.base = (char*)sb->base;
     carve(real, sb);
@@ -547,6 +558,7 @@ int gfpl_cross_lines(gfpl_seqbatch* sb) {
 int gfpl_line_cut(gfpl_seqbatch* sb) {
     if (!sb) return GFPL_E_INVALID;
     if (!sb->initialized || !sb->has_curr) return GFPL_E_STATE;
+    sb->last_cut_mode = sb->ctx->cfg.cut_proof;
     HIPCHK(launch_line_cut(params(sb, nullptr), sb->ctx->stream, nullptr));
     return GFPL_OK;
 }
@@ -571,6 +583,7 @@ int gfpl_insert_stereo_pair(gfpl_seqbatch* sb, const gfpl_frames* in) {
     tmark(c, 3);
     HIPCHK(launch_cross_lines(p, c->stream));
     tmark(c, 4);
+    sb->last_cut_mode = c->cfg.use_line_conf_cut ? c->cfg.cut_proof : -1;
     if (c->cfg.use_line_conf_cut)
         HIPCHK(launch_line_cut(p, c->stream, c->timing ? &c->ev[7] : nullptr));
     HIPCHK(launch_step_bytes(p, c->stream));
@@ -674,6 +687,9 @@ int stage_alloc(gfpl_seqbatch* sb, int slot) {
     gfpl_frames f{};
     stage_layout(c, sb, f);   // sizing pass (base == nullptr)
     HIPCHK(hipMalloc(&sb->stage[slot], c.off));
+    // (debug fill: on the copy stream, ahead of the uploads — hipMemset is asynchronous to the host and
+    // the non-blocking copy stream does not wait for the null stream)
+    if (const int fill = debug_fill_byte()) HIPCHK(hipMemsetAsync(sb->stage[slot], fill, c.off, sb->copy));
     sb->stage_bytes[slot] = c.off;
     c.off = 0;
     c.base = (char*)sb->stage[slot];
@@ -1342,7 +1358,8 @@ int gfpl_last_step_cut_proof(gfpl_seqbatch* sb, int64_t* counts4) {
     int64_t v[STEP_REC];
     int e = step_rec_sums(sb, v);
     if (e) return e;
-    const bool on = sb->ctx->cfg.cut_proof == 1 || sb->ctx->cfg.cut_proof == 3;
+    // slots [20..23] are written by k_cut_verify only: report them for a step that ran it
+    const bool on = sb->last_cut_mode == 1 || sb->last_cut_mode == 3;
     for (int s = 0; s < 4; ++s) counts4[s] = on ? v[20 + s] : 0;
     return GFPL_OK;
 }

@@ -104,8 +104,10 @@ struct DevScratch {
     double* pose_H;    // [B*36] last evaluated H
     double* pose_err;  // [B]
     int32_t* pose_ok;  // [B] 1: stage-2 result usable
-    double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs (SoA by list position)
-    uint32_t* pose_idx; // [B*max(mpt_cap, mls_cap)] the active entries' list positions in list order
+    double* pose_in;   // [B*(6*mpt_cap + 10*mls_cap)] gathered GN inputs, one AoS record per list
+                       // entry (points 6 doubles, then lines 10), list order
+    double* pose_act;  // [B*(6*mpt_cap + 10*mls_cap)] the active entries' records, compacted in list
+                       // order per GN run (unused while every entry is active)
                         // (k_pose: points in the low, lines in the high 16 bits)
     double* pose_dtini; // [B*16] staging of gfpl_optimize_pose_ini's DT_ini
     int32_t* kf_mask;  // [B] staging of gfpl_curr_frame_is_kf's mask

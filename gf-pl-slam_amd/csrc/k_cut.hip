@@ -758,19 +758,25 @@ __device__ __forceinline__ double cut_ours_info(const double* xs, double is, dou
     return __builtin_fma(xs[1 + ra] * is, xs[1 + cb], (xs[8 + ra] * ie) * xs[8 + cb]);
 }
 
-// Comparison polynomials of the current line, one copy per lane (registers).
-struct CutCmp {
+// Comparison polynomials of the current line, one copy per lane (registers).  The fields a step
+// reads (ns .. bnd, doubles 0-31) come first and the struct is 16-B aligned, 336 B (84 dwords)
+// long: the per-step load is 16 ds_read_b128 (4 LDS cycles each, 256 B/clk) instead of
+// ds_read2_b64 pairs (8 cycles each, 128 B/clk), and the 8 groups' rows start in 8 disjoint bank
+// quads (84 g mod 64) of a b128 lane group.  Raw offsets (cl[]): ns 0, ne 5, vs 10, ve 15, cc 20,
+// bnd 29, bs 32, be 35.
+struct __attribute__((aligned(16))) CutCmp {
     double ns[5], ne[5];     // |W_s(t)|^2, |W_e(t)|^2
     double vs[5], ve[5];     // v'_s, v'_e
     double cc[9];            // C(t0, t1): cc[3 i + k] multiplies t0^i t1^k
-    double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2); line open only
     double bnd[3];           // the line's bound terms at |t| = T = max(|rlo|, |rhi|): P1, VsA, VeA
+    double bs[3], be[3];     // |W_{side,k}| (error bounds: |Ns| terms <= (sum_k bs_k t^k)^2); line open only
     // the line's agreement bound: a step's neighbour value differs from the
     // reference's metric by at most E = 1/v's (A1 + A2/v's) + 1/v'e (B1 + B2/v'e) + K0 (+ a
     // per-step constant common to the step); the margins need E <= R0 = tau/8 - K0 and
     // EV (1/v's + 1/v'e) <= 1/4.  Floats: R0 rounded down, the others up.
     float eb[6];             // R0, A1, A2, B1, B2, EV
 };
+static_assert(sizeof(CutCmp) == 336, "CutCmp: 84 dwords (bank spread of the 8 groups' rows)");
 // The step's operands (CutCmp without bs / be), read from LDS each step.
 struct CutReg {
     double ns[5], ne[5], vs[5], ve[5], cc[9], bnd[3];
@@ -1067,7 +1073,7 @@ __device__ __attribute__((noinline)) void cut_bound_row(int j, double T, const d
 __device__ __attribute__((noinline)) void cut_bound_line(double T, double tau, const double* cl, const double* fs,
                                                          const double* wg, float* eb) {
     const float* ef = reinterpret_cast<const float*>(fs + PD_ERR);
-    const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
+    const double Bs = h2(cl[32], cl[33], cl[34], T), Be = h2(cl[35], cl[36], cl[37], T);
     double sum[8];
     for (int q = 0; q < 8; ++q) {
         double a = wg[6 * q];
@@ -1292,8 +1298,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             for (int k = 0; k < 3; ++k) cl[20 + 3 * i + k] = gm[tri(3 + k, i)];
             // |W| with a 1% allowance for the approximate square root (bounds only)
             const double gs = fmax(gm[tri(i, i)], 0.0), ge = fmax(gm[tri(3 + i, 3 + i)], 0.0);
-            cl[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
-            cl[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+            cl[32 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
+            cl[35 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
         }
         wave_lds_sync();
         // the line's bound terms at T (lane 7; see cut_dval), and lanes 0-5 the per-row terms of
@@ -1306,12 +1312,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         // (CutCmp::eb): per-row terms by lanes 0-5, combined by lane 7
         const double T = fmax(fabs(rlo), fabs(rhi));
         if (j == 7) {
-            const double Bs = h2(cl[29], cl[30], cl[31], T), Be = h2(cl[32], cl[33], cl[34], T);
+            const double Bs = h2(cl[32], cl[33], cl[34], T), Be = h2(cl[35], cl[36], cl[37], T);
             const double VsA = h4abs(cl + 10, T), VeA = h4abs(cl + 15, T);
             const double Bs2 = Bs * Bs, Be2 = Be * Be;
-            cl[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
-            cl[36] = VsA;
-            cl[37] = VeA;
+            cl[29] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+            cl[30] = VsA;
+            cl[31] = VeA;
         } else if (PROOF && j < 6) {
             cut_bound_row(j, T, fst[g], sumA[g], tmp[g], wg);
         }
@@ -1328,7 +1334,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         // the centre of the first step: d at (0, 0)
         const double vs0 = PROOF ? vtab[g][0] : cl[10], ve0 = PROOF ? vtab[g][CUT_KS] : cl[15];
-        dc = cut_dcore_p1<PROOF>(cl[0], vs0, cl[5], ve0, cl[20], cl[35], cl[36], cl[37], cmpl[g].eb, tq, c_ok);
+        dc = cut_dcore_p1<PROOF>(cl[0], vs0, cl[5], ve0, cl[20], cl[29], cl[30], cl[31], cmpl[g].eb, tq, c_ok);
     };
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
@@ -1691,17 +1697,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
             for (int k = 0; k < 3; ++k) cv[20 + 3 * i + k] = G[tri(3 + k, i)];
             const double gs = fmax(G[tri(i, i)], 0.0), ge = fmax(G[tri(3 + i, 3 + i)], 0.0);
-            cv[29 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
-            cv[32 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
+            cv[32 + i] = gs > 0.0 ? 1.01 * gs * __builtin_amdgcn_rsq(gs) : 0.0;
+            cv[35 + i] = ge > 0.0 ? 1.01 * ge * __builtin_amdgcn_rsq(ge) : 0.0;
         }
         {
             const double T = fmax(fabs(rlo), fabs(rhi));
-            const double Bs = h2(cv[29], cv[30], cv[31], T), Be = h2(cv[32], cv[33], cv[34], T);
+            const double Bs = h2(cv[32], cv[33], cv[34], T), Be = h2(cv[35], cv[36], cv[37], T);
             const double VsA = h4abs(cv + 10, T), VeA = h4abs(cv + 15, T);
             const double Bs2 = Bs * Bs, Be2 = Be * Be;
-            cv[35] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
-            cv[36] = VsA;
-            cv[37] = VeA;
+            cv[29] = __builtin_fma(Bs2 + VsA, Be2 + VeA, Bs2 * Be2);
+            cv[30] = VsA;
+            cv[31] = VeA;
         }
         if (lane == 0) {
 #pragma unroll
@@ -1709,7 +1715,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         wave_lds_sync();
         TCK(5);
-        dc = cut_dcore_p1<false>(cv[0], cv[10], cv[5], cv[15], cv[20], cv[35], cv[36], cv[37], cmpl.eb, tq, c_ok);
+        dc = cut_dcore_p1<false>(cv[0], cv[10], cv[5], cv[15], cv[20], cv[29], cv[30], cv[31], cmpl.eb, tq, c_ok);
         TCK(6);
     };
     if (nls > 0) {

@@ -5,9 +5,11 @@
 //
 // One 64-lane wave owns one sequence for the whole two-stage solve:
 //  * the matched list's inputs (P, pl_obs, sigma2 / sP, eP, le_obs, sigma2) are
-//    gathered once into a per-sequence SoA scratch (coalesced re-reads, L2/MALL
-//    resident) — lane l owns list positions l, l+64, ... for gather, evaluation
-//    and residuals, so it only ever reads back its own stores;
+//    gathered once into per-sequence scratch, one contiguous record per list entry
+//    (48 / 80 B) — lane l owns list positions l, l+64, ... for gather and residuals;
+//    each GN run compacts the active entries' records in list order (when any entry
+//    is inactive), so a chunk's lane reads its own record with 16-B loads at an
+//    address known without an index load;
 //  * every GN iteration walks the lists in chunks of 64: each lane evaluates one
 //    point and one line (J[6], |e|, Cauchy weight; inactive or past-the-end
 //    entries are zero rows) into LDS, then lanes 0-27 (points) and 28-55 (lines)
@@ -50,6 +52,7 @@ struct PoseLDS {
     int cnt[2];
     double err;
     int cmd, c0, np_act, nl_act, nch;   // k_pose<W > 1>: helper command (0 exit, 1 evaluate chunks c0 + w)
+    int pcomp, lcomp;                   // k_pose<W > 1>: the run reads the compacted records (pose_act)
     int gen;                            // k_pose<W > 1>: GN run number (the helpers' register-held inputs)
 #ifdef GFPL_POSE_CLOCK   // (diagnostic build: wave 0's shader-clock cycles per phase, scr.dbg 0-7)
     unsigned long long ck[8], ck0;
@@ -193,22 +196,39 @@ __device__ __forceinline__ void eval_line(const DevCam& cam, double homog, const
 }
 
 struct PoseCtx {
-    const double* pin;   // [PT_K][mpt_cap] of this sequence
-    const double* lin;   // [LS_K][mls_cap]
-    size_t mpt_cap, mls_cap;
+    const double* pin;   // [npt][PT_K] records of this sequence, list order
+    const double* lin;   // [nls][LS_K]
+    double* pact;        // [np_act][PT_K] the active points' records, compacted per GN run (HBM)
+    double* lact;        // [nl_act][LS_K]
     const uint8_t* act;  // LDS [npt + nls] list-position inlier flags
-    uint32_t* idx;       // HBM [max(mpt_cap, mls_cap)] the active points' (low 16 bits) and lines'
-                         // (high 16 bits) list positions, in list order
     int npt, nls;
 };
+
+// one record: 16-B loads (records are 16-B aligned: 48 / 80 B, the scratch 256-B aligned)
+template <int K>
+__device__ __forceinline__ void load_rec(const double* base, int f, double* v) {
+    const double2* r = reinterpret_cast<const double2*>(base + (size_t)K * f);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+        const double2 t = r[i];
+        v[2 * i] = t.x;
+        v[2 * i + 1] = t.y;
+    }
+}
+template <int K>
+__device__ __forceinline__ void store_rec(double* base, int f, const double* v) {
+    double2* r = reinterpret_cast<double2*>(base + (size_t)K * f);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) r[i] = make_double2(v[2 * i], v[2 * i + 1]);
+}
 
 // k_pose<W > 1>: chunk c0 + w of the active entries (points and lines) evaluated into wave w's rows.
 // The chunk's inputs are gathered into pv / lv when `load`; a GN run whose chunks fit one round
 // (nch <= W) evaluates the same entries every iteration, so the callers keep them in registers and
 // load once per run (only DT changes between iterations).
 template <int W>
-__device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx& X, const double* DT, int c0,
-                                                int np_act, int nl_act, int ntot, double* cp, double* cl, int w,
+__device__ __forceinline__ void pose_eval_chunk(const KParams& p, const double* pa, const double* la, const double* DT,
+                                                int c0, int np_act, int nl_act, double* cp, double* cl, int w,
                                                 double* pv, double* lv, bool load) {
     const int lane = threadIdx.x & 63;
     const int c = c0 + w;
@@ -216,12 +236,8 @@ __device__ __forceinline__ void pose_eval_chunk(const KParams& p, const PoseCtx&
     double* cpw = cp + w * (16 * CH_STRIDE);
     double* clw = cl + w * (16 * CH_STRIDE);
     if (load) {
-        const uint32_t ix = f < ntot ? X.idx[f] : 0u;
-        const int fp = f < np_act ? (int)(ix & 0xFFFFu) : 0, fl = f < nl_act ? (int)(ix >> 16) : 0;
-#pragma unroll
-        for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
-#pragma unroll
-        for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
+        load_rec<PT_K>(pa, f < np_act ? f : 0, pv);
+        load_rec<LS_K>(la, f < nl_act ? f : 0, lv);
     }
     double o[8];
     if (f < np_act) {
@@ -255,8 +271,8 @@ __device__ void pose_helper(const KParams& p, const PoseCtx& X, PoseLDS& S, doub
         const int c0 = S.c0, nch = S.nch;
         if (c0 + w < nch) {
             const bool keep = W >= 8 && nch <= W;   // (see gauss_newton)
-            pose_eval_chunk<W>(p, X, S.DT, c0, S.np_act, S.nl_act, max(S.np_act, S.nl_act), cp, cl, w, pv, lv,
-                               !(keep && gen == S.gen));
+            pose_eval_chunk<W>(p, S.pcomp ? X.pact : X.pin, S.lcomp ? X.lact : X.lin, S.DT, c0, S.np_act, S.nl_act,
+                               cp, cl, w, pv, lv, !(keep && gen == S.gen));
             gen = keep ? S.gen : -1;
         }
         __syncthreads();   // (B)
@@ -301,31 +317,51 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
     const uint8_t* actl = X.act + X.npt;
     // the active entries, compacted in list order (an inactive entry is a zero row, and adding
     // +0.0 to a sum that started at +0.0 never changes it: skipping them leaves H bit-identical);
-    // after removeOutliers about a third of the entries are inactive
+    // after removeOutliers about a third of the entries are inactive.  Their records are copied
+    // into pose_act, contiguous, so chunk c is records [64 c, 64 c + 64) of one array: no index
+    // load ahead of the inputs' loads, no inactive records between them
     int np_act = 0, nl_act = 0;
     {
+        for (int b0 = 0; b0 < X.npt; b0 += 64) np_act += __popcll(__ballot(b0 + lane < X.npt && actp[b0 + lane]));
+        for (int b0 = 0; b0 < X.nls; b0 += 64) nl_act += __popcll(__ballot(b0 + lane < X.nls && actl[b0 + lane]));
+    }
+    const bool cpts = np_act != X.npt, clns = nl_act != X.nls;   // (wave-uniform)
+    {
         const unsigned long long lt = (1ull << lane) - 1ull;
-        for (int b0 = 0; b0 < X.npt; b0 += 64) {
-            const int f = b0 + lane;
-            const bool a = f < X.npt && actp[f];
-            const unsigned long long m = __ballot(a);
-            if (a) reinterpret_cast<uint16_t*>(X.idx + np_act + __popcll(m & lt))[0] = (uint16_t)f;
-            np_act += __popcll(m);
+        if (cpts) {
+            int n = 0;
+            for (int b0 = 0; b0 < X.npt; b0 += 64) {
+                const int f = b0 + lane;
+                const bool a = f < X.npt && actp[f];
+                const unsigned long long m = __ballot(a);
+                if (a) {
+                    double v[PT_K];
+                    load_rec<PT_K>(X.pin, f, v);
+                    store_rec<PT_K>(X.pact, n + __popcll(m & lt), v);
+                }
+                n += __popcll(m);
+            }
         }
-        for (int b0 = 0; b0 < X.nls; b0 += 64) {
-            const int f = b0 + lane;
-            const bool a = f < X.nls && actl[f];
-            const unsigned long long m = __ballot(a);
-            if (a) reinterpret_cast<uint16_t*>(X.idx + nl_act + __popcll(m & lt))[1] = (uint16_t)f;
-            nl_act += __popcll(m);
+        if (clns) {
+            int n = 0;
+            for (int b0 = 0; b0 < X.nls; b0 += 64) {
+                const int f = b0 + lane;
+                const bool a = f < X.nls && actl[f];
+                const unsigned long long m = __ballot(a);
+                if (a) {
+                    double v[LS_K];
+                    load_rec<LS_K>(X.lin, f, v);
+                    store_rec<LS_K>(X.lact, n + __popcll(m & lt), v);
+                }
+                n += __popcll(m);
+            }
         }
+        if (W > 1 && lane == 0) { S.pcomp = cpts ? 1 : 0; S.lcomp = clns ? 1 : 0; }
         pose_bar<W>();
     }
+    const double* pa = cpts ? X.pact : X.pin;
+    const double* la = clns ? X.lact : X.lin;
     const int ntot = max(np_act, nl_act), nch = (ntot + 63) >> 6;
-    // a chunk's list positions are loaded one chunk ahead of its inputs (the inputs' loads
-    // depend on them); chunk 0's are reloaded per iteration (kept in a register across the
-    // iterations and the se3_update_wave call, they cost 45 VGPR spills at 128 registers)
-    auto load_idx = [&](int c) { const int f = (c << 6) + lane; return f < ntot ? X.idx[f] : 0u; };
     // k_pose<W >= 8>: wave 0's chunk inputs, kept over a one-round run (k_pose<4> at B <= 1024 keeps its
     // occupancy: 4 waves / SIMD need <= 128 VGPRs)
     constexpr bool KEEP = W >= 8;
@@ -344,17 +380,13 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
         // raw inputs of chunk c + 1 are loaded into registers while chunk c is
         // reduced, so the SoA scratch latency hides behind the LDS reduction
         double pv[PT_K], lv[LS_K];
-        auto load_chunk = [&](int c, uint32_t ix) {
+        auto load_chunk = [&](int c) {
             const int f = (c << 6) + lane;
-            const int fp = f < np_act ? (int)(ix & 0xFFFFu) : 0, fl = f < nl_act ? (int)(ix >> 16) : 0;
-#pragma unroll
-            for (int i = 0; i < PT_K; ++i) pv[i] = X.pin[i * X.mpt_cap + fp];
-#pragma unroll
-            for (int i = 0; i < LS_K; ++i) lv[i] = X.lin[i * X.mls_cap + fl];
+            load_rec<PT_K>(pa, f < np_act ? f : 0, pv);
+            load_rec<LS_K>(la, f < nl_act ? f : 0, lv);
         };
         if (W == 1) {
-            load_chunk(0, load_idx(0));
-            uint32_t ix = load_idx(1);
+            load_chunk(0);
             for (int c = 0; c < nch; ++c) {
                 const int f = (c << 6) + lane;
                 double o[8];
@@ -372,10 +404,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
                 }
     #pragma unroll
                 for (int i = 0; i < 8; ++i) cl[i * CH_STRIDE + lane] = o[i];
-                if (c + 1 < nch) {
-                    load_chunk(c + 1, ix);
-                    ix = load_idx(c + 2);
-                }
+                if (c + 1 < nch) load_chunk(c + 1);
                 pose_bar<W>();
                 const double* A = buf + ia * CH_STRIDE;
                 const double* Bv = buf + ib * CH_STRIDE;
@@ -402,7 +431,7 @@ __device__ void gauss_newton(const KParams& p, const PoseCtx& X, PoseLDS& S, dou
             for (int c0 = 0; c0 < nch; c0 += W) {
                 if (lane == 0) { S.cmd = 1; S.c0 = c0; }
                 __syncthreads();   // (A) the helpers read the command, DT and the positions
-                pose_eval_chunk<W>(p, X, S.DT, c0, np_act, nl_act, ntot, cp, cl, 0, pv0, lv0, !(KEEP && nch <= W && it > 0));
+                pose_eval_chunk<W>(p, pa, la, S.DT, c0, np_act, nl_act, cp, cl, 0, pv0, lv0, !(KEEP && nch <= W && it > 0));
                 __syncthreads();   // (B) the round's rows are in LDS
                 POSE_CK(S, 5);
                 const int nw = min(W, nch - c0);
@@ -595,30 +624,31 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// removeOutliers(DT_) (:2058-2116): the residual of list entry k (inputs gathered SoA in pose_in)
+// removeOutliers(DT_) (:2058-2116): the residual of list entry k (its record in pose_in)
 __device__ __forceinline__ double point_residual(const KParams& p, const double* pin, const double* DTs, int k) {
-    const double* in = pin + k;
-    const double Pp[3] = {in[0], in[p.mpt_cap], in[2 * p.mpt_cap]};
+    double in[PT_K];
+    load_rec<PT_K>(pin, k, in);
+    const double Pp[3] = {in[0], in[1], in[2]};
     double Pc[3], uv[2];
     se3_apply(DTs, Pp, Pc);
     projection(p.cam, Pc, uv);
-    const double ex = uv[0] - in[3 * p.mpt_cap], ey = uv[1] - in[4 * p.mpt_cap];
-    return sqrt(ex * ex + ey * ey) * sqrt(in[5 * p.mpt_cap]);
+    const double ex = uv[0] - in[3], ey = uv[1] - in[4];
+    return sqrt(ex * ex + ey * ey) * sqrt(in[5]);
 }
 __device__ __forceinline__ double line_residual(const KParams& p, const double* lin, const double* DTs, int k) {
-    const double* in = lin + k;
-    const size_t st = p.mls_cap;
-    const double sP[3] = {in[0], in[st], in[2 * st]};
-    const double eP[3] = {in[3 * st], in[4 * st], in[5 * st]};
+    double in[LS_K];
+    load_rec<LS_K>(lin, k, in);
+    const double sP[3] = {in[0], in[1], in[2]};
+    const double eP[3] = {in[3], in[4], in[5]};
     double sc[3], ec[3], su[2], eu[2];
     se3_apply(DTs, sP, sc);
     se3_apply(DTs, eP, ec);
     projection(p.cam, sc, su);
     projection(p.cam, ec, eu);
-    const double l0 = in[6 * st], l1 = in[7 * st], l2 = in[8 * st];
+    const double l0 = in[6], l1 = in[7], l2 = in[8];
     const double e0 = (l0 * su[0] + l1 * su[1]) + l2;
     const double e1 = (l0 * eu[0] + l1 * eu[1]) + l2;
-    return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9 * st]);
+    return sqrt(e0 * e0 + e1 * e1) * sqrt(in[9]);
 }
 
 // the line list's outlier flags from register-held residuals (n <= 64 POSE_MAD_R): returns the
@@ -665,11 +695,11 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
     const int32_t* mls = p.tr.matched_ls + (size_t)b * p.mls_cap;
     const size_t pb = (size_t)b * p.kp_cap, lb = (size_t)b * p.kl_cap;
     PoseCtx X;
-    X.mpt_cap = p.mpt_cap; X.mls_cap = p.mls_cap;
     double* pin = p.scr.pose_in + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
     double* lin = pin + PT_K * p.mpt_cap;
     X.pin = pin; X.lin = lin; X.act = act; X.npt = npt; X.nls = nls;
-    X.idx = p.scr.pose_idx + (size_t)b * (size_t)max(p.mpt_cap, p.mls_cap);
+    X.pact = p.scr.pose_act + (size_t)b * (PT_K * p.mpt_cap + LS_K * p.mls_cap);
+    X.lact = X.pact + PT_K * p.mpt_cap;
     if (W > 1 && threadIdx.x >= 64) {   // helper waves: GN chunk evaluation on wave 0's commands
         pose_helper<W>(p, X, S, cp, cl);
         return;
@@ -687,21 +717,17 @@ __global__ void __launch_bounds__(64 * W, W == 1 ? GFPL_POSE_WAVES : 1) k_pose(K
     int cpn = 0, cln = 0;
     for (int f = lane; f < npt; f += 64) {
         const size_t q = pb + mpt[f];
-        pin[f] = P.P[3 * q]; pin[p.mpt_cap + f] = P.P[3 * q + 1]; pin[2 * p.mpt_cap + f] = P.P[3 * q + 2];
-        pin[3 * p.mpt_cap + f] = P.pl_obs[2 * q]; pin[4 * p.mpt_cap + f] = P.pl_obs[2 * q + 1];
-        pin[5 * p.mpt_cap + f] = P.sigma2[q];
+        const double v[PT_K] = {P.P[3 * q], P.P[3 * q + 1], P.P[3 * q + 2], P.pl_obs[2 * q], P.pl_obs[2 * q + 1],
+                                P.sigma2[q]};
+        store_rec<PT_K>(pin, f, v);
         act[f] = P.inlier[q] ? 1 : 0;
         cpn += act[f];
     }
     for (int f = lane; f < nls; f += 64) {
         const size_t q = lb + mls[f];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            lin[k * p.mls_cap + f] = L.sP[3 * q + k];
-            lin[(3 + k) * p.mls_cap + f] = L.eP[3 * q + k];
-            lin[(6 + k) * p.mls_cap + f] = L.le_obs[3 * q + k];
-        }
-        lin[9 * p.mls_cap + f] = L.sigma2[q];
+        const double v[LS_K] = {L.sP[3 * q], L.sP[3 * q + 1], L.sP[3 * q + 2], L.eP[3 * q], L.eP[3 * q + 1],
+                                L.eP[3 * q + 2], L.le_obs[3 * q], L.le_obs[3 * q + 1], L.le_obs[3 * q + 2], L.sigma2[q]};
+        store_rec<LS_K>(lin, f, v);
         act[npt + f] = L.inlier[q] ? 1 : 0;
         cln += act[npt + f];
     }

@@ -1205,6 +1205,9 @@ __global__ void k_step_bytes(KParams p) {
     if (!(p.cfg.use_line_conf_cut && Ml > 0)) rec[16] = rec[17] = 0;   // k_cut_search writes them otherwise
     rec[18] = rec[15];   // until optimize_pose (k_pose_finish) records its inliers
     if (!(p.cfg.use_line_conf_cut && Ml > 0)) rec[19] = 0;   // k_cut_search writes it otherwise
+    // 20-23: the proven line cut's counts (k_cut_verify, cut_proof 1 / 3); zero for a step without it
+    if (!(p.cfg.use_line_conf_cut && (p.cfg.cut_proof == 1 || p.cfg.cut_proof == 3)))
+        rec[20] = rec[21] = rec[22] = rec[23] = 0;
     // insertStereoPair's last statement, numFrameSinceKeyframe++ (src/stereoFrameHandler.cpp:150):
     // this per-sequence kernel closes every gfpl_insert_stereo_pair
     p.tr.kf_nsince[b] = p.tr.kf_nsince[b] + 1;

@@ -151,19 +151,12 @@ void BFMatcher::radiusMatch(const std::vector<Descriptor>& query, const std::vec
 }
 
 // ---------------------------------------------- StereoFrame frame members --
-namespace {
-std::mutex g_engine_mu;
-std::map<const PinholeStereoCamera*, std::unique_ptr<StereoFrameHandler>>& engines() {
-    static std::map<const PinholeStereoCamera*, std::unique_ptr<StereoFrameHandler>> m;
-    return m;
-}
-}  // namespace
+PinholeStereoCamera::~PinholeStereoCamera() = default;   // (StereoFrameHandler complete here)
 
 StereoFrameHandler& StereoFrame::engine() {
-    std::lock_guard<std::mutex> lk(g_engine_mu);
-    auto& e = engines()[cam];
-    if (!e) e.reset(new StereoFrameHandler(cam));
-    return *e;
+    std::lock_guard<std::mutex> lk(cam->engine_mu_);
+    if (!cam->engine_) cam->engine_.reset(new StereoFrameHandler(cam));
+    return *cam->engine_;
 }
 
 void StereoFrame::extractInitialStereoFeatures(int /*fast_th*/) { engine().frame_stereo(this, true); }

@@ -27,6 +27,7 @@
 #include <cfloat>
 #include <cstdint>
 #include <list>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -168,9 +169,18 @@ private:
 
 // ---------------------------------------------------- PinholeStereoCamera --
 // include/pinholeStereoCamera.h:37-103 (rectified, distortion-free subset).
+class StereoFrameHandler;
+
 class PinholeStereoCamera {
 public:
     PinholeStereoCamera(int width, int height, double fx, double fy, double cx, double cy, double b);
+    // a copy is a new camera: it gets its own frame engine (StereoFrame's frame-level members)
+    PinholeStereoCamera(const PinholeStereoCamera& o) : cam_(o.cam_) {}
+    PinholeStereoCamera& operator=(const PinholeStereoCamera& o) {
+        if (this != &o) { cam_ = o.cam_; engine_.reset(); }
+        return *this;
+    }
+    ~PinholeStereoCamera();
     int getWidth() const { return cam_.width; }
     int getHeight() const { return cam_.height; }
     double getFx() const { return cam_.fx; }
@@ -183,7 +193,12 @@ public:
     const gfpl_camera& abi() const { return cam_; }
 
 private:
+    friend class StereoFrame;
     gfpl_camera cam_{};
+    // the GPU engine behind StereoFrame's frame-level members on this camera (one sequence),
+    // created on first use and destroyed with the camera (not in a static destructor)
+    mutable std::unique_ptr<StereoFrameHandler> engine_;
+    mutable std::mutex engine_mu_;
 };
 
 // -------------------------------------------------------------- features --

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GFPL_ABI_VERSION 5
+#define GFPL_ABI_VERSION 6   /* 6: STEP_REC 24 (gfpl_debug_step_records writes B x 24 int64), cut_proof 0-3 */
 
 #define GFPL_DESC_BYTES 32          /* ORB rBRIEF / binarised LBD: 256 bit        */
 #define GFPL_MAX_LEVELS 8           /* ORB pyramid levels supported              */
@@ -117,11 +117,17 @@ typedef struct gfpl_config {
     double cut_certify;          /* (new) 1e-9: relative margin of the certified line-cut
                                     search; 0 = every neighbour evaluated with
                                     the reference's LLT; nonzero values below 1e-10 are rejected */
-    int    cut_proof;            /* (new) 0: a margined decision also rests on the measured
-                                    agreement of the comparison operands with the reference's
-                                    (DESIGN.md §3); 1: only on the proven per-step agreement
-                                    bound — a step it does not cover takes the reference's
-                                    evaluation.  Default 0. */
+    int    cut_proof;            /* (new) what ties a margined line-cut decision to the
+                                    reference's own logdet:
+                                    0 measured: the comparison operands' measured agreement
+                                      with the reference's (not a proof);
+                                    1 proven after the fact: the measured search records its
+                                      decisions, k_cut_verify proves them with the per-step
+                                      agreement bound; a sequence not proven is redone by the
+                                      eager-proven search;
+                                    2 eager-proven: every step of the search carries the bound;
+                                    3 (test hook) as 1, but every sequence is redone eagerly.
+                                    A step no bound covers takes the reference's evaluation. */
 } gfpl_config;
 
 /* cv::KeyPoint subset used by the path */

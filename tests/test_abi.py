@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = gfpl.hiplib()
-    assert L.gfpl_abi_version() == 5   # 5: gfpl_config.cut_proof; 4: gfpl_detector (image input), event record counts
+    assert L.gfpl_abi_version() == 6   # 6: STEP_REC 24, cut_proof 0-3; 5: gfpl_config.cut_proof; 4: gfpl_detector (image input), event record counts
     assert L.gfpl_strerror(-4) == b"knn-2 needs at least 2 train descriptors"
 
 
