@@ -260,6 +260,7 @@ class ParitySampler:
     def _par(self, fn):
         todo = list(range(len(self.seqs)))
         lock = threading.Lock()
+        done = [0]
 
         def work():
             while True:
@@ -268,6 +269,10 @@ class ParitySampler:
                         return
                     i = todo.pop()
                 fn(i)
+                with lock:   # progress of long (full-batch) replays: a watchdog sees output
+                    done[0] += 1
+                    if done[0] % 4096 == 0:
+                        print(f"[parity] {done[0]} / {len(self.seqs)} sequences", file=sys.stderr, flush=True)
         th = [threading.Thread(target=work) for _ in range(self.threads)]
         for t in th:
             t.start()

@@ -1367,6 +1367,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (lane == 0) __hip_atomic_store(prog.own, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int partner_done = 0;   // the partner's lines done as read at the previous transition
     __builtin_amdgcn_s_setprio(2);
+#ifdef GFPL_CUT_PCLOCK   // (diagnostic build: shader-clock cycles per phase of the wave in scr.dbg 0-3:
+                         //  step evaluation + decision, exact rounds, bookkeeping, transitions)
+    uint64_t pk[4] = {0, 0, 0, 0};
+    uint64_t pk0 = clock64();
+    int n_it = 0, n_tr = 0;   // loop iterations, transitions (scr.dbg 7: n_it << 32 | n_tr)
+    uint64_t tk[3] = {0, 0, 0}, tk0 = 0;   // transition phases (scr.dbg 4-6): finished line's info + next
+                                           // line's record and S, open_line + prefetch, progress exchange
+#define PCK(i) do { const uint64_t t_ = clock64(); pk[i] += t_ - pk0; pk0 = t_; } while (0)
+#define TCK0() do { tk0 = clock64(); } while (0)
+#define TCK(i) do { const uint64_t t_ = clock64(); tk[i] += t_ - tk0; tk0 = t_; } while (0)
+#else
+#define PCK(i) do { } while (0)
+#define TCK0() do { } while (0)
+#define TCK(i) do { } while (0)
+#endif
     while (__any(m < nls)) {   // wave-uniform loop; groups that are done idle
         const bool act = m < nls && !pend;
         // ---- lane j: d of neighbour j; the group decision and its margins
@@ -1406,6 +1421,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         n_exact += exact ? 1 : 0;
         double dnext = top;   // d of the next centre (the chosen neighbour, same bits)
         int cnext = 1;
+        PCK(0);
         if (__any(exact)) {
             // ---- X: the reference's evaluation of this step for the groups that need it
             const CutX xr = cut_exact_round(exact, valid, first, m, m_sync, r0, r1, q_cur, lb, best, mls, rec_l, L.sP, L.eP,
@@ -1419,6 +1435,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const int sb = __shfl(bok, src);
             if (exact) { dnext = sd; cnext = sb; }
         }
+        PCK(1);
         int finalize = 0;
         if (rec && act) {   // move j | CUT_P_STAY (no better neighbour) | CUT_P_EXACT, into the group's LDS row
             if (j == 0 && lstep < CUT_PATH)
@@ -1446,14 +1463,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 finalize = 1;
             }
         }
-        if (rec && act && finalize) {   // the line's recorded steps to HBM: 8 bytes per group lane
-            __builtin_amdgcn_wave_barrier();
+        if (rec && act && finalize && m + 1 >= nls) {   // the last line's recorded steps to HBM: 8 bytes per
+            __builtin_amdgcn_wave_barrier();                // group lane (the others' at their transition)
             if (8 * j < lstep)
                 *reinterpret_cast<unsigned long long*>(path + (size_t)m * CUT_PATH + 8 * j) =
                     *reinterpret_cast<const unsigned long long*>(&pth[g][8 * j]);
         }
         if (act && finalize) {
-            if (j == 0) {
+            // (measured mode: the cut of a line with a successor is stored at the transition, after its
+            // vmcnt wait, so that wait does not include these stores' write acknowledgements; nothing
+            // reads it before: an exact round's flush serves lines below its own group's open line)
+            if (j == 0 && (PROOF || m + 1 >= nls)) {
                 L.cut[2 * q_cur] = r0;
                 L.cut[2 * q_cur + 1] = r1;
             }
@@ -1465,8 +1485,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         // CUT_BATCH groups of the wave wait, one has waited CUT_WAIT iterations, or no
         // group has steps left; one transition then serves all of them, so the wave
         // pays its serial chain (factor, solves, LDS exchanges) fewer times.
+        PCK(2);
         const int npend = __popcll(__ballot(pend)) >> 3;
+#ifdef GFPL_CUT_PCLOCK
+        ++n_it;
+#endif
         if (npend > 0 && (npend >= CUT_BATCH || __any(pend && wait >= CUT_WAIT) || __ballot(m < nls && !pend) == 0)) {
+#ifdef GFPL_CUT_PCLOCK
+            ++n_tr;
+#endif
+            TCK0();
             double info[3];
             if (pend) {
                 // approximate invCov_sum += info of the chosen ratio (the exact one is
@@ -1515,6 +1543,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                     for (int k = 0; k < CUT_FAST / 8; ++k) fst[g][j + 8 * k] = rec_l[(size_t)m * CUT_REC + j + 8 * k];
                 } else {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (j == 0) {   // the finished line's cut (deferred from its finalisation)
+                        L.cut[2 * q_cur] = r0;
+                        L.cut[2 * q_cur + 1] = r1;
+                    }
+                    if (rec && 8 * j < lstep)   // ... and its recorded steps (line m - 1: m moved on)
+                        *reinterpret_cast<unsigned long long*>(path + (size_t)(m - 1) * CUT_PATH + 8 * j) =
+                            *reinterpret_cast<const unsigned long long*>(&pth[g][8 * j]);
 #pragma unroll
                     for (int k = 0; k < CUT_FAST / 8; ++k) {
                         const int e = j + 8 * k;
@@ -1545,11 +1580,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 }
             }
             wave_lds_sync();
+            TCK(0);
             if (pend) {   // group-uniform; open_line exchanges through LDS only
                 open_line();
                 if (m + 1 < nls) pf_issue(m + 1);
                 pend = 0;
             }
+            TCK(1);
             {
                 const int done = wave_sum8(j == 0 ? m : 0);
                 if (done > __builtin_amdgcn_readfirstlane(partner_done)) __builtin_amdgcn_s_setprio(0);
@@ -1557,10 +1594,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
                 if (lane == 0) __hip_atomic_store(prog.own, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 partner_done = __hip_atomic_load(prog.partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used next time
             }
+            TCK(2);
         } else if (pend) {
             ++wait;
         }
+        PCK(3);
     }
+#ifdef GFPL_CUT_PCLOCK
+    if (live && j == 0)
+        for (int i = 0; i < 4; ++i) p.scr.dbg[8 * (size_t)b + i] = (int64_t)pk[i];
+    if (live && j == 0) {
+        for (int i = 0; i < 3; ++i) p.scr.dbg[8 * (size_t)b + 4 + i] = (int64_t)tk[i];
+        p.scr.dbg[8 * (size_t)b + 7] = ((int64_t)n_it << 32) | n_tr;
+    }
+#endif
+#undef PCK
+#undef TCK0
+#undef TCK
     if (live && j == 0) {
         p.scr.bytes[(size_t)STEP_REC * b + 16] = n_steps;
         p.scr.bytes[(size_t)STEP_REC * b + 17] = n_exact;

@@ -13,6 +13,9 @@
 #   cfg                 tools/cfg_lines.sh (cfg3 / cfg4 / cfg5 lines and LSD)
 #   profile[:ARGS]      tools/round_profile.sh (PMC passes, bench line, rocprofv3 statistics), SKIP_TESTS=1
 #   rocprof[:ARGS]      rocprofv3 --kernel-trace --stats of a tracking-only bench
+#   dump:LIBDIR         a short tracking-only bench on a diagnostic build (tools/build_variant.sh) with
+#                       --dump-records: step records + clock slots in $O/dump_<tag>[_clk].npy
+#   fullparity[:ARGS]   bench.py --parity-seqs -1 (every sequence replayed on the oracle), short window
 set -o pipefail
 name=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -57,6 +60,18 @@ for step in "$@"; do
           || { tail -5 $O/rocprof.log; exit 1; }
       find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
       cut -d, -f1-4 $O/kernel_stats.csv | head -14 ;;
+    dump)
+      tag=$(basename $arg)
+      GFPL_LIB_DIR=$(realpath $arg) timeout -k 10 400 python bench.py --steps 3 --warmup 2 --distinct 16384 --no-cpu \
+          --no-detect --no-host-fed --no-b1 --proven-steps 0 --parity-seqs 0 --dump-records $O/dump_$tag.npy \
+          > $O/dump_$tag.log 2>&1 || { tail -5 $O/dump_$tag.log; exit 1; }
+      summary $O/dump_$tag.log
+      python3 tools/cut_phases.py $O/dump_${tag}_clk.npy || true ;;
+    fullparity)
+      tag=$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_')
+      timeout -k 10 900 python -u bench.py --steps 3 --warmup 2 --parity-seqs -1 --no-cpu --no-detect --no-host-fed \
+          --no-b1 --proven-steps 0 $(args "$arg") > $O/fullparity$tag.log 2>&1 || { tail -5 $O/fullparity$tag.log; exit 1; }
+      summary $O/fullparity$tag.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
