@@ -231,6 +231,24 @@ def load_pmc(path, kernel_name, batch, workload, steps, warmup):
     return k, None if k else f"{kernel_name} not in the PMC summary"
 
 
+def kernel_traffic(path, batch, workload, steps, warmup, km, kb, sp_ms, sp_bytes):
+    """Per-kernel algorithmic bytes per launch (gfpl_last_step_kernel_bytes; k_stereo_points: its
+    stage's) beside the PMC-counted traffic of the same launches when the PMC summary covers this
+    window (tools/pmc_summary.py: FETCH_SIZE / 0.95 + WRITE_SIZE, the gather calibration)."""
+    names = ["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"]
+    rows = {n: (float(ms), float(by)) for n, ms, by in zip(names, km, kb)}
+    rows["k_stereo_points"] = (float(sp_ms), float(sp_bytes))
+    out = {}
+    for n, (ms, by) in rows.items():
+        pmc, _ = load_pmc(path, n, batch, workload, steps, warmup)
+        cnt = (pmc or {}).get("hbm_bytes_per_launch_gather_cal")
+        out[n] = {"algorithmic_bytes": int(by), "avg_launch_ms": round(ms, 4),
+                  "algorithmic_GBps": round(by / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
+                  "counted_bytes_gather_cal": int(cnt) if cnt else None,
+                  "counted_over_algorithmic": round(cnt / by, 2) if cnt and by > 0 else None}
+    return out
+
+
 def rank_share(cores: int, world: int) -> int:
     """Host threads one rank may use: the process's cores (cgroup quota) split over the
     ranks of this node (the quota is shared by every rank's process)."""
@@ -1009,6 +1027,7 @@ def main():
             "host_fed": host_fed,
             "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES, sm)},
             "kernel_ms": {n: round(float(v), 4) for n, v in zip(["k_cut_prep", "k_cut_search", "k_cut_finish", "k_pose"], km)},
+            "kernel_bytes": kernel_traffic(args.pmc, B, args.workload, K, W, km, kb, sm[0], sb[0]),
             "stage_bytes_per_step": {n: int(v) for n, v in zip(STAGES, sb)},
             "cpu_baseline": cpu,
             "latency_b1_ms": b1.get("latency_b1_ms") if b1 else None,

@@ -1319,9 +1319,17 @@ int gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4) {
     int64_t v[STEP_REC];
     int e = step_rec_sums(sb, v);
     if (e) return e;
-    // k_cut_search bytes are recorded per sequence; k_pose's are the pose stage's
-    bytes4[0] = bytes4[2] = -1;   // not split out
+    // k_cut_search bytes are recorded per sequence; k_pose's are the pose stage's.  k_cut_prep and
+    // k_cut_finish from the summed matched counts (v[13] M_p, v[14] M_l):
+    //   prep:   per matched line its cut inputs sP eP covS covE le_obs (208 B) + index (4 B), per
+    //           matched point P + pl_obs (40 B) + index (4 B); per sequence the two Tfw (256 B),
+    //           DT_inv and invCov_sum out (128 + 168 B)
+    //   finish: per matched line its cut inputs + index + ratios (228 B) read, invCovPose (288 B) and
+    //           the cut endpoints sP eP spl epl sdisp edisp (96 B) written
+    const bool cut = sb->last_cut_mode >= 0;
+    bytes4[0] = cut ? 212 * v[14] + 44 * v[13] + 552 * (int64_t)sb->B : 0;
     bytes4[1] = v[7];
+    bytes4[2] = cut ? 612 * v[14] : 0;
     bytes4[3] = v[5];
     return GFPL_OK;
 }

@@ -701,7 +701,8 @@ int  gfpl_debug_clocks(gfpl_seqbatch* sb, int64_t* out);
 /* Per-kernel view of the dominant stages (timing enabled, line cut on):
  * ms4 = device ms of [k_cut_prep, k_cut_search, k_cut_finish, k_pose] of the last
  * step (HIP events on the context stream); bytes4 = algorithmic bytes of the same
- * kernels (-1 where not split out: DESIGN.md §4).                              */
+ * kernels, summed over the batch (each kernel's own inputs read once and
+ * outputs written once; 0 for the cut kernels when the step ran no line cut).  */
 int  gfpl_get_kernel_times(gfpl_ctx* ctx, float* ms4);
 int  gfpl_last_step_kernel_bytes(gfpl_seqbatch* sb, int64_t* bytes4);
 

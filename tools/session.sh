@@ -66,7 +66,8 @@ for step in "$@"; do
           --no-detect --no-host-fed --no-b1 --proven-steps 0 --parity-seqs 0 --dump-records $O/dump_$tag.npy \
           > $O/dump_$tag.log 2>&1 || { tail -5 $O/dump_$tag.log; exit 1; }
       summary $O/dump_$tag.log
-      python3 tools/cut_phases.py $O/dump_${tag}_clk.npy || true ;;
+      python3 tools/cut_phases.py $O/dump_${tag}_clk.npy || true
+      python3 tools/sp_phases.py $O/dump_${tag}_clk.npy || true ;;
     fullparity)
       tag=$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_')
       timeout -k 10 900 python -u bench.py --steps 3 --warmup 2 --parity-seqs -1 --no-cpu --no-detect --no-host-fed \
