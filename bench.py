@@ -9,7 +9,8 @@ maxIters = maxItersRef = 10 and minError = minErrorChange = 0.
 
 A "step" = one StereoFrameHandler step (insertStereoPair + optimizePose +
 updateFrame, app/plslam_mod.cpp:387-477) for every one of the B independent
-sequences resident on a GPU (B = 16384 by default, independent of --steps).
+sequences resident on a GPU (B = 32768 by default, independent of --steps; ~70 GB of the
+288 GB HBM with both staging buffers).
 
 Input ring: before each step the host generates the next input frame of all B
 sequences (splitmix64, deterministic; gfpl_synth) chunk by chunk into a ring of
@@ -94,7 +95,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=16384, help="sequences per GPU (reduced only if HBM is short)")
+    ap.add_argument("--batch", type=int, default=32768, help="sequences per GPU (reduced only if HBM is short)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-detect", action="store_true", help="skip the ORB / LBD detection rates")
     ap.add_argument("--gen-threads", type=int, default=16,
@@ -104,7 +105,7 @@ def parse(argv=None):
                          "worth (8 ranks sharing a host; each uploaded to every chunk of the batch) — a fixed rule "
                          "of (B, threads), never a timing, so one command always tracks the same inputs")
     ap.add_argument("--chunk", type=int, default=0,
-                    help="sequences per pinned host chunk of the input ring (0: B/8, at least 256)")
+                    help="sequences per pinned host chunk of the input ring (0: B/8 within [256, 2048])")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the pipelined host-fed (PCIe) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work (timed seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = the cores this process may use)")
@@ -731,7 +732,7 @@ def main():
     cores, cores_info = host_cores()
     share = rank_share(cores, world)
     gen_threads = max(1, min(args.gen_threads, share))
-    chunk = args.chunk or max(256, (B // 8 + 63) // 64 * 64)
+    chunk = args.chunk or min(2048, max(256, (B // 8 + 63) // 64 * 64))   # (<= 4.2 GB pinned per rank)
     chunk = min(chunk, B)
     ring = [gfpl.HostBatch(cam, sp_up, chunk, KP, KL, seq0=seq0, pinned=not dry) for _ in range(2)]
     pinned_bytes = 0 if dry else sum(r.nbytes() for r in ring)

@@ -1339,13 +1339,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // Next-line prefetch: right after a line opens the group's lanes copy the next line's
     // record (640 B) from HBM straight into LDS (global_load_lds, no registers); it is
     // waited for (vmcnt) and moved into fst / nxi when that line opens, >= 1 iteration later.
+    // The DMA is issued by inline asm: the compiler treats a pending __builtin_amdgcn_global_load_lds
+    // as a write to any LDS and put an s_waitcnt vmcnt(0) before the next step's first LDS read, so the
+    // record's HBM latency was exposed right after the line opened; the only reader of nxl waits for
+    // it explicitly (the transition's vmcnt(0)).  An op the compiler does not count can only make its
+    // own vmcnt waits stricter (loads complete in order).
     auto pf_issue = [&](int mm) {
         if (PROOF) return;
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
-        for (int k = 0; k < (PROOF ? 1 : 5); ++k)
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 128 * k),
-                                             (__attribute__((address_space(3))) void*)&nxl[k][0], 16, 0, 0);
+        for (int k = 0; k < (PROOF ? 1 : 5); ++k) {
+            const uint32_t dst = (uint32_t)(uintptr_t)&nxl[k][0];   // LDS byte address (M0; lane l lands at + 16 l)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src + 128 * k), "s"(dst)
+                         : "memory", "m0");
+        }
     };
     if (m < nls) {
         q_cur = lb + mls[0];
@@ -1366,6 +1373,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const CutProg prog = cut_prog_slots(p.scr.cut_prog);
     if (lane == 0) __hip_atomic_store(prog.own, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int partner_done = 0;   // the partner's lines done as read at the previous transition
+    // measured mode: the partner's progress word is fetched by an untracked LDS DMA (lane 0) at the
+    // end of a transition and read at the next one, after its vmcnt(0): as a load into a register the
+    // compiler waited for it at once (a copy into the loop-carried register, then a WAW hazard on
+    // that register at the next step's first LDS read), exposing its HBM latency every transition
+    __shared__ int pslot[1];
+    if (!PROOF && lane == 0) pslot[0] = 0;
     __builtin_amdgcn_s_setprio(2);
 #ifdef GFPL_CUT_PCLOCK   // (diagnostic build: shader-clock cycles per phase of the wave in scr.dbg 0-3:
                          //  step evaluation + decision, exact rounds, bookkeeping, transitions)
@@ -1588,11 +1601,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
             TCK(1);
             {
+                // (measured mode: the word the previous transition's DMA landed, after this
+                // transition's vmcnt(0))
+                if (!PROOF) partner_done = pslot[0];
                 const int done = wave_sum8(j == 0 ? m : 0);
                 if (done > __builtin_amdgcn_readfirstlane(partner_done)) __builtin_amdgcn_s_setprio(0);
                 else __builtin_amdgcn_s_setprio(2);
                 if (lane == 0) __hip_atomic_store(prog.own, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                partner_done = __hip_atomic_load(prog.partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used next time
+                if (PROOF) {
+                    partner_done = __hip_atomic_load(prog.partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used next time
+                } else if (lane == 0) {
+                    const uint32_t dst = (uint32_t)(uintptr_t)&pslot[0];
+                    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off sc1" ::"v"(prog.partner), "s"(dst)
+                                 : "memory", "m0");
+                }
             }
             TCK(2);
         } else if (pend) {

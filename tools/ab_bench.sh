@@ -9,7 +9,7 @@ rm -f $out/.ab_keys
 for d in "$@"; do
   tag=$(basename $d)
   if [ "$d" = default ]; then unset GFPL_LIB_DIR; else export GFPL_LIB_DIR=$(realpath $d); fi
-  timeout -k 10 300 python bench.py --steps $steps --warmup 3 --distinct 16384 --no-cpu --no-detect --no-host-fed --no-b1 --proven-steps 0 \
+  timeout -k 10 300 python bench.py --steps $steps --warmup 3 --batch 16384 --distinct 16384 --no-cpu --no-detect --no-host-fed --no-b1 --proven-steps 0 \
       --parity-seqs 4 > $out/ab_$tag.log 2>&1 || { echo "$tag failed"; tail -5 $out/ab_$tag.log; exit 1; }
   python -c "
 import json; d=json.loads(open('$out/ab_$tag.log').read().strip().splitlines()[-1])

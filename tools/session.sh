@@ -62,7 +62,7 @@ for step in "$@"; do
       cut -d, -f1-4 $O/kernel_stats.csv | head -14 ;;
     dump)
       tag=$(basename $arg)
-      GFPL_LIB_DIR=$(realpath $arg) timeout -k 10 400 python bench.py --steps 3 --warmup 2 --distinct 16384 --no-cpu \
+      GFPL_LIB_DIR=$(realpath $arg) timeout -k 10 400 python bench.py --steps 3 --warmup 2 --batch 16384 --distinct 16384 --no-cpu \
           --no-detect --no-host-fed --no-b1 --proven-steps 0 --parity-seqs 0 --dump-records $O/dump_$tag.npy \
           > $O/dump_$tag.log 2>&1 || { tail -5 $O/dump_$tag.log; exit 1; }
       summary $O/dump_$tag.log
