@@ -73,9 +73,14 @@ __device__ void knn_lut_fill(uint32_t* lut) {
 template <int CELL>
 constexpr int knn_lut_dwords() { return CELL == 2 ? 1024 : 512; }
 
-// A fragment of k-step ks from the LUT (same element order as knn_frag)
+// A fragment of k-step ks from the LUT (same element order as knn_frag).  GFPL_KNN_ALUT 0: formed by
+// VALU instead (knn_frag), under the MFMA's cycles, without the LUT's LDS reads and bank conflicts
+#ifndef GFPL_KNN_ALUT
+#define GFPL_KNN_ALUT 1
+#endif
 template <int CELL>
 __device__ __forceinline__ mfma_v4i knn_frag_lut(const uint32_t* lut, const uint32_t* d, int ks, int h) {
+    if (!GFPL_KNN_ALUT) return knn_frag<CELL, false>(d, ks, h);
     mfma_v4i f;
     if (CELL == 2) {
         const uint32_t v = (d[ks >> 1] >> (8u * (2u * (ks & 1) + (uint32_t)h))) & 0xFFu;

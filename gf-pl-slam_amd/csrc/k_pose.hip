@@ -204,22 +204,28 @@ struct PoseCtx {
     int npt, nls;
 };
 
-// one record: 16-B loads (records are 16-B aligned: 48 / 80 B, the scratch 256-B aligned)
+// one record: 16-B loads (records are 16-B aligned: 48 / 80 B, the scratch 256-B aligned).  The
+// address space is stated: through PoseCtx the compiler lost it for the line records and issued
+// flat loads, which count in lgkmcnt as well — every LDS sync of the chunk loop then waited for the
+// next chunk's prefetch
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const f64x2 g_double2;
 template <int K>
 __device__ __forceinline__ void load_rec(const double* base, int f, double* v) {
-    const double2* r = reinterpret_cast<const double2*>(base + (size_t)K * f);
+    const g_double2* r = (const g_double2*)(base + (size_t)K * f);
 #pragma unroll
     for (int i = 0; i < K / 2; ++i) {
-        const double2 t = r[i];
+        const f64x2 t = r[i];
         v[2 * i] = t.x;
         v[2 * i + 1] = t.y;
     }
 }
+typedef __attribute__((address_space(1))) f64x2 g_double2w;
 template <int K>
 __device__ __forceinline__ void store_rec(double* base, int f, const double* v) {
-    double2* r = reinterpret_cast<double2*>(base + (size_t)K * f);
+    g_double2w* r = (g_double2w*)(base + (size_t)K * f);
 #pragma unroll
-    for (int i = 0; i < K / 2; ++i) r[i] = make_double2(v[2 * i], v[2 * i + 1]);
+    for (int i = 0; i < K / 2; ++i) r[i] = f64x2{v[2 * i], v[2 * i + 1]};
 }
 
 // k_pose<W > 1>: chunk c0 + w of the active entries (points and lines) evaluated into wave w's rows.
