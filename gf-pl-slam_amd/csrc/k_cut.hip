@@ -1133,8 +1133,11 @@ __device__ __forceinline__ CutProg cut_prog_slots(int* base) {
 }
 // REC (PROOF false): record every step's decision for k_cut_verify (proven mode's first pass); a
 // template parameter so that the measured mode's kernel carries none of its registers
+#ifndef GFPL_CUT_WPE
+#define GFPL_CUT_WPE 2   // waves per SIMD (2: 256 VGPRs; LDS allows no more: 19 KB per wave)
+#endif
 template <bool PROOF, bool REC = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_cut_search(KParams p) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CUT_WPE, GFPL_CUT_WPE))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
     __shared__ double sumA[CUT_G][25];          // approximate S of the current line (invCov_sum - its r = 0 info)
