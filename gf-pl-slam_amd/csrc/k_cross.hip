@@ -53,11 +53,19 @@ __global__ void __launch_bounds__(64) k_predict_pose(KParams p) {
     }
 }
 
-// dynamic LDS: cnt[ncell+2] start[ncell+2] i32 | sq[cap] i32 | spx[cap] spy[cap] f32 |
-//              lastT[cap] i32 | prevT[16] Tinv[16] f64 | misc[64] i32
+// dynamic LDS: prevT[16] Tinv[16] f64 | (XL) spxy[cap] f64x2 | cnt[ncell+2] start[ncell+2] i32 |
+//              sq[cap] i32 | spx[cap] spy[cap] f32 | lastT[cap] i32 | misc[64] i32
+// XL: the exact projections of the bucketed points in LDS too (bucket order, beside their float
+// copies), so a candidate that passes the float pre-filter reads them from LDS instead of an L2
+// round trip ahead of its descriptor load; for capacities whose LDS then leaves two workgroups
+// per CU (kp_cap <= 2048)
 #ifndef GFPL_CP_WAVES
 #define GFPL_CP_WAVES 8   // 2 workgroups / CU (84-B spill; 3.2 -> 2.6 ms measured)
 #endif
+#ifndef GFPL_CP_XL
+#define GFPL_CP_XL 1
+#endif
+template <bool XL>
 __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p, CrossGrid G) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
@@ -65,7 +73,8 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
     const int NB = G.ncell + 1;   // buckets incl. wild
     double* prevT = (double*)smem;
     double* Tinv = prevT + 16;
-    int* cnt = (int*)(Tinv + 16);
+    double2* spxy = reinterpret_cast<double2*>(Tinv + 16);   // (XL)
+    int* cnt = (int*)(XL ? reinterpret_cast<double*>(spxy + cap) : Tinv + 16);
     int* start = cnt + NB + 1;
     int* sq = start + NB + 1;
     float* spx = (float*)(sq + cap);
@@ -121,8 +130,10 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
             const int cell = lastT[q];
             const int pos = start[cell] + atomicAdd(&cnt[cell], 1);
             sq[pos] = q;
-            spx[pos] = (float)proj[2 * q];
-            spy[pos] = (float)proj[2 * q + 1];
+            const double ux = proj[2 * q], uy = proj[2 * q + 1];
+            spx[pos] = (float)ux;
+            spy[pos] = (float)uy;
+            if (XL) spxy[pos] = make_double2(ux, uy);
             lastT[q] = -1;
         }
         __syncthreads();
@@ -142,13 +153,22 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
                 uint32_t dt[8];
                 load_desc(Cc.desc + (pb + t) * 32, dt);
                 int bestd = 0x7FFFFFFF;
-                auto consider = [&](int q) {
-                    const double dx = proj[2 * q] - plx, dy = proj[2 * q + 1] - ply;
+                auto consider_at = [&](int q, double ux, double uy) {
+                    const double dx = ux - plx, dy = uy - ply;
                     if (sqrt(dx * dx + dy * dy) > gate) return;   // :536 (NaN passes, as in the reference)
                     uint32_t dq[8];
                     load_desc(PD + (size_t)q * 32, dq);
                     const int d = hamming8<1>(dq, dt);
                     if ((float)d <= radius && (d < bestd || (d == bestd && q < bestq))) { bestd = d; bestq = q; }
+                };
+                auto consider = [&](int q) { consider_at(q, proj[2 * q], proj[2 * q + 1]); };
+                auto consider_k = [&](int k) {   // bucketed entry k
+                    if (XL) {
+                        const double2 u = spxy[k];
+                        consider_at(sq[k], u.x, u.y);
+                    } else {
+                        consider(sq[k]);
+                    }
                 };
                 const bool normal = fabs(plx) < 1e6 && fabs(ply) < 1e6;   // false for NaN too
                 if (normal) {
@@ -159,10 +179,10 @@ __global__ void __launch_bounds__(1024, GFPL_CP_WAVES) k_cross_points(KParams p,
                         const int k1 = start[yy * G.gx + x1 + 1];
                         for (int k = start[yy * G.gx + x0]; k < k1; ++k) {
                             if (fabsf(spx[k] - fx) > fpre || fabsf(spy[k] - fy) > fpre) continue;
-                            consider(sq[k]);
+                            consider_k(k);
                         }
                     }
-                    for (int k = start[G.ncell]; k < start[NB]; ++k) consider(sq[k]);   // wild bucket
+                    for (int k = start[G.ncell]; k < start[NB]; ++k) consider_k(k);   // wild bucket
                 } else {
                     for (int q = 0; q < Sp; ++q) consider(q);   // exact slow path (NaN / huge pl)
                 }
@@ -322,14 +342,22 @@ CrossGrid cross_grid(const KParams& p) {
     return G;
 }
 
-size_t cross_points_lds(const KParams& p, const CrossGrid& G) {
-    return 32 * 8 + (size_t)(G.ncell + 2) * 8 + (size_t)p.kp_cap * 16 + 64 * 4;
+size_t cross_points_lds(const KParams& p, const CrossGrid& G, bool xl) {
+    return 32 * 8 + (size_t)(G.ncell + 2) * 8 + (size_t)p.kp_cap * (xl ? 32 : 16) + 64 * 4;
 }
 
 hipError_t launch_cross_points(const KParams& p, hipStream_t s) {
     const CrossGrid G = cross_grid(p);
     hipLaunchKernelGGL(k_predict_pose, dim3((p.B + 63) / 64), dim3(64), 0, s, p);
-    hipLaunchKernelGGL(k_cross_points, dim3(p.B), dim3(1024), cross_points_lds(p, G), s, p, G);
+    const size_t lxl = cross_points_lds(p, G, true);
+    if (GFPL_CP_XL && p.kp_cap <= 2048 && lxl <= 80 * 1024) {
+        static std::atomic<unsigned long long> attr{0};
+        const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(k_cross_points<true>), (int)lxl, &attr);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_cross_points<true>, dim3(p.B), dim3(1024), lxl, s, p, G);
+    } else {
+        hipLaunchKernelGGL(k_cross_points<false>, dim3(p.B), dim3(1024), cross_points_lds(p, G, false), s, p, G);
+    }
     return hipGetLastError();
 }
 
