@@ -17,6 +17,7 @@
 // dot products are exact whatever the hardware's k permutation inside a step.
 #pragma once
 #include "gfpl_device.hpp"
+#include <type_traits>
 
 namespace gfpl {
 
@@ -110,13 +111,36 @@ __device__ __forceinline__ void knn_stage_soa(uint32_t* T, int stride, const uin
     }
 }
 
-// One knn pass of a workgroup: every query q < nq against the train rows of T
-// (LDS, structure-of-arrays, knn_stage_soa).  Queries are read from Q (global,
-// 32-byte rows).  Writes out_k0[q] = lexicographic minimum key (dist << 16 | t) and, when
-// TOP2, out_k1[q] = the second one.  Waves split the query column tiles.
-// The accumulator starts at the distance offset (128 for HAMMING2 with the query
-// one-hot negated, popc(q) for HAMMING), so the MFMA result IS the distance.
-// lut: knn_lut_fill<CELL> table in LDS.
+// Train rows for knn2_mfma, staged once per workgroup as per-lane-half views: the A fragment of
+// k-step ks on lane half h takes descriptor byte 2 ks + h (CELL 2) or bytes 4 ks + 2 h, +1 (CELL 1),
+// so view h of row t holds, in its dwords j = 0..3, exactly the bytes half h reads for k-steps
+// 4j..4j+3 (CELL 2) / 2j, 2j+1 (CELL 1), in k-step order: V[(4 h + j) * stride + t].  A lane then
+// reads its row's 16 bytes (4 dwords) per tile, and every fragment byte sits at a compile-time
+// position of a view dword (no lane-dependent shifts).
+template <int CELL>
+__device__ __forceinline__ void knn_stage_views(uint32_t* T, int stride, const uint8_t* src, int nt) {
+    constexpr uint32_t S0 = CELL == 2 ? 0x06040200u : 0x05040100u;   // v_perm selectors: bytes of (d[2j+1]:d[2j])
+    constexpr uint32_t S1 = CELL == 2 ? 0x07050301u : 0x07060302u;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    for (int k = threadIdx.x; k < nt * 2; k += blockDim.x) {   // coalesced 16-B reads: dwords 4p .. 4p+3 of row t
+        const uint4 v = s4[k];
+        const int t = k >> 1, j = (k & 1) * 2;
+        T[(0 + j) * stride + t] = __builtin_amdgcn_perm(v.y, v.x, S0);
+        T[(1 + j) * stride + t] = __builtin_amdgcn_perm(v.w, v.z, S0);
+        T[(4 + j) * stride + t] = __builtin_amdgcn_perm(v.y, v.x, S1);
+        T[(5 + j) * stride + t] = __builtin_amdgcn_perm(v.w, v.z, S1);
+    }
+}
+
+// One knn pass of a workgroup: every query q < nq against the train rows of T (LDS,
+// knn_stage_views).  Queries are read from Q (global, 32-byte rows).  Writes out_k0[q] =
+// lexicographic minimum key (dist << 16 | t) and, when TOP2, out_k1[q] = the second one.  Waves
+// split the query column tiles.  The accumulator starts at 0 (the first MFMA takes an inline
+// constant) and the distance offset (128 for HAMMING2 with the query one-hot negated, popc(q) for
+// HAMMING) is added with the keys: acc + off is the distance, and (acc << 16) + (off << 16) its
+// key bits (mod 2^32).
+// lut: knn_lut_fill<CELL> table in LDS — at the start of the caller's LDS, so its base folds into
+// the reads' offset field.
 // inlined into its callers: as a called function its register save area sat in
 // scratch and capped k_stereo_lines at 128 VGPRs (inlined: 121, no scratch; 4.95 -> 4.27 ms)
 #ifndef GFPL_KNN_INLINE
@@ -127,7 +151,10 @@ __device__ __forceinline__ void knn_stage_soa(uint32_t* T, int stride, const uin
 // lexicographic minimum of (dist << 16 | q) over the queries is taken by a DPP row_ror
 // min over the 16 lanes of each lane row, then one LDS atomicMin per lane row into
 // rl_key[t] (initialised to 0xFFFFFFFF by the caller): the knn-1 of the train rows
-// against the queries, the OpenCV tie rule included, without a second MFMA pass.
+// against the queries, the OpenCV tie rule included, without a second MFMA pass.  A padded
+// query column (q >= nq) carries keys above every real one (0x7FFF0000 + dist << 16).
+// The tile epilogue has no per-row branches: the 16 rows' keys and their DPP minima first, then
+// the row leaders' atomics in one branch; full tiles skip the row-bound tests.
 template <int CELL, bool TOP2, bool RL = false>
 __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt, const uint8_t* Q, int nq, uint32_t* out_k0,
                           uint32_t* out_k1, const uint32_t* lut, uint32_t* rl_key = nullptr) {
@@ -136,6 +163,7 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
     const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
     const int h = lane >> 5, c = lane & 31;
     const int nct = (nq + 31) >> 5, nrt = (nt + 31) >> 5;
+    const uint32_t* Th = T + 4 * h * tstride;   // this lane half's view
     for (int ct = wave; ct < nct; ct += nwave) {
         const int q = ct * 32 + c;
         uint32_t qd[8];
@@ -149,47 +177,81 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
         for (int ks = 0; ks < KS; ++ks) {
             bq[ks] = knn_frag<CELL, true>(qd, ks, h);
         }
-        const int off = CELL == 2 ? 128 : popc8(qd);
+        const uint32_t offk = (uint32_t)(CELL == 2 ? 128 : popc8(qd)) << 16;
+        const uint32_t qo = offk + (q < nq ? (uint32_t)q : 0x7FFF0000u);   // (RL)
         uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
         for (int rt = 0; rt < nrt; ++rt) {
             const int t = rt * 32 + c;
-            uint32_t td[8];
+            uint32_t tv[4];
             if (t < nt) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) td[i] = T[i * tstride + t];
+                for (int j = 0; j < 4; ++j) tv[j] = Th[j * tstride + t];
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) td[i] = 0;
+                for (int j = 0; j < 4; ++j) tv[j] = 0;
             }
-            mfma_v16i acc;
+            mfma_v16i acc = {};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = off;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(knn_frag_lut<CELL>(lut, td, ks, h), bq[ks], acc, 0, 0, 0);
-            const uint32_t tb = (uint32_t)(rt * 32 + 4 * h);
-            const bool full = rt * 32 + 32 <= nt;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const uint32_t tr = tb + (uint32_t)((r & 3) + 8 * (r >> 2));
-                uint32_t key = ((uint32_t)acc[r] << 16) + tr;
-                if (!full && (int)tr >= nt) key = 0xFFFFFFFFu;
-                if (TOP2) {
-                    const uint32_t hi = max(k0, key);
-                    k0 = min(k0, key);
-                    k1 = min(k1, hi);
+            for (int ks = 0; ks < KS; ++ks) {
+                mfma_v4i f;
+                if (CELL == 2) {
+                    const uint32_t v = (tv[ks >> 2] >> (8 * (ks & 3))) & 0xFFu;
+                    const uint4 e = *reinterpret_cast<const uint4*>(lut + 4 * v);
+                    f[0] = (int)e.x; f[1] = (int)e.y; f[2] = (int)e.z; f[3] = (int)e.w;
                 } else {
-                    k0 = min(k0, key);
+                    const uint32_t w = tv[ks >> 1] >> (16 * (ks & 1));
+                    const uint2 lo = *reinterpret_cast<const uint2*>(lut + 2 * (w & 0xFFu));
+                    const uint2 hi = *reinterpret_cast<const uint2*>(lut + 2 * ((w >> 8) & 0xFFu));
+                    f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)hi.x; f[3] = (int)hi.y;
                 }
-                if (RL) {
-                    uint32_t v = q < nq ? (((uint32_t)acc[r] << 16) | (uint32_t)q) : 0xFFFFFFFFu;
-                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
-                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
-                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
-                    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
-                    if ((lane & 15) == 0 && (int)tr < nt) atomicMin(&rl_key[tr], v);
-                }
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, bq[ks], acc, 0, 0, 0);
             }
+            const uint32_t tb = (uint32_t)(rt * 32 + 4 * h);
+            const uint32_t tko = offk + tb;
+            // rows in two groups of 8: each row's keys and DPP minimum, then the group's atomics by
+            // the row leaders in one branch (8 live minima, not 16); a full tile (wave-uniform) has no
+            // row-bound tests
+            auto epilogue = [&](auto chk_t) {
+                constexpr bool chk = decltype(chk_t)::value;
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int r = 8 * g; r < 8 * g + 8; ++r) {
+                        const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
+                        const uint32_t sh = (uint32_t)acc[r] << 16;
+                        uint32_t key = sh + tko + ro;
+                        if (chk && (int)(tb + ro) >= nt) key = 0xFFFFFFFFu;
+                        if (TOP2) {
+                            const uint32_t hi = max(k0, key);
+                            k0 = min(k0, key);
+                            k1 = min(k1, hi);
+                        } else {
+                            k0 = min(k0, key);
+                        }
+                        if (RL) {
+                            uint32_t x = sh + qo;
+                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xF, 0xF, false));   // row_ror:1
+                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xF, 0xF, false));   // row_ror:2
+                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xF, 0xF, false));   // row_ror:4
+                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xF, 0xF, false));   // row_ror:8
+                            // (computed here by every lane: sunk into the leaders' branch, the last step was a
+                            // separate v_mov_dpp + v_min with its own -1 old value)
+                            asm volatile("" : "+v"(x));
+                            v[r - 8 * g] = x;
+                        }
+                    }
+                    if (RL && (lane & 15) == 0) {
+#pragma unroll
+                        for (int r = 8 * g; r < 8 * g + 8; ++r) {
+                            const uint32_t tr = tb + (uint32_t)((r & 3) + 8 * (r >> 2));
+                            if (!chk || (int)tr < nt) atomicMin(&rl_key[tr], v[r - 8 * g]);
+                        }
+                    }
+                }
+            };
+            if (rt * 32 + 32 <= nt) epilogue(std::false_type{});   // (wave-uniform)
+            else epilogue(std::true_type{});
         }
         // the two lane halves hold disjoint train rows of the same query column
         const uint32_t o0 = __shfl_xor(k0, 32, 64);

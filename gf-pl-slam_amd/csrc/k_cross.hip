@@ -235,7 +235,7 @@ __device__ int hist_rank_c(const int* h, int r) {
     return 256;
 }
 
-// dynamic LDS: tb[cap*8] u32 (train rows: curr for 12, then prev for 21) |
+// dynamic LDS: knn LUT | tb[cap*8] u32 (train rows: curr, knn_stage_views) |
 //              i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
 #ifndef GFPL_CL_WAVES
 #define GFPL_CL_WAVES 1
@@ -245,7 +245,8 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
-    uint32_t* tb = (uint32_t*)smem;
+    uint32_t* lut = (uint32_t*)smem;   // (first: a compile-time LDS address, folded into the reads' offsets)
+    uint32_t* tb = lut + knn_lut_dwords<1>();
     int* i12 = (int*)(tb + cap * 8);
     int* d012 = i12 + cap;
     int* d112 = d012 + cap;
@@ -253,7 +254,6 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
     int* h12 = i21 + cap;
     int* h0 = h12 + 260;
     int* misc = h0 + 260;
-    uint32_t* lut = (uint32_t*)(misc + 64);
     const int tid = threadIdx.x;
     const int Sl = p.prev.ls.n[b], Sc = p.curr.ls.n[b];
     int total = 0;
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         const size_t pb = (size_t)b * cap;
         const uint8_t* DP = P.desc + pb * 32;
         const uint8_t* DC = Cc.desc + pb * 32;
-        knn_stage_soa(tb, cap, DC, Sc);
+        knn_stage_views<1>(tb, cap, DC, Sc);
         for (int i = tid; i < 520; i += blockDim.x) h12[i] = 0;
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = -1;   // 21 keys (atomicMin)
         knn_lut_fill<1>(lut);

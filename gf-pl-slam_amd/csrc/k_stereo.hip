@@ -944,8 +944,8 @@ __device__ int hist_rank(const int* h, int r) {
     return 256;
 }
 
-// dynamic LDS: tb[cap*8] u32 (train rows: R for L->R, then L for R->L) |
-//              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64] | knn LUT
+// dynamic LDS: knn LUT | tb[cap*8] u32 (train rows R, knn_stage_views) |
+//              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
 // Query rows stream from HBM into registers; only the train set sits in LDS, so
 // 2000 lines per side (config 5) fit.
 template <int CELL, bool INITIAL, int BLOCK>
@@ -953,14 +953,14 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     extern __shared__ __align__(16) unsigned char smem[];
     const int b = blockIdx.x;
     const int cap = p.kl_cap;
-    uint32_t* tb = (uint32_t*)smem;
+    uint32_t* lut = (uint32_t*)smem;   // (first: a compile-time LDS address, folded into the reads' offsets)
+    uint32_t* tb = lut + knn_lut_dwords<CELL>();
     int* lr_i = (int*)(tb + cap * 8);
     int* lr_d0 = lr_i + cap;
     int* lr_d1 = lr_d0 + cap;
     int* rl_i = lr_d1 + cap;
     int* hist = rl_i + cap;
     int* misc = hist + 260;
-    uint32_t* lut = (uint32_t*)(misc + 64);
     const int tid = threadIdx.x;
     const int NL = min(p.in.n_kl_l[b], cap), NR = min(p.in.n_kl_r[b], cap);
     DevLines& C = p.curr.ls;   // INITIAL writes the slot passed as curr
@@ -971,7 +971,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     const uint8_t* DLg = p.in.ldesc_l + (size_t)b * cap * 32;
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
     SL_PRIO(3);   // issue priority by phase (as k_stereo_points: the last-dispatched workgroups keep up)
-    knn_stage_soa(tb, cap, DRg, NR);
+    knn_stage_views<CELL>(tb, cap, DRg, NR);
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = -1;   // R->L keys (atomicMin)
     knn_lut_fill<CELL>(lut);
