@@ -148,13 +148,13 @@ __device__ __forceinline__ void knn_stage_views(uint32_t* T, int stride, const u
 #endif
 // RL (the reverse direction in the same pass): Hamming distance is symmetric, so tile
 // (t, q) also holds the train-side query's distances — for every train row t the
-// lexicographic minimum of (dist << 16 | q) over the queries is taken by a DPP row_ror
-// min over the 16 lanes of each lane row, then one LDS atomicMin per lane row into
+// lexicographic minimum of (dist << 16 | q) over the queries is taken over the 16 lanes of each
+// DPP row by a reduce-scatter (in the epilogue), then one LDS atomicMin per lane into
 // rl_key[t] (initialised to 0xFFFFFFFF by the caller): the knn-1 of the train rows
 // against the queries, the OpenCV tie rule included, without a second MFMA pass.  A padded
 // query column (q >= nq) carries keys above every real one (0x7FFF0000 + dist << 16).
-// The tile epilogue has no per-row branches: the 16 rows' keys and their DPP minima first, then
-// the row leaders' atomics in one branch; full tiles skip the row-bound tests.
+// The tile epilogue has no per-row branches (round 6: 356 -> 180 VALU per tile); full tiles skip
+// the row-bound tests.
 template <int CELL, bool TOP2, bool RL = false>
 __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt, const uint8_t* Q, int nq, uint32_t* out_k0,
                           uint32_t* out_k1, const uint32_t* lut, uint32_t* rl_key = nullptr) {
@@ -164,6 +164,9 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
     const int h = lane >> 5, c = lane & 31;
     const int nct = (nq + 31) >> 5, nrt = (nt + 31) >> 5;
     const uint32_t* Th = T + 4 * h * tstride;   // this lane half's view
+    const int pr = lane & 15;   // position in the 16-lane DPP row: the train row (of the lane half) it reduces
+    const bool rb3 = (pr & 8) != 0, rb2 = (pr & 4) != 0, rb1 = (pr & 2) != 0, rb0 = (pr & 1) != 0;
+    const uint32_t lro = (uint32_t)(4 * h + (pr & 3) + 8 * (pr >> 2));
     for (int ct = wave; ct < nct; ct += nwave) {
         const int q = ct * 32 + c;
         uint32_t qd[8];
@@ -208,47 +211,50 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
             }
             const uint32_t tb = (uint32_t)(rt * 32 + 4 * h);
             const uint32_t tko = offk + tb;
-            // rows in two groups of 8: each row's keys and DPP minimum, then the group's atomics by
-            // the row leaders in one branch (8 live minima, not 16); a full tile (wave-uniform) has no
-            // row-bound tests
+            // RL by a reduce-scatter over each 16-lane DPP row: four exchange steps (row_mirror,
+            // row_half_mirror, quad_perm 3210, quad_perm 1032: partners p ^ 15, p ^ 7, p ^ 3, p ^ 1)
+            // each halve the rows a lane carries — it keeps the half its lane bit selects and takes
+            // the partner's minimum of that half — so lane p ends with the 16-lane minimum of row p
+            // (45 operations instead of 16 rows x 4 DPP minima), and every lane does one atomic
             auto epilogue = [&](auto chk_t) {
                 constexpr bool chk = decltype(chk_t)::value;
-#pragma unroll
-                for (int g = 0; g < 2; ++g) {
-                    uint32_t v[8];
-#pragma unroll
-                    for (int r = 8 * g; r < 8 * g + 8; ++r) {
-                        const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
-                        const uint32_t sh = (uint32_t)acc[r] << 16;
-                        uint32_t key = sh + tko + ro;
-                        if (chk && (int)(tb + ro) >= nt) key = 0xFFFFFFFFu;
-                        if (TOP2) {
-                            const uint32_t hi = max(k0, key);
-                            k0 = min(k0, key);
-                            k1 = min(k1, hi);
-                        } else {
-                            k0 = min(k0, key);
-                        }
-                        if (RL) {
-                            uint32_t x = sh + qo;
-                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xF, 0xF, false));   // row_ror:1
-                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xF, 0xF, false));   // row_ror:2
-                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xF, 0xF, false));   // row_ror:4
-                            x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xF, 0xF, false));   // row_ror:8
-                            // (computed here by every lane: sunk into the leaders' branch, the last step was a
-                            // separate v_mov_dpp + v_min with its own -1 old value)
-                            asm volatile("" : "+v"(x));
-                            v[r - 8 * g] = x;
-                        }
+                auto top2 = [&](int r, uint32_t sh) {
+                    const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
+                    uint32_t key = sh + tko + ro;
+                    if (chk && (int)(tb + ro) >= nt) key = 0xFFFFFFFFu;
+                    if (TOP2) {
+                        const uint32_t hi = max(k0, key);
+                        k0 = min(k0, key);
+                        k1 = min(k1, hi);
+                    } else {
+                        k0 = min(k0, key);
                     }
-                    if (RL && (lane & 15) == 0) {
+                };
+                if (!RL) {
 #pragma unroll
-                        for (int r = 8 * g; r < 8 * g + 8; ++r) {
-                            const uint32_t tr = tb + (uint32_t)((r & 3) + 8 * (r >> 2));
-                            if (!chk || (int)tr < nt) atomicMin(&rl_key[tr], v[r - 8 * g]);
-                        }
-                    }
+                    for (int r = 0; r < 16; ++r) top2(r, (uint32_t)acc[r] << 16);
+                    return;
                 }
+                auto xchg = [](uint32_t a, uint32_t b, bool upper, auto ctrl_t) {   // keep one, take the partner's other
+                    const uint32_t send = upper ? a : b, keep = upper ? b : a;
+                    return min(keep, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)send, decltype(ctrl_t)::value, 0xF, 0xF, false));
+                };
+                uint32_t y[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t s0 = (uint32_t)acc[j] << 16, s1 = (uint32_t)acc[j + 8] << 16;
+                    top2(j, s0);
+                    top2(j + 8, s1);
+                    y[j] = xchg(s0 + qo, s1 + qo, rb3, std::integral_constant<int, 0x140>{});   // row_mirror
+                }
+                uint32_t z[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) z[j] = xchg(y[j], y[j + 4], rb2, std::integral_constant<int, 0x141>{});   // row_half_mirror
+                const uint32_t w0 = xchg(z[0], z[2], rb1, std::integral_constant<int, 0x1B>{});   // quad_perm 3210
+                const uint32_t w1 = xchg(z[1], z[3], rb1, std::integral_constant<int, 0x1B>{});
+                const uint32_t f = xchg(w0, w1, rb0, std::integral_constant<int, 0xB1>{});       // quad_perm 1032
+                const uint32_t tr = (uint32_t)(rt * 32) + lro;
+                if (!chk || (int)tr < nt) atomicMin(&rl_key[tr], f);
             };
             if (rt * 32 + 32 <= nt) epilogue(std::false_type{});   // (wave-uniform)
             else epilogue(std::true_type{});
