@@ -139,8 +139,8 @@ __device__ __forceinline__ void knn_stage_views(uint32_t* T, int stride, const u
 // constant) and the distance offset (128 for HAMMING2 with the query one-hot negated, popc(q) for
 // HAMMING) is added with the keys: acc + off is the distance, and (acc << 16) + (off << 16) its
 // key bits (mod 2^32).
-// lut: knn_lut_fill<CELL> table in LDS — at the start of the caller's LDS, so its base folds into
-// the reads' offset field.
+// lut: knn_lut_fill<CELL> table in LDS — at LDS address 0 (the start of the caller's dynamic LDS,
+// with no static LDS in the kernel): the reads use that address directly.
 // inlined into its callers: as a called function its register save area sat in
 // scratch and capped k_stereo_lines at 128 VGPRs (inlined: 121, no scratch; 4.95 -> 4.27 ms)
 #ifndef GFPL_KNN_INLINE
@@ -163,6 +163,14 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
     const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
     const int h = lane >> 5, c = lane & 31;
     const int nct = (nq + 31) >> 5, nrt = (nt + 31) >> 5;
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const u32x4v lds_cu4;
+    typedef __attribute__((address_space(3))) const u32x2v lds_cu2;
+    // the table's LDS address: both callers place it first in their dynamic LDS and have no static
+    // LDS, so it is 0 (as a constant the address of a table entry is one SDWA shift of the byte)
+    constexpr uint32_t lb = 0;
+    (void)lut;
     const uint32_t* Th = T + 4 * h * tstride;   // this lane half's view
     const int pr = lane & 15;   // position in the 16-lane DPP row: the train row (of the lane half) it reduces
     const bool rb3 = (pr & 8) != 0, rb2 = (pr & 4) != 0, rb1 = (pr & 2) != 0, rb0 = (pr & 1) != 0;
@@ -186,7 +194,10 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
         for (int rt = 0; rt < nrt; ++rt) {
             const int t = rt * 32 + c;
             uint32_t tv[4];
-            if (t < nt) {
+            if (rt * 32 + 32 <= nt) {   // (wave-uniform: a full tile loads without bound tests)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tv[j] = Th[j * tstride + t];
+            } else if (t < nt) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) tv[j] = Th[j * tstride + t];
             } else {
@@ -196,15 +207,19 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
             mfma_v16i acc = {};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
+                // table reads at integer LDS addresses (lut is at LDS offset 0): a byte's address is
+                // then one shift with an SDWA byte select
                 mfma_v4i f;
                 if (CELL == 2) {
-                    const uint32_t v = (tv[ks >> 2] >> (8 * (ks & 3))) & 0xFFu;
-                    const uint4 e = *reinterpret_cast<const uint4*>(lut + 4 * v);
+                    const uint32_t a = lb + (((tv[ks >> 2] >> (8 * (ks & 3))) & 0xFFu) << 4);
+                    const u32x4v e = *reinterpret_cast<lds_cu4*>((uintptr_t)a);
                     f[0] = (int)e.x; f[1] = (int)e.y; f[2] = (int)e.z; f[3] = (int)e.w;
                 } else {
-                    const uint32_t w = tv[ks >> 1] >> (16 * (ks & 1));
-                    const uint2 lo = *reinterpret_cast<const uint2*>(lut + 2 * (w & 0xFFu));
-                    const uint2 hi = *reinterpret_cast<const uint2*>(lut + 2 * ((w >> 8) & 0xFFu));
+                    const uint32_t w = tv[ks >> 1];
+                    const uint32_t alo = lb + (((w >> (16 * (ks & 1))) & 0xFFu) << 3);
+                    const uint32_t ahi = lb + (((w >> (16 * (ks & 1) + 8)) & 0xFFu) << 3);
+                    const u32x2v lo = *reinterpret_cast<lds_cu2*>((uintptr_t)alo);
+                    const u32x2v hi = *reinterpret_cast<lds_cu2*>((uintptr_t)ahi);
                     f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)hi.x; f[3] = (int)hi.y;
                 }
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, bq[ks], acc, 0, 0, 0);
@@ -222,10 +237,9 @@ __device__ GFPL_KNN_INLINE void knn2_mfma(const uint32_t* T, int tstride, int nt
                     const uint32_t ro = (uint32_t)((r & 3) + 8 * (r >> 2));
                     uint32_t key = sh + tko + ro;
                     if (chk && (int)(tb + ro) >= nt) key = 0xFFFFFFFFu;
-                    if (TOP2) {
-                        const uint32_t hi = max(k0, key);
+                    if (TOP2) {   // k0 <= k1: the new second key is med3(k0, k1, key)
+                        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(k1) : "v"(k0), "v"(k1), "v"(key));
                         k0 = min(k0, key);
-                        k1 = min(k1, hi);
                     } else {
                         k0 = min(k0, key);
                     }
