@@ -871,6 +871,39 @@ GFPL_DEV double overlapStereo(double spl_obs, double epl_obs, double spl_proj, d
 
 // --------------------------------------------------------- block helpers
 // exclusive prefix sum of one int per thread over the block (blockDim <= 1024)
+// The value at rank r (0-based) of a histogram h[0 .. nb) of small integers (nb <= 320): the first v
+// with h[0] + ... + h[v] > r, or nb - 1 when the total is <= r — called by a whole wave, the result in
+// every lane.  Five bins per lane, a wave prefix sum, the crossing lane scans its bins: one LDS read
+// per lane instead of a one-thread loop of nb dependent reads (round 6).
+__device__ __forceinline__ int wave_hist_rank(const int* h, int r, int nb) {
+    const int lane = threadIdx.x & 63;
+    int loc[5], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int v = lane * 5 + i;
+        loc[i] = v < nb ? h[v] : 0;
+        sum += loc[i];
+    }
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    int res = 0x7FFFFFFF;
+    if (inc - sum <= r && r < inc) {
+        int c = inc - sum;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            c += loc[i];
+            if (c > r && res == 0x7FFFFFFF) res = lane * 5 + i;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) res = min(res, __shfl_xor(res, o, 64));
+    return res == 0x7FFFFFFF ? nb - 1 : res;
+}
+
 template <int BLOCK>
 GFPL_DEV int block_exclusive_scan(int v, int* lds /* >= BLOCK/64 + 1 ints */, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;

@@ -229,11 +229,6 @@ __device__ __forceinline__ void knn2_lds(const uint32_t* q, const uint32_t* T, i
     i0 = idx0; d0 = dist0; d1 = dist1;
 }
 
-__device__ int hist_rank_c(const int* h, int r) {
-    int c = 0;
-    for (int v = 0; v <= 256; ++v) { c += h[v]; if (c > r) return v; }
-    return 256;
-}
 
 // dynamic LDS: knn LUT | tb[cap*8] u32 (train rows: curr, knn_stage_views) |
 //              i12 d0 d1 i21 [cap] | h12[260] h0[260] | misc[64]
@@ -281,11 +276,15 @@ __global__ void __launch_bounds__(BLOCK, GFPL_CL_WAVES) k_cross_lines(KParams p)
         }
         for (int j = tid; j < Sc; j += blockDim.x) i21[j] = (int)((uint32_t)i21[j] & 0xFFFFu);
         __syncthreads();
-        if (tid == 0) {
-            const int v = hist_rank_c(h12, Sl / 2);
-            reinterpret_cast<double*>(misc + 16)[0] = (1.4826 * (double)(float)v) * p.cfg.desc_th_l;
-            const int k = min(p.cfg.max_line_match_num, Sl) - 1;
-            reinterpret_cast<double*>(misc + 16)[1] = (double)(float)hist_rank_c(h0, k);
+        if (tid < 128) {   // (waves 0 and 1: the two medians side by side)
+            if (tid < 64) {
+                const int v = wave_hist_rank(h12, Sl / 2, 257);
+                if (tid == 0) reinterpret_cast<double*>(misc + 16)[0] = (1.4826 * (double)(float)v) * p.cfg.desc_th_l;
+            } else {
+                const int k = min(p.cfg.max_line_match_num, Sl) - 1;
+                const int v = wave_hist_rank(h0, k, 257);
+                if (tid == 64) reinterpret_cast<double*>(misc + 16)[1] = (double)(float)v;
+            }
         }
         __syncthreads();
         const double nn12 = reinterpret_cast<double*>(misc + 16)[0];

@@ -432,7 +432,11 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     // order[t] / pairs[iL] are private to the thread that owns slot t.
     auto finish_kp = [&](int t, int iL, const gfpl_keypoint& kpL, int bestDist, int bestIdxR) {
         uint32_t job = 0xFFFFFFFFu;
+#ifdef GFPL_SP_PROBE_NOSAD   // timing probe only (wrong output): no sub-pixel jobs
+        if (bestDist < 0) {
+#else
         if (bestDist < 80) {
+#endif
             atomicAdd(&misc[2], 1);
             SadJob J;
             // job: iL | uL << 16 (order[t]); bestDist | o << 7 | vL << 10 | uR << 21
@@ -507,7 +511,11 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                             const int minr = (int)((k >> 16) & 0xFFFu) - 1024;
                             const int iR = (int)(k & 0xFFFFu);
                             const uint32_t dr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#ifdef GFPL_SP_PROBE_NOHAM   // timing probe only (wrong output): the band scan without its distances
+                            const uint32_t key = ((uint32_t)(90 + (dr[0] & dl[0] & 1u)) << 16) | (uint32_t)iR;
+#else
                             const uint32_t key = ((uint32_t)hamming8<1>(dl, dr) << 16) | (uint32_t)iR;
+#endif
                             // the tests as one mask and the minimum as a select: no branch around the distance
                             bool pass = (minr + (int)(m >> 8) >= row) & (uR >= minU) & (uR <= maxU);   // maxr >= row
                             if (!decltype(oseg)::value) {
@@ -937,17 +945,17 @@ __device__ __forceinline__ void knn2_row(const uint32_t* q, const uint32_t* T, i
     i0 = idx0; d0 = dist0; d1 = dist1;
 }
 
-// histogram median helper: value at rank r (0-based) of a histogram h[0..256]
-__device__ int hist_rank(const int* h, int r) {
-    int c = 0;
-    for (int v = 0; v <= 256; ++v) { c += h[v]; if (c > r) return v; }
-    return 256;
-}
-
 // dynamic LDS: knn LUT | tb[cap*8] u32 (train rows R, knn_stage_views) |
 //              lr_i[cap] lr_d0 lr_d1 rl_i | hist[260] | misc[64]
 // Query rows stream from HBM into registers; only the train set sits in LDS, so
 // 2000 lines per side (config 5) fit.
+// diagnostic build (-DGFPL_SL_CLOCK): the phase boundaries' wall clock per sequence (scr.dbg): start,
+// train rows staged, knn pass, medians, end (tools/sp_phases.py --lines)
+#ifdef GFPL_SL_CLOCK
+#define SL_CLK(k) do { if (threadIdx.x == 0 && !INITIAL) p.scr.dbg[8 * (size_t)blockIdx.x + (k)] = (int64_t)wall_clock64(); } while (0)
+#else
+#define SL_CLK(k) do { } while (0)
+#endif
 template <int CELL, bool INITIAL, int BLOCK>
 __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -970,16 +978,19 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     }
     const uint8_t* DLg = p.in.ldesc_l + (size_t)b * cap * 32;
     const uint8_t* DRg = p.in.ldesc_r + (size_t)b * cap * 32;
+    SL_CLK(0);
     SL_PRIO(3);   // issue priority by phase (as k_stereo_points: the last-dispatched workgroups keep up)
     knn_stage_views<CELL>(tb, cap, DRg, NR);
     for (int i = tid; i < 260; i += blockDim.x) hist[i] = 0;
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = -1;   // R->L keys (atomicMin)
     knn_lut_fill<CELL>(lut);
     __syncthreads();
+    SL_CLK(1);
     // L->R knn-2 on the matrix cores (gfpl_knn.hpp): keys (dist << 16 | iR); the R->L knn
     // (only its best index is used) from the same distance tiles (RL)
     knn2_mfma<CELL, true, true>(tb, cap, NR, DLg, NL, (uint32_t*)lr_i, (uint32_t*)lr_d1, lut, (uint32_t*)rl_i);
     __syncthreads();
+    SL_CLK(2);
     SL_PRIO(1);
     for (int i = tid; i < NL; i += blockDim.x) {
         const uint32_t k0 = (uint32_t)lr_i[i], k1 = (uint32_t)lr_d1[i];
@@ -989,13 +1000,16 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
     }
     for (int j = tid; j < NR; j += blockDim.x) rl_i[j] = (int)((uint32_t)rl_i[j] & 0xFFFFu);
     __syncthreads();
-    if (tid == 0) {
-        const int v = hist_rank(hist, NL / 2);
-        double th = (1.4826 * (double)(float)v) * p.cfg.desc_th_l;
-        reinterpret_cast<double*>(misc + 8)[0] = th;
+    if (tid < 64) {   // (wave 0)
+        const int v = wave_hist_rank(hist, NL / 2, 257);
+        if (tid == 0) {
+            double th = (1.4826 * (double)(float)v) * p.cfg.desc_th_l;
+            reinterpret_cast<double*>(misc + 8)[0] = th;
+        }
     }
     __syncthreads();
     const double nn12_dist_th = reinterpret_cast<double*>(misc + 8)[0];
+    SL_CLK(3);
     const int n_matches = min(NL, NR);   // Q5
     const gfpl_keyline* KL = p.in.kl_l + (size_t)b * cap;
     const gfpl_keyline* KR = p.in.kl_r + (size_t)b * cap;
@@ -1018,6 +1032,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SL_WAVES) k_stereo_lines(KParams p
         off += tot;
     }
     if (tid == 0) C.n[b] = off;
+    SL_CLK(4);
 }
 
 // ------------------------------------------------------- knn2 (global) --
