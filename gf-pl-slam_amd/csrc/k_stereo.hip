@@ -533,6 +533,14 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
                 else walk(std::false_type{});
             }
             const int bestDist = (int)(best >> 16), bestIdxR = (int)(best & 0xFFFFu);
+#ifdef GFPL_SP_PROBE_NOSAD   // (keeps the scan live: its keys folded into a diagnostic word)
+            {
+                uint32_t xk = best;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) xk ^= __shfl_xor(xk, o);
+                if (lane == 0) p.scr.dbg[8 * (size_t)b + 7] += (int64_t)xk;
+            }
+#endif
             if (t < N) finish_kp(t, iL, kpL, bestDist, bestIdxR);
         }
     } else {
