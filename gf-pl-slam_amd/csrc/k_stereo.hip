@@ -665,6 +665,10 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
             J.img = p.in.pyr_r + (size_t)b * (size_t)p.cam.pyr_bytes;
             J.lvl = p.cam.lvl_offset[J.o];
             J.scaleduR0 = (float)J.uR;
+#ifdef GFPL_SP_PROBE_SAMEWIN   // timing probe only (wrong output): every job reads one window (L1 hits)
+            J.o = 0; J.vL = 20; J.uL = 60; J.uR = 40;
+            J.cols = p.cam.lvl_cols[0]; J.lvl = p.cam.lvl_offset[0];
+#endif
             sad_rows(J, q, acc);
         }
 #pragma unroll
