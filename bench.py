@@ -9,8 +9,9 @@ maxIters = maxItersRef = 10 and minError = minErrorChange = 0.
 
 A "step" = one StereoFrameHandler step (insertStereoPair + optimizePose +
 updateFrame, app/plslam_mod.cpp:387-477) for every one of the B independent
-sequences resident on a GPU (B = 32768 by default, independent of --steps; ~70 GB of the
-288 GB HBM with both staging buffers).
+sequences resident on a GPU (B = 65536 by default, independent of --steps; ~140 GB of the
+288 GB HBM with both staging buffers: every kernel's grid tail is amortised over more waves —
+DESIGN.md §5g, 741.6k / 759.9k / 774.4k frames/s at 32768 / 49152 / 65536 on one box).
 
 Input ring: before each step the host generates the next input frame of all B
 sequences (splitmix64, deterministic; gfpl_synth) chunk by chunk into a ring of
@@ -95,7 +96,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32768, help="sequences per GPU (reduced only if HBM is short)")
+    ap.add_argument("--batch", type=int, default=65536, help="sequences per GPU (reduced only if HBM is short)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-detect", action="store_true", help="skip the ORB / LBD detection rates")
     ap.add_argument("--gen-threads", type=int, default=16,
