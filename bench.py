@@ -694,7 +694,8 @@ def main():
     B, W, K = args.batch, args.warmup, args.steps
     KP, KL = (8192, 2048) if args.workload == "cfg5" else (2048, 512)
     keep = []
-    n_frames_needed = W + K + 3   # init + warmup + timed + the two host-fed frames
+    # init + warmup + timed + the proven leg's (one untimed + --proven-steps) + the two host-fed frames
+    n_frames_needed = W + K + 3 + (args.proven_steps + 1 if args.proven_steps > 0 else 0)
     if args.workload == "cfg4":
         if n_frames_needed > gfpl.EUROC_MAX_POSES:
             print(f"error: cfg4 needs {n_frames_needed} ground-truth poses, {gfpl.EUROC_MAX_POSES} stored",

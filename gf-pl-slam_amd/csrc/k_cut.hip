@@ -1136,18 +1136,26 @@ __device__ __forceinline__ CutProg cut_prog_slots(int* base) {
 #ifndef GFPL_CUT_WPE
 #define GFPL_CUT_WPE 2   // waves per SIMD (2: 256 VGPRs; LDS allows no more: 19 KB per wave)
 #endif
+// GFPL_CUT_NOPF (experiment): no next-line record prefetch (measured mode reads the record from HBM when
+// the line opens, as proven mode does) and 21-double sum rows: 13.5 KB of LDS per wave, so that three
+// waves fit a SIMD (with GFPL_CUT_WPE 3)
+#ifndef GFPL_CUT_NOPF
+#define GFPL_CUT_NOPF 0
+#endif
+#define CUT_SSTR (GFPL_CUT_NOPF ? 21 : 25)   // sum row stride (doubles; odd multiples of 2 banks apart)
 template <bool PROOF, bool REC = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CUT_WPE, GFPL_CUT_WPE))) k_cut_search(KParams p) {
     // per-group rows padded to odd strides so the 8 groups of a wave sit in
     // different LDS banks when their lanes read the same entry
-    __shared__ double sumA[CUT_G][25];          // approximate S of the current line (invCov_sum - its r = 0 info)
-    __shared__ double sumE[CUT_G][25];          // exact invCov_sum before line m_sync (lazy, for exact steps)
+    __shared__ double sumA[CUT_G][CUT_SSTR];    // approximate S of the current line (invCov_sum - its r = 0 info)
+    __shared__ double sumE[CUT_G][CUT_SSTR];    // exact invCov_sum before line m_sync (lazy, for exact steps)
     __shared__ double fst[CUT_G][CUT_FAST + 1]; // comparison data of the current line
     // next-line records, written by LDS-DMA: 16-B piece k of group g's record lands at
     // nxl[k][16 g + ...] (the DMA writes base + 16 * lane)
     // (proven mode: no prefetch buffer — its v'-tables take the LDS, and 5 KB more would cost the
     // eighth wave of a CU; the record is read from HBM when the line opens)
-    __shared__ __attribute__((aligned(16))) double nxl[PROOF ? 1 : 5][128];
+    constexpr bool PF = !PROOF && !GFPL_CUT_NOPF;   // the next-line record prefetch (measured mode)
+    __shared__ __attribute__((aligned(16))) double nxl[PF ? 5 : 1][PF ? 128 : 2];
     // per-group scratch, used either by an exact step (X) or by a line open, never both at once:
     //   X:    exact endpoints of the step's six slots [CUT_EP] | exact S / flush endpoints [25]
     //   open: W coefficient vectors [side * 3 + k][6] (36) | their Gram matrix, lower triangle (21)
@@ -1348,10 +1356,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CU
     // it explicitly (the transition's vmcnt(0)).  An op the compiler does not count can only make its
     // own vmcnt waits stricter (loads complete in order).
     auto pf_issue = [&](int mm) {
-        if (PROOF) return;
+        if (!PF) return;
         const char* src = reinterpret_cast<const char*>(rec_l + (size_t)mm * CUT_REC) + 16 * j;
 #pragma unroll
-        for (int k = 0; k < (PROOF ? 1 : 5); ++k) {
+        for (int k = 0; k < (PF ? 5 : 0); ++k) {
             const uint32_t dst = (uint32_t)(uintptr_t)&nxl[k][0];   // LDS byte address (M0; lane l lands at + 16 l)
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src + 128 * k), "s"(dst)
                          : "memory", "m0");
@@ -1554,11 +1562,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CU
                     }
                 }
                 // line m from its prefetched record (the DMA was issued >= 1 iteration ago)
-                if (PROOF) {
+                if (!PF) {
 #pragma unroll
                     for (int k = 0; k < CUT_FAST / 8; ++k) fst[g][j + 8 * k] = rec_l[(size_t)m * CUT_REC + j + 8 * k];
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (!PROOF) {
+                    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (j == 0) {   // the finished line's cut (deferred from its finalisation)
                         L.cut[2 * q_cur] = r0;
                         L.cut[2 * q_cur + 1] = r1;
@@ -1567,9 +1576,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CU
                         *reinterpret_cast<unsigned long long*>(path + (size_t)(m - 1) * CUT_PATH + 8 * j) =
                             *reinterpret_cast<const unsigned long long*>(&pth[g][8 * j]);
 #pragma unroll
-                    for (int k = 0; k < CUT_FAST / 8; ++k) {
+                    for (int k = 0; k < (PF ? CUT_FAST / 8 : 0); ++k) {
                         const int e = j + 8 * k;
-                        // (proven mode: the entries past the prefetched pieces from HBM)
                         fst[g][e] = nxl[e >> 4][16 * g + (e & 15)];
                     }
                 }
@@ -1589,7 +1597,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GFPL_CU
                     const int x = CUT_FAST + e;   // the new line's r = 0 info, straight from its record
                     if (e < 21) {
                         const double mid = sumA[g][e] + info[kk];
-                        const double nw = mid - (PROOF ? rec_l[(size_t)m * CUT_REC + x] : nxl[x >> 4][16 * g + (x & 15)]);
+                        const double nw = mid - (PF ? nxl[x >> 4][16 * g + (x & 15)] : rec_l[(size_t)m * CUT_REC + x]);
                         sumA[g][e] = nw;
                         if (PROOF) sumE[g][e] = mid;   // the exact invCov_sum, kept current (m_sync = m)
                     }
