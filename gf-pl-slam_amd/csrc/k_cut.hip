@@ -2366,6 +2366,8 @@ __global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
     __shared__ uint16_t items[64 * 2 * CUT_KS];
     __shared__ unsigned long long red[4][64];   // ivm0, rim0, ivm1, rim1 (non-negative doubles' bits)
     __shared__ int nbl[64];
+    __shared__ int qln[64];   // each line's index in the prev frame (pass B reads it here: no dependent
+                              // global load ahead of the line's data loads)
     const int b = blockIdx.y;
     const int lane = threadIdx.x;
     const int m = blockIdx.x * 64 + lane;
@@ -2431,7 +2433,9 @@ __global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
                 if (!(r[0] + r[1] <= 1.0)) done = true;
             }
         }
-        const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+        const int qi = p.tr.matched_ls[(size_t)b * p.mls_cap + m];
+        qln[lane] = qi;
+        const size_t q = (size_t)b * p.kl_cap + qi;
         // a path that does not end where the search's final ratios are counts as a failure
         if (!done || __double_as_longlong(r[0]) != __double_as_longlong(p.prev.ls.cut[2 * q]) ||
             __double_as_longlong(r[1]) != __double_as_longlong(p.prev.ls.cut[2 * q + 1]))
@@ -2469,7 +2473,7 @@ __global__ void __launch_bounds__(64) k_cut_vref(KParams p) {
             const int it = items[i];
             const int ln = it >> 6, side = (it >> 5) & 1, kk = it & 31;
             const int mm = blockIdx.x * 64 + ln;
-            const size_t q = (size_t)b * p.kl_cap + p.tr.matched_ls[(size_t)b * p.mls_cap + mm];
+            const size_t q = (size_t)b * p.kl_cap + qln[ln];
             const double* fd = p.scr.cut_rec + ((size_t)b * p.mls_cap + mm) * CUT_REC;
             double P0[3], P1[3], C0[9], C1[9], Jl[2], qc[5];
             const double* A3 = side ? L.eP : L.sP;
