@@ -212,6 +212,12 @@ __device__ __forceinline__ void sad_finish(const KParams& p, const SadJob& J, fl
 #define GFPL_SP_WAVES 6   // waves per SIMD: <= 84 VGPRs; LDS holds three 512-thread workgroups per CU (6 waves per SIMD)
 #endif
 #define SP_CHUNK 32       // sorted right-keypoint entries per staged descriptor chunk (k_stereo_points, SEG)
+#ifndef GFPL_SP_TY
+#define GFPL_SP_TY 3      // SAD job tiles (SEG): 2^TY rows x 2^TX columns, coarser when the bins exceed 4094
+#endif
+#ifndef GFPL_SP_TX
+#define GFPL_SP_TX 6
+#endif
 #define SP_MINR_PAD 32    // minr bins span [-PAD, H + PAD) (k_stereo_points, SEG): every band is shorter
 
 // LDS-only wave sync: the wave's earlier LDS writes / reads have completed (LDS executes a
@@ -594,7 +600,7 @@ __global__ void __launch_bounds__(BLOCK, GFPL_SP_WAVES) k_stereo_points(KParams 
     if (SEG) {
         uint32_t* sj = rkey;                 // sorted jobs (rkey is dead after the band scan)
         uint32_t* hb = stg;                  // u16 tile counts, two per word (the stage buffers are dead)
-        int ty = 3, tx = 6;
+        int ty = GFPL_SP_TY, tx = GFPL_SP_TX;   // log2 of the tile's rows / columns (8 x 64 px)
         auto nbins = [&](int a, int c) {
             return nlev * (((p.cam.lvl_rows[0] - 1) >> a) + 1) * (((p.cam.lvl_cols[0] - 1) >> c) + 1);
         };
