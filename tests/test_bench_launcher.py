@@ -80,3 +80,15 @@ def test_cfg4_refuses_frames_past_the_trajectory():
 def test_world_size_mismatch_refused():
     r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_cfg4_trajectory_covers_the_proven_leg():
+    """cfg4's ground-truth trajectory must hold every frame the run generates, the proven leg's
+    (one untimed + --proven-steps) included: 505 timed steps + init + 2 host-fed frames fit the 512
+    stored poses only without the leg (a run that passed the check once failed at its first proven step)."""
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "cfg4", "--steps", "505",
+            "--warmup", "0", "--batch", "4", "--no-cpu", "--gen-threads", "1"]
+    r = subprocess.run(base, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 2 and "ground-truth poses" in r.stderr
+    r = subprocess.run(base + ["--proven-steps", "0"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
